@@ -1,0 +1,156 @@
+/*
+ * pfr.h -- C ABI of the MI355X plate frequency-response solver (libpfr.so).
+ *
+ * Drop-in boundary for the reference's native solver path:
+ *   pybind11 class InnerState (source/jax_plate_lib/src/main.cpp:6-19) bound by
+ *   SolverState (source/jax_plate/Sparse.py:19-44) and called through the JAX
+ *   primitives' CPU lowering (Sparse.py:150-160, 187-197).
+ *
+ * Plain C: opaque handles, integer status codes (no exceptions cross the ABI),
+ * plain pointers and sizes.  Complex numbers are interleaved (re, im) doubles
+ * (numpy complex128 / torch.complex128 memory layout).  Every *_dev pointer is
+ * a device (HBM) pointer; `stream` is a hipStream_t (NULL = default stream).
+ * Host pointers are only read during the call.
+ */
+#ifndef PFR_H
+#define PFR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PFR_API __attribute__((visibility("default")))
+
+/* status codes */
+#define PFR_OK 0
+#define PFR_ERR_ARG 1        /* invalid argument (cf. Sparse.py:120-140 checks) */
+#define PFR_ERR_SYMBOLIC 2   /* symbolic analysis failed (cf. umfpack_interface.h:10-18) */
+#define PFR_ERR_HIP 3        /* HIP runtime error */
+#define PFR_ERR_NOMEM 4      /* device allocation failed */
+#define PFR_ERR_STATE 5      /* call out of order (e.g. operator not set) */
+
+/* per-frequency status flags (bitwise OR into an int32 array) */
+#define PFR_FLAG_BAD_PIVOT 1 /* zero / non-finite static pivot */
+
+/* loss types (Problem.py:948-975) */
+#define PFR_LOSS_NONE -1
+#define PFR_LOSS_MSE 0
+#define PFR_LOSS_RMSE 1
+#define PFR_LOSS_MSE_AFC 2
+#define PFR_LOSS_MSE_LOG_AFC 3
+#define PFR_LOSS_COTANGENT 4  /* ref holds dL/dfr (real part), loss not computed */
+
+typedef struct pfr_symbolic pfr_symbolic;
+typedef struct pfr_solver pfr_solver;
+
+typedef struct pfr_symbolic_options {
+  int32_t leaf_size;   /* nested-dissection leaf size (default 96) */
+  int32_t ordering;    /* 0 nested dissection (default), 1 natural */
+  int32_t relax_small, relax_mid, relax_big; /* supernode amalgamation (4, 16, 48) */
+  double zrelax_mid, zrelax_big;             /* (0.5, 0.1) */
+} pfr_symbolic_options;
+
+typedef struct pfr_symbolic_stats {
+  int32_t n;
+  int64_t nnz;
+  int32_t n_fronts;
+  int32_t n_levels;
+  int32_t max_front;
+  int64_t total_rows;      /* sum of front sizes */
+  int64_t factor_entries;  /* sum of squared front sizes (dense front storage per frequency) */
+  int64_t nnz_lu;          /* entries of L + U (per frequency) */
+  double factor_flops;     /* real flops of one numeric factorisation */
+} pfr_symbolic_stats;
+
+/* export ids for pfr_symbolic_export (int32 arrays unless noted) */
+#define PFR_EXPORT_PERM 0        /* n: new -> old */
+#define PFR_EXPORT_IPERM 1       /* n: old -> new */
+#define PFR_EXPORT_FRONTS 2      /* n_fronts x 8 int64: ns, f, row0, col0, parent, level, off, wv */
+#define PFR_EXPORT_IDX 3         /* total_rows */
+#define PFR_EXPORT_RELPOS 4      /* total_rows */
+#define PFR_EXPORT_ASM_PTR 5     /* total_rows + 1 */
+#define PFR_EXPORT_ASM_COL 6     /* nnz */
+#define PFR_EXPORT_ASM_NZ 7      /* nnz */
+#define PFR_EXPORT_EA_PTR 8      /* total_rows + 1 */
+#define PFR_EXPORT_EA_SRC 9      /* ea_ptr[total_rows] */
+#define PFR_EXPORT_LEVEL_PTR 10  /* n_levels + 1 */
+#define PFR_EXPORT_LEVEL_FRONTS 11 /* n_fronts */
+
+PFR_API const char* pfr_version(void);
+/* Message of the last failed call on this thread ("" if none). */
+PFR_API const char* pfr_last_error(void);
+PFR_API void pfr_symbolic_options_default(pfr_symbolic_options* opt);
+
+/* ---------------------------------------------------------------- symbolic (host only, no GPU)
+ * Replaces InnerState::add_mat -> umfpack_zi_symbolic (InnerState.h:120-162) and
+ * create_symbolic (Sparse.py:92-116).  Pattern = n x n CSC (colptr n+1, rowind nnz),
+ * the union pattern of Problem.py:317-332.  opt may be NULL (defaults). */
+PFR_API int pfr_symbolic_create(int32_t n, int64_t nnz, const int32_t* colptr, const int32_t* rowind,
+                                const pfr_symbolic_options* opt, pfr_symbolic** out);
+PFR_API int pfr_symbolic_stats_get(const pfr_symbolic* sym, pfr_symbolic_stats* out);
+PFR_API int pfr_symbolic_export(const pfr_symbolic* sym, int32_t what, void* dst, int64_t capacity_bytes);
+PFR_API void pfr_symbolic_destroy(pfr_symbolic* sym);
+
+/* ---------------------------------------------------------------- device solver
+ * Uploads the symbolic maps and allocates frequency-minor workspaces for up to
+ * max_batch frequencies per chunk.  Keeps a copy of colptr/rowind for matvec. */
+PFR_API int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int32_t* rowind,
+                              int32_t device, int32_t max_batch, pfr_solver** out);
+PFR_API void pfr_solver_destroy(pfr_solver* s);
+/* device bytes pfr_solver_create would allocate for max_batch */
+PFR_API int64_t pfr_solver_workspace_bytes(const pfr_symbolic* sym, int32_t max_batch);
+PFR_API int32_t pfr_solver_max_batch(const pfr_solver* s);
+
+/* ---------------------------------------------------------------- InnerState-compatible entry points
+ * pfr_solve: x[q] = A_q^{-1} b[q]  (transpose != 0: A_q^{-T} b[q], NON-conjugate, = UMFPACK_Aat,
+ * InnerState.h:183-185).  A_q values on the CSC pattern: data_dev + q * data_stride (complex, nnz);
+ * data_stride = 0 broadcasts one matrix (modes 0/2 of InnerState::solve, InnerState.h:192-233);
+ * b_stride likewise (0 = broadcast b, mode 1).  Batch-major (batch, n) complex output.
+ * Replaces InnerState::solve (InnerState.h:164-308).  flags_dev: int32 per batch item (may be NULL). */
+PFR_API int pfr_solve(pfr_solver* s, int32_t batch, const double* data_dev, int64_t data_stride,
+                      const double* b_dev, int64_t b_stride, double* x_dev, int32_t transpose,
+                      int32_t* flags_dev, void* stream);
+/* pfr_matvec: y[q] = A_q x[q] (or A_q^T x[q]); replaces InnerState::matvec (InnerState.h:310-470). */
+PFR_API int pfr_matvec(pfr_solver* s, int32_t batch, const double* data_dev, int64_t data_stride,
+                       const double* x_dev, int64_t x_stride, double* y_dev, int32_t transpose, void* stream);
+
+/* ---------------------------------------------------------------- fused operator-form sweep
+ * The hot path of Problem.getFRFunction / getLossFunction (Problem.py:432-477, 948-975) fused
+ * with the reverse pass JAX derives from Sparse.py:162-222:
+ *   A(omega) = K - omega^2 M,  b(omega) = rhs * (beta - omega^2 mass_sum),
+ *   fr = sqrt(ts^2|aU.x|^2 + ts^2|aV.x|^2 + |aW.x|^2),
+ *   loss = scale * sum_q term(fr_q, ref_q),
+ *   w_k = sum_q ( -lam_q^T S_k x_q + e_k lam_q^T rhs ),   A^T lam_q = d loss / d x_q.
+ * The (F, nnz) matrix batch is never materialised. */
+
+/* K_out_dev = sum_k coef_k * S_k  (S registered by pfr_set_stiffness), complex nnz */
+PFR_API int pfr_set_stiffness(pfr_solver* s, int32_t n_stiff, const double* stiff_dev /* (nnz, n_stiff) */,
+                              const double* rhs_weights /* host, n_stiff: e_k */);
+PFR_API int pfr_combine(pfr_solver* s, const double* coef /* host complex n_stiff */, double* K_out_dev,
+                        void* stream);
+PFR_API int pfr_set_operator(pfr_solver* s, const double* K_dev /* complex nnz */, const double* M_dev /* real nnz */);
+PFR_API int pfr_set_rhs(pfr_solver* s, const double* rhs_host /* real n, caller numbering */, double beta_re,
+                        double beta_im, double mass_sum);
+PFR_API int pfr_set_functional(pfr_solver* s, int32_t n_support, const int32_t* index_host /* caller numbering */,
+                               const double* a_host /* 3 x n_support: aU, aV, aW */, double ts);
+/* nfreq frequencies [Hz] (device).  loss_type PFR_LOSS_NONE: forward only (fr_dev).  Otherwise ref_dev
+ * (complex nfreq) and the reverse pass: loss_dev[0] += sum of terms * scale ... (raw sum, unscaled),
+ * w_dev (complex n_stiff) += gradient partials.  fr_dev / loss_dev / w_dev / flags_dev may be NULL. */
+PFR_API int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t loss_type,
+                      const double* ref_dev, double scale, double* fr_dev, double* loss_dev, double* w_dev,
+                      int32_t* flags_dev, void* stream);
+
+/* Per-phase device times [ms] of the last pfr_sweep/pfr_solve call on this solver, measured with HIP
+ * events on the call's stream (0 = factor, 1 = forward solves, 2 = functional, 3 = adjoint solves,
+ * 4 = contraction).  Timing is enabled by pfr_set_timing(s, 1). */
+PFR_API int pfr_set_timing(pfr_solver* s, int32_t enable);
+PFR_API int pfr_last_timings(const pfr_solver* s, double* ms_out /* 5 */);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PFR_H */

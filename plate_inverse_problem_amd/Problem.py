@@ -1,0 +1,374 @@
+"""``Problem``: differentiable plate frequency response on MI355X.
+
+Mirrors ``source/jax_plate/Problem.py`` (constructor semantics, ``getFRFunction``,
+``solveForward``, ``getLossFunction``, ``solveInverse``) -- the unsymmetric
+(accelerometer) branch, which is the reference's only live branch (SURVEY.md
+§2).  The reference's JAX ``jit(vmap(_solve))`` + UMFPACK-callback hot path is
+replaced by one fused HIP sweep per frequency chunk (``_native.Solver.sweep``):
+
+    assemble K(theta) - omega^2 M -> static-pivot multifrontal LU -> L/U solves
+    -> FR functional [-> loss cotangent -> U^T/L^T adjoint solves ->
+    stiffness contraction]
+
+Autodiff: the sweep is a ``torch.autograd.Function`` of the 18 complex laminate
+coefficients ``c = (A, B, D)``; torch autograd carries the gradient through the
+material transform to ``theta``.  Gradients are exact adjoints (no finite
+differences), with the reference's non-conjugate transpose (``Sparse.py:211-219``).
+"""
+from __future__ import annotations
+
+import functools
+import json
+import os
+import warnings
+from typing import Callable
+
+import numpy as np
+import torch
+
+from . import _native
+from .Accelerometer import Accelerometer, AccelerometerParams
+from .Geometry import Geometry, GeometryParams
+from .Material import Material, get_material
+from .fem.layout import load_matrices_unsymm, union_pattern
+
+RHS_WEIGHTS_D = np.array([1.0, 2.0, 4.0, 1.0, 4.0, 4.0])   # Problem.py:447-448
+KB_SLICE = slice(6, 12)                                     # the 6 coupling (B) matrices
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+
+
+def _default_device():
+    if not torch.cuda.is_available():
+        raise _native.NativeError("the plate solver runs on a ROCm GPU; torch.cuda.is_available() is False "
+                                  "(there is no CPU fallback)")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+class _Engine:
+    """Device state of one Problem: symbolic analysis, solver, operator data."""
+
+    def __init__(self, prob: "Problem", device, n_freqs: int, max_batch: int | None):
+        self.device = device
+        mats = prob.mats
+        # structural pattern of the matrices that can be non-zero: for a mid-plane
+        # symmetric material the B coefficients are identically zero, the KB
+        # entries carry exact zeros and are dropped from the factorised pattern.
+        active = [k for k in range(26) if not (prob.material.is_mps and KB_SLICE.start <= k < KB_SLICE.stop)]
+        keep = prob.present[active].any(axis=0)
+        self.keep = np.nonzero(keep)[0]
+        rows, cols = prob.rows[self.keep], prob.cols[self.keep]
+        n = prob.mat_size
+        colptr = np.zeros(n + 1, dtype=np.int64)
+        np.add.at(colptr, cols.astype(np.int64) + 1, 1)
+        colptr = np.cumsum(colptr).astype(np.int32)
+        self.sym = _native.Symbolic(n, colptr, rows.astype(np.int32))
+        self.stats = self.sym.stats()
+        if not max_batch:
+            # as many frequencies per chunk as fit in ~60% of free HBM (multiple of 64, <= 4096)
+            want = min(max(64, (n_freqs + 63) // 64 * 64), 4096)
+            free, _ = torch.cuda.mem_get_info(device)
+            cap = int(0.6 * free / self.sym.workspace_bytes(64)) * 64
+            max_batch = max(64, min(want, cap))
+        self.solver = _native.Solver(self.sym, device.index, max_batch)
+        vals = mats[:, self.keep]
+        self.stiff = torch.as_tensor(np.ascontiguousarray(vals[:18].T), device=device)       # (nnz, 18)
+        I0, I0c, I2, I2c = prob.I0, prob.I0Corr, prob.I2, prob.I2Corr
+        mass = I0 * (vals[18] + vals[20] + vals[22]) + I0c * (vals[19] + vals[21] + vals[23]) \
+            + I2 * vals[24] + I2c * vals[25]                                                  # Problem.py:441-443
+        self.mass = torch.as_tensor(np.ascontiguousarray(mass), device=device)
+        self.mass_sum = I0 + I0c + I2 + I2c
+        self.K = torch.empty(self.keep.size, dtype=torch.complex128, device=device)
+        self.e = np.concatenate([np.zeros(12), RHS_WEIGHTS_D])
+        self.solver.set_stiffness(self.stiff, self.e)
+        self.solver.set_operator(torch.view_as_real(self.K), self.mass)
+        aU, aV, aW = prob.averaging_vectors()
+        sup = np.nonzero((aU != 0) | (aV != 0) | (aW != 0))[0]
+        self.solver.set_functional(sup, np.stack([aU[sup], aV[sup], aW[sup]]), prob.accelerometer.transverse_sensitivity)
+        self.rhs = prob.vec
+        self._coef_key = None
+
+    def set_coefficients(self, c: np.ndarray):
+        """Precombine K(theta) = sum_k c_k S_k on the device and the rhs scale."""
+        key = c.tobytes()
+        if key == self._coef_key:
+            return
+        self.solver.combine(c, torch.view_as_real(self.K))
+        beta = complex(self.e @ c)
+        self.solver.set_rhs(self.rhs, beta, self.mass_sum)
+        self._coef_key = key
+
+
+def _coeffs18(transform, params: torch.Tensor) -> torch.Tensor:
+    A, B, D = transform(params)
+    return torch.cat([A, B, D]).to(torch.complex128)
+
+
+class _SweepFR(torch.autograd.Function):
+    """fr(c) for a frequency vector; backward = adjoint sweep with dL/dfr."""
+
+    @staticmethod
+    def forward(ctx, c, engine, freqs):
+        cn = c.detach().cpu().numpy()
+        engine.set_coefficients(cn)
+        fr = torch.empty(freqs.numel(), dtype=torch.float64, device=engine.device)
+        flags = torch.zeros(freqs.numel(), dtype=torch.int32, device=engine.device)
+        engine.solver.sweep(freqs, _native.LOSS_NONE, fr=fr, flags=flags)
+        _check_flags(flags)
+        ctx.engine, ctx.freqs, ctx.cn = engine, freqs, cn
+        return fr
+
+    @staticmethod
+    def backward(ctx, grad_fr):
+        engine = ctx.engine
+        engine.set_coefficients(ctx.cn)
+        ref = torch.zeros(ctx.freqs.numel(), dtype=torch.complex128, device=engine.device)
+        ref.real.copy_(grad_fr.to(torch.float64))
+        w = torch.zeros(18, dtype=torch.complex128, device=engine.device)
+        loss = torch.zeros(1, dtype=torch.float64, device=engine.device)
+        engine.solver.sweep(ctx.freqs, _native.LOSS_COTANGENT, ref=torch.view_as_real(ref), scale=1.0,
+                            loss=loss, w=torch.view_as_real(w))
+        return torch.conj(w).to(torch.complex128).cpu(), None, None
+
+
+class _SweepLoss(torch.autograd.Function):
+    """Fused loss + gradient: one factorisation per frequency (forward + adjoint)."""
+
+    @staticmethod
+    def forward(ctx, c, engine, freqs, ref, loss_id, n_total, reduce_fn):
+        cn = c.detach().cpu().numpy()
+        engine.set_coefficients(cn)
+        w = torch.zeros(18, dtype=torch.complex128, device=engine.device)
+        loss = torch.zeros(1, dtype=torch.float64, device=engine.device)
+        flags = torch.zeros(freqs.numel(), dtype=torch.int32, device=engine.device)
+        engine.solver.sweep(freqs, loss_id, ref=torch.view_as_real(ref), scale=1.0 / n_total,
+                            loss=loss, w=torch.view_as_real(w), flags=flags)
+        _check_flags(flags)
+        packed = torch.cat([loss.to(torch.complex128), w])
+        if reduce_fn is not None:
+            packed = reduce_fn(packed)
+        ctx.save_for_backward(packed[1:].cpu())
+        return (packed[0].real / n_total).cpu()
+
+    @staticmethod
+    def backward(ctx, g):
+        (w,) = ctx.saved_tensors
+        return torch.conj(w) * g, None, None, None, None, None, None
+
+
+def _check_flags(flags):
+    bad = int((flags != 0).sum().item())
+    if bad:
+        warnings.warn(f"{bad} frequencies hit a zero/non-finite static pivot (PFR_FLAG_BAD_PIVOT); "
+                      "their results are not reliable", RuntimeWarning)
+
+
+class Problem:
+    """Geometry + known parameters; builds the FE system once, exposes differentiable FR/loss."""
+
+    def __init__(self, geometry: Geometry = None, material: Material = None, accel: Accelerometer = None,
+                 ref_fr: tuple = None, *, cpu: int | None = 0, spath: str | os.PathLike = None,
+                 device=None, max_batch: int | None = None):
+        if (geometry, accel, material, spath) == (None,) * 4:                       # Problem.py:86-87
+            raise ValueError('Cannot create a Problem object without arguments.')
+        self.n_cpu = cpu
+        self.geometry, self.material, self.accelerometer = geometry, material, accel
+        if spath is None:
+            if None in (geometry, accel, material):
+                raise ValueError('Cannot create a Problem object without `spath` argument if any of '
+                                 '`geometry`, `accel`, `material` arguments is `None`.')
+        else:
+            self._load_setup(spath, geometry, material, accel)
+        if self.material.has_params:
+            self.parameters = self.material.get_parameters()
+        else:
+            warnings.warn('Some elastic moduli of a material were not provided, solving forward problem as '
+                          'standalone will not be possible.', RuntimeWarning)
+        if ref_fr is not None:
+            self.reference_fr = ref_fr
+        self.e = self.geometry.height / 2.0
+        self.rho = self.material.density
+        self._device = device
+        self._max_batch = max_batch
+        self._engine = None
+        self._build_system()
+
+    # ------------------------------------------------------------------ setup
+    def _load_setup(self, spath, geometry, material, accel):
+        """``setup.json`` folder semantics of Problem.py:102-214."""
+        if not isinstance(spath, (str, os.PathLike)):
+            raise TypeError(f'Argument `spath` should have one of the following types: str | os.PathLike, '
+                            f'not {type(spath)}.')
+        if not os.path.isabs(spath):
+            spath = os.path.join(_PKG_DIR, 'setups', spath)
+        if not os.path.exists(spath):
+            raise ValueError(f'Path of the setup {spath} does not exist.')
+        if not os.path.isdir(spath):
+            raise ValueError(f'Selected path {spath} is not a directory.')
+        fpath = os.path.join(spath, 'setup.json')
+        if not os.path.exists(fpath):
+            raise FileNotFoundError(f'`setup.json` file was not found in setup directory {spath}.')
+        with open(fpath) as f:
+            sp = json.load(f)
+        if 'accelerometer' in sp:
+            v = sp['accelerometer']
+            if isinstance(v, str):
+                self.accelerometer = Accelerometer(v)
+            elif isinstance(v, dict):
+                self.accelerometer = Accelerometer(AccelerometerParams(**v))
+            else:
+                raise TypeError(f'In file {fpath} key `accelerometer` should have a value with type `str` or `dict`.')
+        if 'material' in sp:
+            v = sp['material']
+            if not isinstance(v, (str, dict)):
+                raise TypeError(f'In file {fpath} key `material` should have a value with type `str` or `dict`.')
+            self.material = get_material(v)
+        if material is not None:
+            self.material = material
+        if accel is not None:
+            self.accelerometer = accel
+        if geometry is not None:
+            self.geometry = geometry
+        elif 'geometry' in sp:
+            g = dict(sp['geometry'])
+            if 'template' not in g:
+                raise ValueError(f'Cannot create Geometry object, file {fpath} should contain `template` inside '
+                                 '`geometry` (FreeFEM `edp` geometries need FreeFem++, not available).')
+            templ = g.pop('template')
+            ny = g.pop('ny', 6)
+            self.geometry = Geometry(templ, accelerometer=self.accelerometer, params=GeometryParams(**g), ny=ny)
+        freq_file = os.path.join(spath, 'freqs.npy')
+        if os.path.exists(freq_file):
+            freqs = np.load(freq_file)
+            amp = np.load(os.path.join(spath, 'amp.npy'))
+            ph = os.path.join(spath, 'phase.npy')
+            phase = np.load(ph) if os.path.exists(ph) else np.zeros_like(amp)
+            self.reference_fr = (freqs, amp * np.exp(1j * phase))
+        if None in (self.accelerometer, self.geometry, self.material):
+            raise RuntimeError('One of the `geometry`, `accelerometer`, `materials` attributes was not provided '
+                               'in setup.json nor as an argument.')
+
+    def _build_system(self):
+        """FE matrices + union pattern + inertia constants (Problem.py:310-374)."""
+        out = load_matrices_unsymm(self.geometry.build_varfs())
+        mats = out[0]
+        self.mat_size = mats[0].shape[0]
+        up = union_pattern(mats)
+        self.sparsity = up.nnz / self.mat_size ** 2
+        self.rows, self.cols = up.rows, up.cols
+        self.colptr, self.rowind = up.colptr, up.rowind
+        self.mats = up.values                                   # (26, nnz), CSC order
+        self.present = np.zeros_like(up.values, dtype=bool)
+        n = self.mat_size
+        keys = up.rows.astype(np.int64) + n * up.cols.astype(np.int64)
+        for k, m in enumerate(mats):
+            c = m.tocoo()
+            self.present[k, np.searchsorted(keys, c.row.astype(np.int64) + n * c.col.astype(np.int64))] = True
+        (self.vec, self.interp_mat, self.interp_mat_Lh, self.Lh_size, self.Mh_size, self.mesh,
+         self.interp_mat_Wx, self.interp_mat_Wy) = out[1:]
+        acc = self.accelerometer
+        rho_corr = acc.mass / (np.pi * acc.radius ** 2) / acc.height if acc is not None else 0.0
+        h = self.geometry.height
+        self.I0 = h * self.rho                                                  # Problem.py:367-374
+        self.I0Corr = acc.height * rho_corr
+        self.I2 = self.rho * h ** 3 / 12
+        self.I2Corr = rho_corr / 3 * ((h / 2 + acc.height) ** 3 - h ** 3 / 8)
+
+    def averaging_vectors(self):
+        """aU, aV, aW with U = aU . x etc.: ``mean(I @ x) = (1^T I / P) @ x`` (Problem.py:454-462)."""
+        L, n = self.Lh_size, self.mat_size
+        k = self.accelerometer.effective_height * self.accelerometer.height
+        P = self.interp_mat_Lh.shape[0]
+        aU, aV, aW = np.zeros(n), np.zeros(n), np.zeros(n)
+        aU[:L] = self.interp_mat_Lh.sum(0) / P
+        aU[2 * L:] = -k * self.interp_mat_Wx.sum(0) / P
+        aV[L:2 * L] = self.interp_mat_Lh.sum(0) / P
+        aV[2 * L:] = -k * self.interp_mat_Wy.sum(0) / P
+        aW[2 * L:] = self.interp_mat.sum(0) / P
+        return aU, aV, aW
+
+    # ------------------------------------------------------------------ engine
+    @property
+    def device(self):
+        if self._device is None:
+            self._device = _default_device()
+        return torch.device(self._device)
+
+    def engine(self, n_freqs: int = 1024) -> _Engine:
+        if self._engine is None:
+            dev = self.device
+            if dev.type != 'cuda':
+                raise _native.NativeError('the plate solver needs a ROCm device (no CPU fallback)')
+            self._engine = _Engine(self, dev, n_freqs, self._max_batch)
+        return self._engine
+
+    def _transform(self):
+        return self.material.get_ABD_transform(self.geometry.height)
+
+    def _freqs(self, freqs) -> torch.Tensor:
+        return torch.as_tensor(np.asarray(freqs, dtype=np.float64) if not isinstance(freqs, torch.Tensor)
+                               else freqs, dtype=torch.float64, device=self.device).contiguous()
+
+    # ------------------------------------------------------------------ API
+    @functools.cache
+    def getFRFunction(self) -> Callable:
+        """``fr(freqs, params) -> (F,) float64 tensor`` on the device, differentiable in params
+        (``Problem.py:377-518``)."""
+        transform = self._transform()
+
+        def fr_function(freqs, params):
+            f = self._freqs(freqs)
+            p = params if isinstance(params, torch.Tensor) else torch.as_tensor(np.asarray(params, dtype=np.float64))
+            c = _coeffs18(transform, p.to(torch.float64).cpu())
+            return _SweepFR.apply(c, self.engine(f.numel()), f)
+
+        return fr_function
+
+    getAFCFunction = getFRFunction
+
+    def solveForward(self, freqs, params=None) -> np.ndarray:
+        """Frequency response at ``freqs`` [Hz] (``Problem.py:611-639``)."""
+        if params is None:
+            params = self.parameters
+        with torch.no_grad():
+            return self.getFRFunction()(freqs, params).cpu().numpy()
+
+    solve_forward = solveForward
+
+    def getLossFunction(self, frequencies, reference_fr, func_type: str, scaling_params=None,
+                        *, distributed: bool = False) -> Callable:
+        """``loss(params) -> 0-dim tensor`` (``Problem.py:933-980``).
+
+        With ``distributed=True`` and an initialised ``torch.distributed`` group,
+        every rank sweeps its contiguous block of the frequencies and one
+        all-reduce combines loss and gradient partials.
+        """
+        frequencies = np.asarray(frequencies)
+        reference_fr = np.asarray(reference_fr)
+        assert frequencies.shape[0] == reference_fr.shape[0]
+        if func_type not in _native.LOSS_IDS:
+            raise ValueError(f'Function type "{func_type}" is not supported!')
+        loss_id = _native.LOSS_IDS[func_type]
+        scaling = 1.0 if scaling_params is None else torch.as_tensor(np.array(scaling_params, dtype=np.float64))
+        n_total = frequencies.shape[0]
+        lo, hi, reduce_fn = 0, n_total, None
+        if distributed:
+            from .distributed import shard_range, all_reduce_sum
+            lo, hi = shard_range(n_total)
+            reduce_fn = all_reduce_sum
+        transform = self._transform()
+        f_local = self._freqs(frequencies[lo:hi])
+        ref_local = torch.as_tensor(reference_fr[lo:hi].astype(np.complex128), device=self.device)
+
+        def loss(params):
+            p = params if isinstance(params, torch.Tensor) else torch.as_tensor(np.asarray(params, dtype=np.float64))
+            c = _coeffs18(transform, p.to(torch.float64).cpu() * scaling)
+            return _SweepLoss.apply(c, self.engine(max(1, hi - lo)), f_local, ref_local, loss_id, n_total, reduce_fn)
+
+        return loss
+
+    def solveInverse(self, *args, **kwargs):
+        from .inverse import solve_inverse
+        return solve_inverse(self, *args, **kwargs)
+
+    def solveInverseLocal(self, *args, **kwargs):
+        return self.solveInverse(*args, **kwargs)

@@ -1,0 +1,255 @@
+"""ctypes binding of ``libpfr.so`` (C ABI declared in ``include/pfr.h``).
+
+This is the reference-side binding a maintainer would add in place of the
+pybind11 module ``jax_plate_lib`` (``source/jax_plate_lib/src/main.cpp:4-20``,
+used by ``SolverState`` at ``source/jax_plate/Sparse.py:19-44``).
+
+The library is built in-tree (``plate_inverse_problem_amd/_lib/libpfr.so``) by
+``__graft_entry__.build()``; there is no CPU fallback: every compute entry
+point raises if the library is missing or a call fails.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libpfr.so")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "pfr.h")
+
+PFR_OK = 0
+PFR_FLAG_BAD_PIVOT = 1
+LOSS_NONE, LOSS_MSE, LOSS_RMSE, LOSS_MSE_AFC, LOSS_MSE_LOG_AFC, LOSS_COTANGENT = -1, 0, 1, 2, 3, 4
+LOSS_IDS = {"MSE": LOSS_MSE, "RMSE": LOSS_RMSE, "MSE_AFC": LOSS_MSE_AFC, "MSE_LOG_AFC": LOSS_MSE_LOG_AFC}
+
+EXPORT = dict(PERM=0, IPERM=1, FRONTS=2, IDX=3, RELPOS=4, ASM_PTR=5, ASM_COL=6, ASM_NZ=7, EA_PTR=8,
+              EA_SRC=9, LEVEL_PTR=10, LEVEL_FRONTS=11)
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+class SymbolicOptions(C.Structure):
+    _fields_ = [("leaf_size", C.c_int32), ("ordering", C.c_int32), ("relax_small", C.c_int32),
+                ("relax_mid", C.c_int32), ("relax_big", C.c_int32), ("zrelax_mid", C.c_double),
+                ("zrelax_big", C.c_double)]
+
+
+class SymbolicStats(C.Structure):
+    _fields_ = [("n", C.c_int32), ("nnz", C.c_int64), ("n_fronts", C.c_int32), ("n_levels", C.c_int32),
+                ("max_front", C.c_int32), ("total_rows", C.c_int64), ("factor_entries", C.c_int64),
+                ("nnz_lu", C.c_int64), ("factor_flops", C.c_double)]
+
+
+_P = C.c_void_p
+_I32P = C.POINTER(C.c_int32)
+_DP = C.POINTER(C.c_double)
+
+_PROTOS = {
+    "pfr_version": (C.c_char_p, []),
+    "pfr_last_error": (C.c_char_p, []),
+    "pfr_symbolic_options_default": (None, [C.POINTER(SymbolicOptions)]),
+    "pfr_symbolic_create": (C.c_int, [C.c_int32, C.c_int64, _I32P, _I32P, C.POINTER(SymbolicOptions), C.POINTER(_P)]),
+    "pfr_symbolic_stats_get": (C.c_int, [_P, C.POINTER(SymbolicStats)]),
+    "pfr_symbolic_export": (C.c_int, [_P, C.c_int32, _P, C.c_int64]),
+    "pfr_symbolic_destroy": (None, [_P]),
+    "pfr_solver_create": (C.c_int, [_P, _I32P, _I32P, C.c_int32, C.c_int32, C.POINTER(_P)]),
+    "pfr_solver_destroy": (None, [_P]),
+    "pfr_solver_workspace_bytes": (C.c_int64, [_P, C.c_int32]),
+    "pfr_solver_max_batch": (C.c_int32, [_P]),
+    "pfr_solve": (C.c_int, [_P, C.c_int32, _P, C.c_int64, _P, C.c_int64, _P, C.c_int32, _P, _P]),
+    "pfr_matvec": (C.c_int, [_P, C.c_int32, _P, C.c_int64, _P, C.c_int64, _P, C.c_int32, _P]),
+    "pfr_set_stiffness": (C.c_int, [_P, C.c_int32, _P, _DP]),
+    "pfr_combine": (C.c_int, [_P, _DP, _P, _P]),
+    "pfr_set_operator": (C.c_int, [_P, _P, _P]),
+    "pfr_set_rhs": (C.c_int, [_P, _DP, C.c_double, C.c_double, C.c_double]),
+    "pfr_set_functional": (C.c_int, [_P, C.c_int32, _I32P, _DP, C.c_double]),
+    "pfr_sweep": (C.c_int, [_P, C.c_int32, _P, C.c_int32, _P, C.c_double, _P, _P, _P, _P, _P]),
+    "pfr_set_timing": (C.c_int, [_P, C.c_int32]),
+    "pfr_last_timings": (C.c_int, [_P, _DP]),
+}
+
+_lib = None
+
+
+def header_symbols() -> list[str]:
+    """Function names declared ``PFR_API`` in include/pfr.h."""
+    with open(HEADER_PATH) as f:
+        txt = f.read()
+    return re.findall(r"PFR_API\s+[\w\s\*]+?\b(pfr_\w+)\s*\(", txt)
+
+
+def lib():
+    """Load libpfr.so (once).  Raises NativeError if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                          " (no CPU fallback exists for the solver path)")
+    L = C.CDLL(LIB_PATH)
+    for name, (res, args) in _PROTOS.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != PFR_OK:
+        msg = lib().pfr_last_error().decode(errors="replace")
+        raise NativeError(f"{what} failed (status {rc}): {msg}")
+
+
+def _i32(a):
+    a = np.ascontiguousarray(a, dtype=np.int32)
+    return a, a.ctypes.data_as(_I32P)
+
+
+def _f64(a):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    return a, a.ctypes.data_as(_DP)
+
+
+def _ptr(t) -> int:
+    """Device pointer of a torch tensor (or None -> NULL)."""
+    if t is None:
+        return None
+    if not t.is_contiguous():
+        raise ValueError("device tensors passed to libpfr must be contiguous")
+    return t.data_ptr()
+
+
+class Symbolic:
+    """Host-only symbolic analysis (nested dissection + supernodal maps)."""
+
+    def __init__(self, n: int, colptr, rowind, *, leaf_size=None, ordering=0, relax=None):
+        L = lib()
+        opt = SymbolicOptions()
+        L.pfr_symbolic_options_default(C.byref(opt))
+        if leaf_size is not None:
+            opt.leaf_size = int(leaf_size)
+        opt.ordering = int(ordering)
+        if relax is not None:
+            opt.relax_small, opt.relax_mid, opt.relax_big = relax
+        self.colptr, cp = _i32(colptr)
+        self.rowind, ri = _i32(rowind)
+        self.n = int(n)
+        h = _P()
+        check(L.pfr_symbolic_create(self.n, int(self.rowind.size), cp, ri, C.byref(opt), C.byref(h)),
+              "pfr_symbolic_create")
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    def stats(self) -> dict:
+        st = SymbolicStats()
+        check(lib().pfr_symbolic_stats_get(self._h, C.byref(st)), "pfr_symbolic_stats_get")
+        return {k: getattr(st, k) for k, _ in SymbolicStats._fields_}
+
+    def export(self, what: str) -> np.ndarray:
+        st = self.stats()
+        sizes = {"PERM": st["n"], "IPERM": st["n"], "FRONTS": 8 * st["n_fronts"], "IDX": st["total_rows"],
+                 "RELPOS": st["total_rows"], "ASM_PTR": st["total_rows"] + 1, "ASM_COL": st["nnz"],
+                 "ASM_NZ": st["nnz"], "EA_PTR": st["total_rows"] + 1, "LEVEL_PTR": st["n_levels"] + 1,
+                 "LEVEL_FRONTS": st["n_fronts"]}
+        if what == "EA_SRC":
+            size = int(self.export("EA_PTR")[-1])
+        else:
+            size = sizes[what]
+        dtype = np.int64 if what == "FRONTS" else np.int32
+        out = np.zeros(size, dtype=dtype)
+        check(lib().pfr_symbolic_export(self._h, EXPORT[what], out.ctypes.data_as(_P), out.nbytes),
+              "pfr_symbolic_export")
+        return out.reshape(-1, 8) if what == "FRONTS" else out
+
+    def workspace_bytes(self, max_batch: int) -> int:
+        return int(lib().pfr_solver_workspace_bytes(self._h, int(max_batch)))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _lib is not None:
+            _lib.pfr_symbolic_destroy(h)
+            self._h = None
+
+
+class Solver:
+    """Device-resident batched solver for one pattern (one per device)."""
+
+    def __init__(self, sym: Symbolic, device_index: int, max_batch: int):
+        L = lib()
+        self.sym = sym
+        self.device_index = int(device_index)
+        h = _P()
+        _, cp = _i32(sym.colptr)
+        _, ri = _i32(sym.rowind)
+        check(L.pfr_solver_create(sym.handle, cp, ri, self.device_index, int(max_batch), C.byref(h)),
+              "pfr_solver_create")
+        self._h = h
+        self.max_batch = int(L.pfr_solver_max_batch(h))
+        self._keep = {}
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and _lib is not None:
+            _lib.pfr_solver_destroy(h)
+            self._h = None
+
+    @staticmethod
+    def _stream(t):
+        import torch
+        return torch.cuda.current_stream(t.device).cuda_stream
+
+    # ---- operator-form state
+    def set_stiffness(self, stiff_nz_k, rhs_weights):
+        self._keep["stiff"] = stiff_nz_k
+        w, wp = _f64(rhs_weights)
+        check(lib().pfr_set_stiffness(self._h, int(stiff_nz_k.shape[1]), _ptr(stiff_nz_k), wp), "pfr_set_stiffness")
+
+    def combine(self, coef: np.ndarray, out):
+        c = np.ascontiguousarray(np.asarray(coef, dtype=np.complex128))
+        check(lib().pfr_combine(self._h, c.view(np.float64).ctypes.data_as(_DP), _ptr(out), self._stream(out)),
+              "pfr_combine")
+        return out
+
+    def set_operator(self, K, M):
+        self._keep["K"], self._keep["M"] = K, M
+        check(lib().pfr_set_operator(self._h, _ptr(K), _ptr(M)), "pfr_set_operator")
+
+    def set_rhs(self, rhs, beta: complex, mass_sum: float):
+        r, rp = _f64(rhs)
+        check(lib().pfr_set_rhs(self._h, rp, float(np.real(beta)), float(np.imag(beta)), float(mass_sum)),
+              "pfr_set_rhs")
+
+    def set_functional(self, index, a3, ts: float):
+        i, ip = _i32(index)
+        a, ap = _f64(np.asarray(a3).reshape(-1))
+        check(lib().pfr_set_functional(self._h, int(i.size), ip, ap, float(ts)), "pfr_set_functional")
+
+    def sweep(self, freqs, loss_type=LOSS_NONE, ref=None, scale=1.0, fr=None, loss=None, w=None, flags=None):
+        check(lib().pfr_sweep(self._h, int(freqs.numel()), _ptr(freqs), int(loss_type), _ptr(ref), float(scale),
+                              _ptr(fr), _ptr(loss), _ptr(w), _ptr(flags), self._stream(freqs)), "pfr_sweep")
+
+    # ---- InnerState-compatible
+    def solve(self, data, data_stride, b, b_stride, x, transpose, batch, flags=None):
+        check(lib().pfr_solve(self._h, int(batch), _ptr(data), int(data_stride), _ptr(b), int(b_stride), _ptr(x),
+                              int(bool(transpose)), _ptr(flags), self._stream(x)), "pfr_solve")
+
+    def matvec(self, data, data_stride, x, x_stride, y, transpose, batch):
+        check(lib().pfr_matvec(self._h, int(batch), _ptr(data), int(data_stride), _ptr(x), int(x_stride), _ptr(y),
+                               int(bool(transpose)), self._stream(y)), "pfr_matvec")
+
+    # ---- timing
+    def set_timing(self, on: bool):
+        check(lib().pfr_set_timing(self._h, int(bool(on))), "pfr_set_timing")
+
+    def last_timings(self) -> np.ndarray:
+        out = np.zeros(5)
+        check(lib().pfr_last_timings(self._h, out.ctypes.data_as(_DP)), "pfr_last_timings")
+        return out

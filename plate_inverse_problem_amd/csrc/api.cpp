@@ -1,0 +1,542 @@
+// C ABI of libpfr.so (see include/pfr.h).  Host orchestration of the HIP kernels:
+// level-scheduled launches over frequency chunks, workspaces, timing.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "launch.hpp"
+
+using pfr::DevPattern;
+using pfr::Front;
+using pfr::Symbolic;
+
+struct pfr_symbolic {
+  Symbolic S;
+};
+
+namespace {
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+  do {                                                                                    \
+    hipError_t _e = (expr);                                                               \
+    if (_e != hipSuccess)                                                                 \
+      return fail(_e == hipErrorOutOfMemory ? PFR_ERR_NOMEM : PFR_ERR_HIP,                \
+                  std::string(#expr) + ": " + hipGetErrorString(_e));                     \
+  } while (0)
+
+template <class T>
+int upload(T** dst, const std::vector<T>& src) {
+  *dst = nullptr;
+  if (src.empty()) return PFR_OK;
+  HIP_TRY(hipMalloc(dst, src.size() * sizeof(T)));
+  HIP_TRY(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+  return PFR_OK;
+}
+
+int64_t round64(int64_t x) { return (x + 63) / 64 * 64; }
+
+constexpr int kContractBlocks = 64;
+}  // namespace
+
+struct pfr_solver {
+  int device = 0;
+  int n = 0;
+  int64_t nnz = 0;
+  int64_t Fc = 0;  // frequencies per chunk (multiple of 64)
+  std::vector<int32_t> level_ptr, level_maxf, level_W, perm, iperm;
+  DevPattern P{};
+  // owned device arrays
+  std::vector<void*> owned;
+  int32_t* d_level_fronts = nullptr;
+  int32_t* d_colptr = nullptr;
+  int32_t* d_rowind = nullptr;
+  double2 *F = nullptr, *WV = nullptr, *X = nullptr, *Y = nullptr, *XA = nullptr, *G = nullptr;
+  double2 *partial = nullptr, *tq = nullptr;
+  double *freqs = nullptr, *loss_terms = nullptr;
+  int32_t* flags = nullptr;
+  // operator / rhs / functional / stiffness state
+  const double2* K = nullptr;
+  const double* M = nullptr;
+  double* rhsP = nullptr;
+  int32_t* rhs_sup = nullptr;
+  double* rhs_val = nullptr;
+  int n_rhs_sup = 0;
+  double beta_re = 0, beta_im = 0, mass_sum = 0;
+  bool has_rhs = false;
+  pfr::FunctionalArgs fn{};
+  bool has_fn = false;
+  const double* stiff = nullptr;
+  int n_stiff = 0;
+  pfr::CoefPack e{};
+  // timing
+  bool timing = false;
+  hipEvent_t ev[6]{};
+  double last_ms[5]{};
+
+  ~pfr_solver() {
+    for (void* p : owned) (void)hipFree(p);
+    for (auto& x : ev)
+      if (x) (void)hipEventDestroy(x);
+  }
+  template <class T>
+  int alloc(T** p, int64_t count) {
+    *p = nullptr;
+    if (count <= 0) return PFR_OK;
+    HIP_TRY(hipMalloc(p, count * sizeof(T)));
+    owned.push_back(*p);
+    return PFR_OK;
+  }
+  template <class T>
+  int up(T** p, const std::vector<T>& v) {
+    int rc = upload(p, v);
+    if (rc == PFR_OK && *p) owned.push_back(*p);
+    return rc;
+  }
+};
+
+namespace {
+
+int64_t workspace_bytes(const Symbolic& S, int64_t Fc) {
+  int64_t b = 0;
+  b += S.factor_entries * Fc * 16;   // F
+  b += S.total_rows * Fc * 16;       // WV
+  b += 4 * (int64_t)S.n * Fc * 16;   // X, Y, XA, G
+  b += Fc * (8 + 8 + 4 + 16);        // freqs, loss terms, flags, tq
+  return b;
+}
+
+// waves per workgroup for a level whose largest front is maxf
+int waves_for(int maxf) { return std::max(1, std::min(8, (maxf + 23) / 24)); }
+
+void record(pfr_solver* s, int i, hipStream_t st) {
+  if (s->timing) (void)hipEventRecord(s->ev[i], st);
+}
+
+int finish_timing(pfr_solver* s, const bool* used) {
+  if (!s->timing) return PFR_OK;
+  HIP_TRY(hipEventSynchronize(s->ev[5]));
+  for (int i = 0; i < 5; ++i) {
+    float ms = 0;
+    if (used[i]) HIP_TRY(hipEventElapsedTime(&ms, s->ev[i], s->ev[i + 1]));
+    s->last_ms[i] += used[i] ? ms : 0.0;
+  }
+  return PFR_OK;
+}
+
+int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nvalid, hipStream_t st) {
+  const int L = (int)s->level_ptr.size() - 1;
+  const int ngroups = (int)(s->Fc / 64);
+  for (int l = 0; l < L; ++l) {
+    int nf = s->level_ptr[l + 1] - s->level_ptr[l];
+    pfr::launch_factor(mode, s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_W[l], ngroups, s->F, s->Fc,
+                       s->freqs, s->K, s->M, data, ds, nvalid, s->flags, st);
+  }
+  HIP_TRY(hipGetLastError());
+  return PFR_OK;
+}
+
+// which: 0 L, 1 U, 2 U^T, 3 L^T ; bottom-up for 0/2, top-down for 1/3
+int solve_all(pfr_solver* s, int which, int rhs_mode, const pfr::RhsDesc& rd, const double2* Yin, double2* Out,
+              hipStream_t st) {
+  const int L = (int)s->level_ptr.size() - 1;
+  const int ngroups = (int)(s->Fc / 64);
+  const bool up = (which == 0 || which == 2);
+  for (int t = 0; t < L; ++t) {
+    int l = up ? t : L - 1 - t;
+    int nf = s->level_ptr[l + 1] - s->level_ptr[l];
+    pfr::launch_solve(which, rhs_mode, s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_W[l], ngroups, s->F,
+                      s->Fc, s->WV, rd, Yin, Out, st);
+  }
+  HIP_TRY(hipGetLastError());
+  return PFR_OK;
+}
+
+}  // namespace
+
+namespace pfr {
+void launch_pad_freqs(double* freqs, int nvalid, int64_t Fc, hipStream_t st);
+void launch_flags_merge(const int* chunk, int nvalid, int* out, hipStream_t st);
+}
+
+extern "C" {
+
+const char* pfr_version(void) { return "pfr 0.1.0 (gfx950, frequency-minor multifrontal)"; }
+const char* pfr_last_error(void) { return g_last_error.c_str(); }
+
+void pfr_symbolic_options_default(pfr_symbolic_options* o) {
+  pfr::SymbolicOptions d;
+  o->leaf_size = d.leaf_size;
+  o->ordering = d.ordering;
+  o->relax_small = d.relax_small;
+  o->relax_mid = d.relax_mid;
+  o->relax_big = d.relax_big;
+  o->zrelax_mid = d.zrelax_mid;
+  o->zrelax_big = d.zrelax_big;
+}
+
+int pfr_symbolic_create(int32_t n, int64_t nnz, const int32_t* colptr, const int32_t* rowind,
+                        const pfr_symbolic_options* opt, pfr_symbolic** out) {
+  if (!out || !colptr || (nnz > 0 && !rowind) || n <= 0 || nnz < 0) return fail(PFR_ERR_ARG, "bad arguments");
+  if (nnz > INT32_MAX) return fail(PFR_ERR_ARG, "nnz exceeds int32 (cf. Problem.py:311 TODO)");
+  pfr::SymbolicOptions o;
+  if (opt) {
+    o.leaf_size = opt->leaf_size;
+    o.ordering = opt->ordering;
+    o.relax_small = opt->relax_small;
+    o.relax_mid = opt->relax_mid;
+    o.relax_big = opt->relax_big;
+    o.zrelax_mid = opt->zrelax_mid;
+    o.zrelax_big = opt->zrelax_big;
+  }
+  auto* sym = new pfr_symbolic();
+  if (pfr::analyse(n, nnz, colptr, rowind, o, sym->S) != 0) {
+    std::string msg = "symbolic analysis failed: " + sym->S.error;
+    delete sym;
+    return fail(PFR_ERR_SYMBOLIC, msg);
+  }
+  *out = sym;
+  return PFR_OK;
+}
+
+int pfr_symbolic_stats_get(const pfr_symbolic* sym, pfr_symbolic_stats* o) {
+  if (!sym || !o) return fail(PFR_ERR_ARG, "null argument");
+  const Symbolic& S = sym->S;
+  o->n = S.n;
+  o->nnz = S.nnz;
+  o->n_fronts = (int32_t)S.fronts.size();
+  o->n_levels = (int32_t)S.level_ptr.size() - 1;
+  o->max_front = S.max_front;
+  o->total_rows = S.total_rows;
+  o->factor_entries = S.factor_entries;
+  o->nnz_lu = S.nnz_lu;
+  o->factor_flops = S.factor_flops;
+  return PFR_OK;
+}
+
+int pfr_symbolic_export(const pfr_symbolic* sym, int32_t what, void* dst, int64_t cap) {
+  if (!sym || !dst) return fail(PFR_ERR_ARG, "null argument");
+  const Symbolic& S = sym->S;
+  const void* src = nullptr;
+  int64_t bytes = 0;
+  std::vector<int64_t> fr;
+  auto pick = [&](const std::vector<int32_t>& v) {
+    src = v.data();
+    bytes = (int64_t)v.size() * 4;
+  };
+  switch (what) {
+    case PFR_EXPORT_PERM: pick(S.perm); break;
+    case PFR_EXPORT_IPERM: pick(S.iperm); break;
+    case PFR_EXPORT_FRONTS:
+      for (const Front& f : S.fronts) {
+        int64_t v[8] = {f.ns, f.f, f.row0, f.col0, f.parent, f.level, f.off, f.wv};
+        fr.insert(fr.end(), v, v + 8);
+      }
+      src = fr.data();
+      bytes = (int64_t)fr.size() * 8;
+      break;
+    case PFR_EXPORT_IDX: pick(S.idx); break;
+    case PFR_EXPORT_RELPOS: pick(S.relpos); break;
+    case PFR_EXPORT_ASM_PTR: pick(S.asm_ptr); break;
+    case PFR_EXPORT_ASM_COL: pick(S.asm_col); break;
+    case PFR_EXPORT_ASM_NZ: pick(S.asm_nz); break;
+    case PFR_EXPORT_EA_PTR: pick(S.ea_ptr); break;
+    case PFR_EXPORT_EA_SRC: pick(S.ea_src); break;
+    case PFR_EXPORT_LEVEL_PTR: pick(S.level_ptr); break;
+    case PFR_EXPORT_LEVEL_FRONTS: pick(S.level_fronts); break;
+    default: return fail(PFR_ERR_ARG, "unknown export id");
+  }
+  if (bytes > cap) return fail(PFR_ERR_ARG, "destination too small");
+  if (bytes) std::memcpy(dst, src, bytes);
+  return PFR_OK;
+}
+
+void pfr_symbolic_destroy(pfr_symbolic* sym) { delete sym; }
+
+int64_t pfr_solver_workspace_bytes(const pfr_symbolic* sym, int32_t max_batch) {
+  if (!sym || max_batch <= 0) return -1;
+  return workspace_bytes(sym->S, round64(max_batch));
+}
+
+int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int32_t* rowind, int32_t device,
+                      int32_t max_batch, pfr_solver** out) {
+  if (!sym || !out || max_batch <= 0 || !colptr || !rowind) return fail(PFR_ERR_ARG, "bad arguments");
+  HIP_TRY(hipSetDevice(device));
+  const Symbolic& S = sym->S;
+  auto* s = new pfr_solver();
+  auto bail = [&](int rc) {
+    delete s;
+    return rc;
+  };
+  s->device = device;
+  s->n = S.n;
+  s->nnz = S.nnz;
+  s->Fc = round64(max_batch);
+  s->level_ptr = S.level_ptr;
+  s->level_maxf = S.level_maxf;
+  s->perm = S.perm;
+  s->iperm = S.iperm;
+  for (int m : S.level_maxf) s->level_W.push_back(waves_for(m));
+  Front* d_fronts = nullptr;
+  int rc = PFR_OK;
+  std::vector<Front> fv(S.fronts);
+  if ((rc = s->up(&d_fronts, fv))) return bail(rc);
+  int32_t *idx, *relpos, *rowf, *ap, *ac, *an, *ep, *es, *pm, *pr, *pc;
+  if ((rc = s->up(&idx, S.idx)) || (rc = s->up(&relpos, S.relpos)) || (rc = s->up(&rowf, S.row_front)) ||
+      (rc = s->up(&ap, S.asm_ptr)) || (rc = s->up(&ac, S.asm_col)) || (rc = s->up(&an, S.asm_nz)) ||
+      (rc = s->up(&ep, S.ea_ptr)) || (rc = s->up(&es, S.ea_src)) || (rc = s->up(&pm, S.perm)) ||
+      (rc = s->up(&pr, S.prow)) || (rc = s->up(&pc, S.pcol)) || (rc = s->up(&s->d_level_fronts, S.level_fronts)))
+    return bail(rc);
+  std::vector<int32_t> cp(colptr, colptr + S.n + 1), ri(rowind, rowind + S.nnz);
+  if ((rc = s->up(&s->d_colptr, cp)) || (rc = s->up(&s->d_rowind, ri))) return bail(rc);
+  s->P = DevPattern{d_fronts, idx, relpos, rowf, ap, ac, an, ep, es, pm, pr, pc, S.n};
+  const int64_t Fc = s->Fc;
+  if ((rc = s->alloc(&s->F, S.factor_entries * Fc)) || (rc = s->alloc(&s->WV, S.total_rows * Fc)) ||
+      (rc = s->alloc(&s->X, (int64_t)S.n * Fc)) || (rc = s->alloc(&s->Y, (int64_t)S.n * Fc)) ||
+      (rc = s->alloc(&s->XA, (int64_t)S.n * Fc)) || (rc = s->alloc(&s->G, (int64_t)S.n * Fc)) ||
+      (rc = s->alloc(&s->freqs, Fc)) || (rc = s->alloc(&s->loss_terms, Fc)) || (rc = s->alloc(&s->flags, Fc)) ||
+      (rc = s->alloc(&s->tq, Fc)))
+    return bail(rc);
+  for (auto& e : s->ev)
+    if (hipEventCreate(&e) != hipSuccess) return bail(fail(PFR_ERR_HIP, "hipEventCreate failed"));
+  *out = s;
+  return PFR_OK;
+}
+
+void pfr_solver_destroy(pfr_solver* s) {
+  if (!s) return;
+  (void)hipSetDevice(s->device);
+  (void)hipDeviceSynchronize();
+  delete s;
+}
+
+int32_t pfr_solver_max_batch(const pfr_solver* s) { return s ? (int32_t)s->Fc : 0; }
+
+int pfr_set_timing(pfr_solver* s, int32_t enable) {
+  if (!s) return fail(PFR_ERR_ARG, "null solver");
+  s->timing = enable != 0;
+  return PFR_OK;
+}
+
+int pfr_last_timings(const pfr_solver* s, double* ms) {
+  if (!s || !ms) return fail(PFR_ERR_ARG, "null argument");
+  for (int i = 0; i < 5; ++i) ms[i] = s->last_ms[i];
+  return PFR_OK;
+}
+
+int pfr_set_stiffness(pfr_solver* s, int32_t n_stiff, const double* stiff_dev, const double* w) {
+  if (!s || n_stiff <= 0 || n_stiff > 18 || !stiff_dev || !w) return fail(PFR_ERR_ARG, "bad stiffness arguments");
+  s->stiff = stiff_dev;
+  s->n_stiff = n_stiff;
+  std::memset(&s->e, 0, sizeof(s->e));
+  for (int k = 0; k < n_stiff; ++k) s->e.re[k] = w[k];
+  if (!s->partial) {
+    HIP_TRY(hipSetDevice(s->device));
+    int rc = s->alloc(&s->partial, (int64_t)kContractBlocks * 18 * s->Fc);
+    if (rc) return rc;
+  }
+  return PFR_OK;
+}
+
+int pfr_combine(pfr_solver* s, const double* coef, double* K_out, void* stream) {
+  if (!s || !coef || !K_out) return fail(PFR_ERR_ARG, "null argument");
+  if (!s->stiff) return fail(PFR_ERR_STATE, "pfr_set_stiffness not called");
+  HIP_TRY(hipSetDevice(s->device));
+  pfr::CoefPack c{};
+  for (int k = 0; k < s->n_stiff; ++k) {
+    c.re[k] = coef[2 * k];
+    c.im[k] = coef[2 * k + 1];
+  }
+  pfr::launch_combine(s->stiff, s->n_stiff, s->nnz, c, reinterpret_cast<double2*>(K_out), (hipStream_t)stream);
+  HIP_TRY(hipGetLastError());
+  return PFR_OK;
+}
+
+int pfr_set_operator(pfr_solver* s, const double* K_dev, const double* M_dev) {
+  if (!s || !K_dev || !M_dev) return fail(PFR_ERR_ARG, "null argument");
+  s->K = reinterpret_cast<const double2*>(K_dev);
+  s->M = M_dev;
+  return PFR_OK;
+}
+
+int pfr_set_rhs(pfr_solver* s, const double* rhs, double beta_re, double beta_im, double mass_sum) {
+  if (!s || !rhs) return fail(PFR_ERR_ARG, "null argument");
+  HIP_TRY(hipSetDevice(s->device));
+  std::vector<double> rp(s->n);
+  std::vector<int32_t> sup;
+  std::vector<double> val;
+  for (int p = 0; p < s->n; ++p) {
+    rp[p] = rhs[s->perm[p]];
+    if (rp[p] != 0.0) {
+      sup.push_back(p);
+      val.push_back(rp[p]);
+    }
+  }
+  int rc;
+  if (!s->rhsP && (rc = s->alloc(&s->rhsP, s->n))) return rc;
+  HIP_TRY(hipMemcpy(s->rhsP, rp.data(), s->n * 8, hipMemcpyHostToDevice));
+  s->rhs_sup = nullptr;
+  s->rhs_val = nullptr;
+  if (!sup.empty()) {
+    if ((rc = s->up(&s->rhs_sup, sup)) || (rc = s->up(&s->rhs_val, val))) return rc;
+  }
+  s->n_rhs_sup = (int)sup.size();
+  s->beta_re = beta_re;
+  s->beta_im = beta_im;
+  s->mass_sum = mass_sum;
+  s->has_rhs = true;
+  return PFR_OK;
+}
+
+int pfr_set_functional(pfr_solver* s, int32_t n_support, const int32_t* index, const double* a, double ts) {
+  if (!s || n_support <= 0 || !index || !a) return fail(PFR_ERR_ARG, "bad functional arguments");
+  HIP_TRY(hipSetDevice(s->device));
+  std::vector<int32_t> pidx(n_support);
+  for (int i = 0; i < n_support; ++i) {
+    if (index[i] < 0 || index[i] >= s->n) return fail(PFR_ERR_ARG, "functional index out of range");
+    pidx[i] = s->iperm[index[i]];
+  }
+  std::vector<double> av(a, a + 3 * (int64_t)n_support);
+  int32_t* d_idx;
+  double* d_a;
+  int rc;
+  if ((rc = s->up(&d_idx, pidx)) || (rc = s->up(&d_a, av))) return rc;
+  s->fn.n_support = n_support;
+  s->fn.pidx = d_idx;
+  s->fn.a = d_a;
+  s->fn.ts = ts;
+  s->has_fn = true;
+  return PFR_OK;
+}
+
+int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t loss_type, const double* ref_dev,
+              double scale, double* fr_dev, double* loss_dev, double* w_dev, int32_t* flags_dev, void* stream) {
+  if (!s || nfreq <= 0 || !freqs_dev) return fail(PFR_ERR_ARG, "bad sweep arguments");
+  if (!s->K || !s->M) return fail(PFR_ERR_STATE, "operator not set (pfr_set_operator)");
+  if (!s->has_rhs) return fail(PFR_ERR_STATE, "rhs not set (pfr_set_rhs)");
+  if (!s->has_fn) return fail(PFR_ERR_STATE, "functional not set (pfr_set_functional)");
+  const bool reverse = loss_type != PFR_LOSS_NONE;
+  if (reverse && (loss_type < 0 || loss_type > PFR_LOSS_COTANGENT || !ref_dev))
+    return fail(PFR_ERR_ARG, "bad loss type / missing ref");
+  if (reverse && (!s->stiff || !w_dev)) return fail(PFR_ERR_STATE, "reverse pass needs pfr_set_stiffness and w_dev");
+  HIP_TRY(hipSetDevice(s->device));
+  hipStream_t st = (hipStream_t)stream;
+  for (double& m : s->last_ms) m = 0;
+  const int64_t Fc = s->Fc;
+  const int ngroups = (int)(Fc / 64);
+  bool used[5] = {true, true, true, reverse, reverse};
+  for (int64_t q0 = 0; q0 < nfreq; q0 += Fc) {
+    const int nv = (int)std::min<int64_t>(Fc, nfreq - q0);
+    HIP_TRY(hipMemcpyAsync(s->freqs, freqs_dev + q0, nv * sizeof(double), hipMemcpyDeviceToDevice, st));
+    pfr::launch_pad_freqs(s->freqs, nv, Fc, st);
+    HIP_TRY(hipMemsetAsync(s->flags, 0, Fc * sizeof(int32_t), st));
+    record(s, 0, st);
+    int rc = factor_all(s, 0, nullptr, 0, nv, st);
+    if (rc) return rc;
+    record(s, 1, st);
+    pfr::RhsDesc rd;
+    rd.rhsP = s->rhsP;
+    rd.beta_re = s->beta_re;
+    rd.beta_im = s->beta_im;
+    rd.mass_sum = s->mass_sum;
+    rd.freqs = s->freqs;
+    if ((rc = solve_all(s, 0, 0, rd, nullptr, s->Y, st))) return rc;
+    if ((rc = solve_all(s, 1, 0, rd, s->Y, s->X, st))) return rc;
+    record(s, 2, st);
+    pfr::FunctionalArgs fa = s->fn;
+    fa.loss_type = reverse ? loss_type : -1;
+    fa.ref = reinterpret_cast<const double2*>(ref_dev);
+    fa.scale = scale;
+    if (reverse) HIP_TRY(hipMemsetAsync(s->G, 0, (size_t)s->n * Fc * 16, st));
+    pfr::launch_functional(fa, s->X, Fc, nv, q0, fr_dev, s->loss_terms, s->G, st);
+    record(s, 3, st);
+    if (reverse) {
+      pfr::RhsDesc rg;
+      rg.G = s->G;
+      if ((rc = solve_all(s, 2, 2, rg, nullptr, s->Y, st))) return rc;
+      if ((rc = solve_all(s, 3, 0, rg, s->Y, s->XA, st))) return rc;
+      record(s, 4, st);
+      pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->XA, s->X, Fc, s->partial,
+                           st);
+      pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st);
+      pfr::launch_reduce(s->partial, kContractBlocks, s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
+                         reinterpret_cast<double2*>(w_dev), loss_dev, st);
+    } else {
+      record(s, 4, st);
+    }
+    record(s, 5, st);
+    if (flags_dev) pfr::launch_flags_merge(s->flags, nv, flags_dev + q0, st);
+    HIP_TRY(hipGetLastError());
+    if ((rc = finish_timing(s, used))) return rc;
+  }
+  return PFR_OK;
+}
+
+int pfr_solve(pfr_solver* s, int32_t batch, const double* data_dev, int64_t data_stride, const double* b_dev,
+              int64_t b_stride, double* x_dev, int32_t transpose, int32_t* flags_dev, void* stream) {
+  if (!s || batch <= 0 || !data_dev || !b_dev || !x_dev || data_stride < 0 || b_stride < 0)
+    return fail(PFR_ERR_ARG, "bad solve arguments");
+  if (data_stride != 0 && data_stride < s->nnz) return fail(PFR_ERR_ARG, "data_stride < nnz");
+  if (b_stride != 0 && b_stride < s->n) return fail(PFR_ERR_ARG, "b_stride < n");
+  HIP_TRY(hipSetDevice(s->device));
+  hipStream_t st = (hipStream_t)stream;
+  for (double& m : s->last_ms) m = 0;
+  const int64_t Fc = s->Fc;
+  const double2* data = reinterpret_cast<const double2*>(data_dev);
+  const double2* B = reinterpret_cast<const double2*>(b_dev);
+  double2* Xo = reinterpret_cast<double2*>(x_dev);
+  bool used[5] = {true, !transpose, false, (bool)transpose, false};
+  for (int64_t q0 = 0; q0 < batch; q0 += Fc) {
+    const int nv = (int)std::min<int64_t>(Fc, batch - q0);
+    HIP_TRY(hipMemsetAsync(s->flags, 0, Fc * sizeof(int32_t), st));
+    record(s, 0, st);
+    // padded lanes repeat the last valid item (stride 0 broadcast handled by the kernel's clamp)
+    int rc = factor_all(s, 1, data + q0 * data_stride, data_stride, nv, st);
+    if (rc) return rc;
+    record(s, 1, st);
+    pfr::RhsDesc rd;
+    rd.B = B + q0 * b_stride;
+    rd.b_stride = b_stride;
+    rd.nvalid = nv;
+    if (!transpose) {
+      if ((rc = solve_all(s, 0, 1, rd, nullptr, s->Y, st))) return rc;
+      if ((rc = solve_all(s, 1, 1, rd, s->Y, s->X, st))) return rc;
+    }
+    record(s, 2, st);
+    record(s, 3, st);
+    if (transpose) {
+      if ((rc = solve_all(s, 2, 1, rd, nullptr, s->Y, st))) return rc;
+      if ((rc = solve_all(s, 3, 1, rd, s->Y, s->X, st))) return rc;
+    }
+    record(s, 4, st);
+    pfr::launch_unpermute(s->P.perm, s->n, s->X, Fc, nv, Xo + q0 * s->n, st);
+    record(s, 5, st);
+    if (flags_dev) pfr::launch_flags_merge(s->flags, nv, flags_dev + q0, st);
+    HIP_TRY(hipGetLastError());
+    if ((rc = finish_timing(s, used))) return rc;
+  }
+  return PFR_OK;
+}
+
+int pfr_matvec(pfr_solver* s, int32_t batch, const double* data_dev, int64_t data_stride, const double* x_dev,
+               int64_t x_stride, double* y_dev, int32_t transpose, void* stream) {
+  if (!s || batch <= 0 || !data_dev || !x_dev || !y_dev) return fail(PFR_ERR_ARG, "bad matvec arguments");
+  HIP_TRY(hipSetDevice(s->device));
+  hipStream_t st = (hipStream_t)stream;
+  if (!transpose) HIP_TRY(hipMemsetAsync(y_dev, 0, (size_t)batch * s->n * 16, st));
+  pfr::launch_matvec(s->d_colptr, s->d_rowind, s->n, reinterpret_cast<const double2*>(data_dev), data_stride,
+                     reinterpret_cast<const double2*>(x_dev), x_stride, reinterpret_cast<double2*>(y_dev),
+                     transpose, batch, st);
+  HIP_TRY(hipGetLastError());
+  return PFR_OK;
+}
+
+}  // extern "C"

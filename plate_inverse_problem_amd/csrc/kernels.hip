@@ -1,0 +1,704 @@
+// Batched multifrontal LU, forward/adjoint triangular solves, FR functional and
+// adjoint gradient contraction for CDNA4 (gfx950).
+//
+// Layout: FREQUENCY-MINOR.  Every scalar of the factorisation (a front entry, a
+// work-vector entry, a solution entry) is stored as `Fc` consecutive complex
+// doubles, one per frequency of the chunk.  A wavefront = 64 consecutive
+// frequencies of the same entry: every index is wave-uniform (scalar loads),
+// every value load/store is one 1 KiB contiguous wave-instruction, no lane ever
+// diverges (all frequencies share the pattern and the static pivot order).
+// Workgroup = (front, 64 frequencies); its W waves split the rows of the front.
+//
+// Reference hot loop replaced: InnerState::solve mode 3, one UMFPACK numeric
+// factorisation + solve per frequency inside `omp parallel for`
+// (source/jax_plate_lib/include/InnerState.h:276-288), plus the XLA-fused
+// assembly and functional of source/jax_plate/Problem.py:437-477 and the
+// spsolve/matvec transpose rules of source/jax_plate/Sparse.py:162-222.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "launch.hpp"
+
+namespace pfr {
+
+using cplx = double2;
+
+__device__ __forceinline__ cplx cadd(cplx a, cplx b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ cplx cmul(cplx a, cplx b) {
+  return make_double2(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
+}
+// c - a*b
+__device__ __forceinline__ cplx cfms(cplx c, cplx a, cplx b) {
+  return make_double2(fma(-a.x, b.x, fma(a.y, b.y, c.x)), fma(-a.x, b.y, fma(-a.y, b.x, c.y)));
+}
+__device__ __forceinline__ cplx crecip(cplx b) {
+  double d = fma(b.x, b.x, b.y * b.y);
+  double inv = 1.0 / d;
+  return make_double2(b.x * inv, -b.y * inv);
+}
+__device__ __forceinline__ void pivot_check(cplx p, int* flags, int64_t q) {
+  double m = fabs(p.x) + fabs(p.y);
+  if (!(m > 0.0) || !isfinite(m)) atomicOr(flags + q, PFR_FLAG_BAD_PIVOT);
+}
+
+constexpr int KB = 4;    // factorisation pivot block
+constexpr int KBS = 16;  // triangular-solve block
+
+// ------------------------------------------------------------------ helpers
+struct Ctx {
+  int lane, w, W;
+  int64_t q;
+};
+__device__ __forceinline__ Ctx ctx() {
+  Ctx c;
+  c.lane = threadIdx.x & 63;
+  c.w = threadIdx.x >> 6;
+  c.W = blockDim.x >> 6;
+  c.q = (int64_t)blockIdx.y * 64 + c.lane;
+  return c;
+}
+
+// ------------------------------------------------------------------ K1: combine
+// K[nz] = sum_k coef_k * stiff[nz * n_stiff + k]   (Problem.py:440-445, theta part)
+__global__ void k_combine(const double* __restrict__ stiff, int n_stiff, int64_t nnz, CoefPack coef,
+                          cplx* __restrict__ K) {
+  int64_t nz = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (nz >= nnz) return;
+  const double* s = stiff + nz * n_stiff;
+  double re = 0, im = 0;
+  for (int k = 0; k < n_stiff; ++k) {
+    re = fma(coef.re[k], s[k], re);
+    im = fma(coef.im[k], s[k], im);
+  }
+  K[nz] = make_double2(re, im);
+}
+
+// ------------------------------------------------------------------ K2: factor
+// MODE 0: A_q = K - omega_q^2 M assembled on the fly (operator form).
+// MODE 1: A_q = data[q * data_stride + nz] (explicit batch, InnerState::solve data).
+template <int MODE>
+__global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* __restrict__ lvl, cplx* __restrict__ F, int64_t Fc,
+                               const double* __restrict__ freqs, const cplx* __restrict__ K,
+                               const double* __restrict__ M, const cplx* __restrict__ data,
+                               int64_t data_stride, int nvalid, int* __restrict__ flags) {
+  const Ctx c = ctx();
+  const Front fr = P.fronts[lvl[blockIdx.x]];
+  const int f = fr.f, ns = fr.ns;
+  cplx* __restrict__ base = F + fr.off * Fc + c.q;
+#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+
+  double om2 = 0.0;
+  if (MODE == 0) {
+    double om = 6.283185307179586 * freqs[c.q];
+    om2 = om * om;
+  }
+  // 1. assemble: zero, original entries, children's update matrices
+  for (int a = c.w; a < f; a += c.W) {
+    for (int b = 0; b < f; ++b) E(a, b) = make_double2(0.0, 0.0);
+    const int r = fr.row0 + a;
+    const int e1 = P.asm_ptr[r + 1];
+    for (int e = P.asm_ptr[r]; e < e1; ++e) {
+      const int b = P.asm_col[e];
+      const int nz = P.asm_nz[e];
+      cplx v;
+      if (MODE == 0) {
+        const cplx k = K[nz];
+        v = make_double2(fma(-om2, M[nz], k.x), k.y);
+      } else {
+        v = data[min(c.q, (int64_t)nvalid - 1) * data_stride + nz];
+      }
+      E(a, b) = cadd(E(a, b), v);
+    }
+    const int x1 = P.ea_ptr[r + 1];
+    for (int e = P.ea_ptr[r]; e < x1; ++e) {
+      const int src = P.ea_src[e];
+      const Front cf = P.fronts[P.row_front[src]];
+      const cplx* __restrict__ cb = F + (cf.off + (int64_t)(src - cf.row0) * cf.f) * Fc + c.q;
+      const int* __restrict__ rp = P.relpos + cf.row0;
+      for (int b = cf.ns; b < cf.f; ++b) {
+        const int pb = rp[b];
+        E(a, pb) = cadd(E(a, pb), cb[(int64_t)b * Fc]);
+      }
+    }
+  }
+  __syncthreads();
+
+  // 2. blocked right-looking partial LU of the first ns pivots (static pivots)
+  for (int k0 = 0; k0 < ns; k0 += KB) {
+    const int kb = min(KB, ns - k0);
+    const int k1 = k0 + kb;
+    if (c.w == 0) {
+      for (int k = k0; k < k1; ++k) {
+        const cplx piv = E(k, k);
+        pivot_check(piv, flags, c.q);
+        const cplx inv = crecip(piv);
+        for (int i = k + 1; i < k1; ++i) {
+          const cplx l = cmul(E(i, k), inv);
+          E(i, k) = l;
+          for (int j = k + 1; j < k1; ++j) E(i, j) = cfms(E(i, j), l, E(k, j));
+        }
+      }
+    }
+    __syncthreads();
+    // U12 = L11^{-1} A12 : columns distributed over waves
+    {
+      cplx L[KB][KB];
+#pragma unroll
+      for (int i = 0; i < KB; ++i)
+#pragma unroll
+        for (int j = 0; j < KB; ++j)
+          if (j < i && i < kb) L[i][j] = E(k0 + i, k0 + j);
+      for (int j = k1 + c.w; j < f; j += c.W) {
+        cplx x[KB];
+#pragma unroll
+        for (int i = 0; i < KB; ++i)
+          if (i < kb) x[i] = E(k0 + i, j);
+#pragma unroll
+        for (int i = 1; i < KB; ++i)
+          if (i < kb) {
+#pragma unroll
+            for (int t = 0; t < KB; ++t)
+              if (t < i) x[i] = cfms(x[i], L[i][t], x[t]);
+          }
+#pragma unroll
+        for (int i = 1; i < KB; ++i)
+          if (i < kb) E(k0 + i, j) = x[i];
+      }
+    }
+    __syncthreads();
+    // L21 = A21 U11^{-1}, then trailing update A22 -= L21 U12 : rows over waves
+    {
+      cplx U[KB][KB];
+      cplx Dinv[KB];
+#pragma unroll
+      for (int i = 0; i < KB; ++i)
+#pragma unroll
+        for (int j = 0; j < KB; ++j)
+          if (i < j && j < kb) U[i][j] = E(k0 + i, k0 + j);
+#pragma unroll
+      for (int i = 0; i < KB; ++i)
+        if (i < kb) Dinv[i] = crecip(E(k0 + i, k0 + i));
+      for (int i = k1 + c.w; i < f; i += c.W) {
+        cplx l[KB];
+#pragma unroll
+        for (int t = 0; t < KB; ++t)
+          if (t < kb) l[t] = E(i, k0 + t);
+#pragma unroll
+        for (int t = 0; t < KB; ++t)
+          if (t < kb) {
+#pragma unroll
+            for (int s = 0; s < KB; ++s)
+              if (s < t) l[t] = cfms(l[t], l[s], U[s][t]);
+            l[t] = cmul(l[t], Dinv[t]);
+            E(i, k0 + t) = l[t];
+          }
+        for (int j = k1; j < f; ++j) {
+          cplx v = E(i, j);
+#pragma unroll
+          for (int t = 0; t < KB; ++t)
+            if (t < kb) v = cfms(v, l[t], E(k0 + t, j));
+          E(i, j) = v;
+        }
+      }
+    }
+    __syncthreads();
+  }
+#undef E
+}
+
+// ------------------------------------------------------------------ right-hand sides
+// RHS 0: b_p = rhsP[p] * (beta0 - omega^2 * mass_sum)   (Problem.py:447-449)
+// RHS 1: b_p = B[q * b_stride + perm[p]]                 (explicit batch)
+// RHS 2: b_p = G[p * Fc + q]                             (permuted device vector)
+struct RhsArgs {
+  const double* rhsP;     // RHS 0: permuted Dirichlet vector
+  double beta_re, beta_im, mass_sum;
+  const double* freqs;
+  const cplx* B;          // RHS 1
+  int64_t b_stride;
+  const cplx* G;          // RHS 2
+  int nvalid;             // RHS 1: padded lanes repeat the last valid item
+};
+
+template <int RHS>
+__device__ __forceinline__ cplx rhs_value(const DevPattern& P, const RhsArgs& R, int p, int64_t q, int64_t Fc) {
+  if (RHS == 0) {
+    const double v = R.rhsP[p];
+    if (v == 0.0) return make_double2(0.0, 0.0);
+    const double om = 6.283185307179586 * R.freqs[q];
+    return make_double2(v * fma(-om * om, R.mass_sum, R.beta_re), v * R.beta_im);
+  } else if (RHS == 1) {
+    return R.B[min(q, (int64_t)R.nvalid - 1) * R.b_stride + P.perm[p]];
+  } else {
+    return R.G[(int64_t)p * Fc + q];
+  }
+}
+
+// Gather the frontal vector: pivot rows from the rhs, plus children's update vectors.
+template <int RHS>
+__device__ __forceinline__ void gather_frontal(const DevPattern& P, const Front& fr, const RhsArgs& R,
+                                               cplx* __restrict__ WV, int64_t Fc, const Ctx& c) {
+  for (int a = c.w; a < fr.f; a += c.W) {
+    const int r = fr.row0 + a;
+    cplx v = make_double2(0.0, 0.0);
+    if (a < fr.ns) v = rhs_value<RHS>(P, R, P.idx[r], c.q, Fc);
+    const int x1 = P.ea_ptr[r + 1];
+    for (int e = P.ea_ptr[r]; e < x1; ++e) v = cadd(v, WV[(int64_t)P.ea_src[e] * Fc + c.q]);
+    WV[(int64_t)r * Fc + c.q] = v;
+  }
+}
+
+// ------------------------------------------------------------------ K3a: L y = b (bottom-up)
+template <int RHS>
+__global__ void k_lsolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
+                               cplx* __restrict__ WV, RhsArgs R, cplx* __restrict__ Y) {
+  const Ctx c = ctx();
+  const Front fr = P.fronts[lvl[blockIdx.x]];
+  const int f = fr.f, ns = fr.ns;
+  const cplx* __restrict__ base = F + fr.off * Fc + c.q;
+  cplx* __restrict__ wv = WV + (int64_t)fr.row0 * Fc + c.q;
+#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+#define V(a) wv[(int64_t)(a) * Fc]
+  gather_frontal<RHS>(P, fr, R, WV, Fc, c);
+  __syncthreads();
+  for (int k0 = 0; k0 < ns; k0 += KBS) {
+    const int kb = min(KBS, ns - k0), k1 = k0 + kb;
+    if (c.w == 0)
+      for (int k = k0; k < k1; ++k) {
+        const cplx z = V(k);
+        for (int i = k + 1; i < k1; ++i) V(i) = cfms(V(i), E(i, k), z);
+      }
+    __syncthreads();
+    cplx z[KBS];
+#pragma unroll
+    for (int t = 0; t < KBS; ++t)
+      if (t < kb) z[t] = V(k0 + t);
+    for (int i = k1 + c.w; i < f; i += c.W) {
+      cplx v = V(i);
+#pragma unroll
+      for (int t = 0; t < KBS; ++t)
+        if (t < kb) v = cfms(v, E(i, k0 + t), z[t]);
+      V(i) = v;
+    }
+    __syncthreads();
+  }
+  for (int a = c.w; a < ns; a += c.W) Y[(int64_t)(fr.col0 + a) * Fc + c.q] = V(a);
+#undef E
+#undef V
+}
+
+// ------------------------------------------------------------------ K3b: U x = y (top-down)
+__global__ void k_usolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
+                               cplx* __restrict__ WV, const cplx* __restrict__ Y, cplx* __restrict__ X) {
+  const Ctx c = ctx();
+  const Front fr = P.fronts[lvl[blockIdx.x]];
+  const int f = fr.f, ns = fr.ns;
+  const cplx* __restrict__ base = F + fr.off * Fc + c.q;
+  cplx* __restrict__ wv = WV + (int64_t)fr.row0 * Fc + c.q;
+  const int* __restrict__ ix = P.idx + fr.row0;
+#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+#define V(a) wv[(int64_t)(a) * Fc]
+  for (int a = c.w; a < ns; a += c.W) {
+    cplx v = Y[(int64_t)(fr.col0 + a) * Fc + c.q];
+    for (int b = ns; b < f; ++b) v = cfms(v, E(a, b), X[(int64_t)ix[b] * Fc + c.q]);
+    V(a) = v;
+  }
+  __syncthreads();
+  for (int k1 = ns; k1 > 0; k1 -= KBS) {
+    const int k0 = max(0, k1 - KBS), kb = k1 - k0;
+    if (c.w == 0)
+      for (int k = k1 - 1; k >= k0; --k) {
+        const cplx x = cmul(V(k), crecip(E(k, k)));
+        V(k) = x;
+        X[(int64_t)(fr.col0 + k) * Fc + c.q] = x;
+        for (int i = k0; i < k; ++i) V(i) = cfms(V(i), E(i, k), x);
+      }
+    __syncthreads();
+    cplx x[KBS];
+#pragma unroll
+    for (int t = 0; t < KBS; ++t)
+      if (t < kb) x[t] = V(k0 + t);
+    for (int i = c.w; i < k0; i += c.W) {
+      cplx v = V(i);
+#pragma unroll
+      for (int t = 0; t < KBS; ++t)
+        if (t < kb) v = cfms(v, E(i, k0 + t), x[t]);
+      V(i) = v;
+    }
+    __syncthreads();
+  }
+#undef E
+#undef V
+}
+
+// ------------------------------------------------------------------ K3c: U^T y = g (bottom-up)
+template <int RHS>
+__global__ void k_utsolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
+                                cplx* __restrict__ WV, RhsArgs R, cplx* __restrict__ Y) {
+  const Ctx c = ctx();
+  const Front fr = P.fronts[lvl[blockIdx.x]];
+  const int f = fr.f, ns = fr.ns;
+  const cplx* __restrict__ base = F + fr.off * Fc + c.q;
+  cplx* __restrict__ wv = WV + (int64_t)fr.row0 * Fc + c.q;
+#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+#define V(a) wv[(int64_t)(a) * Fc]
+  gather_frontal<RHS>(P, fr, R, WV, Fc, c);
+  __syncthreads();
+  for (int k0 = 0; k0 < ns; k0 += KBS) {
+    const int kb = min(KBS, ns - k0), k1 = k0 + kb;
+    if (c.w == 0)
+      for (int k = k0; k < k1; ++k) {
+        const cplx y = cmul(V(k), crecip(E(k, k)));
+        V(k) = y;
+        for (int i = k + 1; i < k1; ++i) V(i) = cfms(V(i), E(k, i), y);
+      }
+    __syncthreads();
+    cplx y[KBS];
+#pragma unroll
+    for (int t = 0; t < KBS; ++t)
+      if (t < kb) y[t] = V(k0 + t);
+    for (int i = k1 + c.w; i < f; i += c.W) {
+      cplx v = V(i);
+#pragma unroll
+      for (int t = 0; t < KBS; ++t)
+        if (t < kb) v = cfms(v, E(k0 + t, i), y[t]);
+      V(i) = v;
+    }
+    __syncthreads();
+  }
+  for (int a = c.w; a < ns; a += c.W) Y[(int64_t)(fr.col0 + a) * Fc + c.q] = V(a);
+#undef E
+#undef V
+}
+
+// ------------------------------------------------------------------ K3d: L^T x = y (top-down)
+__global__ void k_ltsolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
+                                cplx* __restrict__ WV, const cplx* __restrict__ Y, cplx* __restrict__ X) {
+  const Ctx c = ctx();
+  const Front fr = P.fronts[lvl[blockIdx.x]];
+  const int f = fr.f, ns = fr.ns;
+  const cplx* __restrict__ base = F + fr.off * Fc + c.q;
+  cplx* __restrict__ wv = WV + (int64_t)fr.row0 * Fc + c.q;
+  const int* __restrict__ ix = P.idx + fr.row0;
+#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+#define V(a) wv[(int64_t)(a) * Fc]
+  for (int a = c.w; a < ns; a += c.W) {
+    cplx v = Y[(int64_t)(fr.col0 + a) * Fc + c.q];
+    for (int b = ns; b < f; ++b) v = cfms(v, E(b, a), X[(int64_t)ix[b] * Fc + c.q]);
+    V(a) = v;
+  }
+  __syncthreads();
+  for (int k1 = ns; k1 > 0; k1 -= KBS) {
+    const int k0 = max(0, k1 - KBS), kb = k1 - k0;
+    if (c.w == 0)
+      for (int k = k1 - 1; k >= k0; --k) {
+        const cplx x = V(k);
+        X[(int64_t)(fr.col0 + k) * Fc + c.q] = x;
+        for (int i = k0; i < k; ++i) V(i) = cfms(V(i), E(k, i), x);
+      }
+    __syncthreads();
+    cplx x[KBS];
+#pragma unroll
+    for (int t = 0; t < KBS; ++t)
+      if (t < kb) x[t] = V(k0 + t);
+    for (int i = c.w; i < k0; i += c.W) {
+      cplx v = V(i);
+#pragma unroll
+      for (int t = 0; t < KBS; ++t)
+        if (t < kb) v = cfms(v, E(k0 + t, i), x[t]);
+      V(i) = v;
+    }
+    __syncthreads();
+  }
+#undef E
+#undef V
+}
+
+// ------------------------------------------------------------------ K4: functional + loss cotangent
+// U = aU.x, V = aV.x, W = aW.x; fr = sqrt(ts^2|U|^2 + ts^2|V|^2 + |W|^2)  (Problem.py:454-477)
+// loss terms of Problem.py:948-975; g = dl/fr * (ts^2 conj(U) aU + ts^2 conj(V) aV + conj(W) aW)
+__global__ void k_functional(FunctionalArgs A, const cplx* __restrict__ X, int64_t Fc, int nvalid, int64_t q_global0,
+                             double* __restrict__ fr_out, double* __restrict__ loss_terms, cplx* __restrict__ G) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Fc) return;
+  cplx U = make_double2(0, 0), Vv = make_double2(0, 0), W = make_double2(0, 0);
+  for (int s = 0; s < A.n_support; ++s) {
+    const cplx x = X[(int64_t)A.pidx[s] * Fc + q];
+    const double au = A.a[s], av = A.a[A.n_support + s], aw = A.a[2 * A.n_support + s];
+    U.x = fma(au, x.x, U.x); U.y = fma(au, x.y, U.y);
+    Vv.x = fma(av, x.x, Vv.x); Vv.y = fma(av, x.y, Vv.y);
+    W.x = fma(aw, x.x, W.x); W.y = fma(aw, x.y, W.y);
+  }
+  const double ts2 = A.ts * A.ts;
+  const double u2 = U.x * U.x + U.y * U.y, v2 = Vv.x * Vv.x + Vv.y * Vv.y, w2 = W.x * W.x + W.y * W.y;
+  const double fr = sqrt(ts2 * u2 + ts2 * v2 + w2);
+  const bool valid = q < nvalid;
+  if (valid && fr_out) fr_out[q_global0 + q] = fr;
+  if (A.loss_type < 0) return;
+  double term = 0.0, dl = 0.0;
+  if (valid) {
+    const cplx r = A.ref[q_global0 + q];
+    const double rabs = sqrt(r.x * r.x + r.y * r.y);
+    switch (A.loss_type) {
+      case PFR_LOSS_MSE: {
+        const double dre = fr - r.x;
+        term = dre * dre + r.y * r.y;
+        dl = 2.0 * dre;
+      } break;
+      case PFR_LOSS_RMSE: {
+        const double dre = fr - r.x, r2 = rabs * rabs;
+        term = (dre * dre + r.y * r.y) / r2;
+        dl = 2.0 * dre / r2;
+      } break;
+      case PFR_LOSS_MSE_AFC: {
+        const double d = fr - rabs;
+        term = d * d;
+        dl = 2.0 * d;
+      } break;
+      case PFR_LOSS_MSE_LOG_AFC: {
+        const double d = log(fr) - log(rabs);
+        term = d * d;
+        dl = 2.0 * d / fr;
+      } break;
+      case PFR_LOSS_COTANGENT:
+        dl = r.x;   // dL/dfr supplied by the caller (ref.re), no loss value
+        break;
+      default:
+        break;
+    }
+  }
+  loss_terms[q] = term;
+  const double s = valid && fr > 0.0 ? dl * A.scale / fr : 0.0;
+  const cplx cU = make_double2(s * ts2 * U.x, -s * ts2 * U.y);
+  const cplx cV = make_double2(s * ts2 * Vv.x, -s * ts2 * Vv.y);
+  const cplx cW = make_double2(s * W.x, -s * W.y);
+  for (int t = 0; t < A.n_support; ++t) {
+    const double au = A.a[t], av = A.a[A.n_support + t], aw = A.a[2 * A.n_support + t];
+    cplx g;
+    g.x = au * cU.x + av * cV.x + aw * cW.x;
+    g.y = au * cU.y + av * cV.y + aw * cW.y;
+    G[(int64_t)A.pidx[t] * Fc + q] = g;
+  }
+}
+
+// ------------------------------------------------------------------ K5: gradient contraction
+// s_{q,k} = sum_nz stiff[nz][k] * Lam[prow] * X[pcol]   (Sparse.py:173-176 matrix cotangent,
+// contracted with the stiffness matrices as JAX's einsum transpose does)
+constexpr int NSTIFF_MAX = 18;
+__global__ void k_contract(DevPattern P, const double* __restrict__ stiff, int n_stiff, int64_t nnz, int64_t nz_per_blk,
+                           const cplx* __restrict__ Lam, const cplx* __restrict__ X, int64_t Fc,
+                           cplx* __restrict__ partial) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.y * 64 + lane;
+  const int64_t nz0 = (int64_t)blockIdx.x * nz_per_blk;
+  const int64_t nz1 = min(nnz, nz0 + nz_per_blk);
+  cplx acc[NSTIFF_MAX];
+#pragma unroll
+  for (int k = 0; k < NSTIFF_MAX; ++k) acc[k] = make_double2(0, 0);
+  for (int64_t nz = nz0; nz < nz1; ++nz) {
+    const cplx l = Lam[(int64_t)P.prow[nz] * Fc + q];
+    const cplx x = X[(int64_t)P.pcol[nz] * Fc + q];
+    const cplx p = cmul(l, x);
+    const double* s = stiff + nz * n_stiff;
+#pragma unroll
+    for (int k = 0; k < NSTIFF_MAX; ++k)
+      if (k < n_stiff) {
+        acc[k].x = fma(s[k], p.x, acc[k].x);
+        acc[k].y = fma(s[k], p.y, acc[k].y);
+      }
+  }
+#pragma unroll
+  for (int k = 0; k < NSTIFF_MAX; ++k)
+    if (k < n_stiff) partial[((int64_t)blockIdx.x * n_stiff + k) * Fc + q] = acc[k];
+}
+
+// t_q = sum_p Lam[p] * rhsP[p] over the Dirichlet support (d b / d beta)
+__global__ void k_rhs_dot(const int* __restrict__ sup, const double* __restrict__ val, int n_sup,
+                          const cplx* __restrict__ Lam, int64_t Fc, cplx* __restrict__ t_out) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Fc) return;
+  cplx t = make_double2(0, 0);
+  for (int s = 0; s < n_sup; ++s) {
+    const cplx l = Lam[(int64_t)sup[s] * Fc + q];
+    t.x = fma(val[s], l.x, t.x);
+    t.y = fma(val[s], l.y, t.y);
+  }
+  t_out[q] = t;
+}
+
+// Deterministic reduction over (blocks, valid frequencies):
+//   w[k] += sum_q ( -sum_blk partial[blk][k][q] + e_k * t_q ),  loss += sum_q loss_terms[q]
+__global__ void k_reduce(const cplx* __restrict__ partial, int nblk, int n_stiff, const cplx* __restrict__ t_q,
+                         CoefPack e, const double* __restrict__ loss_terms, int nvalid, int64_t Fc,
+                         cplx* __restrict__ w_out, double* __restrict__ loss_out) {
+  __shared__ double sre[256], sim[256];
+  const int k = blockIdx.x;   // 0..n_stiff-1: stiffness; n_stiff: loss
+  double re = 0, im = 0;
+  for (int q = threadIdx.x; q < nvalid; q += blockDim.x) {
+    if (k < n_stiff) {
+      double pr = 0, pi = 0;
+      for (int b = 0; b < nblk; ++b) {
+        const cplx v = partial[((int64_t)b * n_stiff + k) * Fc + q];
+        pr += v.x;
+        pi += v.y;
+      }
+      const cplx t = t_q[q];
+      re += -pr + e.re[k] * t.x;
+      im += -pi + e.re[k] * t.y;
+    } else {
+      re += loss_terms[q];
+    }
+  }
+  sre[threadIdx.x] = re;
+  sim[threadIdx.x] = im;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      sre[threadIdx.x] += sre[threadIdx.x + s];
+      sim[threadIdx.x] += sim[threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (k < n_stiff) {
+      w_out[k].x += sre[0];
+      w_out[k].y += sim[0];
+    } else if (loss_out) {
+      loss_out[0] += sre[0];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ misc
+// x_out[q * n + perm[p]] = X[p * Fc + q]  (back to the caller's numbering, batch-major)
+__global__ void k_unpermute(const int* __restrict__ perm, int n, const cplx* __restrict__ X, int64_t Fc, int nvalid,
+                            cplx* __restrict__ out) {
+  const int p = blockIdx.x;
+  const int q = blockIdx.y * blockDim.x + threadIdx.x;
+  if (q >= nvalid || p >= n) return;
+  out[(int64_t)q * n + perm[p]] = X[(int64_t)p * Fc + q];
+}
+
+// y = A x (or A^T x) for a batch of matrices on the CSC pattern (InnerState::matvec,
+// InnerState.h:310-470; csc_matvec.h:31-66).  One thread per (column, batch item).
+__global__ void k_matvec(const int* __restrict__ colptr, const int* __restrict__ rowind, int n,
+                         const cplx* __restrict__ data, int64_t data_stride, const cplx* __restrict__ x,
+                         int64_t x_stride, cplx* __restrict__ y, int transpose, int batch) {
+  const int q = blockIdx.y;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n || q >= batch) return;
+  const cplx* d = data + q * data_stride;
+  const cplx* xv = x + q * x_stride;
+  cplx* yv = y + (int64_t)q * n;
+  if (transpose) {
+    cplx acc = make_double2(0, 0);
+    for (int e = colptr[j]; e < colptr[j + 1]; ++e) acc = cadd(acc, cmul(d[e], xv[rowind[e]]));
+    yv[j] = acc;
+  } else {
+    const cplx xj = xv[j];
+    for (int e = colptr[j]; e < colptr[j + 1]; ++e) {
+      const cplx v = cmul(d[e], xj);
+      atomicAdd(&yv[rowind[e]].x, v.x);
+      atomicAdd(&yv[rowind[e]].y, v.y);
+    }
+  }
+}
+
+// ================================================================== launchers
+#define LAUNCH(kern, grid, block, st, ...) hipLaunchKernelGGL(kern, grid, block, 0, st, __VA_ARGS__)
+
+void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPack& coef, double2* K, hipStream_t st) {
+  LAUNCH(k_combine, dim3((unsigned)((nnz + 255) / 256)), dim3(256), st, stiff, n_stiff, nnz, coef, K);
+}
+
+void launch_factor(int mode, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F,
+                   int64_t Fc, const double* freqs, const double2* K, const double* M, const double2* data,
+                   int64_t ds, int nvalid, int* flags, hipStream_t st) {
+  dim3 g(nfronts, ngroups), b(64 * W);
+  if (mode == 0) LAUNCH(k_factor_level<0>, g, b, st, P, lvl, F, Fc, freqs, K, M, data, ds, nvalid, flags);
+  else LAUNCH(k_factor_level<1>, g, b, st, P, lvl, F, Fc, freqs, K, M, data, ds, nvalid, flags);
+}
+
+static RhsArgs make_rhs(const RhsDesc& d) {
+  RhsArgs r;
+  r.rhsP = d.rhsP; r.beta_re = d.beta_re; r.beta_im = d.beta_im; r.mass_sum = d.mass_sum;
+  r.freqs = d.freqs; r.B = d.B; r.b_stride = d.b_stride; r.G = d.G; r.nvalid = d.nvalid;
+  return r;
+}
+
+void launch_solve(int which, int rhs_mode, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups,
+                  const double2* F, int64_t Fc, double2* WV, const RhsDesc& rd, const double2* Yin, double2* Out,
+                  hipStream_t st) {
+  dim3 g(nfronts, ngroups), b(64 * W);
+  RhsArgs R = make_rhs(rd);
+  switch (which) {
+    case 0:  // L solve
+      if (rhs_mode == 0) LAUNCH(k_lsolve_level<0>, g, b, st, P, lvl, F, Fc, WV, R, Out);
+      else if (rhs_mode == 1) LAUNCH(k_lsolve_level<1>, g, b, st, P, lvl, F, Fc, WV, R, Out);
+      else LAUNCH(k_lsolve_level<2>, g, b, st, P, lvl, F, Fc, WV, R, Out);
+      break;
+    case 1:  // U solve
+      LAUNCH(k_usolve_level, g, b, st, P, lvl, F, Fc, WV, Yin, Out);
+      break;
+    case 2:  // U^T solve
+      if (rhs_mode == 0) LAUNCH(k_utsolve_level<0>, g, b, st, P, lvl, F, Fc, WV, R, Out);
+      else if (rhs_mode == 1) LAUNCH(k_utsolve_level<1>, g, b, st, P, lvl, F, Fc, WV, R, Out);
+      else LAUNCH(k_utsolve_level<2>, g, b, st, P, lvl, F, Fc, WV, R, Out);
+      break;
+    default:  // L^T solve
+      LAUNCH(k_ltsolve_level, g, b, st, P, lvl, F, Fc, WV, Yin, Out);
+      break;
+  }
+}
+
+void launch_functional(const FunctionalArgs& A, const double2* X, int64_t Fc, int nvalid, int64_t q0, double* fr_out,
+                       double* loss_terms, double2* G, hipStream_t st) {
+  LAUNCH(k_functional, dim3((unsigned)((Fc + 63) / 64)), dim3(64), st, A, X, Fc, nvalid, q0, fr_out, loss_terms, G);
+}
+
+void launch_contract(const DevPattern& P, const double* stiff, int n_stiff, int64_t nnz, int nblk, int ngroups,
+                     const double2* Lam, const double2* X, int64_t Fc, double2* partial, hipStream_t st) {
+  int64_t per = (nnz + nblk - 1) / nblk;
+  LAUNCH(k_contract, dim3(nblk, ngroups), dim3(64), st, P, stiff, n_stiff, nnz, per, Lam, X, Fc, partial);
+}
+
+void launch_rhs_dot(const int* sup, const double* val, int n_sup, const double2* Lam, int64_t Fc, double2* t_out,
+                    hipStream_t st) {
+  LAUNCH(k_rhs_dot, dim3((unsigned)((Fc + 63) / 64)), dim3(64), st, sup, val, n_sup, Lam, Fc, t_out);
+}
+
+void launch_reduce(const double2* partial, int nblk, int n_stiff, const double2* t_q, const CoefPack& e,
+                   const double* loss_terms, int nvalid, int64_t Fc, double2* w_out, double* loss_out,
+                   hipStream_t st) {
+  LAUNCH(k_reduce, dim3(n_stiff + 1), dim3(256), st, partial, nblk, n_stiff, t_q, e, loss_terms, nvalid, Fc, w_out,
+         loss_out);
+}
+
+void launch_unpermute(const int* perm, int n, const double2* X, int64_t Fc, int nvalid, double2* out, hipStream_t st) {
+  LAUNCH(k_unpermute, dim3(n, (nvalid + 63) / 64), dim3(64), st, perm, n, X, Fc, nvalid, out);
+}
+
+void launch_matvec(const int* colptr, const int* rowind, int n, const double2* data, int64_t ds, const double2* x,
+                   int64_t xs, double2* y, int transpose, int batch, hipStream_t st) {
+  LAUNCH(k_matvec, dim3((n + 255) / 256, batch), dim3(256), st, colptr, rowind, n, data, ds, x, xs, y, transpose,
+         batch);
+}
+
+// fill padded frequency slots with the last valid frequency (keeps padded lanes well-posed)
+__global__ void k_pad_freqs(double* freqs, int nvalid, int64_t Fc) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nvalid && q < Fc) freqs[q] = freqs[nvalid - 1];
+}
+void launch_pad_freqs(double* freqs, int nvalid, int64_t Fc, hipStream_t st) {
+  LAUNCH(k_pad_freqs, dim3((unsigned)((Fc + 63) / 64)), dim3(64), st, freqs, nvalid, Fc);
+}
+__global__ void k_flags_merge(const int* chunk, int nvalid, int* out) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < nvalid) out[q] |= chunk[q];
+}
+void launch_flags_merge(const int* chunk, int nvalid, int* out, hipStream_t st) {
+  LAUNCH(k_flags_merge, dim3((nvalid + 63) / 64), dim3(64), st, chunk, nvalid, out);
+}
+
+}  // namespace pfr

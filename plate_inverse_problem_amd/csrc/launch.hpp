@@ -1,0 +1,39 @@
+// Host launchers of the HIP kernels (defined in kernels.hip).
+#pragma once
+
+#include "device_types.hpp"
+
+namespace pfr {
+
+struct RhsDesc {
+  const double* rhsP = nullptr;   // RHS 0: permuted Dirichlet vector (device)
+  double beta_re = 0, beta_im = 0, mass_sum = 0;
+  const double* freqs = nullptr;  // chunk frequencies (device, padded)
+  const double2* B = nullptr;     // RHS 1: explicit batch (device, batch-major, caller numbering)
+  int64_t b_stride = 0;
+  const double2* G = nullptr;     // RHS 2: permuted frequency-minor vector (device)
+  int nvalid = 1;                 // RHS 1: valid batch items of the chunk
+};
+
+void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPack& coef, double2* K, hipStream_t st);
+void launch_factor(int mode, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F,
+                   int64_t Fc, const double* freqs, const double2* K, const double* M, const double2* data,
+                   int64_t ds, int nvalid, int* flags, hipStream_t st);
+// which: 0 = L (bottom-up), 1 = U (top-down), 2 = U^T (bottom-up), 3 = L^T (top-down)
+void launch_solve(int which, int rhs_mode, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups,
+                  const double2* F, int64_t Fc, double2* WV, const RhsDesc& rd, const double2* Yin, double2* Out,
+                  hipStream_t st);
+void launch_functional(const FunctionalArgs& A, const double2* X, int64_t Fc, int nvalid, int64_t q0, double* fr_out,
+                       double* loss_terms, double2* G, hipStream_t st);
+void launch_contract(const DevPattern& P, const double* stiff, int n_stiff, int64_t nnz, int nblk, int ngroups,
+                     const double2* Lam, const double2* X, int64_t Fc, double2* partial, hipStream_t st);
+void launch_rhs_dot(const int* sup, const double* val, int n_sup, const double2* Lam, int64_t Fc, double2* t_out,
+                    hipStream_t st);
+void launch_reduce(const double2* partial, int nblk, int n_stiff, const double2* t_q, const CoefPack& e,
+                   const double* loss_terms, int nvalid, int64_t Fc, double2* w_out, double* loss_out,
+                   hipStream_t st);
+void launch_unpermute(const int* perm, int n, const double2* X, int64_t Fc, int nvalid, double2* out, hipStream_t st);
+void launch_matvec(const int* colptr, const int* rowind, int n, const double2* data, int64_t ds, const double2* x,
+                   int64_t xs, double2* y, int transpose, int batch, hipStream_t st);
+
+}  // namespace pfr

@@ -1,0 +1,566 @@
+// Host-side symbolic analysis: nested dissection + supernodal multifrontal maps.
+// See symbolic.hpp.  Reference counterpart: umfpack_zi_symbolic called from
+// InnerState::add_mat (source/jax_plate_lib/include/InnerState.h:159-161).
+#include "symbolic.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+#include <stdexcept>
+
+namespace pfr {
+namespace {
+
+struct Graph {
+  int n = 0;
+  std::vector<int> ptr, adj;   // symmetric, no self loops, sorted rows
+  int deg(int v) const { return ptr[v + 1] - ptr[v]; }
+};
+
+Graph symmetric_graph(int n, const int32_t* colptr, const int32_t* rowind) {
+  std::vector<int> cnt(n + 1, 0);
+  for (int j = 0; j < n; ++j)
+    for (int k = colptr[j]; k < colptr[j + 1]; ++k) {
+      int i = rowind[k];
+      if (i == j) continue;
+      cnt[i + 1]++;
+      cnt[j + 1]++;
+    }
+  for (int i = 0; i < n; ++i) cnt[i + 1] += cnt[i];
+  std::vector<int> tmp(cnt[n]);
+  std::vector<int> pos(cnt.begin(), cnt.end() - 1);
+  for (int j = 0; j < n; ++j)
+    for (int k = colptr[j]; k < colptr[j + 1]; ++k) {
+      int i = rowind[k];
+      if (i == j) continue;
+      tmp[pos[i]++] = j;
+      tmp[pos[j]++] = i;
+    }
+  Graph g;
+  g.n = n;
+  g.ptr.assign(n + 1, 0);
+  g.adj.reserve(tmp.size());
+  for (int v = 0; v < n; ++v) {
+    auto b = tmp.begin() + cnt[v], e = tmp.begin() + cnt[v + 1];
+    std::sort(b, e);
+    auto last = std::unique(b, e);
+    g.adj.insert(g.adj.end(), b, last);
+    g.ptr[v + 1] = (int)g.adj.size();
+  }
+  return g;
+}
+
+// ---------------------------------------------------------------- nested dissection
+class NestedDissection {
+ public:
+  NestedDissection(const Graph& g, const SymbolicOptions& opt)
+      : g_(g), opt_(opt), set_(g.n, -1), lev_(g.n, -1), side_(g.n, 0) {}
+
+  std::vector<int> run() {
+    std::vector<int> all(g_.n);
+    std::iota(all.begin(), all.end(), 0);
+    order_.reserve(g_.n);
+    dissect(all);
+    return order_;
+  }
+
+ private:
+  const Graph& g_;
+  const SymbolicOptions& opt_;
+  std::vector<int> set_, lev_, side_;
+  std::vector<int> order_;
+  int next_id_ = 0;
+
+  int tag(const std::vector<int>& nodes) {
+    int id = next_id_++;
+    for (int v : nodes) set_[v] = id;
+    return id;
+  }
+
+  // BFS inside set `id` from `src`; fills lev_ and returns nodes in BFS order.
+  std::vector<int> bfs(int id, int src, int* depth) {
+    std::vector<int> q;
+    q.push_back(src);
+    lev_[src] = 0;
+    // mark visited with a temporary set id
+    int vis = -2 - id;
+    set_[src] = vis;
+    for (size_t h = 0; h < q.size(); ++h) {
+      int v = q[h];
+      for (int k = g_.ptr[v]; k < g_.ptr[v + 1]; ++k) {
+        int u = g_.adj[k];
+        if (set_[u] != id) continue;
+        set_[u] = vis;
+        lev_[u] = lev_[v] + 1;
+        q.push_back(u);
+      }
+    }
+    for (int v : q) set_[v] = id;
+    *depth = lev_[q.back()];
+    return q;
+  }
+
+  void leaf_order(const std::vector<int>& nodes) {
+    // exact minimum degree on the induced subgraph; external neighbours count
+    // once towards the degree (they are eliminated later, as separator nodes)
+    const int m = (int)nodes.size();
+    int id = tag(nodes);
+    std::vector<int> loc(m);
+    std::vector<std::vector<int>> adj(m);
+    std::vector<int> ext(m, 0);
+    std::vector<int> index_of;  // global -> local via lev_ scratch
+    for (int i = 0; i < m; ++i) lev_[nodes[i]] = i;
+    for (int i = 0; i < m; ++i) {
+      int v = nodes[i];
+      for (int k = g_.ptr[v]; k < g_.ptr[v + 1]; ++k) {
+        int u = g_.adj[k];
+        if (set_[u] == id) adj[i].push_back(lev_[u]);
+        else ext[i]++;
+      }
+      std::sort(adj[i].begin(), adj[i].end());
+    }
+    std::vector<char> done(m, 0);
+    std::vector<int> merged;
+    for (int step = 0; step < m; ++step) {
+      int best = -1;
+      long bdeg = 0;
+      for (int i = 0; i < m; ++i) {
+        if (done[i]) continue;
+        long d = (long)adj[i].size() + ext[i];
+        if (best < 0 || d < bdeg) { best = i; bdeg = d; }
+      }
+      done[best] = 1;
+      order_.push_back(nodes[best]);
+      const std::vector<int> nb = adj[best];
+      for (int a : nb) {
+        // adj[a] = (adj[a] U nb) \ {a, best}
+        merged.clear();
+        std::set_union(adj[a].begin(), adj[a].end(), nb.begin(), nb.end(), std::back_inserter(merged));
+        adj[a].clear();
+        for (int x : merged)
+          if (x != a && x != best) adj[a].push_back(x);
+        ext[a] = std::max(ext[a], ext[best]);
+      }
+      adj[best].clear();
+    }
+    for (int v : nodes) set_[v] = -1;
+  }
+
+  void dissect(std::vector<int> nodes) {
+    if ((int)nodes.size() <= opt_.leaf_size) {
+      leaf_order(nodes);
+      return;
+    }
+    int id = tag(nodes);
+    // connected components
+    int depth = 0;
+    std::vector<int> first = bfs(id, nodes[0], &depth);
+    if (first.size() < nodes.size()) {
+      std::vector<char> in_first(0);
+      for (int v : first) side_[v] = 1;
+      std::vector<int> rest;
+      for (int v : nodes)
+        if (!side_[v]) rest.push_back(v);
+      for (int v : first) side_[v] = 0;
+      for (int v : nodes) set_[v] = -1;
+      dissect(first);
+      dissect(rest);
+      return;
+    }
+    // pseudo-peripheral start
+    int src = nodes[0], best_depth = -1;
+    std::vector<int> q;
+    for (int it = 0; it < 5; ++it) {
+      q = bfs(id, src, &depth);
+      if (depth <= best_depth) break;
+      best_depth = depth;
+      // min-degree node of the last level
+      int cand = q.back(), cdeg = g_.deg(cand);
+      for (auto itq = q.rbegin(); itq != q.rend() && lev_[*itq] == depth; ++itq)
+        if (g_.deg(*itq) < cdeg) { cand = *itq; cdeg = g_.deg(*itq); }
+      src = cand;
+    }
+    q = bfs(id, src, &depth);
+    const int total = (int)q.size();
+    if (depth < 2) {
+      for (int v : nodes) set_[v] = -1;
+      leaf_order(nodes);
+      return;
+    }
+    std::vector<int> cnt(depth + 1, 0);
+    for (int v : q) cnt[lev_[v]]++;
+    std::vector<int> pre(depth + 2, 0);
+    for (int l = 0; l <= depth; ++l) pre[l + 1] = pre[l] + cnt[l];
+    int sep = -1;
+    double best = 0;
+    for (int l = 1; l < depth; ++l) {
+      int a = pre[l], b = total - pre[l + 1];
+      double bal = (double)std::min(a, b) / total;
+      if (bal < 0.2) continue;
+      // prefer small separators, then balance
+      double score = cnt[l] * (1.0 + 0.5 * (0.5 - bal));
+      if (sep < 0 || score < best) { sep = l; best = score; }
+    }
+    if (sep < 0) {
+      // fall back to the median level
+      for (int l = 1; l < depth; ++l)
+        if (pre[l + 1] >= total / 2) { sep = l; break; }
+    }
+    // side_: 1 = A (lower levels), 2 = B (upper), 3 = separator
+    for (int v : q) side_[v] = lev_[v] < sep ? 1 : (lev_[v] > sep ? 2 : 3);
+    // thin: separator nodes with no neighbour in B move to A
+    for (int v : q) {
+      if (side_[v] != 3) continue;
+      bool touches_b = false;
+      for (int k = g_.ptr[v]; k < g_.ptr[v + 1] && !touches_b; ++k) {
+        int u = g_.adj[k];
+        if (set_[u] == id && side_[u] == 2) touches_b = true;
+      }
+      if (!touches_b) side_[v] = 1;
+    }
+    // thin: separator nodes with no neighbour in A move to B
+    for (int v : q) {
+      if (side_[v] != 3) continue;
+      bool touches_a = false;
+      for (int k = g_.ptr[v]; k < g_.ptr[v + 1] && !touches_a; ++k) {
+        int u = g_.adj[k];
+        if (set_[u] == id && side_[u] == 1) touches_a = true;
+      }
+      if (!touches_a) side_[v] = 2;
+    }
+    std::vector<int> A, B, S;
+    for (int v : q) {
+      if (side_[v] == 1) A.push_back(v);
+      else if (side_[v] == 2) B.push_back(v);
+      else S.push_back(v);
+      side_[v] = 0;
+    }
+    for (int v : nodes) set_[v] = -1;
+    if (A.empty() || B.empty()) {
+      leaf_order(nodes);
+      return;
+    }
+    dissect(std::move(A));
+    dissect(std::move(B));
+    for (int v : S) order_.push_back(v);
+  }
+};
+
+}  // namespace
+
+int analyse(int32_t n, int64_t nnz, const int32_t* colptr, const int32_t* rowind,
+            const SymbolicOptions& opt, Symbolic& S) {
+  try {
+    if (n <= 0) throw std::runtime_error("n must be positive");
+    if (colptr[0] != 0 || colptr[n] != nnz) throw std::runtime_error("colptr inconsistent with nnz");
+    for (int j = 0; j < n; ++j) {
+      if (colptr[j + 1] < colptr[j]) throw std::runtime_error("colptr not monotone");
+      for (int k = colptr[j]; k < colptr[j + 1]; ++k)
+        if (rowind[k] < 0 || rowind[k] >= n) throw std::runtime_error("row index out of range");
+    }
+    S = Symbolic();
+    S.n = n;
+    S.nnz = nnz;
+    Graph g = symmetric_graph(n, colptr, rowind);
+
+    // ---- ordering
+    std::vector<int> perm;
+    if (opt.ordering == 1) {
+      perm.resize(n);
+      std::iota(perm.begin(), perm.end(), 0);
+    } else {
+      NestedDissection nd(g, opt);
+      perm = nd.run();
+    }
+    if ((int)perm.size() != n) throw std::runtime_error("ordering lost nodes");
+    std::vector<int> iperm(n, -1);
+    for (int k = 0; k < n; ++k) iperm[perm[k]] = k;
+
+    // ---- elimination tree (Liu), then postorder
+    auto etree = [&](const std::vector<int>& pm, const std::vector<int>& ipm) {
+      std::vector<int> parent(n, -1), anc(n, -1);
+      for (int k = 0; k < n; ++k) {
+        int v = pm[k];
+        for (int e = g.ptr[v]; e < g.ptr[v + 1]; ++e) {
+          int i = ipm[g.adj[e]];
+          if (i >= k) continue;
+          while (anc[i] != -1 && anc[i] != k) {
+            int nx = anc[i];
+            anc[i] = k;
+            i = nx;
+          }
+          if (anc[i] == -1) {
+            anc[i] = k;
+            parent[i] = k;
+          }
+        }
+      }
+      return parent;
+    };
+    std::vector<int> parent = etree(perm, iperm);
+    {
+      std::vector<int> head(n, -1), next(n, -1);
+      for (int k = n - 1; k >= 0; --k)
+        if (parent[k] >= 0) {
+          next[k] = head[parent[k]];
+          head[parent[k]] = k;
+        }
+      std::vector<int> post;
+      post.reserve(n);
+      std::vector<int> stack;
+      for (int r = 0; r < n; ++r) {
+        if (parent[r] != -1) continue;
+        stack.push_back(r);
+        while (!stack.empty()) {
+          int v = stack.back();
+          if (head[v] != -1) {
+            int c = head[v];
+            head[v] = next[c];
+            stack.push_back(c);
+          } else {
+            stack.pop_back();
+            post.push_back(v);
+          }
+        }
+      }
+      std::vector<int> np(n);
+      for (int k = 0; k < n; ++k) np[k] = perm[post[k]];
+      perm.swap(np);
+      for (int k = 0; k < n; ++k) iperm[perm[k]] = k;
+      parent = etree(perm, iperm);
+    }
+
+    // ---- column structures of L (rows > j), children merged
+    std::vector<std::vector<int>> cs(n);
+    std::vector<int> nchild(n, 0);
+    {
+      std::vector<std::vector<int>> kids(n);
+      for (int j = 0; j < n; ++j)
+        if (parent[j] >= 0) {
+          kids[parent[j]].push_back(j);
+          nchild[parent[j]]++;
+        }
+      std::vector<int> buf, tmp;
+      for (int j = 0; j < n; ++j) {
+        buf.clear();
+        int v = perm[j];
+        for (int e = g.ptr[v]; e < g.ptr[v + 1]; ++e) {
+          int i = iperm[g.adj[e]];
+          if (i > j) buf.push_back(i);
+        }
+        std::sort(buf.begin(), buf.end());
+        for (int c : kids[j]) {
+          tmp.clear();
+          // child structure minus j
+          std::set_union(buf.begin(), buf.end(), cs[c].begin(), cs[c].end(), std::back_inserter(tmp));
+          buf.clear();
+          for (int x : tmp)
+            if (x != j) buf.push_back(x);
+        }
+        cs[j] = buf;
+      }
+    }
+
+    // ---- fundamental supernodes
+    std::vector<int> sn_first, sn_last;  // inclusive column ranges
+    for (int j = 0; j < n; ++j) {
+      bool extend = j > 0 && parent[j - 1] == j && nchild[j] == 1 &&
+                    cs[j - 1].size() == cs[j].size() + 1;
+      if (extend) sn_last.back() = j;
+      else {
+        sn_first.push_back(j);
+        sn_last.push_back(j);
+      }
+    }
+    int nsn = (int)sn_first.size();
+    std::vector<int> col_sn(n);
+    for (int s = 0; s < nsn; ++s)
+      for (int j = sn_first[s]; j <= sn_last[s]; ++j) col_sn[j] = s;
+    std::vector<int> sparent(nsn, -1);
+    std::vector<double> true_nz(nsn, 0);
+    for (int s = 0; s < nsn; ++s) {
+      const auto& R = cs[sn_last[s]];
+      if (!R.empty()) sparent[s] = col_sn[R.front()];
+      for (int j = sn_first[s]; j <= sn_last[s]; ++j) true_nz[s] += 1.0 + cs[j].size();
+    }
+
+    // ---- relaxed amalgamation (child merged into parent when contiguous)
+    std::vector<int> rep(nsn);
+    std::iota(rep.begin(), rep.end(), 0);
+    auto find = [&](int s) {
+      while (rep[s] != s) s = rep[s] = rep[rep[s]];
+      return s;
+    };
+    std::vector<int> first(sn_first), last(sn_last);
+    for (int s = 0; s < nsn; ++s) {
+      if (find(s) != s) continue;
+      if (sparent[s] < 0) continue;
+      int p = find(sparent[s]);
+      if (last[s] + 1 != first[p]) continue;
+      double ns_new = (double)(last[p] - first[s] + 1);
+      double r_p = (double)cs[sn_last[p]].size();   // parent's structure kept
+      double f_new = ns_new + r_p;
+      double stored = ns_new * f_new - ns_new * (ns_new - 1) / 2;
+      double zeros = stored - (true_nz[s] + true_nz[p]);
+      double zfrac = zeros / stored;
+      bool merge = ns_new <= opt.relax_small ||
+                   (ns_new <= opt.relax_mid && zfrac < opt.zrelax_mid) ||
+                   (ns_new <= opt.relax_big && zfrac < opt.zrelax_big);
+      if (!merge) continue;
+      rep[s] = p;
+      first[p] = first[s];
+      true_nz[p] += true_nz[s];
+    }
+    // final supernodes in column order
+    std::vector<int> fin;
+    for (int s = 0; s < nsn; ++s)
+      if (find(s) == s) fin.push_back(s);
+    std::sort(fin.begin(), fin.end(), [&](int a, int b) { return first[a] < first[b]; });
+    const int nf = (int)fin.size();
+    std::vector<int> front_of_col(n);
+    for (int t = 0; t < nf; ++t)
+      for (int j = first[fin[t]]; j <= last[fin[t]]; ++j) front_of_col[j] = t;
+
+    // ---- fronts
+    S.fronts.resize(nf);
+    std::vector<const std::vector<int>*> Rs(nf);
+    int64_t rows = 0, entries = 0;
+    for (int t = 0; t < nf; ++t) {
+      int s = fin[t];
+      Front& F = S.fronts[t];
+      Rs[t] = &cs[sn_last[s]];
+      F.col0 = first[s];
+      F.ns = last[s] - first[s] + 1;
+      F.f = F.ns + (int)Rs[t]->size();
+      F.parent = Rs[t]->empty() ? -1 : front_of_col[Rs[t]->front()];
+      F.row0 = (int32_t)rows;
+      F.off = entries;
+      F.wv = rows;
+      F.level = 0;
+      rows += F.f;
+      entries += (int64_t)F.f * F.f;
+      S.max_front = std::max(S.max_front, F.f);
+      double ns = F.ns, f = F.f;
+      S.nnz_lu += (int64_t)(2 * ns * f - ns * ns);
+      for (int k = 0; k < F.ns; ++k) {
+        double m = f - k - 1;
+        S.factor_flops += 8.0 * m * m + 8.0 * m;
+      }
+    }
+    if (rows > INT32_MAX) throw std::runtime_error("front rows exceed int32");
+    S.total_rows = rows;
+    S.factor_entries = entries;
+    S.idx.resize(rows);
+    S.relpos.assign(rows, -1);
+    S.row_front.resize(rows);
+    for (int t = 0; t < nf; ++t)
+      for (int a = 0; a < S.fronts[t].f; ++a) S.row_front[S.fronts[t].row0 + a] = t;
+    for (int t = 0; t < nf; ++t) {
+      const Front& F = S.fronts[t];
+      for (int a = 0; a < F.ns; ++a) S.idx[F.row0 + a] = F.col0 + a;
+      for (int a = F.ns; a < F.f; ++a) S.idx[F.row0 + a] = (*Rs[t])[a - F.ns];
+    }
+    auto local_pos = [&](int t, int p) -> int {
+      const Front& F = S.fronts[t];
+      if (p >= F.col0 && p < F.col0 + F.ns) return p - F.col0;
+      auto b = S.idx.begin() + F.row0 + F.ns, e = S.idx.begin() + F.row0 + F.f;
+      auto it = std::lower_bound(b, e, p);
+      if (it == e || *it != p) return -1;
+      return F.ns + (int)(it - b);
+    };
+    for (int t = 0; t < nf; ++t) {
+      const Front& F = S.fronts[t];
+      if (F.parent < 0) {
+        if (F.f != F.ns) throw std::runtime_error("root front with update rows");
+        continue;
+      }
+      if (F.parent <= t) throw std::runtime_error("parent front not after child");
+      for (int a = F.ns; a < F.f; ++a) {
+        int pos = local_pos(F.parent, S.idx[F.row0 + a]);
+        if (pos < 0) throw std::runtime_error("child row missing from parent front");
+        S.relpos[F.row0 + a] = pos;
+      }
+    }
+    // levels
+    for (int t = 0; t < nf; ++t) {
+      const Front& F = S.fronts[t];
+      if (F.parent >= 0) S.fronts[F.parent].level = std::max(S.fronts[F.parent].level, F.level + 1);
+    }
+    int nlev = 0;
+    for (auto& F : S.fronts) nlev = std::max(nlev, F.level + 1);
+    S.level_ptr.assign(nlev + 1, 0);
+    S.level_maxf.assign(nlev, 0);
+    for (auto& F : S.fronts) {
+      S.level_ptr[F.level + 1]++;
+      S.level_maxf[F.level] = std::max(S.level_maxf[F.level], F.f);
+    }
+    for (int l = 0; l < nlev; ++l) S.level_ptr[l + 1] += S.level_ptr[l];
+    S.level_fronts.resize(nf);
+    {
+      std::vector<int> pos(S.level_ptr.begin(), S.level_ptr.end() - 1);
+      // larger fronts first within a level (longest work dispatched first)
+      std::vector<int> ord(nf);
+      std::iota(ord.begin(), ord.end(), 0);
+      std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return S.fronts[a].f > S.fronts[b].f; });
+      for (int t : ord) S.level_fronts[pos[S.fronts[t].level]++] = t;
+    }
+
+    // ---- original-entry assembly lists
+    S.prow.resize(nnz);
+    S.pcol.resize(nnz);
+    std::vector<int32_t> dest(nnz), dcol(nnz);
+    std::vector<int32_t> cnt(rows + 1, 0);
+    for (int j = 0; j < n; ++j)
+      for (int64_t k = colptr[j]; k < colptr[j + 1]; ++k) {
+        int pi = iperm[rowind[k]], pj = iperm[j];
+        S.prow[k] = pi;
+        S.pcol[k] = pj;
+        int t = front_of_col[std::min(pi, pj)];
+        int a = local_pos(t, pi), b = local_pos(t, pj);
+        if (a < 0 || b < 0) throw std::runtime_error("entry outside its front (symbolic bug)");
+        dest[k] = S.fronts[t].row0 + a;
+        dcol[k] = b;
+        cnt[dest[k] + 1]++;
+      }
+    for (int64_t r = 0; r < rows; ++r) cnt[r + 1] += cnt[r];
+    S.asm_ptr = cnt;
+    S.asm_col.resize(nnz);
+    S.asm_nz.resize(nnz);
+    {
+      std::vector<int32_t> pos(cnt.begin(), cnt.end() - 1);
+      for (int64_t k = 0; k < nnz; ++k) {
+        int32_t p = pos[dest[k]]++;
+        S.asm_col[p] = dcol[k];
+        S.asm_nz[p] = (int32_t)k;
+      }
+    }
+    // ---- extend-add lists (child update rows -> parent rows)
+    std::vector<int32_t> ecnt(rows + 1, 0);
+    for (int t = 0; t < nf; ++t) {
+      const Front& F = S.fronts[t];
+      if (F.parent < 0) continue;
+      const Front& P = S.fronts[F.parent];
+      for (int a = F.ns; a < F.f; ++a) ecnt[P.row0 + S.relpos[F.row0 + a] + 1]++;
+    }
+    for (int64_t r = 0; r < rows; ++r) ecnt[r + 1] += ecnt[r];
+    S.ea_ptr = ecnt;
+    S.ea_src.resize(ecnt[rows]);
+    {
+      std::vector<int32_t> pos(ecnt.begin(), ecnt.end() - 1);
+      for (int t = 0; t < nf; ++t) {
+        const Front& F = S.fronts[t];
+        if (F.parent < 0) continue;
+        const Front& P = S.fronts[F.parent];
+        for (int a = F.ns; a < F.f; ++a) S.ea_src[pos[P.row0 + S.relpos[F.row0 + a]]++] = F.row0 + a;
+      }
+    }
+    S.perm.assign(perm.begin(), perm.end());
+    S.iperm.assign(iperm.begin(), iperm.end());
+    return 0;
+  } catch (const std::exception& e) {
+    S.error = e.what();
+    return 1;
+  }
+}
+
+}  // namespace pfr

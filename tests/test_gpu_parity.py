@@ -1,0 +1,138 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Tolerances (fp64 throughout, stated per SURVEY.md §8c and DESIGN.md):
+* fr: relative error <= 1e-8 (static-pivot multifrontal vs SuperLU threshold
+  pivoting on the same matrices; both fp64, orderings differ);
+* loss: relative <= 1e-8; gradient: relative (inf-norm) <= 1e-6 against the
+  oracle adjoint, <= 1e-4 against central finite differences.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import make_problem, oracle_for
+
+pytestmark = pytest.mark.gpu
+
+FR_RTOL = 1e-8
+GRAD_RTOL = 1e-6
+
+
+def _rel(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+@pytest.fixture(scope="module")
+def iso():
+    return make_problem("isotropic", ny=6, device="cuda:0")
+
+
+@pytest.mark.parametrize("material", ["isotropic", "orthotropic", "orthotropic_d4", "sol", "sol_sym", "symm_sol"])
+def test_forward_parity(material):
+    p = make_problem(material, ny=5, device="cuda:0")
+    freqs = np.linspace(40.0, 600.0, 70)
+    fr = p.solveForward(freqs)
+    ref = oracle_for(p).fr(freqs, p.parameters)
+    assert np.all(np.isfinite(fr))
+    assert np.max(np.abs(fr - ref) / np.abs(ref)) < FR_RTOL
+
+
+def test_forward_chunking_and_padding():
+    """151 frequencies through 64-frequency chunks (3 chunks, the last padded)."""
+    p = make_problem("isotropic", ny=4, device="cuda:0", max_batch=64)
+    freqs = np.linspace(40.0, 600.0, 151)
+    fr = p.solveForward(freqs)
+    ref = oracle_for(p).fr(freqs, p.parameters)
+    assert np.max(np.abs(fr - ref) / np.abs(ref)) < FR_RTOL
+
+
+def test_single_frequency(iso):
+    fr = iso.solveForward(np.array([152.0]))
+    ref = oracle_for(iso).fr([152.0], iso.parameters)
+    assert fr.shape == (1,) and abs(fr[0] - ref[0]) / ref[0] < FR_RTOL
+
+
+@pytest.mark.parametrize("loss_type", ["MSE", "RMSE", "MSE_AFC", "MSE_LOG_AFC"])
+def test_loss_and_grad_parity(loss_type):
+    from oracle.plate_oracle import loss_and_grad
+    p = make_problem("orthotropic", ny=5, device="cuda:0")
+    freqs = np.linspace(40.0, 600.0, 48)
+    theta0 = p.parameters
+    ref = p.solveForward(freqs) * np.exp(1j * 0.1)          # complex reference, as Problem.py:209
+    theta = theta0 * (1 + np.array([0.1, 0.1, 0.2, 0.1, 0.1]))
+    loss_fn = p.getLossFunction(freqs, ref, loss_type)
+    x = torch.tensor(theta, requires_grad=True)
+    val = loss_fn(x)
+    val.backward()
+    lo, go = loss_and_grad(oracle_for(p), freqs, ref, loss_type, theta)
+    assert abs(val.item() - lo) / abs(lo) < FR_RTOL
+    assert _rel(x.grad.numpy(), go) < GRAD_RTOL
+
+
+def test_grad_vs_finite_differences():
+    from oracle.plate_oracle import fd_grad
+    p = make_problem("isotropic", ny=4, device="cuda:0")
+    freqs = np.linspace(100.0, 500.0, 24)
+    ref = p.solveForward(freqs)
+    theta = p.parameters * np.array([1.1, 1.1, 1.2])
+    x = torch.tensor(theta, requires_grad=True)
+    p.getLossFunction(freqs, ref, "MSE_LOG_AFC")(x).backward()
+    g_fd = fd_grad(oracle_for(p), freqs, ref, "MSE_LOG_AFC", theta)
+    assert _rel(x.grad.numpy(), g_fd) < 1e-4
+
+
+def test_scaling_params():
+    """getLossFunction(..., scaling_params): params * scaling (Problem.py:943-950)."""
+    from oracle.plate_oracle import loss_and_grad
+    p = make_problem("isotropic", ny=4, device="cuda:0")
+    freqs = np.linspace(100.0, 500.0, 20)
+    ref = p.solveForward(freqs)
+    s = p.parameters
+    x = torch.tensor(np.array([1.05, 0.97, 1.1]), requires_grad=True)
+    p.getLossFunction(freqs, ref, "MSE", scaling_params=s)(x).backward()
+    lo, go = loss_and_grad(oracle_for(p), freqs, ref, "MSE", x.detach().numpy(), scaling=s)
+    assert _rel(x.grad.numpy(), go) < GRAD_RTOL
+
+
+def test_fr_function_autograd(iso):
+    """Arbitrary downstream of getFRFunction: backward = adjoint sweep with dL/dfr."""
+    from oracle.plate_oracle import coeffs18_jacobian
+    freqs = np.linspace(60.0, 580.0, 30)
+    fr_fn = iso.getFRFunction()
+    theta = iso.parameters * np.array([1.02, 0.99, 1.3])
+    x = torch.tensor(theta, requires_grad=True)
+    wts = torch.linspace(0.5, 2.0, 30, dtype=torch.float64, device="cuda:0")
+    (fr_fn(freqs, x) * wts).sum().backward()
+    # oracle: d/dtheta sum_q w_q fr_q by central differences on the oracle fr
+    orc = oracle_for(iso)
+    g = np.zeros(3)
+    for k in range(3):
+        h = 1e-6 * theta[k]
+        tp, tm = theta.copy(), theta.copy()
+        tp[k] += h
+        tm[k] -= h
+        g[k] = (wts.cpu().numpy() @ (orc.fr(freqs, tp) - orc.fr(freqs, tm))) / (2 * h)
+    assert _rel(x.grad.numpy(), g) < 1e-4
+
+
+def test_coupled_laminate_gradient():
+    """Non-symmetric laminate: B != 0 couples in-plane and bending (full union pattern)."""
+    from oracle.plate_oracle import loss_and_grad
+    p = make_problem("sol", ny=4, device="cuda:0")
+    freqs = np.linspace(40.0, 600.0, 32)
+    ref = p.solveForward(freqs) * 1.05
+    theta = p.parameters * 1.03
+    x = torch.tensor(theta, requires_grad=True)
+    val = p.getLossFunction(freqs, ref, "MSE_AFC")(x)
+    val.backward()
+    lo, go = loss_and_grad(oracle_for(p), freqs, ref, "MSE_AFC", theta)
+    assert abs(val.item() - lo) / abs(lo) < FR_RTOL
+    assert _rel(x.grad.numpy(), go) < GRAD_RTOL
+
+
+def test_repeat_is_deterministic(iso):
+    freqs = np.linspace(40.0, 600.0, 65)
+    a = iso.solveForward(freqs)
+    b = iso.solveForward(freqs)
+    assert np.array_equal(a, b)
