@@ -1,0 +1,178 @@
+"""Benchmark: freq-solves/s (forward + adjoint) of the C3 workload on N GPUs.
+
+BASELINE.json metric "freq-solves/sec (forward+adjoint) @20k DOF; achieved HBM
+GB/s vs peak", config C3: orthotropic plate, ~20k DOF, 4096 frequencies,
+forward + adjoint (loss + gradient), fp64.
+
+* one STEP = one loss + gradient evaluation (``getLossFunction`` +
+  ``backward``) over the frequency sweep: per frequency assemble -> LU ->
+  forward solves -> FR -> loss cotangent -> adjoint solves -> contraction;
+* weak scaling: every rank sweeps 4096 frequencies (its contiguous block of
+  ``linspace(40, 600, 4096 * N)``); one all-reduce (RCCL) of the loss/gradient
+  partials per step;
+* ``value`` = 4096 * N / (max-over-ranks seconds per step);
+* ``roofline``: the dominant kernel (static-pivot multifrontal factorisation,
+  fp64) from per-phase HIP-event timings on the sweep's stream; the batched
+  triangular-solve phase (HBM-bound) is reported beside it;
+* ``cpu_baseline``: the oracle (scipy SuperLU, one process per core) on a
+  bounded sample of the same workload, rank 0, N = 1 only.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--freqs F] [--ny NY]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector/matrix (spec; MI355X_MICROARCH.md lists no fp64 row)
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def build_problem(ny, device):
+    from plate_inverse_problem_amd.Accelerometer import Accelerometer
+    from plate_inverse_problem_amd.Geometry import Geometry, GeometryParams
+    from plate_inverse_problem_amd.Material import get_material
+    from plate_inverse_problem_amd.Problem import Problem
+    acc = Accelerometer("AP1030")
+    geom = Geometry("sh_i", acc, GeometryParams(100e-3, 20e-3, 2e-3, None, None), ny=ny)
+    mat = get_material(1500.0, "orthotropic", E1=120e9, E2=8e9, G12=5e9, nu12=0.3, beta=0.01)
+    return Problem(geom, mat, acc, device=device)
+
+
+def cpu_baseline(prob, freqs, ref, theta, sample_per_core=24):
+    """Oracle CPU sweep on a bounded sample (rank 0, N = 1)."""
+    sys.path.insert(0, REPO)
+    from tests.helpers import oracle_for
+    from oracle.plate_oracle import parallel_partials
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    cores = max(1, min(cores, os.cpu_count() or 1, 16))
+    orc = oracle_for(prob)
+    n = min(freqs.size, sample_per_core * cores)
+    idx = np.linspace(0, freqs.size - 1, n).round().astype(int)
+    t0 = time.perf_counter()
+    parallel_partials(orc, freqs[idx], ref[idx], "MSE_LOG_AFC", theta, n_workers=cores)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "freq-solves/s", "cores": cores, "kind": "port",
+            "sample": f"{n} of the {freqs.size} frequencies (evenly spaced), forward+adjoint, one SuperLU "
+                      f"factorisation per frequency reused for the transpose solve (best-CPU), {cores} processes, "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--freqs", type=int, default=4096, help="frequencies per GPU")
+    ap.add_argument("--ny", type=int, default=25, help="mesh cells across the width (25 -> 19,353 DOF)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    prob = build_problem(args.ny, device)
+    n_total = args.freqs * world
+    freqs = np.linspace(40.0, 600.0, n_total)
+    theta_true = prob.parameters.copy()
+    theta = theta_true * (1 + np.array([0.1, 0.1, 0.2, 0.1, 0.1]))
+
+    from plate_inverse_problem_amd.distributed import shard_range
+    lo, hi = shard_range(n_total, rank, world)
+    ref = np.zeros(n_total, dtype=np.complex128)
+    ref[lo:hi] = prob.solveForward(freqs[lo:hi], theta_true)          # synthetic measurement, phase 0
+    loss_fn = prob.getLossFunction(freqs, ref, "MSE_LOG_AFC", distributed=world > 1)
+    eng = prob.engine()
+    solver = eng.solver
+    solver.set_timing(True)
+
+    def step():
+        x = torch.tensor(theta, requires_grad=True)
+        val = loss_fn(x)
+        val.backward()
+        return val.item(), x.grad
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    phase = np.zeros(5)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        val, grad = step()
+        phase += solver.last_timings()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = 1e3 * elapsed / args.steps
+    value = n_total / (elapsed / args.steps)
+
+    st = eng.stats
+    nv = hi - lo
+    phase /= args.steps                      # ms per step, per phase
+    factor_flops = st["factor_flops"] * nv
+    fact_tfs = factor_flops / (phase[0] * 1e-3) / 1e12
+    # triangular solves: 4 passes (L, U, U^T, L^T) over the factors, 16 B per L+U entry
+    # per pass per frequency, plus int32 pattern (shared by 64-frequency wavefronts) and vectors
+    trsv_bytes = nv * (4 * 16 * st["nnz_lu"] + 4 * 2 * 16 * st["n"])
+    trsv_gbs = trsv_bytes / ((phase[1] + phase[3]) * 1e-3) / 1e9
+    out = {
+        "metric": "freq-solves/sec (forward+adjoint) @20k DOF",
+        "value": value,
+        "unit": "freq-solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (FE plate model built in-repo; reference FR = forward sweep at theta_true)",
+        "config": {"workload": "C3: orthotropic CFRP-like plate, sh_i strip 100x20x2 mm + AP1030, "
+                               f"{st['n']} DOF, {args.freqs} freqs/GPU in 40-600 Hz, forward+adjoint, "
+                               "loss MSE_LOG_AFC + gradient",
+                   "n_dofs": st["n"], "freqs_per_gpu": args.freqs, "chunk": solver.max_batch,
+                   "nnz_lu": st["nnz_lu"], "factor_gflop_per_freq": st["factor_flops"] / 1e9,
+                   "parallelism": f"frequency shards x{world} + 1 all-reduce/step"},
+        "roofline": {"bound": "mfma", "kernel": "k_factor_level (fp64 vector FMA; MI355X fp64 peak)",
+                     "achieved": fact_tfs, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": fact_tfs / FP64_PEAK_TFLOPS, "traffic": None},
+        "sptrsv_roofline": {"bound": "hbm", "kernel": "k_{l,u,ut,lt}solve_level", "achieved": trsv_gbs,
+                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": trsv_gbs / HBM_PEAK_GBS,
+                            "traffic": None},
+        "phase_ms": {"factor": phase[0], "fwd_solves": phase[1], "functional": phase[2],
+                     "adj_solves": phase[3], "contract": phase[4]},
+        "loss": val,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(prob, freqs, ref, theta)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

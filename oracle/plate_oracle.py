@@ -321,15 +321,19 @@ def loss_and_grad(prob: OracleProblem, freqs, ref, loss_type, theta, scaling=Non
     return loss_sum / np.asarray(freqs).size, grad
 
 
-def fd_grad(prob: OracleProblem, freqs, ref, loss_type, theta, rel=1e-4):
+def fd_grad(prob: OracleProblem, freqs, ref, loss_type, theta, rel=2e-4):
+    """4th-order central differences (truncation O(h^4): the loss is sharply
+    peaked in the loss factor near resonances, O(h^2) stencils are not enough)."""
     theta = np.asarray(theta, dtype=np.float64)
     g = np.zeros_like(theta)
     for p in range(theta.size):
         h = rel * abs(theta[p])
-        tp, tm = theta.copy(), theta.copy()
-        tp[p] += h
-        tm[p] -= h
-        g[p] = (loss(prob, freqs, ref, loss_type, tp) - loss(prob, freqs, ref, loss_type, tm)) / (2 * h)
+        v = []
+        for m in (-2, -1, 1, 2):
+            t = theta.copy()
+            t[p] += m * h
+            v.append(loss(prob, freqs, ref, loss_type, t))
+        g[p] = (v[0] - 8 * v[1] + 8 * v[2] - v[3]) / (12 * h)
     return g
 
 

@@ -65,10 +65,10 @@ class _Engine:
         self.stats = self.sym.stats()
         if not max_batch:
             # as many frequencies per chunk as fit in ~60% of free HBM (multiple of 64, <= 4096)
-            want = min(max(64, (n_freqs + 63) // 64 * 64), 4096)
             free, _ = torch.cuda.mem_get_info(device)
-            cap = int(0.6 * free / self.sym.workspace_bytes(64)) * 64
-            max_batch = max(64, min(want, cap))
+            cap = max(64, min(4096, int(0.6 * free / self.sym.workspace_bytes(64)) * 64))
+            n_chunks = -(-max(1, n_freqs) // cap)
+            max_batch = (-(-n_freqs // n_chunks) + 63) // 64 * 64   # even chunks, multiple of 64
         self.solver = _native.Solver(self.sym, device.index, max_batch)
         vals = mats[:, self.keep]
         self.stiff = torch.as_tensor(np.ascontiguousarray(vals[:18].T), device=device)       # (nnz, 18)

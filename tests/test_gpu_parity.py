@@ -106,13 +106,16 @@ def test_fr_function_autograd(iso):
     (fr_fn(freqs, x) * wts).sum().backward()
     # oracle: d/dtheta sum_q w_q fr_q by central differences on the oracle fr
     orc = oracle_for(iso)
+    w = wts.cpu().numpy()
     g = np.zeros(3)
-    for k in range(3):
-        h = 1e-6 * theta[k]
-        tp, tm = theta.copy(), theta.copy()
-        tp[k] += h
-        tm[k] -= h
-        g[k] = (wts.cpu().numpy() @ (orc.fr(freqs, tp) - orc.fr(freqs, tm))) / (2 * h)
+    for k in range(3):                      # 4th-order central differences
+        h = 2e-4 * theta[k]
+        v = []
+        for m in (-2, -1, 1, 2):
+            t = theta.copy()
+            t[k] += m * h
+            v.append(w @ orc.fr(freqs, t))
+        g[k] = (v[0] - 8 * v[1] + 8 * v[2] - v[3]) / (12 * h)
     assert _rel(x.grad.numpy(), g) < 1e-4
 
 
