@@ -57,6 +57,8 @@ struct pfr_solver {
   // owned device arrays
   std::vector<void*> owned;
   int32_t* d_level_fronts = nullptr;
+  int4* d_tiles = nullptr;              // Schur tiles (front, i0, j0, 0), grouped by level
+  std::vector<int32_t> tile_ptr;
   int32_t* d_colptr = nullptr;
   int32_t* d_rowind = nullptr;
   double2 *F = nullptr, *WV = nullptr, *X = nullptr, *Y = nullptr, *XA = nullptr, *G = nullptr;
@@ -139,6 +141,8 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     int nf = s->level_ptr[l + 1] - s->level_ptr[l];
     pfr::launch_factor(mode, s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_W[l], ngroups, s->F, s->Fc,
                        s->freqs, s->K, s->M, data, ds, nvalid, s->flags, st);
+    pfr::launch_schur(s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l], ngroups, s->F,
+                      s->Fc, st);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -295,6 +299,23 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       (rc = s->up(&ep, S.ea_ptr)) || (rc = s->up(&es, S.ea_src)) || (rc = s->up(&pm, S.perm)) ||
       (rc = s->up(&pr, S.prow)) || (rc = s->up(&pc, S.pcol)) || (rc = s->up(&s->d_level_fronts, S.level_fronts)))
     return bail(rc);
+  {
+    // Schur-complement tiles (4 x 4) of every front's update block, level by level
+    std::vector<int4> tv;
+    s->tile_ptr.assign(1, 0);
+    const int L = (int)S.level_ptr.size() - 1;
+    for (int l = 0; l < L; ++l) {
+      for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
+        const int t = S.level_fronts[e];
+        const Front& F = S.fronts[t];
+        const int r = F.f - F.ns;
+        for (int i0 = 0; i0 < r; i0 += 4)
+          for (int j0 = 0; j0 < r; j0 += 4) tv.push_back(make_int4(t, i0, j0, 0));
+      }
+      s->tile_ptr.push_back((int32_t)tv.size());
+    }
+    if ((rc = s->up(&s->d_tiles, tv))) return bail(rc);
+  }
   std::vector<int32_t> cp(colptr, colptr + S.n + 1), ri(rowind, rowind + S.nnz);
   if ((rc = s->up(&s->d_colptr, cp)) || (rc = s->up(&s->d_rowind, ri))) return bail(rc);
   s->P = DevPattern{d_fronts, idx, relpos, rowf, ap, ac, an, ep, es, pm, pr, pc, S.n};

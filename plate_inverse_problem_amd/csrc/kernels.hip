@@ -74,14 +74,23 @@ __global__ void k_combine(const double* __restrict__ stiff, int n_stiff, int64_t
   K[nz] = make_double2(re, im);
 }
 
-// ------------------------------------------------------------------ K2: factor
+// ------------------------------------------------------------------ K2a: assemble + panel
 // MODE 0: A_q = K - omega_q^2 M assembled on the fly (operator form).
 // MODE 1: A_q = data[q * data_stride + nz] (explicit batch, InnerState::solve data).
+// The front (f x f, row-major, frequency-minor) is assembled, then the first ns
+// pivots are eliminated with static diagonal pivots, restricted right-looking:
+// every block of KB pivots updates the pivot rows (all columns) and the panel
+// columns of the update rows; the Schur block A22 (update rows x update
+// columns) is left for k_schur_level (a register-tiled GEMM over all pivots).
+constexpr int JB = 4;     // columns per batched read-modify-write step
+
 template <int MODE>
-__global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* __restrict__ lvl, cplx* __restrict__ F, int64_t Fc,
-                               const double* __restrict__ freqs, const cplx* __restrict__ K,
-                               const double* __restrict__ M, const cplx* __restrict__ data,
-                               int64_t data_stride, int nvalid, int* __restrict__ flags) {
+__global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* __restrict__ lvl,
+                                                       cplx* __restrict__ F, int64_t Fc,
+                                                       const double* __restrict__ freqs,
+                                                       const cplx* __restrict__ K, const double* __restrict__ M,
+                                                       const cplx* __restrict__ data, int64_t data_stride,
+                                                       int nvalid, int* __restrict__ flags) {
   const Ctx c = ctx();
   const Front fr = P.fronts[lvl[blockIdx.x]];
   const int f = fr.f, ns = fr.ns;
@@ -90,16 +99,17 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
 
   double om2 = 0.0;
   if (MODE == 0) {
-    double om = 6.283185307179586 * freqs[c.q];
+    const double om = 6.283185307179586 * freqs[c.q];
     om2 = om * om;
   }
-  // 1. assemble: zero, original entries, children's update matrices
+  // 1. assemble.  Zero + original entries are stores only (distinct columns per
+  //    row, program order = last store wins); children's update rows are
+  //    read-modify-write in batches of 8 independent columns.
   for (int a = c.w; a < f; a += c.W) {
     for (int b = 0; b < f; ++b) E(a, b) = make_double2(0.0, 0.0);
     const int r = fr.row0 + a;
     const int e1 = P.asm_ptr[r + 1];
     for (int e = P.asm_ptr[r]; e < e1; ++e) {
-      const int b = P.asm_col[e];
       const int nz = P.asm_nz[e];
       cplx v;
       if (MODE == 0) {
@@ -108,7 +118,7 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
       } else {
         v = data[min(c.q, (int64_t)nvalid - 1) * data_stride + nz];
       }
-      E(a, b) = cadd(E(a, b), v);
+      E(a, P.asm_col[e]) = v;
     }
     const int x1 = P.ea_ptr[r + 1];
     for (int e = P.ea_ptr[r]; e < x1; ++e) {
@@ -116,15 +126,26 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
       const Front cf = P.fronts[P.row_front[src]];
       const cplx* __restrict__ cb = F + (cf.off + (int64_t)(src - cf.row0) * cf.f) * Fc + c.q;
       const int* __restrict__ rp = P.relpos + cf.row0;
-      for (int b = cf.ns; b < cf.f; ++b) {
-        const int pb = rp[b];
-        E(a, pb) = cadd(E(a, pb), cb[(int64_t)b * Fc]);
+      for (int b0 = cf.ns; b0 < cf.f; b0 += 8) {
+        cplx v[8], o[8];
+        int pb[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int b = min(b0 + u, cf.f - 1);
+          pb[u] = rp[b];
+          v[u] = cb[(int64_t)b * Fc];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) o[u] = E(a, pb[u]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (b0 + u < cf.f) E(a, pb[u]) = cadd(o[u], v[u]);
       }
     }
   }
   __syncthreads();
 
-  // 2. blocked right-looking partial LU of the first ns pivots (static pivots)
+  // 2. blocked restricted right-looking elimination of the ns pivots
   for (int k0 = 0; k0 < ns; k0 += KB) {
     const int kb = min(KB, ns - k0);
     const int k1 = k0 + kb;
@@ -141,7 +162,7 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
       }
     }
     __syncthreads();
-    // U12 = L11^{-1} A12 : columns distributed over waves
+    // pivot rows of the block, columns >= k1:  L11^{-1} A12 (columns over waves)
     {
       cplx L[KB][KB];
 #pragma unroll
@@ -167,7 +188,8 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
       }
     }
     __syncthreads();
-    // L21 = A21 U11^{-1}, then trailing update A22 -= L21 U12 : rows over waves
+    // rows >= k1: l = A(i, block) U11^{-1}; then update
+    //   pivot rows (i < ns): columns [k1, f)      update rows (i >= ns): columns [k1, ns)
     {
       cplx U[KB][KB];
       cplx Dinv[KB];
@@ -193,18 +215,82 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
             l[t] = cmul(l[t], Dinv[t]);
             E(i, k0 + t) = l[t];
           }
-        for (int j = k1; j < f; ++j) {
-          cplx v = E(i, j);
+        const int jend = i < ns ? f : ns;
+        for (int j0 = k1; j0 < jend; j0 += JB) {
+          cplx u[KB][JB], v[JB];
 #pragma unroll
-          for (int t = 0; t < KB; ++t)
-            if (t < kb) v = cfms(v, l[t], E(k0 + t, j));
-          E(i, j) = v;
+          for (int jj = 0; jj < JB; ++jj) {
+            const int j = min(j0 + jj, jend - 1);
+            v[jj] = E(i, j);
+#pragma unroll
+            for (int t = 0; t < KB; ++t)
+              if (t < kb) u[t][jj] = E(k0 + t, j);
+          }
+#pragma unroll
+          for (int jj = 0; jj < JB; ++jj)
+#pragma unroll
+            for (int t = 0; t < KB; ++t)
+              if (t < kb) v[jj] = cfms(v[jj], l[t], u[t][jj]);
+#pragma unroll
+          for (int jj = 0; jj < JB; ++jj)
+            if (j0 + jj < jend) E(i, j0 + jj) = v[jj];
         }
       }
     }
     __syncthreads();
   }
 #undef E
+}
+
+// ------------------------------------------------------------------ K2b: Schur complement
+// A22 -= L21 U12 over all ns pivots of the front: one wavefront per TM x TN tile
+// of A22 (64 lanes = 64 frequencies), accumulators in registers, no stores in
+// the K loop so every load of a k-step is independent.
+constexpr int TM = 4, TN = 4;
+
+__global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* __restrict__ tiles, int ntiles,
+                                                      cplx* __restrict__ F, int64_t Fc) {
+  const int lane = threadIdx.x & 63;
+  const int tid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (tid >= ntiles) return;
+  const int64_t q = (int64_t)blockIdx.y * 64 + lane;
+  const int4 t = tiles[tid];
+  const Front fr = P.fronts[t.x];
+  const int f = fr.f, ns = fr.ns;
+  cplx* __restrict__ base = F + fr.off * Fc + q;
+  int ri[TM], cj[TN];
+#pragma unroll
+  for (int m = 0; m < TM; ++m) ri[m] = min(ns + t.y + m, f - 1);
+#pragma unroll
+  for (int n = 0; n < TN; ++n) cj[n] = min(ns + t.z + n, f - 1);
+  cplx acc[TM][TN];
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int n = 0; n < TN; ++n) acc[m][n] = make_double2(0.0, 0.0);
+  for (int k = 0; k < ns; ++k) {
+    cplx a[TM], b[TN];
+#pragma unroll
+    for (int m = 0; m < TM; ++m) a[m] = base[((int64_t)ri[m] * f + k) * Fc];
+#pragma unroll
+    for (int n = 0; n < TN; ++n) b[n] = base[((int64_t)k * f + cj[n]) * Fc];
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int n = 0; n < TN; ++n) {
+        acc[m][n].x = fma(a[m].x, b[n].x, fma(-a[m].y, b[n].y, acc[m][n].x));
+        acc[m][n].y = fma(a[m].x, b[n].y, fma(a[m].y, b[n].x, acc[m][n].y));
+      }
+  }
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int n = 0; n < TN; ++n)
+      if (ns + t.y + m < f && ns + t.z + n < f) {
+        cplx* p = base + ((int64_t)(ns + t.y + m) * f + ns + t.z + n) * Fc;
+        const cplx o = *p;
+        *p = make_double2(o.x - acc[m][n].x, o.y - acc[m][n].y);
+      }
 }
 
 // ------------------------------------------------------------------ right-hand sides
@@ -610,6 +696,12 @@ __global__ void k_matvec(const int* __restrict__ colptr, const int* __restrict__
 
 void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPack& coef, double2* K, hipStream_t st) {
   LAUNCH(k_combine, dim3((unsigned)((nnz + 255) / 256)), dim3(256), st, stiff, n_stiff, nnz, coef, K);
+}
+
+void launch_schur(const DevPattern& P, const int4* tiles, int ntiles, int ngroups, double2* F, int64_t Fc,
+                  hipStream_t st) {
+  if (ntiles <= 0) return;
+  LAUNCH(k_schur_level, dim3((ntiles + 3) / 4, ngroups), dim3(256), st, P, tiles, ntiles, F, Fc);
 }
 
 void launch_factor(int mode, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F,

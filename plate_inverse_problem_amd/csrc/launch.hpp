@@ -19,6 +19,9 @@ void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPac
 void launch_factor(int mode, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F,
                    int64_t Fc, const double* freqs, const double2* K, const double* M, const double2* data,
                    int64_t ds, int nvalid, int* flags, hipStream_t st);
+// Schur complement A22 -= L21 U12 for a level's tile list (TM x TN = 4 x 4 tiles)
+void launch_schur(const DevPattern& P, const int4* tiles, int ntiles, int ngroups, double2* F, int64_t Fc,
+                  hipStream_t st);
 // which: 0 = L (bottom-up), 1 = U (top-down), 2 = U^T (bottom-up), 3 = L^T (top-down)
 void launch_solve(int which, int rhs_mode, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups,
                   const double2* F, int64_t Fc, double2* WV, const RhsDesc& rd, const double2* Yin, double2* Out,
