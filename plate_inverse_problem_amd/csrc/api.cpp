@@ -59,6 +59,8 @@ struct pfr_solver {
   int32_t* d_level_fronts = nullptr;
   int4* d_tiles = nullptr;              // Schur tiles (front, i0, j0, 0), grouped by level
   std::vector<int32_t> tile_ptr;
+  int32_t* d_level_rows = nullptr;      // front rows of each level (assembly work list)
+  std::vector<int32_t> row_ptr;
   int32_t* d_colptr = nullptr;
   int32_t* d_rowind = nullptr;
   double2 *F = nullptr, *WV = nullptr, *X = nullptr, *Y = nullptr, *XA = nullptr, *G = nullptr;
@@ -139,8 +141,10 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
   const int ngroups = (int)(s->Fc / 64);
   for (int l = 0; l < L; ++l) {
     int nf = s->level_ptr[l + 1] - s->level_ptr[l];
-    pfr::launch_factor(mode, s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_W[l], ngroups, s->F, s->Fc,
-                       s->freqs, s->K, s->M, data, ds, nvalid, s->flags, st);
+    pfr::launch_assemble(mode, s->P, s->d_level_rows + s->row_ptr[l], s->row_ptr[l + 1] - s->row_ptr[l], ngroups,
+                         s->F, s->Fc, s->freqs, s->K, s->M, data, ds, nvalid, st);
+    pfr::launch_factor(s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_W[l], ngroups, s->F, s->Fc, s->flags,
+                       st);
     pfr::launch_schur(s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l], ngroups, s->F,
                       s->Fc, st);
   }
@@ -315,6 +319,16 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       s->tile_ptr.push_back((int32_t)tv.size());
     }
     if ((rc = s->up(&s->d_tiles, tv))) return bail(rc);
+    std::vector<int32_t> rv;
+    s->row_ptr.assign(1, 0);
+    for (int l = 0; l < L; ++l) {
+      for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
+        const Front& F = S.fronts[S.level_fronts[e]];
+        for (int a = 0; a < F.f; ++a) rv.push_back(F.row0 + a);
+      }
+      s->row_ptr.push_back((int32_t)rv.size());
+    }
+    if ((rc = s->up(&s->d_level_rows, rv))) return bail(rc);
   }
   std::vector<int32_t> cp(colptr, colptr + S.n + 1), ri(rowind, rowind + S.nnz);
   if ((rc = s->up(&s->d_colptr, cp)) || (rc = s->up(&s->d_rowind, ri))) return bail(rc);

@@ -84,67 +84,107 @@ __global__ void k_combine(const double* __restrict__ stiff, int n_stiff, int64_t
 // columns) is left for k_schur_level (a register-tiled GEMM over all pivots).
 constexpr int JB = 4;     // columns per batched read-modify-write step
 
+// Assembly of a level's fronts: one wavefront per front row (64 frequencies).
+// Zero + original entries are stores only (distinct columns per row, program
+// order = last store wins); children's update rows are read-modify-write in
+// batches of 8 independent columns.
 template <int MODE>
+__global__ __launch_bounds__(256) void k_assemble_level(DevPattern P, const int* __restrict__ rows, int nrows,
+                                                         cplx* __restrict__ F, int64_t Fc,
+                                                         const double* __restrict__ freqs,
+                                                         const cplx* __restrict__ K, const double* __restrict__ M,
+                                                         const cplx* __restrict__ data, int64_t data_stride,
+                                                         int nvalid) {
+  const int lane = threadIdx.x & 63;
+  const int wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wid >= nrows) return;
+  const int64_t q = (int64_t)blockIdx.y * 64 + lane;
+  const int r = rows[wid];
+  const Front fr = P.fronts[P.row_front[r]];
+  const int f = fr.f;
+  const int a = r - fr.row0;
+  cplx* __restrict__ row = F + (fr.off + (int64_t)a * f) * Fc + q;
+  double om2 = 0.0;
+  if (MODE == 0) {
+    const double om = 6.283185307179586 * freqs[q];
+    om2 = om * om;
+  }
+  for (int b = 0; b < f; ++b) row[(int64_t)b * Fc] = make_double2(0.0, 0.0);
+  const int e1 = P.asm_ptr[r + 1];
+  for (int e = P.asm_ptr[r]; e < e1; ++e) {
+    const int nz = P.asm_nz[e];
+    cplx v;
+    if (MODE == 0) {
+      const cplx k = K[nz];
+      v = make_double2(fma(-om2, M[nz], k.x), k.y);
+    } else {
+      v = data[min(q, (int64_t)nvalid - 1) * data_stride + nz];
+    }
+    row[(int64_t)P.asm_col[e] * Fc] = v;
+  }
+  const int x1 = P.ea_ptr[r + 1];
+  for (int e = P.ea_ptr[r]; e < x1; ++e) {
+    const int src = P.ea_src[e];
+    const Front cf = P.fronts[P.row_front[src]];
+    const cplx* __restrict__ cb = F + (cf.off + (int64_t)(src - cf.row0) * cf.f) * Fc + q;
+    const int* __restrict__ rp = P.relpos + cf.row0;
+    for (int b0 = cf.ns; b0 < cf.f; b0 += 8) {
+      cplx v[8], o[8];
+      int pb[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int b = min(b0 + u, cf.f - 1);
+        pb[u] = rp[b];
+        v[u] = cb[(int64_t)b * Fc];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) o[u] = row[(int64_t)pb[u] * Fc];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (b0 + u < cf.f) row[(int64_t)pb[u] * Fc] = cadd(o[u], v[u]);
+    }
+  }
+}
+
+// One row of a rank-kb update, A(i, j) -= sum_t l_t U(k0 + t, j) for j in [j0, jend).
+// Reads through `rd`, writes through `wr` (both the front base): every element
+// is read once and then written once, never re-read, so the two access paths
+// are declared non-aliasing -- this lets the compiler issue the next batch's
+// loads before the current batch's stores (otherwise each batch pays a full
+// store + load round trip).
+__device__ __forceinline__ void row_update(const cplx* __restrict__ rd, cplx* __restrict__ wr, int64_t row_i,
+                                           int64_t row_k0, int f, int64_t Fc, int j0, int jend, int kb,
+                                           const cplx (&l)[KB]) {
+#pragma unroll 2
+  for (int jb = j0; jb < jend; jb += JB) {
+    cplx u[KB][JB], v[JB];
+#pragma unroll
+    for (int jj = 0; jj < JB; ++jj) {
+      const int j = min(jb + jj, jend - 1);
+      v[jj] = rd[(row_i + j) * Fc];
+#pragma unroll
+      for (int t = 0; t < KB; ++t)
+        if (t < kb) u[t][jj] = rd[(row_k0 + (int64_t)t * f + j) * Fc];
+    }
+#pragma unroll
+    for (int jj = 0; jj < JB; ++jj)
+#pragma unroll
+      for (int t = 0; t < KB; ++t)
+        if (t < kb) v[jj] = cfms(v[jj], l[t], u[t][jj]);
+#pragma unroll
+    for (int jj = 0; jj < JB; ++jj)
+      if (jb + jj < jend) wr[(row_i + jb + jj) * Fc] = v[jj];
+  }
+}
+
 __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* __restrict__ lvl,
                                                        cplx* __restrict__ F, int64_t Fc,
-                                                       const double* __restrict__ freqs,
-                                                       const cplx* __restrict__ K, const double* __restrict__ M,
-                                                       const cplx* __restrict__ data, int64_t data_stride,
-                                                       int nvalid, int* __restrict__ flags) {
+                                                       int* __restrict__ flags) {
   const Ctx c = ctx();
   const Front fr = P.fronts[lvl[blockIdx.x]];
   const int f = fr.f, ns = fr.ns;
   cplx* __restrict__ base = F + fr.off * Fc + c.q;
 #define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
-
-  double om2 = 0.0;
-  if (MODE == 0) {
-    const double om = 6.283185307179586 * freqs[c.q];
-    om2 = om * om;
-  }
-  // 1. assemble.  Zero + original entries are stores only (distinct columns per
-  //    row, program order = last store wins); children's update rows are
-  //    read-modify-write in batches of 8 independent columns.
-  for (int a = c.w; a < f; a += c.W) {
-    for (int b = 0; b < f; ++b) E(a, b) = make_double2(0.0, 0.0);
-    const int r = fr.row0 + a;
-    const int e1 = P.asm_ptr[r + 1];
-    for (int e = P.asm_ptr[r]; e < e1; ++e) {
-      const int nz = P.asm_nz[e];
-      cplx v;
-      if (MODE == 0) {
-        const cplx k = K[nz];
-        v = make_double2(fma(-om2, M[nz], k.x), k.y);
-      } else {
-        v = data[min(c.q, (int64_t)nvalid - 1) * data_stride + nz];
-      }
-      E(a, P.asm_col[e]) = v;
-    }
-    const int x1 = P.ea_ptr[r + 1];
-    for (int e = P.ea_ptr[r]; e < x1; ++e) {
-      const int src = P.ea_src[e];
-      const Front cf = P.fronts[P.row_front[src]];
-      const cplx* __restrict__ cb = F + (cf.off + (int64_t)(src - cf.row0) * cf.f) * Fc + c.q;
-      const int* __restrict__ rp = P.relpos + cf.row0;
-      for (int b0 = cf.ns; b0 < cf.f; b0 += 8) {
-        cplx v[8], o[8];
-        int pb[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int b = min(b0 + u, cf.f - 1);
-          pb[u] = rp[b];
-          v[u] = cb[(int64_t)b * Fc];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) o[u] = E(a, pb[u]);
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (b0 + u < cf.f) E(a, pb[u]) = cadd(o[u], v[u]);
-      }
-    }
-  }
-  __syncthreads();
-
   // 2. blocked restricted right-looking elimination of the ns pivots
   for (int k0 = 0; k0 < ns; k0 += KB) {
     const int kb = min(KB, ns - k0);
@@ -216,25 +256,7 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
             E(i, k0 + t) = l[t];
           }
         const int jend = i < ns ? f : ns;
-        for (int j0 = k1; j0 < jend; j0 += JB) {
-          cplx u[KB][JB], v[JB];
-#pragma unroll
-          for (int jj = 0; jj < JB; ++jj) {
-            const int j = min(j0 + jj, jend - 1);
-            v[jj] = E(i, j);
-#pragma unroll
-            for (int t = 0; t < KB; ++t)
-              if (t < kb) u[t][jj] = E(k0 + t, j);
-          }
-#pragma unroll
-          for (int jj = 0; jj < JB; ++jj)
-#pragma unroll
-            for (int t = 0; t < KB; ++t)
-              if (t < kb) v[jj] = cfms(v[jj], l[t], u[t][jj]);
-#pragma unroll
-          for (int jj = 0; jj < JB; ++jj)
-            if (j0 + jj < jend) E(i, j0 + jj) = v[jj];
-        }
+        row_update(base, base, (int64_t)i * f, (int64_t)k0 * f, f, Fc, k1, jend, kb, l);
       }
     }
     __syncthreads();
@@ -704,12 +726,17 @@ void launch_schur(const DevPattern& P, const int4* tiles, int ntiles, int ngroup
   LAUNCH(k_schur_level, dim3((ntiles + 3) / 4, ngroups), dim3(256), st, P, tiles, ntiles, F, Fc);
 }
 
-void launch_factor(int mode, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F,
-                   int64_t Fc, const double* freqs, const double2* K, const double* M, const double2* data,
-                   int64_t ds, int nvalid, int* flags, hipStream_t st) {
-  dim3 g(nfronts, ngroups), b(64 * W);
-  if (mode == 0) LAUNCH(k_factor_level<0>, g, b, st, P, lvl, F, Fc, freqs, K, M, data, ds, nvalid, flags);
-  else LAUNCH(k_factor_level<1>, g, b, st, P, lvl, F, Fc, freqs, K, M, data, ds, nvalid, flags);
+void launch_assemble(int mode, const DevPattern& P, const int* rows, int nrows, int ngroups, double2* F, int64_t Fc,
+                     const double* freqs, const double2* K, const double* M, const double2* data, int64_t ds,
+                     int nvalid, hipStream_t st) {
+  dim3 g((nrows + 3) / 4, ngroups), b(256);
+  if (mode == 0) LAUNCH(k_assemble_level<0>, g, b, st, P, rows, nrows, F, Fc, freqs, K, M, data, ds, nvalid);
+  else LAUNCH(k_assemble_level<1>, g, b, st, P, rows, nrows, F, Fc, freqs, K, M, data, ds, nvalid);
+}
+
+void launch_factor(const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F, int64_t Fc,
+                   int* flags, hipStream_t st) {
+  LAUNCH(k_factor_level, dim3(nfronts, ngroups), dim3(64 * W), st, P, lvl, F, Fc, flags);
 }
 
 static RhsArgs make_rhs(const RhsDesc& d) {
