@@ -1,0 +1,85 @@
+"""Multi-rank path on CPU: world_size-2 gloo process group (127.0.0.1).
+
+Each rank sweeps its contiguous frequency block (oracle as the local compute,
+standing in for the GPU sweep) and the packed [loss_sum, w_0..w_17] partials
+are combined by ``distributed.all_reduce_sum`` -- the single collective of
+the GPU path.  The result must equal the single-process sweep.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from plate_inverse_problem_amd.distributed import all_reduce_sum, shard_range
+
+
+def test_shard_range_partitions():
+    for n in (1, 7, 64, 4096, 4097):
+        for w in (1, 2, 3, 8):
+            spans = [shard_range(n, r, w) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [h - l for l, h in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from helpers import make_problem, oracle_for
+        from oracle.plate_oracle import frequency_partials
+        p = make_problem("orthotropic", ny=3)
+        o = oracle_for(p)
+        freqs = np.linspace(50.0, 550.0, 11)
+        ref = o.fr(freqs, p.parameters) * 1.02
+        th = p.parameters * 1.05
+        lo, hi = shard_range(freqs.size)
+        ls, w = frequency_partials(o, freqs[lo:hi], ref[lo:hi], "MSE_LOG_AFC", th, n_total=freqs.size)
+        packed = torch.tensor(np.concatenate([[ls], w]), dtype=torch.complex128)
+        tot = all_reduce_sum(packed)
+        x = torch.tensor([float(rank + 1)], dtype=torch.float64)
+        all_reduce_sum(x)
+        out_q.put((rank, tot.numpy(), float(x.item()), (lo, hi)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo_reduction_matches_single_process():
+    from helpers import make_problem, oracle_for
+    from oracle.plate_oracle import frequency_partials
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    res.sort()
+    (_, t0, x0, s0), (_, t1, x1, s1) = res
+    assert s0 == (0, 6) and s1 == (6, 11)
+    assert x0 == x1 == 3.0
+    assert np.array_equal(t0, t1)                       # every rank holds the same totals
+    p = make_problem("orthotropic", ny=3)
+    o = oracle_for(p)
+    freqs = np.linspace(50.0, 550.0, 11)
+    ref = o.fr(freqs, p.parameters) * 1.02
+    ls, w = frequency_partials(o, freqs, ref, "MSE_LOG_AFC", p.parameters * 1.05)
+    assert np.isclose(t0[0].real, ls, rtol=1e-12)
+    assert np.allclose(t0[1:], w, rtol=1e-10, atol=1e-12 * np.abs(w).max())
