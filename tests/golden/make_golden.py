@@ -149,6 +149,24 @@ def make_layout_golden():
         print(f"layout_{case}.npz: N={2 * Lh + Mh}")
 
 
+def make_compressor_golden():
+    """Reference ``Input.Compressor`` (scipy only, imports directly) on a synthetic
+    3-resonance FR: selected indices for both algorithms at several sizes."""
+    ref_input = _load_by_path("ref_Input", os.path.join(REF_SRC, "jax_plate", "Input.py"))
+    freqs = np.linspace(40.0, 600.0, 1500)
+    fr = np.ones_like(freqs, dtype=complex)
+    for f0, z in ((150.0, 0.01), (330.0, 0.02), (520.0, 0.015)):
+        fr += 1.0 / (1 - (freqs / f0) ** 2 + 2j * z * freqs / f0)
+    out = {"freqs": freqs, "fr": fr}
+    for alg in (0, 1):
+        for n in (100, 200, 300):
+            fsel, _ = ref_input.Compressor(freqs, fr, 1500, alg)(n)
+            out[f"alg{alg}_n{n}"] = np.searchsorted(freqs, fsel)
+    np.savez_compressed(os.path.join(HERE, "compressor.npz"), **out)
+    print("compressor.npz")
+
+
 if __name__ == "__main__":
     make_material_golden()
     make_layout_golden()
+    make_compressor_golden()
