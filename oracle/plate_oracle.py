@@ -188,9 +188,15 @@ class OracleProblem:
         return I0 * (m[18] + m[20] + m[22]) + I0c * (m[19] + m[21] + m[23]) + I2 * m[24] + I2c * m[25]
 
     def matrix(self, f, c):
+        """A(omega) on the CSC union pattern (rows/cols are already in CSC order)."""
+        if not hasattr(self, "_csc"):
+            colptr = np.zeros(self.n + 1, dtype=np.int64)
+            np.add.at(colptr, self.cols.astype(np.int64) + 1, 1)
+            self._csc = (self.rows.astype(np.int32), np.cumsum(colptr).astype(np.int32), self.mass_values())
+        rowind, colptr, mass = self._csc
         omega = 2 * np.pi * f
-        data = -omega ** 2 * self.mass_values() + _rc(c, self.mats[:18])
-        return sp.csc_matrix((data.astype(complex), (self.rows, self.cols)), shape=(self.n, self.n))
+        data = -omega ** 2 * mass + _rc(c, self.mats[:18])
+        return sp.csc_matrix((data, rowind.copy(), colptr.copy()), shape=(self.n, self.n))
 
     def rhs_scale(self, f, c):
         omega = 2 * np.pi * f
@@ -342,8 +348,12 @@ _POOL_PROB = None
 
 
 def _pool_worker(args):
+    # one process per core: keep BLAS single-threaded (oversubscription otherwise
+    # multiplies the run time many-fold on a cgroup-limited host)
+    from threadpoolctl import threadpool_limits
     freqs, ref, loss_type, theta, n_total, refactor = args
-    return frequency_partials(_POOL_PROB, freqs, ref, loss_type, theta, n_total, refactor)
+    with threadpool_limits(1):
+        return frequency_partials(_POOL_PROB, freqs, ref, loss_type, theta, n_total, refactor)
 
 
 def parallel_partials(prob: OracleProblem, freqs, ref, loss_type, theta, n_workers=None,
