@@ -49,7 +49,7 @@ def build_problem(ny, device):
     return Problem(geom, mat, acc, device=device)
 
 
-def cpu_baseline(prob, freqs, ref, theta, sample_per_core=48):
+def cpu_baseline(prob, freqs, ref, theta, sample_per_core=128):
     """Oracle CPU sweep on a bounded sample (rank 0, N = 1)."""
     sys.path.insert(0, REPO)
     from tests.helpers import oracle_for

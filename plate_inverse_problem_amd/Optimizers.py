@@ -201,33 +201,66 @@ def optimize_cd_mem2(f, x_0, N_steps=100, h=0.01, f_min=1e-8):
 optimize_cd_mem = optimize_cd_mem2
 
 
-def optimize_lbfgs(f, x_0, N_steps=50, history_size=10, lr=1.0, tolerance_grad=1e-12,
-                   tolerance_change=1e-14, f_min=1e-16):
-    """L-BFGS (strong-Wolfe line search) on the fused loss+gradient sweep."""
-    x = _t(x_0).clone().requires_grad_(True)
-    opt = torch.optim.LBFGS([x], lr=lr, max_iter=1, history_size=history_size, line_search_fn="strong_wolfe",
-                            tolerance_grad=tolerance_grad, tolerance_change=tolerance_change)
+def optimize_lbfgs(f, x_0, N_steps=50, history_size=10, max_step=0.05, c1=1e-4, max_backtrack=30,
+                   tolerance_grad=1e-12, f_min=1e-16):
+    """L-BFGS (two-loop recursion) with Armijo backtracking.
+
+    One fused forward + adjoint sweep per function evaluation.  The first step is
+    capped at ``max_step`` (infinity norm, in the optimiser's coordinates): the FR
+    misfit's basin in the stiffness moduli is only a few percent wide (resonances
+    move past each other), so an unscaled gradient step would leave it.
+    """
+    vg = value_and_grad(f)
+    x = np.asarray(x_0, dtype=np.float64).copy()
+    cur_f, g = vg(x)
+    S, Y = [], []
     f_hist, x_hist, g_hist = [], [], []
-    state = {}
-
-    def closure():
-        opt.zero_grad()
-        val = f(x)
-        val.backward()
-        state["f"], state["g"] = float(val.detach()), x.grad.detach().numpy().copy()
-        return val
-
     status, k = "Running", 0
     for k in range(N_steps):
-        x_hist.append(x.detach().numpy().copy())
-        opt.step(closure)
-        f_hist.append(state["f"])
-        g_hist.append(state["g"])
-        if state["f"] <= f_min:
+        f_hist.append(cur_f)
+        x_hist.append(x.copy())
+        g_hist.append(g.copy())
+        if cur_f <= f_min:
             status = "Converged"
             break
-        if np.max(np.abs(state["g"])) <= tolerance_grad:
+        if np.max(np.abs(g)) <= tolerance_grad:
             status = "Converged (gradient)"
             break
-    xf = x.detach().numpy().copy()
-    return optResult(xf, float(f(_t(xf))), f_hist, x_hist, g_hist, k, status)
+        q = -g.copy()
+        alphas = []
+        for s_, y_ in zip(reversed(S), reversed(Y)):
+            a = (s_ @ q) / (y_ @ s_)
+            alphas.append(a)
+            q -= a * y_
+        if S:
+            q *= (S[-1] @ Y[-1]) / (Y[-1] @ Y[-1])
+        for (s_, y_), a in zip(zip(S, Y), reversed(alphas)):
+            q += (a - (y_ @ q) / (y_ @ s_)) * s_
+        d = q
+        gtd = g @ d
+        if gtd >= 0:                                  # not a descent direction: restart
+            S.clear()
+            Y.clear()
+            d = -g
+            gtd = g @ d
+        t = 1.0
+        if not S:
+            t = min(1.0, max_step / max(np.max(np.abs(d)), 1e-300))
+        for _ in range(max_backtrack):
+            x_new = x + t * d
+            f_new, g_new = vg(x_new)
+            if np.isfinite(f_new) and f_new <= cur_f + c1 * t * gtd:
+                break
+            t *= 0.5
+        else:
+            status = "Line search failed"
+            break
+        s_, y_ = x_new - x, g_new - g
+        if s_ @ y_ > 1e-300:
+            S.append(s_)
+            Y.append(y_)
+            if len(S) > history_size:
+                S.pop(0)
+                Y.pop(0)
+        x, cur_f, g = x_new, f_new, g_new
+    return optResult(x, cur_f, f_hist, x_hist, g_hist, k, status)
