@@ -58,6 +58,8 @@ struct pfr_solver {
   std::vector<void*> owned;
   int32_t* d_level_fronts = nullptr;
   int4* d_tiles = nullptr;              // Schur tiles (front, i0, j0, 0), grouped by level
+  int32_t* d_gptr = nullptr;            // per tile: 17 offsets into d_gel (one list per tile position)
+  int32_t* d_gel = nullptr;             // children's update-matrix element ids
   std::vector<int32_t> tile_ptr;
   int32_t* d_level_rows = nullptr;      // front rows of each level (assembly work list)
   std::vector<int32_t> row_ptr;
@@ -145,8 +147,8 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
                          s->F, s->Fc, s->freqs, s->K, s->M, data, ds, nvalid, st);
     pfr::launch_factor(s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_W[l], ngroups, s->F, s->Fc, s->flags,
                        st);
-    pfr::launch_schur(s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l], ngroups, s->F,
-                      s->Fc, st);
+    pfr::launch_schur(s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l],
+                      s->d_gptr + (int64_t)s->tile_ptr[l] * 17, s->d_gel, ngroups, s->F, s->Fc, st);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -305,7 +307,14 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     return bail(rc);
   {
     // Schur-complement tiles (4 x 4) of every front's update block, level by level
+    // plus, per tile and tile position, the children's update-matrix entries that
+    // land there (the extend-add of the Schur block, done as a gather)
+    if (S.factor_entries > INT32_MAX) return bail(fail(PFR_ERR_ARG, "front storage exceeds int32 element ids"));
+    std::vector<std::vector<int>> kids(S.fronts.size());
+    for (size_t t = 0; t < S.fronts.size(); ++t)
+      if (S.fronts[t].parent >= 0) kids[S.fronts[t].parent].push_back((int)t);
     std::vector<int4> tv;
+    std::vector<int32_t> gptr, gel;
     s->tile_ptr.assign(1, 0);
     const int L = (int)S.level_ptr.size() - 1;
     for (int l = 0; l < L; ++l) {
@@ -313,12 +322,37 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
         const int t = S.level_fronts[e];
         const Front& F = S.fronts[t];
         const int r = F.f - F.ns;
+        const int ntj = (r + 3) / 4;
+        std::vector<std::vector<int32_t>> lists((size_t)ntj * ntj * 16);
+        for (int c : kids[t]) {
+          const Front& C = S.fronts[c];
+          const int32_t* rp = S.relpos.data() + C.row0;
+          for (int a = C.ns; a < C.f; ++a) {
+            const int i = rp[a] - F.ns;
+            if (i < 0) continue;
+            for (int b = C.ns; b < C.f; ++b) {
+              const int j = rp[b] - F.ns;
+              if (j < 0) continue;
+              lists[((size_t)(i / 4) * ntj + j / 4) * 16 + (i % 4) * 4 + j % 4].push_back(
+                  (int32_t)(C.off + (int64_t)a * C.f + b));
+            }
+          }
+        }
         for (int i0 = 0; i0 < r; i0 += 4)
-          for (int j0 = 0; j0 < r; j0 += 4) tv.push_back(make_int4(t, i0, j0, 0));
+          for (int j0 = 0; j0 < r; j0 += 4) {
+            tv.push_back(make_int4(t, i0, j0, 0));
+            const auto* L16 = &lists[((size_t)(i0 / 4) * ntj + j0 / 4) * 16];
+            for (int pos = 0; pos < 16; ++pos) {
+              gptr.push_back((int32_t)gel.size());
+              gel.insert(gel.end(), L16[pos].begin(), L16[pos].end());
+            }
+            gptr.push_back((int32_t)gel.size());
+          }
       }
       s->tile_ptr.push_back((int32_t)tv.size());
     }
-    if ((rc = s->up(&s->d_tiles, tv))) return bail(rc);
+    if ((rc = s->up(&s->d_tiles, tv)) || (rc = s->up(&s->d_gptr, gptr)) || (rc = s->up(&s->d_gel, gel)))
+      return bail(rc);
     std::vector<int32_t> rv;
     s->row_ptr.assign(1, 0);
     for (int l = 0; l < L; ++l) {

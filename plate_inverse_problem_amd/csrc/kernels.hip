@@ -109,7 +109,13 @@ __global__ __launch_bounds__(256) void k_assemble_level(DevPattern P, const int*
     const double om = 6.283185307179586 * freqs[q];
     om2 = om * om;
   }
-  for (int b = 0; b < f; ++b) row[(int64_t)b * Fc] = make_double2(0.0, 0.0);
+  // Only the panel region is assembled here: pivot rows (all columns) and the
+  // pivot columns of update rows.  The Schur block (update rows x update
+  // columns) holds no original entries; k_schur_level forms it in one store
+  // from the children's contributions and -L21 U12.
+  const int ns = fr.ns;
+  const int width = a < ns ? f : ns;
+  for (int b = 0; b < width; ++b) row[(int64_t)b * Fc] = make_double2(0.0, 0.0);
   const int e1 = P.asm_ptr[r + 1];
   for (int e = P.asm_ptr[r]; e < e1; ++e) {
     const int nz = P.asm_nz[e];
@@ -128,12 +134,18 @@ __global__ __launch_bounds__(256) void k_assemble_level(DevPattern P, const int*
     const Front cf = P.fronts[P.row_front[src]];
     const cplx* __restrict__ cb = F + (cf.off + (int64_t)(src - cf.row0) * cf.f) * Fc + q;
     const int* __restrict__ rp = P.relpos + cf.row0;
-    for (int b0 = cf.ns; b0 < cf.f; b0 += 8) {
+    // child columns map to increasing parent positions: for an update row only
+    // the prefix landing in the pivot columns belongs to the panel region
+    int bend = cf.f;
+    if (a >= ns)
+      for (bend = cf.ns; bend < cf.f && rp[bend] < ns; ++bend) {
+      }
+    for (int b0 = cf.ns; b0 < bend; b0 += 8) {
       cplx v[8], o[8];
       int pb[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int b = min(b0 + u, cf.f - 1);
+        const int b = min(b0 + u, bend - 1);
         pb[u] = rp[b];
         v[u] = cb[(int64_t)b * Fc];
       }
@@ -141,7 +153,7 @@ __global__ __launch_bounds__(256) void k_assemble_level(DevPattern P, const int*
       for (int u = 0; u < 8; ++u) o[u] = row[(int64_t)pb[u] * Fc];
 #pragma unroll
       for (int u = 0; u < 8; ++u)
-        if (b0 + u < cf.f) row[(int64_t)pb[u] * Fc] = cadd(o[u], v[u]);
+        if (b0 + u < bend) row[(int64_t)pb[u] * Fc] = cadd(o[u], v[u]);
     }
   }
 }
@@ -177,6 +189,31 @@ __device__ __forceinline__ void row_update(const cplx* __restrict__ rd, cplx* __
   }
 }
 
+// Pivot rows of a block, columns j = j0, j0 + stride, ...: x = L11^{-1} x in
+// place (unit lower, strictly-lower part of L11 in registers).  Same
+// read/write split as row_update: each element is read once, written once.
+__device__ __forceinline__ void col_solve(const cplx* __restrict__ rd, cplx* __restrict__ wr, int64_t row_k0, int f,
+                                          int64_t Fc, int j0, int jend, int stride, int kb,
+                                          const cplx (&L)[KB][KB]) {
+#pragma unroll 2
+  for (int j = j0; j < jend; j += stride) {
+    cplx x[KB];
+#pragma unroll
+    for (int i = 0; i < KB; ++i)
+      if (i < kb) x[i] = rd[(row_k0 + (int64_t)i * f + j) * Fc];
+#pragma unroll
+    for (int i = 1; i < KB; ++i)
+      if (i < kb) {
+#pragma unroll
+        for (int t = 0; t < KB; ++t)
+          if (t < i) x[i] = cfms(x[i], L[i][t], x[t]);
+      }
+#pragma unroll
+    for (int i = 1; i < KB; ++i)
+      if (i < kb) wr[(row_k0 + (int64_t)i * f + j) * Fc] = x[i];
+  }
+}
+
 __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* __restrict__ lvl,
                                                        cplx* __restrict__ F, int64_t Fc,
                                                        int* __restrict__ flags) {
@@ -190,16 +227,30 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
     const int kb = min(KB, ns - k0);
     const int k1 = k0 + kb;
     if (c.w == 0) {
-      for (int k = k0; k < k1; ++k) {
-        const cplx piv = E(k, k);
-        pivot_check(piv, flags, c.q);
-        const cplx inv = crecip(piv);
-        for (int i = k + 1; i < k1; ++i) {
-          const cplx l = cmul(E(i, k), inv);
-          E(i, k) = l;
-          for (int j = k + 1; j < k1; ++j) E(i, j) = cfms(E(i, j), l, E(k, j));
+      // diagonal block: one load burst, LU in registers, one store burst
+      cplx D[KB][KB];
+#pragma unroll
+      for (int i = 0; i < KB; ++i)
+#pragma unroll
+        for (int j = 0; j < KB; ++j) D[i][j] = E(k0 + min(i, kb - 1), k0 + min(j, kb - 1));
+#pragma unroll
+      for (int k = 0; k < KB; ++k) {
+        if (k < kb) {
+          pivot_check(D[k][k], flags, c.q);
+          const cplx inv = crecip(D[k][k]);
+#pragma unroll
+          for (int i = k + 1; i < KB; ++i) {
+            D[i][k] = cmul(D[i][k], inv);
+#pragma unroll
+            for (int j = k + 1; j < KB; ++j) D[i][j] = cfms(D[i][j], D[i][k], D[k][j]);
+          }
         }
       }
+#pragma unroll
+      for (int i = 0; i < KB; ++i)
+#pragma unroll
+        for (int j = 0; j < KB; ++j)
+          if (i < kb && j < kb) E(k0 + i, k0 + j) = D[i][j];
     }
     __syncthreads();
     // pivot rows of the block, columns >= k1:  L11^{-1} A12 (columns over waves)
@@ -210,22 +261,7 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
 #pragma unroll
         for (int j = 0; j < KB; ++j)
           if (j < i && i < kb) L[i][j] = E(k0 + i, k0 + j);
-      for (int j = k1 + c.w; j < f; j += c.W) {
-        cplx x[KB];
-#pragma unroll
-        for (int i = 0; i < KB; ++i)
-          if (i < kb) x[i] = E(k0 + i, j);
-#pragma unroll
-        for (int i = 1; i < KB; ++i)
-          if (i < kb) {
-#pragma unroll
-            for (int t = 0; t < KB; ++t)
-              if (t < i) x[i] = cfms(x[i], L[i][t], x[t]);
-          }
-#pragma unroll
-        for (int i = 1; i < KB; ++i)
-          if (i < kb) E(k0 + i, j) = x[i];
-      }
+      col_solve(base, base, (int64_t)k0 * f, f, Fc, k1 + c.w, f, c.W, kb, L);
     }
     __syncthreads();
     // rows >= k1: l = A(i, block) U11^{-1}; then update
@@ -271,6 +307,7 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
 constexpr int TM = 4, TN = 4;
 
 __global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* __restrict__ tiles, int ntiles,
+                                                      const int* __restrict__ gptr, const int* __restrict__ gel,
                                                       cplx* __restrict__ F, int64_t Fc) {
   const int lane = threadIdx.x & 63;
   const int tid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -285,11 +322,18 @@ __global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* _
   for (int m = 0; m < TM; ++m) ri[m] = min(ns + t.y + m, f - 1);
 #pragma unroll
   for (int n = 0; n < TN; ++n) cj[n] = min(ns + t.z + n, f - 1);
+  // children's update-matrix entries landing in this tile (extend-add as a gather)
+  const int* __restrict__ gp = gptr + (int64_t)tid * (TM * TN + 1);
   cplx acc[TM][TN];
 #pragma unroll
   for (int m = 0; m < TM; ++m)
 #pragma unroll
-    for (int n = 0; n < TN; ++n) acc[m][n] = make_double2(0.0, 0.0);
+    for (int n = 0; n < TN; ++n) {
+      cplx s = make_double2(0.0, 0.0);
+      const int e1 = gp[m * TN + n + 1];
+      for (int e = gp[m * TN + n]; e < e1; ++e) s = cadd(s, F[(int64_t)gel[e] * Fc + q]);
+      acc[m][n] = s;
+    }
   for (int k = 0; k < ns; ++k) {
     cplx a[TM], b[TN];
 #pragma unroll
@@ -299,20 +343,14 @@ __global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* _
 #pragma unroll
     for (int m = 0; m < TM; ++m)
 #pragma unroll
-      for (int n = 0; n < TN; ++n) {
-        acc[m][n].x = fma(a[m].x, b[n].x, fma(-a[m].y, b[n].y, acc[m][n].x));
-        acc[m][n].y = fma(a[m].x, b[n].y, fma(a[m].y, b[n].x, acc[m][n].y));
-      }
+      for (int n = 0; n < TN; ++n) acc[m][n] = cfms(acc[m][n], a[m], b[n]);
   }
 #pragma unroll
   for (int m = 0; m < TM; ++m)
 #pragma unroll
     for (int n = 0; n < TN; ++n)
-      if (ns + t.y + m < f && ns + t.z + n < f) {
-        cplx* p = base + ((int64_t)(ns + t.y + m) * f + ns + t.z + n) * Fc;
-        const cplx o = *p;
-        *p = make_double2(o.x - acc[m][n].x, o.y - acc[m][n].y);
-      }
+      if (ns + t.y + m < f && ns + t.z + n < f)
+        base[((int64_t)(ns + t.y + m) * f + ns + t.z + n) * Fc] = acc[m][n];
 }
 
 // ------------------------------------------------------------------ right-hand sides
@@ -720,10 +758,10 @@ void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPac
   LAUNCH(k_combine, dim3((unsigned)((nnz + 255) / 256)), dim3(256), st, stiff, n_stiff, nnz, coef, K);
 }
 
-void launch_schur(const DevPattern& P, const int4* tiles, int ntiles, int ngroups, double2* F, int64_t Fc,
-                  hipStream_t st) {
+void launch_schur(const DevPattern& P, const int4* tiles, int ntiles, const int* gptr, const int* gel, int ngroups,
+                  double2* F, int64_t Fc, hipStream_t st) {
   if (ntiles <= 0) return;
-  LAUNCH(k_schur_level, dim3((ntiles + 3) / 4, ngroups), dim3(256), st, P, tiles, ntiles, F, Fc);
+  LAUNCH(k_schur_level, dim3((ntiles + 3) / 4, ngroups), dim3(256), st, P, tiles, ntiles, gptr, gel, F, Fc);
 }
 
 void launch_assemble(int mode, const DevPattern& P, const int* rows, int nrows, int ngroups, double2* F, int64_t Fc,
