@@ -145,10 +145,13 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     int nf = s->level_ptr[l + 1] - s->level_ptr[l];
     pfr::launch_assemble(mode, s->P, s->d_level_rows + s->row_ptr[l], s->row_ptr[l + 1] - s->row_ptr[l], ngroups,
                          s->F, s->Fc, s->freqs, s->K, s->M, data, ds, nvalid, st);
-    pfr::launch_factor(s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_W[l], ngroups, s->F, s->Fc, s->flags,
-                       st);
+    // panel: enough workgroups (front x 16 frequencies) to fill the chip -> one wave
+    // each (no idle waves at the block barriers); few large fronts -> more waves
+    const int64_t wgs = (int64_t)nf * ngroups * 4;
+    const int Wp = (int)std::max<int64_t>(1, std::min<int64_t>(s->level_W[l], (4096 + wgs - 1) / wgs));
+    pfr::launch_factor(s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st);
     pfr::launch_schur(s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l],
-                      s->d_gptr + (int64_t)s->tile_ptr[l] * 17, s->d_gel, ngroups, s->F, s->Fc, st);
+                      s->d_gptr + (int64_t)s->tile_ptr[l] * 65, s->d_gel, ngroups, s->F, s->Fc, st);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -322,7 +325,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
         const int t = S.level_fronts[e];
         const Front& F = S.fronts[t];
         const int r = F.f - F.ns;
-        const int ntj = (r + 3) / 4;
+        const int ntj = (r + 3) / 4;          // 4 x 4 tiles per dimension
         std::vector<std::vector<int32_t>> lists((size_t)ntj * ntj * 16);
         for (int c : kids[t]) {
           const Front& C = S.fronts[c];
@@ -338,13 +341,21 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
             }
           }
         }
-        for (int i0 = 0; i0 < r; i0 += 4)
-          for (int j0 = 0; j0 < r; j0 += 4) {
+        // 8 x 8 super-tiles = 2 x 2 arrangement of 4 x 4 tiles (one per lane group);
+        // per super-tile 4 x 16 position lists + 1 end offset
+        static const std::vector<int32_t> none;
+        for (int i0 = 0; i0 < r; i0 += 8)
+          for (int j0 = 0; j0 < r; j0 += 8) {
             tv.push_back(make_int4(t, i0, j0, 0));
-            const auto* L16 = &lists[((size_t)(i0 / 4) * ntj + j0 / 4) * 16];
-            for (int pos = 0; pos < 16; ++pos) {
-              gptr.push_back((int32_t)gel.size());
-              gel.insert(gel.end(), L16[pos].begin(), L16[pos].end());
+            for (int sub = 0; sub < 4; ++sub) {
+              const int ti = i0 / 4 + (sub >> 1), tj = j0 / 4 + (sub & 1);
+              for (int pos = 0; pos < 16; ++pos) {
+                gptr.push_back((int32_t)gel.size());
+                if (ti < ntj && tj < ntj) {
+                  const auto& Lp = lists[((size_t)ti * ntj + tj) * 16 + pos];
+                  gel.insert(gel.end(), Lp.begin(), Lp.end());
+                }
+              }
             }
             gptr.push_back((int32_t)gel.size());
           }

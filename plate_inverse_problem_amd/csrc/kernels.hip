@@ -214,10 +214,19 @@ __device__ __forceinline__ void col_solve(const cplx* __restrict__ rd, cplx* __r
   }
 }
 
+// Panel kernel lane map: a wavefront covers 16 frequencies x 4 front rows
+// (lane = 16 * sub + frequency), so every wave-instruction advances four rows
+// (or four columns) at once and the pivot-row values it reads are shared by
+// the four row groups; workgroup = (front, 16 frequencies), W waves.
 __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* __restrict__ lvl,
                                                        cplx* __restrict__ F, int64_t Fc,
                                                        int* __restrict__ flags) {
-  const Ctx c = ctx();
+  Ctx c;
+  c.lane = threadIdx.x & 63;
+  c.w = threadIdx.x >> 6;
+  c.W = blockDim.x >> 6;
+  c.q = (int64_t)blockIdx.y * 16 + (c.lane & 15);
+  const int sub = c.lane >> 4;
   const Front fr = P.fronts[lvl[blockIdx.x]];
   const int f = fr.f, ns = fr.ns;
   cplx* __restrict__ base = F + fr.off * Fc + c.q;
@@ -246,11 +255,13 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
           }
         }
       }
+      if (sub == 0) {
 #pragma unroll
-      for (int i = 0; i < KB; ++i)
+        for (int i = 0; i < KB; ++i)
 #pragma unroll
-        for (int j = 0; j < KB; ++j)
-          if (i < kb && j < kb) E(k0 + i, k0 + j) = D[i][j];
+          for (int j = 0; j < KB; ++j)
+            if (i < kb && j < kb) E(k0 + i, k0 + j) = D[i][j];
+      }
     }
     __syncthreads();
     // pivot rows of the block, columns >= k1:  L11^{-1} A12 (columns over waves)
@@ -261,7 +272,7 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
 #pragma unroll
         for (int j = 0; j < KB; ++j)
           if (j < i && i < kb) L[i][j] = E(k0 + i, k0 + j);
-      col_solve(base, base, (int64_t)k0 * f, f, Fc, k1 + c.w, f, c.W, kb, L);
+      col_solve(base, base, (int64_t)k0 * f, f, Fc, k1 + 4 * c.w + sub, f, 4 * c.W, kb, L);
     }
     __syncthreads();
     // rows >= k1: l = A(i, block) U11^{-1}; then update
@@ -277,7 +288,7 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
 #pragma unroll
       for (int i = 0; i < KB; ++i)
         if (i < kb) Dinv[i] = crecip(E(k0 + i, k0 + i));
-      for (int i = k1 + c.w; i < f; i += c.W) {
+      for (int i = k1 + 4 * c.w + sub; i < f; i += 4 * c.W) {
         cplx l[KB];
 #pragma unroll
         for (int t = 0; t < KB; ++t)
@@ -306,14 +317,20 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
 // the K loop so every load of a k-step is independent.
 constexpr int TM = 4, TN = 4;
 
+// Lane map: a wavefront = 16 frequencies x 4 sub-tiles; the 4 sub-tiles form a
+// 2 x 2 arrangement of 4 x 4 tiles (an 8 x 8 super-tile), so each L21 row and
+// U12 column value a wave-instruction reads serves two sub-tiles.
 __global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* __restrict__ tiles, int ntiles,
                                                       const int* __restrict__ gptr, const int* __restrict__ gel,
                                                       cplx* __restrict__ F, int64_t Fc) {
   const int lane = threadIdx.x & 63;
   const int tid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (tid >= ntiles) return;
-  const int64_t q = (int64_t)blockIdx.y * 64 + lane;
-  const int4 t = tiles[tid];
+  const int sub = lane >> 4;
+  const int64_t q = (int64_t)blockIdx.y * 16 + (lane & 15);
+  int4 t = tiles[tid];
+  t.y += 4 * (sub >> 1);
+  t.z += 4 * (sub & 1);
   const Front fr = P.fronts[t.x];
   const int f = fr.f, ns = fr.ns;
   cplx* __restrict__ base = F + fr.off * Fc + q;
@@ -323,7 +340,7 @@ __global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* _
 #pragma unroll
   for (int n = 0; n < TN; ++n) cj[n] = min(ns + t.z + n, f - 1);
   // children's update-matrix entries landing in this tile (extend-add as a gather)
-  const int* __restrict__ gp = gptr + (int64_t)tid * (TM * TN + 1);
+  const int* __restrict__ gp = gptr + (int64_t)tid * (4 * TM * TN + 1) + sub * TM * TN;
   cplx acc[TM][TN];
 #pragma unroll
   for (int m = 0; m < TM; ++m)
@@ -761,7 +778,7 @@ void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPac
 void launch_schur(const DevPattern& P, const int4* tiles, int ntiles, const int* gptr, const int* gel, int ngroups,
                   double2* F, int64_t Fc, hipStream_t st) {
   if (ntiles <= 0) return;
-  LAUNCH(k_schur_level, dim3((ntiles + 3) / 4, ngroups), dim3(256), st, P, tiles, ntiles, gptr, gel, F, Fc);
+  LAUNCH(k_schur_level, dim3((ntiles + 3) / 4, ngroups * 4), dim3(256), st, P, tiles, ntiles, gptr, gel, F, Fc);
 }
 
 void launch_assemble(int mode, const DevPattern& P, const int* rows, int nrows, int ngroups, double2* F, int64_t Fc,
@@ -774,7 +791,7 @@ void launch_assemble(int mode, const DevPattern& P, const int* rows, int nrows, 
 
 void launch_factor(const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F, int64_t Fc,
                    int* flags, hipStream_t st) {
-  LAUNCH(k_factor_level, dim3(nfronts, ngroups), dim3(64 * W), st, P, lvl, F, Fc, flags);
+  LAUNCH(k_factor_level, dim3(nfronts, ngroups * 4), dim3(64 * W), st, P, lvl, F, Fc, flags);
 }
 
 static RhsArgs make_rhs(const RhsDesc& d) {
