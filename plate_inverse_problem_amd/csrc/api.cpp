@@ -58,8 +58,9 @@ struct pfr_solver {
   std::vector<void*> owned;
   int32_t* d_level_fronts = nullptr;
   int4* d_tiles = nullptr;              // Schur tiles (front, i0, j0, 0), grouped by level
-  int32_t* d_gptr = nullptr;            // per tile: 17 offsets into d_gel (one list per tile position)
-  int32_t* d_gel = nullptr;             // children's update-matrix element ids
+  int32_t* d_g1 = nullptr;              // per super-tile, lane group, position: first child source (or -1)
+  int32_t* d_gxp = nullptr;             // per super-tile: range of further sources in d_gx
+  int2* d_gx = nullptr;                 // (lane group * 16 + position, element id) of the rare extra sources
   std::vector<int32_t> tile_ptr;
   int32_t* d_level_rows = nullptr;      // front rows of each level (assembly work list)
   std::vector<int32_t> row_ptr;
@@ -151,7 +152,8 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     const int Wp = (int)std::max<int64_t>(1, std::min<int64_t>(s->level_W[l], (4096 + wgs - 1) / wgs));
     pfr::launch_factor(s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st);
     pfr::launch_schur(s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l],
-                      s->d_gptr + (int64_t)s->tile_ptr[l] * 65, s->d_gel, ngroups, s->F, s->Fc, st);
+                      s->d_g1 + (int64_t)s->tile_ptr[l] * 64, s->d_gxp + s->tile_ptr[l], s->d_gx, ngroups, s->F,
+                      s->Fc, st);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -317,7 +319,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     for (size_t t = 0; t < S.fronts.size(); ++t)
       if (S.fronts[t].parent >= 0) kids[S.fronts[t].parent].push_back((int)t);
     std::vector<int4> tv;
-    std::vector<int32_t> gptr, gel;
+    std::vector<int32_t> g1, gxp(1, 0);
+    std::vector<int2> gx;
     s->tile_ptr.assign(1, 0);
     const int L = (int)S.level_ptr.size() - 1;
     for (int l = 0; l < L; ++l) {
@@ -341,28 +344,37 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
             }
           }
         }
-        // 8 x 8 super-tiles = 2 x 2 arrangement of 4 x 4 tiles (one per lane group);
-        // per super-tile 4 x 16 position lists + 1 end offset
-        static const std::vector<int32_t> none;
+        // 8 x 8 super-tiles = 2 x 2 arrangement of 4 x 4 tiles (one per lane group).
+        // Almost every position has at most one source (one child covers it): that
+        // one is stored densely (64 ids per super-tile, -1 = none) so the kernel
+        // issues all gather loads at once; the rare further sources go to a
+        // per-super-tile overflow list
         for (int i0 = 0; i0 < r; i0 += 8)
           for (int j0 = 0; j0 < r; j0 += 8) {
             tv.push_back(make_int4(t, i0, j0, 0));
             for (int sub = 0; sub < 4; ++sub) {
               const int ti = i0 / 4 + (sub >> 1), tj = j0 / 4 + (sub & 1);
               for (int pos = 0; pos < 16; ++pos) {
-                gptr.push_back((int32_t)gel.size());
+                int32_t first = -1;
                 if (ti < ntj && tj < ntj) {
                   const auto& Lp = lists[((size_t)ti * ntj + tj) * 16 + pos];
-                  gel.insert(gel.end(), Lp.begin(), Lp.end());
+                  for (size_t u = 0; u < Lp.size(); ++u)
+                    if (u == 0)
+                      first = Lp[0];
+                    else
+                      gx.push_back(make_int2(sub * 16 + pos, Lp[u]));
                 }
+                g1.push_back(first);
               }
             }
-            gptr.push_back((int32_t)gel.size());
+            gxp.push_back((int32_t)gx.size());
           }
       }
       s->tile_ptr.push_back((int32_t)tv.size());
     }
-    if ((rc = s->up(&s->d_tiles, tv)) || (rc = s->up(&s->d_gptr, gptr)) || (rc = s->up(&s->d_gel, gel)))
+    if (gx.empty()) gx.push_back(make_int2(0, 0));   // keep the buffer non-null
+    if ((rc = s->up(&s->d_tiles, tv)) || (rc = s->up(&s->d_g1, g1)) || (rc = s->up(&s->d_gxp, gxp)) ||
+        (rc = s->up(&s->d_gx, gx)))
       return bail(rc);
     std::vector<int32_t> rv;
     s->row_ptr.assign(1, 0);

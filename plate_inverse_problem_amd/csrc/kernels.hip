@@ -46,6 +46,15 @@ constexpr int KB = 4;    // factorisation pivot block
 constexpr int KBS = 16;  // triangular-solve block
 
 // ------------------------------------------------------------------ helpers
+// XCD-aware workgroup order: the dispatcher deals workgroups round-robin over
+// the 8 XCDs (each with its own L2), so workgroup `orig` is renumbered such that
+// every XCD receives one contiguous range of logical ids (bijective for any
+// count; MI355X_MICROARCH.md, workgroup dispatch / T1 swizzle).  Speed only.
+__device__ __forceinline__ int64_t xcd_swizzle(int64_t orig, int64_t nwg) {
+  const int64_t q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
 struct Ctx {
   int lane, w, W;
   int64_t q;
@@ -321,13 +330,17 @@ constexpr int TM = 4, TN = 4;
 // 2 x 2 arrangement of 4 x 4 tiles (an 8 x 8 super-tile), so each L21 row and
 // U12 column value a wave-instruction reads serves two sub-tiles.
 __global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* __restrict__ tiles, int ntiles,
-                                                      const int* __restrict__ gptr, const int* __restrict__ gel,
-                                                      cplx* __restrict__ F, int64_t Fc) {
+                                                      const int* __restrict__ g1, const int* __restrict__ gxp,
+                                                      const int2* __restrict__ gx, cplx* __restrict__ F, int64_t Fc) {
   const int lane = threadIdx.x & 63;
-  const int tid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  // all super-tiles of one (front, 16 frequencies) on one XCD: the L21 rows and
+  // U12 columns they share are fetched into that XCD's L2 once
+  const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
+  const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
+  const int tid = bx * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (tid >= ntiles) return;
   const int sub = lane >> 4;
-  const int64_t q = (int64_t)blockIdx.y * 16 + (lane & 15);
+  const int64_t q = (int64_t)by * 16 + (lane & 15);
   int4 t = tiles[tid];
   t.y += 4 * (sub >> 1);
   t.z += 4 * (sub & 1);
@@ -339,18 +352,43 @@ __global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* _
   for (int m = 0; m < TM; ++m) ri[m] = min(ns + t.y + m, f - 1);
 #pragma unroll
   for (int n = 0; n < TN; ++n) cj[n] = min(ns + t.z + n, f - 1);
-  // children's update-matrix entries landing in this tile (extend-add as a gather)
-  const int* __restrict__ gp = gptr + (int64_t)tid * (4 * TM * TN + 1) + sub * TM * TN;
+  // children's update-matrix entries landing in this tile (extend-add as a
+  // gather): 16 source ids per lane group in 4 vector loads, then all 16 value
+  // loads in flight at once (a missing source reads entry 0 and is dropped)
   cplx acc[TM][TN];
+  {
+    const int4* __restrict__ g4 = reinterpret_cast<const int4*>(g1 + (int64_t)tid * 64 + sub * 16);
+    int src[TM * TN];
 #pragma unroll
-  for (int m = 0; m < TM; ++m)
-#pragma unroll
-    for (int n = 0; n < TN; ++n) {
-      cplx s = make_double2(0.0, 0.0);
-      const int e1 = gp[m * TN + n + 1];
-      for (int e = gp[m * TN + n]; e < e1; ++e) s = cadd(s, F[(int64_t)gel[e] * Fc + q]);
-      acc[m][n] = s;
+    for (int u = 0; u < 4; ++u) {
+      const int4 v = g4[u];
+      src[4 * u] = v.x;
+      src[4 * u + 1] = v.y;
+      src[4 * u + 2] = v.z;
+      src[4 * u + 3] = v.w;
     }
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int n = 0; n < TN; ++n) {
+        const int e = src[m * TN + n];
+        const cplx v = F[(int64_t)max(e, 0) * Fc + q];
+        acc[m][n] = e >= 0 ? v : make_double2(0.0, 0.0);
+      }
+    // rare further sources (two or more children covering one position)
+    const int x1 = gxp[tid + 1];
+    for (int x = gxp[tid]; x < x1; ++x) {
+      const int2 g = gx[x];
+      if ((g.x >> 4) == sub) {
+        const cplx v = F[(int64_t)g.y * Fc + q];
+#pragma unroll
+        for (int m = 0; m < TM; ++m)
+#pragma unroll
+          for (int n = 0; n < TN; ++n)
+            if ((g.x & 15) == m * TN + n) acc[m][n] = cadd(acc[m][n], v);
+      }
+    }
+  }
   for (int k = 0; k < ns; ++k) {
     cplx a[TM], b[TN];
 #pragma unroll
@@ -775,10 +813,10 @@ void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPac
   LAUNCH(k_combine, dim3((unsigned)((nnz + 255) / 256)), dim3(256), st, stiff, n_stiff, nnz, coef, K);
 }
 
-void launch_schur(const DevPattern& P, const int4* tiles, int ntiles, const int* gptr, const int* gel, int ngroups,
-                  double2* F, int64_t Fc, hipStream_t st) {
+void launch_schur(const DevPattern& P, const int4* tiles, int ntiles, const int* g1, const int* gxp, const int2* gx,
+                  int ngroups, double2* F, int64_t Fc, hipStream_t st) {
   if (ntiles <= 0) return;
-  LAUNCH(k_schur_level, dim3((ntiles + 3) / 4, ngroups * 4), dim3(256), st, P, tiles, ntiles, gptr, gel, F, Fc);
+  LAUNCH(k_schur_level, dim3((ntiles + 3) / 4, ngroups * 4), dim3(256), st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
 }
 
 void launch_assemble(int mode, const DevPattern& P, const int* rows, int nrows, int ngroups, double2* F, int64_t Fc,
