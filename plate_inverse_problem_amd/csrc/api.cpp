@@ -58,6 +58,8 @@ struct pfr_solver {
   std::vector<void*> owned;
   int32_t* d_level_fronts = nullptr;
   int4* d_tiles = nullptr;              // Schur tiles (front, i0, j0, 0), grouped by level
+  int4* d_items = nullptr;              // off-diagonal panel items (front, first row/col, kind, 0), by level
+  std::vector<int32_t> item_ptr;
   int32_t* d_g1 = nullptr;              // per super-tile, lane group, position: first child source (or -1)
   int32_t* d_gxp = nullptr;             // per super-tile: range of further sources in d_gx
   int2* d_gx = nullptr;                 // (lane group * 16 + position, element id) of the rare extra sources
@@ -151,6 +153,8 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     const int64_t wgs = (int64_t)nf * ngroups * 4;
     const int Wp = (int)std::max<int64_t>(1, std::min<int64_t>(s->level_W[l], (4096 + wgs - 1) / wgs));
     pfr::launch_factor(s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st);
+    pfr::launch_offdiag(s->P, s->d_items + s->item_ptr[l], s->item_ptr[l + 1] - s->item_ptr[l], ngroups, s->F, s->Fc,
+                        st);
     pfr::launch_schur(s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l],
                       s->d_g1 + (int64_t)s->tile_ptr[l] * 64, s->d_gxp + s->tile_ptr[l], s->d_gx, ngroups, s->F,
                       s->Fc, st);
@@ -318,7 +322,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     std::vector<std::vector<int>> kids(S.fronts.size());
     for (size_t t = 0; t < S.fronts.size(); ++t)
       if (S.fronts[t].parent >= 0) kids[S.fronts[t].parent].push_back((int)t);
-    std::vector<int4> tv;
+    std::vector<int4> tv, iv;
+    s->item_ptr.assign(1, 0);
     std::vector<int32_t> g1, gxp(1, 0);
     std::vector<int2> gx;
     s->tile_ptr.assign(1, 0);
@@ -329,6 +334,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
         const Front& F = S.fronts[t];
         const int r = F.f - F.ns;
         const int ntj = (r + 3) / 4;          // 4 x 4 tiles per dimension
+        for (int i0 = F.ns; i0 < F.f; i0 += 4) iv.push_back(make_int4(t, i0, 0, 0));   // L21 rows
+        for (int j0 = F.ns; j0 < F.f; j0 += 4) iv.push_back(make_int4(t, j0, 1, 0));   // U12 columns
         std::vector<std::vector<int32_t>> lists((size_t)ntj * ntj * 16);
         for (int c : kids[t]) {
           const Front& C = S.fronts[c];
@@ -371,8 +378,11 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
           }
       }
       s->tile_ptr.push_back((int32_t)tv.size());
+      s->item_ptr.push_back((int32_t)iv.size());
     }
-    if (gx.empty()) gx.push_back(make_int2(0, 0));   // keep the buffer non-null
+    if (gx.empty()) gx.push_back(make_int2(0, 0));   // keep the buffers non-null
+    if (iv.empty()) iv.push_back(make_int4(0, 0, 0, 0));
+    if ((rc = s->up(&s->d_items, iv))) return bail(rc);
     if ((rc = s->up(&s->d_tiles, tv)) || (rc = s->up(&s->d_g1, g1)) || (rc = s->up(&s->d_gxp, gxp)) ||
         (rc = s->up(&s->d_gx, gx)))
       return bail(rc);

@@ -227,6 +227,9 @@ __device__ __forceinline__ void col_solve(const cplx* __restrict__ rd, cplx* __r
 // (lane = 16 * sub + frequency), so every wave-instruction advances four rows
 // (or four columns) at once and the pivot-row values it reads are shared by
 // the four row groups; workgroup = (front, 16 frequencies), W waves.
+// DIAG = true: only the diagonal block A11 = L11 U11 (rows and columns < ns);
+// L21 and U12 are then formed row / column-wise by k_offdiag_level.
+template <bool DIAG>
 __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* __restrict__ lvl,
                                                        cplx* __restrict__ F, int64_t Fc,
                                                        int* __restrict__ flags) {
@@ -238,6 +241,7 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
   const int sub = c.lane >> 4;
   const Front fr = P.fronts[lvl[blockIdx.x]];
   const int f = fr.f, ns = fr.ns;
+  const int lim = DIAG ? ns : f;     // rows / pivot-row columns handled here
   cplx* __restrict__ base = F + fr.off * Fc + c.q;
 #define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
   // 2. blocked restricted right-looking elimination of the ns pivots
@@ -281,7 +285,7 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
 #pragma unroll
         for (int j = 0; j < KB; ++j)
           if (j < i && i < kb) L[i][j] = E(k0 + i, k0 + j);
-      col_solve(base, base, (int64_t)k0 * f, f, Fc, k1 + 4 * c.w + sub, f, 4 * c.W, kb, L);
+      col_solve(base, base, (int64_t)k0 * f, f, Fc, k1 + 4 * c.w + sub, lim, 4 * c.W, kb, L);
     }
     __syncthreads();
     // rows >= k1: l = A(i, block) U11^{-1}; then update
@@ -297,7 +301,7 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
 #pragma unroll
       for (int i = 0; i < KB; ++i)
         if (i < kb) Dinv[i] = crecip(E(k0 + i, k0 + i));
-      for (int i = k1 + 4 * c.w + sub; i < f; i += 4 * c.W) {
+      for (int i = k1 + 4 * c.w + sub; i < lim; i += 4 * c.W) {
         cplx l[KB];
 #pragma unroll
         for (int t = 0; t < KB; ++t)
@@ -311,13 +315,81 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
             l[t] = cmul(l[t], Dinv[t]);
             E(i, k0 + t) = l[t];
           }
-        const int jend = i < ns ? f : ns;
+        const int jend = i < ns ? lim : ns;
         row_update(base, base, (int64_t)i * f, (int64_t)k0 * f, f, Fc, k1, jend, kb, l);
       }
     }
     __syncthreads();
   }
 #undef E
+}
+
+// Off-diagonal panel blocks once A11 = L11 U11 is factored, every row of L21 and
+// every column of U12 independently (read once, written once):
+//   kind 0, row i >= ns:     L(i, :ns) = A(i, :ns) U11^{-1}
+//   kind 1, column j >= ns:  U(:ns, j) = L11^{-1} A(:ns, j)
+// left-looking in chunks of OB columns (rows) held in registers; the L11 / U11
+// entries each step reads are the same for the four lane groups of a wave.
+// Item = (front, first row / column, kind): one wave = 16 frequencies x 4
+// consecutive rows (columns).
+constexpr int OB = 8;
+__global__ __launch_bounds__(256) void k_offdiag_level(DevPattern P, const int4* __restrict__ items, int nitems,
+                                                        cplx* __restrict__ F, int64_t Fc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
+  const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
+  const int wid = bx * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wid >= nitems) return;
+  const int sub = lane >> 4;
+  const int64_t q = (int64_t)by * 16 + (lane & 15);
+  const int4 it = items[wid];
+  const Front fr = P.fronts[it.x];
+  const int f = fr.f, ns = fr.ns;
+  const int idx = it.y + sub;
+  const bool valid = idx < f;
+  const int r = min(idx, f - 1);
+  cplx* __restrict__ base = F + fr.off * Fc + q;
+  // kind 0: own(c) = E(r, c), shared(a, b) = U(a, b) = E(a, b)
+  // kind 1: own(c) = E(c, r), shared(a, b) = L(b, a) = E(b, a)   (transposed roles)
+  const int64_t so = it.z == 0 ? (int64_t)r * f : r;           // own element c at so + c * sc
+  const int64_t sc = it.z == 0 ? 1 : f;
+  const int64_t sa = it.z == 0 ? f : 1, sb = it.z == 0 ? 1 : f;  // shared (a, b) at a * sa + b * sb
+  const bool unit = it.z != 0;                                   // L11 has a unit diagonal
+  for (int c0 = 0; c0 < ns; c0 += OB) {
+    const int nb = min(OB, ns - c0);
+    cplx x[OB];
+#pragma unroll
+    for (int j = 0; j < OB; ++j) x[j] = base[(so + (int64_t)(c0 + min(j, nb - 1)) * sc) * Fc];
+    // x -= own(0:c0) * shared(0:c0, c0:c0+nb)
+#pragma unroll 2
+    for (int t = 0; t < c0; ++t) {
+      const cplx l = base[(so + (int64_t)t * sc) * Fc];
+      cplx u[OB];
+#pragma unroll
+      for (int j = 0; j < OB; ++j) u[j] = base[((int64_t)t * sa + (int64_t)(c0 + min(j, nb - 1)) * sb) * Fc];
+#pragma unroll
+      for (int j = 0; j < OB; ++j) x[j] = cfms(x[j], l, u[j]);
+    }
+    // triangular block shared(c0:c0+nb, c0:c0+nb)
+    cplx T[OB][OB];
+#pragma unroll
+    for (int a = 0; a < OB; ++a)
+#pragma unroll
+      for (int b = 0; b < OB; ++b)
+        if (a <= b) T[a][b] = base[((int64_t)(c0 + min(a, nb - 1)) * sa + (int64_t)(c0 + min(b, nb - 1)) * sb) * Fc];
+#pragma unroll
+    for (int j = 0; j < OB; ++j) {
+#pragma unroll
+      for (int a = 0; a < OB; ++a)
+        if (a < j) x[j] = cfms(x[j], x[a], T[a][j]);
+      if (!unit) x[j] = cmul(x[j], crecip(T[j][j]));
+    }
+    if (valid) {
+#pragma unroll
+      for (int j = 0; j < OB; ++j)
+        if (j < nb) base[(so + (int64_t)(c0 + j) * sc) * Fc] = x[j];
+    }
+  }
 }
 
 // ------------------------------------------------------------------ K2b: Schur complement
@@ -829,7 +901,13 @@ void launch_assemble(int mode, const DevPattern& P, const int* rows, int nrows, 
 
 void launch_factor(const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F, int64_t Fc,
                    int* flags, hipStream_t st) {
-  LAUNCH(k_factor_level, dim3(nfronts, ngroups * 4), dim3(64 * W), st, P, lvl, F, Fc, flags);
+  LAUNCH(k_factor_level<true>, dim3(nfronts, ngroups * 4), dim3(64 * W), st, P, lvl, F, Fc, flags);
+}
+
+void launch_offdiag(const DevPattern& P, const int4* items, int nitems, int ngroups, double2* F, int64_t Fc,
+                    hipStream_t st) {
+  if (nitems <= 0) return;
+  LAUNCH(k_offdiag_level, dim3((nitems + 3) / 4, ngroups * 4), dim3(256), st, P, items, nitems, F, Fc);
 }
 
 static RhsArgs make_rhs(const RhsDesc& d) {
