@@ -64,8 +64,10 @@ struct pfr_solver {
   int32_t* d_gxp = nullptr;             // per super-tile: range of further sources in d_gx
   int2* d_gx = nullptr;                 // (lane group * 16 + position, element id) of the rare extra sources
   std::vector<int32_t> tile_ptr;
-  int32_t* d_level_rows = nullptr;      // front rows of each level (assembly work list)
-  std::vector<int32_t> row_ptr;
+  int4* d_asm = nullptr;                // panel-entry assembly records (dst, nz, first child source, 0), by level
+  int32_t* d_asm_xp = nullptr;          // per 8-record chunk: range of further child sources in d_asm_x
+  int2* d_asm_x = nullptr;              // (record within chunk, child element id)
+  std::vector<int32_t> asm_ptr;         // record offset of each level (multiple of 8)
   int32_t* d_colptr = nullptr;
   int32_t* d_rowind = nullptr;
   double2 *F = nullptr, *WV = nullptr, *X = nullptr, *Y = nullptr, *XA = nullptr, *G = nullptr;
@@ -146,8 +148,9 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
   const int ngroups = (int)(s->Fc / 64);
   for (int l = 0; l < L; ++l) {
     int nf = s->level_ptr[l + 1] - s->level_ptr[l];
-    pfr::launch_assemble(mode, s->P, s->d_level_rows + s->row_ptr[l], s->row_ptr[l + 1] - s->row_ptr[l], ngroups,
-                         s->F, s->Fc, s->freqs, s->K, s->M, data, ds, nvalid, st);
+    pfr::launch_assemble(mode, s->d_asm + s->asm_ptr[l], s->asm_ptr[l + 1] - s->asm_ptr[l],
+                         s->d_asm_xp + s->asm_ptr[l] / 8, s->d_asm_x, ngroups, s->F, s->Fc, s->freqs, s->K, s->M,
+                         data, ds, nvalid, st);
     // panel: enough workgroups (front x 16 frequencies) to fill the chip -> one wave
     // each (no idle waves at the block barriers); few large fronts -> more waves
     const int64_t wgs = (int64_t)nf * ngroups * 4;
@@ -386,16 +389,59 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     if ((rc = s->up(&s->d_tiles, tv)) || (rc = s->up(&s->d_g1, g1)) || (rc = s->up(&s->d_gxp, gxp)) ||
         (rc = s->up(&s->d_gx, gx)))
       return bail(rc);
-    std::vector<int32_t> rv;
-    s->row_ptr.assign(1, 0);
+    // assembly of the panel region (pivot rows: all columns; update rows: pivot
+    // columns) as a gather: one record per entry = original matrix entry (or -1)
+    // + the first child update-matrix entry landing there (or -1); rare further
+    // child sources in a per-chunk overflow list.  Levels padded to 8 records.
+    std::vector<int4> av;
+    std::vector<int32_t> axp(1, 0);
+    std::vector<int2> ax;
+    s->asm_ptr.assign(1, 0);
+    std::vector<int32_t> nzpos, src1;
+    std::vector<std::vector<int32_t>> more;
     for (int l = 0; l < L; ++l) {
       for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
         const Front& F = S.fronts[S.level_fronts[e]];
-        for (int a = 0; a < F.f; ++a) rv.push_back(F.row0 + a);
+        for (int a = 0; a < F.f; ++a) {
+          const int r = F.row0 + a;
+          const int width = a < F.ns ? F.f : F.ns;
+          nzpos.assign(width, -1);
+          src1.assign(width, -1);
+          more.assign(width, {});
+          for (int x = S.asm_ptr[r]; x < S.asm_ptr[r + 1]; ++x)
+            if (S.asm_col[x] < width) nzpos[S.asm_col[x]] = S.asm_nz[x];
+          for (int x = S.ea_ptr[r]; x < S.ea_ptr[r + 1]; ++x) {
+            const int src = S.ea_src[x];
+            const Front& C = S.fronts[S.row_front[src]];
+            const int32_t* rp = S.relpos.data() + C.row0;
+            for (int b = C.ns; b < C.f; ++b) {
+              const int pb = rp[b];
+              if (pb >= width) continue;
+              const int32_t id = (int32_t)(C.off + (int64_t)(src - C.row0) * C.f + b);
+              if (src1[pb] < 0)
+                src1[pb] = id;
+              else
+                more[pb].push_back(id);
+            }
+          }
+          for (int b = 0; b < width; ++b) {
+            const int k = (int)(av.size() % 8);
+            av.push_back(make_int4((int32_t)(F.off + (int64_t)a * F.f + b), nzpos[b], src1[b], 0));
+            for (int32_t id : more[b]) ax.push_back(make_int2(k, id));
+            if (av.size() % 8 == 0) axp.push_back((int32_t)ax.size());
+          }
+        }
       }
-      s->row_ptr.push_back((int32_t)rv.size());
+      while (av.size() % 8) {        // pad: no-op records (dst = -1)
+        av.push_back(make_int4(-1, -1, -1, 0));
+        if (av.size() % 8 == 0) axp.push_back((int32_t)ax.size());
+      }
+      s->asm_ptr.push_back((int32_t)av.size());
     }
-    if ((rc = s->up(&s->d_level_rows, rv))) return bail(rc);
+    if (av.empty()) av.assign(8, make_int4(-1, -1, -1, 0));
+    if (ax.empty()) ax.push_back(make_int2(0, 0));
+    if ((rc = s->up(&s->d_asm, av)) || (rc = s->up(&s->d_asm_xp, axp)) || (rc = s->up(&s->d_asm_x, ax)))
+      return bail(rc);
   }
   std::vector<int32_t> cp(colptr, colptr + S.n + 1), ri(rowind, rowind + S.nnz);
   if ((rc = s->up(&s->d_colptr, cp)) || (rc = s->up(&s->d_rowind, ri))) return bail(rc);

@@ -93,78 +93,59 @@ __global__ void k_combine(const double* __restrict__ stiff, int n_stiff, int64_t
 // columns) is left for k_schur_level (a register-tiled GEMM over all pivots).
 constexpr int JB = 4;     // columns per batched read-modify-write step
 
-// Assembly of a level's fronts: one wavefront per front row (64 frequencies).
-// Zero + original entries are stores only (distinct columns per row, program
-// order = last store wins); children's update rows are read-modify-write in
-// batches of 8 independent columns.
+// Assembly of a level's panel regions as a gather: a wavefront = 64 frequencies
+// x 8 consecutive records (dst, nz, src, -); every record is one store of
+// original entry (K - omega^2 M, or the explicit batch) + the first child
+// update-matrix entry landing there; the rare further child entries of the
+// chunk come from the overflow list.  All loads of a chunk are in flight
+// together; each panel entry is written exactly once.
 template <int MODE>
-__global__ __launch_bounds__(256) void k_assemble_level(DevPattern P, const int* __restrict__ rows, int nrows,
+__global__ __launch_bounds__(256) void k_assemble_level(const int4* __restrict__ recs, int nrec,
+                                                         const int* __restrict__ xptr, const int2* __restrict__ xl,
                                                          cplx* __restrict__ F, int64_t Fc,
                                                          const double* __restrict__ freqs,
                                                          const cplx* __restrict__ K, const double* __restrict__ M,
                                                          const cplx* __restrict__ data, int64_t data_stride,
                                                          int nvalid) {
   const int lane = threadIdx.x & 63;
-  const int wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (wid >= nrows) return;
+  const int chunk = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  if (chunk * 8 >= nrec) return;
   const int64_t q = (int64_t)blockIdx.y * 64 + lane;
-  const int r = rows[wid];
-  const Front fr = P.fronts[P.row_front[r]];
-  const int f = fr.f;
-  const int a = r - fr.row0;
-  cplx* __restrict__ row = F + (fr.off + (int64_t)a * f) * Fc + q;
   double om2 = 0.0;
   if (MODE == 0) {
     const double om = 6.283185307179586 * freqs[q];
     om2 = om * om;
   }
-  // Only the panel region is assembled here: pivot rows (all columns) and the
-  // pivot columns of update rows.  The Schur block (update rows x update
-  // columns) holds no original entries; k_schur_level forms it in one store
-  // from the children's contributions and -L21 U12.
-  const int ns = fr.ns;
-  const int width = a < ns ? f : ns;
-  for (int b = 0; b < width; ++b) row[(int64_t)b * Fc] = make_double2(0.0, 0.0);
-  const int e1 = P.asm_ptr[r + 1];
-  for (int e = P.asm_ptr[r]; e < e1; ++e) {
-    const int nz = P.asm_nz[e];
-    cplx v;
-    if (MODE == 0) {
-      const cplx k = K[nz];
-      v = make_double2(fma(-om2, M[nz], k.x), k.y);
-    } else {
-      v = data[min(q, (int64_t)nvalid - 1) * data_stride + nz];
-    }
-    row[(int64_t)P.asm_col[e] * Fc] = v;
-  }
-  const int x1 = P.ea_ptr[r + 1];
-  for (int e = P.ea_ptr[r]; e < x1; ++e) {
-    const int src = P.ea_src[e];
-    const Front cf = P.fronts[P.row_front[src]];
-    const cplx* __restrict__ cb = F + (cf.off + (int64_t)(src - cf.row0) * cf.f) * Fc + q;
-    const int* __restrict__ rp = P.relpos + cf.row0;
-    // child columns map to increasing parent positions: for an update row only
-    // the prefix landing in the pivot columns belongs to the panel region
-    int bend = cf.f;
-    if (a >= ns)
-      for (bend = cf.ns; bend < cf.f && rp[bend] < ns; ++bend) {
+  const cplx* __restrict__ dq = data + min(q, (int64_t)nvalid - 1) * data_stride;
+  int4 r[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) r[k] = recs[chunk * 8 + k];
+  cplx v[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    cplx o = make_double2(0.0, 0.0), c = make_double2(0.0, 0.0);
+    if (r[k].y >= 0) {
+      if (MODE == 0) {
+        const cplx kk = K[r[k].y];
+        o = make_double2(fma(-om2, M[r[k].y], kk.x), kk.y);
+      } else {
+        o = dq[r[k].y];
       }
-    for (int b0 = cf.ns; b0 < bend; b0 += 8) {
-      cplx v[8], o[8];
-      int pb[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int b = min(b0 + u, bend - 1);
-        pb[u] = rp[b];
-        v[u] = cb[(int64_t)b * Fc];
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) o[u] = row[(int64_t)pb[u] * Fc];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (b0 + u < bend) row[(int64_t)pb[u] * Fc] = cadd(o[u], v[u]);
     }
+    if (r[k].z >= 0) c = F[(int64_t)r[k].z * Fc + q];
+    v[k] = cadd(o, c);
   }
+  const int x1 = xptr[chunk + 1];
+  for (int x = xptr[chunk]; x < x1; ++x) {
+    const int2 g = xl[x];
+    const cplx c = F[(int64_t)g.y * Fc + q];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (g.x == k) v[k] = cadd(v[k], c);
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    if (r[k].x >= 0) F[(int64_t)r[k].x * Fc + q] = v[k];
 }
 
 // One row of a rank-kb update, A(i, j) -= sum_t l_t U(k0 + t, j) for j in [j0, jend).
@@ -891,12 +872,13 @@ void launch_schur(const DevPattern& P, const int4* tiles, int ntiles, const int*
   LAUNCH(k_schur_level, dim3((ntiles + 3) / 4, ngroups * 4), dim3(256), st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
 }
 
-void launch_assemble(int mode, const DevPattern& P, const int* rows, int nrows, int ngroups, double2* F, int64_t Fc,
-                     const double* freqs, const double2* K, const double* M, const double2* data, int64_t ds,
-                     int nvalid, hipStream_t st) {
-  dim3 g((nrows + 3) / 4, ngroups), b(256);
-  if (mode == 0) LAUNCH(k_assemble_level<0>, g, b, st, P, rows, nrows, F, Fc, freqs, K, M, data, ds, nvalid);
-  else LAUNCH(k_assemble_level<1>, g, b, st, P, rows, nrows, F, Fc, freqs, K, M, data, ds, nvalid);
+void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, const int2* xl, int ngroups, double2* F,
+                     int64_t Fc, const double* freqs, const double2* K, const double* M, const double2* data,
+                     int64_t ds, int nvalid, hipStream_t st) {
+  if (nrec <= 0) return;
+  dim3 g((nrec / 8 + 3) / 4, ngroups), b(256);
+  if (mode == 0) LAUNCH(k_assemble_level<0>, g, b, st, recs, nrec, xptr, xl, F, Fc, freqs, K, M, data, ds, nvalid);
+  else LAUNCH(k_assemble_level<1>, g, b, st, recs, nrec, xptr, xl, F, Fc, freqs, K, M, data, ds, nvalid);
 }
 
 void launch_factor(const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F, int64_t Fc,

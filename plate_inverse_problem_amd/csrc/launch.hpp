@@ -16,9 +16,9 @@ struct RhsDesc {
 };
 
 void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPack& coef, double2* K, hipStream_t st);
-void launch_assemble(int mode, const DevPattern& P, const int* rows, int nrows, int ngroups, double2* F, int64_t Fc,
-                     const double* freqs, const double2* K, const double* M, const double2* data, int64_t ds,
-                     int nvalid, hipStream_t st);
+void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, const int2* xl, int ngroups, double2* F,
+                     int64_t Fc, const double* freqs, const double2* K, const double* M, const double2* data,
+                     int64_t ds, int nvalid, hipStream_t st);
 void launch_factor(const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F, int64_t Fc,
                    int* flags, hipStream_t st);
 // Schur complement A22 -= L21 U12 for a level's tile list (TM x TN = 4 x 4 tiles)
