@@ -62,7 +62,7 @@ struct Ctx {
 __device__ __forceinline__ Ctx ctx() {
   Ctx c;
   c.lane = threadIdx.x & 63;
-  c.w = threadIdx.x >> 6;
+  c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   c.W = blockDim.x >> 6;
   c.q = (int64_t)blockIdx.y * 64 + c.lane;
   return c;
@@ -216,7 +216,7 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
                                                        int* __restrict__ flags) {
   Ctx c;
   c.lane = threadIdx.x & 63;
-  c.w = threadIdx.x >> 6;
+  c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   c.W = blockDim.x >> 6;
   c.q = (int64_t)blockIdx.y * 16 + (c.lane & 15);
   const int sub = c.lane >> 4;
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(256) void k_offdiag_level(DevPattern P, const int4*
   const int lane = threadIdx.x & 63;
   const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
   const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
-  const int wid = bx * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int wid = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (wid >= nitems) return;
   const int sub = lane >> 4;
   const int64_t q = (int64_t)by * 16 + (lane & 15);
@@ -390,7 +390,7 @@ __global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* _
   // U12 columns they share are fetched into that XCD's L2 once
   const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
   const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
-  const int tid = bx * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int tid = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (tid >= ntiles) return;
   const int sub = lane >> 4;
   const int64_t q = (int64_t)by * 16 + (lane & 15);
