@@ -314,6 +314,48 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
 // Item = (front, first row / column, kind): one wave = 16 frequencies x 4
 // consecutive rows (columns).
 constexpr int OB = 8;
+
+// One chunk of NB consecutive columns (kind 0) / rows (kind 1) c0 .. c0+NB-1.
+template <int NB>
+__device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, int64_t so, int64_t sc, int64_t sa, int64_t sb,
+                                              bool unit, bool valid, int c0, int64_t Fc) {
+  cplx x[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) x[j] = base[(so + (int64_t)(c0 + j) * sc) * Fc];
+  // x -= own(0:c0) * shared(0:c0, c0:c0+NB)
+#pragma unroll 2
+  for (int t = 0; t < c0; ++t) {
+    const cplx l = base[(so + (int64_t)t * sc) * Fc];
+    cplx u[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) u[j] = base[((int64_t)t * sa + (int64_t)(c0 + j) * sb) * Fc];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) x[j] = cfms(x[j], l, u[j]);
+  }
+  // triangular block shared(c0:c0+NB, c0:c0+NB)
+  cplx T[NB][NB];
+#pragma unroll
+  for (int a = 0; a < NB; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+      if (a < b) T[a][b] = base[((int64_t)(c0 + a) * sa + (int64_t)(c0 + b) * sb) * Fc];
+  if (!unit) {
+#pragma unroll
+    for (int a = 0; a < NB; ++a) T[a][a] = crecip(base[((int64_t)(c0 + a) * (sa + sb)) * Fc]);
+  }
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+#pragma unroll
+    for (int a = 0; a < NB; ++a)
+      if (a < j) x[j] = cfms(x[j], x[a], T[a][j]);
+    if (!unit) x[j] = cmul(x[j], T[j][j]);
+  }
+  if (valid) {
+#pragma unroll
+    for (int j = 0; j < NB; ++j) base[(so + (int64_t)(c0 + j) * sc) * Fc] = x[j];
+  }
+}
+
 __global__ __launch_bounds__(256) void k_offdiag_level(DevPattern P, const int4* __restrict__ items, int nitems,
                                                         cplx* __restrict__ F, int64_t Fc) {
   const int lane = threadIdx.x & 63;
@@ -336,40 +378,17 @@ __global__ __launch_bounds__(256) void k_offdiag_level(DevPattern P, const int4*
   const int64_t sc = it.z == 0 ? 1 : f;
   const int64_t sa = it.z == 0 ? f : 1, sb = it.z == 0 ? 1 : f;  // shared (a, b) at a * sa + b * sb
   const bool unit = it.z != 0;                                   // L11 has a unit diagonal
-  for (int c0 = 0; c0 < ns; c0 += OB) {
-    const int nb = min(OB, ns - c0);
-    cplx x[OB];
-#pragma unroll
-    for (int j = 0; j < OB; ++j) x[j] = base[(so + (int64_t)(c0 + min(j, nb - 1)) * sc) * Fc];
-    // x -= own(0:c0) * shared(0:c0, c0:c0+nb)
-#pragma unroll 2
-    for (int t = 0; t < c0; ++t) {
-      const cplx l = base[(so + (int64_t)t * sc) * Fc];
-      cplx u[OB];
-#pragma unroll
-      for (int j = 0; j < OB; ++j) u[j] = base[((int64_t)t * sa + (int64_t)(c0 + min(j, nb - 1)) * sb) * Fc];
-#pragma unroll
-      for (int j = 0; j < OB; ++j) x[j] = cfms(x[j], l, u[j]);
-    }
-    // triangular block shared(c0:c0+nb, c0:c0+nb)
-    cplx T[OB][OB];
-#pragma unroll
-    for (int a = 0; a < OB; ++a)
-#pragma unroll
-      for (int b = 0; b < OB; ++b)
-        if (a <= b) T[a][b] = base[((int64_t)(c0 + min(a, nb - 1)) * sa + (int64_t)(c0 + min(b, nb - 1)) * sb) * Fc];
-#pragma unroll
-    for (int j = 0; j < OB; ++j) {
-#pragma unroll
-      for (int a = 0; a < OB; ++a)
-        if (a < j) x[j] = cfms(x[j], x[a], T[a][j]);
-      if (!unit) x[j] = cmul(x[j], crecip(T[j][j]));
-    }
-    if (valid) {
-#pragma unroll
-      for (int j = 0; j < OB; ++j)
-        if (j < nb) base[(so + (int64_t)(c0 + j) * sc) * Fc] = x[j];
-    }
+  int c0 = 0;
+  for (; c0 + OB <= ns; c0 += OB) offdiag_chunk<OB>(base, so, sc, sa, sb, unit, valid, c0, Fc);
+  switch (ns - c0) {     // wave-uniform tail width
+    case 1: offdiag_chunk<1>(base, so, sc, sa, sb, unit, valid, c0, Fc); break;
+    case 2: offdiag_chunk<2>(base, so, sc, sa, sb, unit, valid, c0, Fc); break;
+    case 3: offdiag_chunk<3>(base, so, sc, sa, sb, unit, valid, c0, Fc); break;
+    case 4: offdiag_chunk<4>(base, so, sc, sa, sb, unit, valid, c0, Fc); break;
+    case 5: offdiag_chunk<5>(base, so, sc, sa, sb, unit, valid, c0, Fc); break;
+    case 6: offdiag_chunk<6>(base, so, sc, sa, sb, unit, valid, c0, Fc); break;
+    case 7: offdiag_chunk<7>(base, so, sc, sa, sb, unit, valid, c0, Fc); break;
+    default: break;
   }
 }
 
