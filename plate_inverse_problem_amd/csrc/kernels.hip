@@ -561,6 +561,29 @@ __global__ void k_lsolve_level(DevPattern P, const int* __restrict__ lvl, const 
 #undef V
 }
 
+// v - sum_{b in [ns, f)} e[b * es] * X[ix[b]]: the update-row solution values are
+// gathered 8 at a time (one scalar index load, then 16 independent vector loads)
+__device__ __forceinline__ cplx offdiag_dot(cplx v, const cplx* __restrict__ e, int64_t es,
+                                            const cplx* __restrict__ X, const int* __restrict__ ix, int ns, int f,
+                                            int64_t Fc, int64_t q) {
+  int b = ns;
+  for (; b + 8 <= f; b += 8) {
+    int iv[8];
+    cplx ev[8], xv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) iv[u] = ix[b + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      ev[u] = e[(int64_t)(b + u) * es];
+      xv[u] = X[(int64_t)iv[u] * Fc + q];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v = cfms(v, ev[u], xv[u]);
+  }
+  for (; b < f; ++b) v = cfms(v, e[(int64_t)b * es], X[(int64_t)ix[b] * Fc + q]);
+  return v;
+}
+
 // ------------------------------------------------------------------ K3b: U x = y (top-down)
 __global__ void k_usolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
                                cplx* __restrict__ WV, const cplx* __restrict__ Y, cplx* __restrict__ X) {
@@ -574,7 +597,7 @@ __global__ void k_usolve_level(DevPattern P, const int* __restrict__ lvl, const 
 #define V(a) wv[(int64_t)(a) * Fc]
   for (int a = c.w; a < ns; a += c.W) {
     cplx v = Y[(int64_t)(fr.col0 + a) * Fc + c.q];
-    for (int b = ns; b < f; ++b) v = cfms(v, E(a, b), X[(int64_t)ix[b] * Fc + c.q]);
+    v = offdiag_dot(v, &E(a, 0), Fc, X, ix, ns, f, Fc, c.q);
     V(a) = v;
   }
   __syncthreads();
@@ -658,7 +681,7 @@ __global__ void k_ltsolve_level(DevPattern P, const int* __restrict__ lvl, const
 #define V(a) wv[(int64_t)(a) * Fc]
   for (int a = c.w; a < ns; a += c.W) {
     cplx v = Y[(int64_t)(fr.col0 + a) * Fc + c.q];
-    for (int b = ns; b < f; ++b) v = cfms(v, E(b, a), X[(int64_t)ix[b] * Fc + c.q]);
+    v = offdiag_dot(v, &E(0, a), (int64_t)f * Fc, X, ix, ns, f, Fc, c.q);
     V(a) = v;
   }
   __syncthreads();
