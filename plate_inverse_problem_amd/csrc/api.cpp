@@ -58,7 +58,10 @@ struct pfr_solver {
   std::vector<void*> owned;
   int32_t* d_level_fronts = nullptr;
   int4* d_tiles = nullptr;              // Schur tiles (front, i0, j0, 0), grouped by level
-  int4* d_items = nullptr;              // off-diagonal panel items (front, first row/col, kind, 0), by level
+  int4* d_items = nullptr;              // off-diagonal panel items (front, first row/col, kind, record offset)
+  int2* d_orec = nullptr;               // per item x lane group x pivot: (nz, first child source) of the entry
+  int32_t* d_oxp = nullptr;             // per item: range of further child sources in d_ox
+  int2* d_ox = nullptr;                 // (pivot * 4 + lane group, element id)
   std::vector<int32_t> item_ptr;
   int32_t* d_g1 = nullptr;              // per super-tile, lane group, position: first child source (or -1)
   int32_t* d_gxp = nullptr;             // per super-tile: range of further sources in d_gx
@@ -156,8 +159,9 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     const int64_t wgs = (int64_t)nf * ngroups * 4;
     const int Wp = (int)std::max<int64_t>(1, std::min<int64_t>(s->level_W[l], (4096 + wgs - 1) / wgs));
     pfr::launch_factor(s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st);
-    pfr::launch_offdiag(s->P, s->d_items + s->item_ptr[l], s->item_ptr[l + 1] - s->item_ptr[l], ngroups, s->F, s->Fc,
-                        st);
+    pfr::launch_offdiag(mode, s->P, s->d_items + s->item_ptr[l], s->item_ptr[l + 1] - s->item_ptr[l], s->d_orec,
+                        s->d_oxp + s->item_ptr[l], s->d_ox, ngroups, s->F, s->Fc, s->freqs, s->K, s->M, data, ds,
+                        nvalid, st);
     pfr::launch_schur(s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l],
                       s->d_g1 + (int64_t)s->tile_ptr[l] * 64, s->d_gxp + s->tile_ptr[l], s->d_gx, ngroups, s->F,
                       s->Fc, st);
@@ -337,8 +341,6 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
         const Front& F = S.fronts[t];
         const int r = F.f - F.ns;
         const int ntj = (r + 3) / 4;          // 4 x 4 tiles per dimension
-        for (int i0 = F.ns; i0 < F.f; i0 += 4) iv.push_back(make_int4(t, i0, 0, 0));   // L21 rows
-        for (int j0 = F.ns; j0 < F.f; j0 += 4) iv.push_back(make_int4(t, j0, 1, 0));   // U12 columns
         std::vector<std::vector<int32_t>> lists((size_t)ntj * ntj * 16);
         for (int c : kids[t]) {
           const Front& C = S.fronts[c];
@@ -381,11 +383,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
           }
       }
       s->tile_ptr.push_back((int32_t)tv.size());
-      s->item_ptr.push_back((int32_t)iv.size());
     }
     if (gx.empty()) gx.push_back(make_int2(0, 0));   // keep the buffers non-null
-    if (iv.empty()) iv.push_back(make_int4(0, 0, 0, 0));
-    if ((rc = s->up(&s->d_items, iv))) return bail(rc);
     if ((rc = s->up(&s->d_tiles, tv)) || (rc = s->up(&s->d_g1, g1)) || (rc = s->up(&s->d_gxp, gxp)) ||
         (rc = s->up(&s->d_gx, gx)))
       return bail(rc);
@@ -393,23 +392,34 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     // columns) as a gather: one record per entry = original matrix entry (or -1)
     // + the first child update-matrix entry landing there (or -1); rare further
     // child sources in a per-chunk overflow list.  Levels padded to 8 records.
+    // Panel-region sources of every front, as a gather: per entry the original
+    // matrix entry (or -1) and the first child update-matrix entry landing there
+    // (or -1); rare further child entries in overflow lists.
+    //  * A11 (pivot rows x pivot columns): assembly records (dst, nz, src, -) in
+    //    chunks of 8 (k_assemble_level), levels padded to 8 records;
+    //  * L21 rows / U12 columns: gathered by k_offdiag_level itself when it loads
+    //    them (records (nz, src) per item x lane group x pivot, item.w = offset),
+    //    so those entries are never stored before their final value.
     std::vector<int4> av;
-    std::vector<int32_t> axp(1, 0);
-    std::vector<int2> ax;
+    std::vector<int32_t> axp(1, 0), oxp(1, 0);
+    std::vector<int2> ax, orec, ox;
     s->asm_ptr.assign(1, 0);
-    std::vector<int32_t> nzpos, src1;
-    std::vector<std::vector<int32_t>> more;
+    s->item_ptr.assign(1, 0);
+    std::vector<int32_t> nzm, s1m;
+    std::vector<std::pair<int32_t, int32_t>> morem;   // (a * f + b, id)
     for (int l = 0; l < L; ++l) {
       for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
-        const Front& F = S.fronts[S.level_fronts[e]];
-        for (int a = 0; a < F.f; ++a) {
+        const int t = S.level_fronts[e];
+        const Front& F = S.fronts[t];
+        const int f = F.f, ns = F.ns;
+        nzm.assign((size_t)f * f, -1);
+        s1m.assign((size_t)f * f, -1);
+        morem.clear();
+        for (int a = 0; a < f; ++a) {
           const int r = F.row0 + a;
-          const int width = a < F.ns ? F.f : F.ns;
-          nzpos.assign(width, -1);
-          src1.assign(width, -1);
-          more.assign(width, {});
+          const int width = a < ns ? f : ns;
           for (int x = S.asm_ptr[r]; x < S.asm_ptr[r + 1]; ++x)
-            if (S.asm_col[x] < width) nzpos[S.asm_col[x]] = S.asm_nz[x];
+            if (S.asm_col[x] < width) nzm[(size_t)a * f + S.asm_col[x]] = S.asm_nz[x];
           for (int x = S.ea_ptr[r]; x < S.ea_ptr[r + 1]; ++x) {
             const int src = S.ea_src[x];
             const Front& C = S.fronts[S.row_front[src]];
@@ -418,29 +428,61 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
               const int pb = rp[b];
               if (pb >= width) continue;
               const int32_t id = (int32_t)(C.off + (int64_t)(src - C.row0) * C.f + b);
-              if (src1[pb] < 0)
-                src1[pb] = id;
+              int32_t& s1 = s1m[(size_t)a * f + pb];
+              if (s1 < 0)
+                s1 = id;
               else
-                more[pb].push_back(id);
+                morem.emplace_back(a * f + pb, id);
             }
           }
-          for (int b = 0; b < width; ++b) {
+        }
+        std::sort(morem.begin(), morem.end());
+        auto extras = [&](int a, int b) {
+          auto lo = std::lower_bound(morem.begin(), morem.end(), std::make_pair(a * f + b, INT32_MIN));
+          std::vector<int32_t> out;
+          for (; lo != morem.end() && lo->first == a * f + b; ++lo) out.push_back(lo->second);
+          return out;
+        };
+        for (int a = 0; a < ns; ++a)
+          for (int b = 0; b < ns; ++b) {
             const int k = (int)(av.size() % 8);
-            av.push_back(make_int4((int32_t)(F.off + (int64_t)a * F.f + b), nzpos[b], src1[b], 0));
-            for (int32_t id : more[b]) ax.push_back(make_int2(k, id));
+            av.push_back(make_int4((int32_t)(F.off + (int64_t)a * f + b), nzm[(size_t)a * f + b],
+                                   s1m[(size_t)a * f + b], 0));
+            for (int32_t id : extras(a, b)) ax.push_back(make_int2(k, id));
             if (av.size() % 8 == 0) axp.push_back((int32_t)ax.size());
           }
-        }
+        for (int kind = 0; kind < 2; ++kind)
+          for (int i0 = ns; i0 < f; i0 += 4) {
+            iv.push_back(make_int4(t, i0, kind, (int32_t)orec.size()));
+            for (int sub = 0; sub < 4; ++sub)
+              for (int c = 0; c < ns; ++c) {
+                const int idx = i0 + sub;
+                if (idx >= f) {
+                  orec.push_back(make_int2(-1, -1));
+                  continue;
+                }
+                const int a = kind == 0 ? idx : c, b = kind == 0 ? c : idx;
+                orec.push_back(make_int2(nzm[(size_t)a * f + b], s1m[(size_t)a * f + b]));
+                for (int32_t id : extras(a, b)) ox.push_back(make_int2(c * 4 + sub, id));
+              }
+            oxp.push_back((int32_t)ox.size());
+          }
       }
       while (av.size() % 8) {        // pad: no-op records (dst = -1)
         av.push_back(make_int4(-1, -1, -1, 0));
         if (av.size() % 8 == 0) axp.push_back((int32_t)ax.size());
       }
       s->asm_ptr.push_back((int32_t)av.size());
+      s->item_ptr.push_back((int32_t)iv.size());
     }
     if (av.empty()) av.assign(8, make_int4(-1, -1, -1, 0));
     if (ax.empty()) ax.push_back(make_int2(0, 0));
-    if ((rc = s->up(&s->d_asm, av)) || (rc = s->up(&s->d_asm_xp, axp)) || (rc = s->up(&s->d_asm_x, ax)))
+    if (iv.empty()) iv.push_back(make_int4(0, 0, 0, 0));
+    if (orec.empty()) orec.push_back(make_int2(-1, -1));
+    if (ox.empty()) ox.push_back(make_int2(0, 0));
+    if ((rc = s->up(&s->d_asm, av)) || (rc = s->up(&s->d_asm_xp, axp)) || (rc = s->up(&s->d_asm_x, ax)) ||
+        (rc = s->up(&s->d_items, iv)) || (rc = s->up(&s->d_orec, orec)) || (rc = s->up(&s->d_oxp, oxp)) ||
+        (rc = s->up(&s->d_ox, ox)))
       return bail(rc);
   }
   std::vector<int32_t> cp(colptr, colptr + S.n + 1), ri(rowind, rowind + S.nnz);

@@ -315,13 +315,54 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
 // consecutive rows (columns).
 constexpr int OB = 8;
 
+// Where the off-diagonal entries come from (the panel entries of L21 / U12 are
+// assembled here, at their first load, instead of being stored by the assembly
+// kernel and read back): record (nz, first child element) per entry, further
+// child elements in the item's overflow list.
+struct OffSrc {
+  const int2* rec;        // this lane group's records, indexed by pivot
+  const int2* ox;         // overflow (pivot * 4 + lane group, element id)
+  int ox0, ox1, sub;
+  double om2;             // MODE 0: omega^2 of this lane's frequency
+  const cplx* K;
+  const double* M;
+  const cplx* dq;         // MODE 1: this lane's explicit matrix values
+};
+
+template <int MODE>
+__device__ __forceinline__ cplx off_source(const OffSrc& S, const cplx* __restrict__ F, int64_t Fc, int64_t q,
+                                           int c) {
+  const int2 g = S.rec[c];
+  cplx o;
+  if (MODE == 0) {
+    const cplx k = S.K[max(g.x, 0)];
+    o = make_double2(fma(-S.om2, S.M[max(g.x, 0)], k.x), k.y);
+  } else {
+    o = S.dq[max(g.x, 0)];
+  }
+  const cplx ch = F[(int64_t)max(g.y, 0) * Fc + q];
+  const cplx z = make_double2(0.0, 0.0);
+  return cadd(g.x >= 0 ? o : z, g.y >= 0 ? ch : z);
+}
+
 // One chunk of NB consecutive columns (kind 0) / rows (kind 1) c0 .. c0+NB-1.
-template <int NB>
+template <int MODE, int NB>
 __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, int64_t so, int64_t sc, int64_t sa, int64_t sb,
-                                              bool unit, bool valid, int c0, int64_t Fc) {
+                                              bool unit, bool valid, int c0, const OffSrc& S,
+                                              const cplx* __restrict__ F, int64_t Fc, int64_t q) {
   cplx x[NB];
 #pragma unroll
-  for (int j = 0; j < NB; ++j) x[j] = base[(so + (int64_t)(c0 + j) * sc) * Fc];
+  for (int j = 0; j < NB; ++j) x[j] = off_source<MODE>(S, F, Fc, q, c0 + j);
+  for (int e = S.ox0; e < S.ox1; ++e) {       // rare: several children cover one entry
+    const int2 g = S.ox[e];
+    const int c = (g.x >> 2) - c0;
+    if ((g.x & 3) == S.sub && c >= 0 && c < NB) {
+      const cplx v = F[(int64_t)g.y * Fc + q];
+#pragma unroll
+      for (int j = 0; j < NB; ++j)
+        if (j == c) x[j] = cadd(x[j], v);
+    }
+  }
   // x -= own(0:c0) * shared(0:c0, c0:c0+NB)
 #pragma unroll 2
   for (int t = 0; t < c0; ++t) {
@@ -356,8 +397,13 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, int64_t s
   }
 }
 
+template <int MODE>
 __global__ __launch_bounds__(256) void k_offdiag_level(DevPattern P, const int4* __restrict__ items, int nitems,
-                                                        cplx* __restrict__ F, int64_t Fc) {
+                                                        const int2* __restrict__ orec, const int* __restrict__ oxp,
+                                                        const int2* __restrict__ ox, cplx* __restrict__ F, int64_t Fc,
+                                                        const double* __restrict__ freqs, const cplx* __restrict__ K,
+                                                        const double* __restrict__ M, const cplx* __restrict__ data,
+                                                        int64_t data_stride, int nvalid) {
   const int lane = threadIdx.x & 63;
   const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
   const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
@@ -372,6 +418,20 @@ __global__ __launch_bounds__(256) void k_offdiag_level(DevPattern P, const int4*
   const bool valid = idx < f;
   const int r = min(idx, f - 1);
   cplx* __restrict__ base = F + fr.off * Fc + q;
+  OffSrc S;
+  S.rec = orec + it.w + (int64_t)sub * ns;
+  S.ox = ox;
+  S.ox0 = oxp[wid];
+  S.ox1 = oxp[wid + 1];
+  S.sub = sub;
+  S.om2 = 0.0;
+  if (MODE == 0) {
+    const double om = 6.283185307179586 * freqs[q];
+    S.om2 = om * om;
+  }
+  S.K = K;
+  S.M = M;
+  S.dq = data + min(q, (int64_t)nvalid - 1) * data_stride;
   // kind 0: own(c) = E(r, c), shared(a, b) = U(a, b) = E(a, b)
   // kind 1: own(c) = E(c, r), shared(a, b) = L(b, a) = E(b, a)   (transposed roles)
   const int64_t so = it.z == 0 ? (int64_t)r * f : r;           // own element c at so + c * sc
@@ -379,15 +439,12 @@ __global__ __launch_bounds__(256) void k_offdiag_level(DevPattern P, const int4*
   const int64_t sa = it.z == 0 ? f : 1, sb = it.z == 0 ? 1 : f;  // shared (a, b) at a * sa + b * sb
   const bool unit = it.z != 0;                                   // L11 has a unit diagonal
   int c0 = 0;
-  for (; c0 + OB <= ns; c0 += OB) offdiag_chunk<OB>(base, so, sc, sa, sb, unit, valid, c0, Fc);
+  for (; c0 + OB <= ns; c0 += OB) offdiag_chunk<MODE, OB>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q);
   switch (ns - c0) {     // wave-uniform tail width
-    case 1: offdiag_chunk<1>(base, so, sc, sa, sb, unit, valid, c0, Fc); break;
-    case 2: offdiag_chunk<2>(base, so, sc, sa, sb, unit, valid, c0, Fc); break;
-    case 3: offdiag_chunk<3>(base, so, sc, sa, sb, unit, valid, c0, Fc); break;
-    case 4: offdiag_chunk<4>(base, so, sc, sa, sb, unit, valid, c0, Fc); break;
-    case 5: offdiag_chunk<5>(base, so, sc, sa, sb, unit, valid, c0, Fc); break;
-    case 6: offdiag_chunk<6>(base, so, sc, sa, sb, unit, valid, c0, Fc); break;
-    case 7: offdiag_chunk<7>(base, so, sc, sa, sb, unit, valid, c0, Fc); break;
+#define TAIL(n) \
+  case n: offdiag_chunk<MODE, n>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q); break;
+    TAIL(1) TAIL(2) TAIL(3) TAIL(4) TAIL(5) TAIL(6) TAIL(7)
+#undef TAIL
     default: break;
   }
 }
@@ -928,10 +985,15 @@ void launch_factor(const DevPattern& P, const int* lvl, int nfronts, int W, int 
   LAUNCH(k_factor_level<true>, dim3(nfronts, ngroups * 4), dim3(64 * W), st, P, lvl, F, Fc, flags);
 }
 
-void launch_offdiag(const DevPattern& P, const int4* items, int nitems, int ngroups, double2* F, int64_t Fc,
-                    hipStream_t st) {
+void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
+                    const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,
+                    const double* M, const double2* data, int64_t ds, int nvalid, hipStream_t st) {
   if (nitems <= 0) return;
-  LAUNCH(k_offdiag_level, dim3((nitems + 3) / 4, ngroups * 4), dim3(256), st, P, items, nitems, F, Fc);
+  dim3 g((nitems + 3) / 4, ngroups * 4), b(256);
+  if (mode == 0)
+    LAUNCH(k_offdiag_level<0>, g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid);
+  else
+    LAUNCH(k_offdiag_level<1>, g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid);
 }
 
 static RhsArgs make_rhs(const RhsDesc& d) {

@@ -22,8 +22,9 @@ void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, cons
 void launch_factor(const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F, int64_t Fc,
                    int* flags, hipStream_t st);
 // Schur complement A22 -= L21 U12 for a level's tile list (TM x TN = 4 x 4 tiles)
-void launch_offdiag(const DevPattern& P, const int4* items, int nitems, int ngroups, double2* F, int64_t Fc,
-                    hipStream_t st);
+void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
+                    const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,
+                    const double* M, const double2* data, int64_t ds, int nvalid, hipStream_t st);
 void launch_schur(const DevPattern& P, const int4* tiles, int ntiles, const int* g1, const int* gxp, const int2* gx,
                   int ngroups, double2* F, int64_t Fc, hipStream_t st);
 // which: 0 = L (bottom-up), 1 = U (top-down), 2 = U^T (bottom-up), 3 = L^T (top-down)
