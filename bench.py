@@ -11,9 +11,14 @@ forward + adjoint (loss + gradient), fp64.
   ``linspace(40, 600, 4096 * N)``); one all-reduce (RCCL) of the loss/gradient
   partials per step;
 * ``value`` = 4096 * N / (max-over-ranks seconds per step);
-* ``roofline``: the dominant kernel (static-pivot multifrontal factorisation,
-  fp64) from per-phase HIP-event timings on the sweep's stream; the batched
-  triangular-solve phase (HBM-bound) is reported beside it;
+* ``roofline``: the dominant kernel, ``k_schur_level`` (Schur complement of the
+  multifrontal factorisation; HBM-bound), from HIP events bracketing each of its
+  launches on the sweep's stream: algorithmic bytes per launch (the solver's
+  count: A22 stores + gathered children's entries + L21/U12 read once, 16 B per
+  complex entry) / average launch time; ``traffic`` = measured HBM bytes per
+  launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes
+  (profiles/r01/pmc_traffic.json, gfx950-corrected); the whole factorisation
+  (``factor_roofline``) and the triangular solves (``sptrsv_roofline``) beside it;
 * ``cpu_baseline``: the oracle (scipy SuperLU, one process per core) on a
   bounded sample of the same workload, rank 0, N = 1 only.
 
@@ -36,6 +41,22 @@ sys.path.insert(0, REPO)
 
 FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector/matrix (spec; MI355X_MICROARCH.md lists no fp64 row)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+PMC_FILE = os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")
+KERNELS = ("k_assemble_level<0>", "k_factor_level<true>", "k_offdiag_level<0>", "k_schur_level")
+
+
+def pmc_traffic(chunk):
+    """Measured HBM bytes per launch of each factorisation kernel class, scaled to ``chunk``."""
+    try:
+        d = json.load(open(PMC_FILE))
+    except (OSError, ValueError):
+        return [None] * 4
+    out = []
+    for k in KERNELS:
+        e = d["kernels"].get(k)
+        out.append(None if e is None else
+                   (e["read_bytes"] + e["write_bytes"]) / e["dispatches"] * chunk / d["freqs_per_sweep"])
+    return out
 
 
 def build_problem(ny, device):
@@ -99,7 +120,7 @@ def main():
     loss_fn = prob.getLossFunction(freqs, ref, "MSE_LOG_AFC", distributed=world > 1)
     eng = prob.engine()
     solver = eng.solver
-    solver.set_timing(True)
+    solver.set_timing(True, kernels=True)
 
     def step():
         x = torch.tensor(theta, requires_grad=True)
@@ -113,10 +134,15 @@ def main():
     if world > 1:
         dist.barrier()
     phase = np.zeros(5)
+    kms = np.zeros(4)
+    klaunch = np.zeros(4)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         val, grad = step()
         phase += solver.last_timings()
+        m, n = solver.last_kernel_timings()
+        kms += m
+        klaunch += n
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -131,8 +157,17 @@ def main():
     st = eng.stats
     nv = hi - lo
     phase /= args.steps                      # ms per step, per phase
+    kms /= args.steps
+    klaunch /= args.steps
     factor_flops = st["factor_flops"] * nv
     fact_tfs = factor_flops / (phase[0] * 1e-3) / 1e12
+    alg = solver.alg_bytes().astype(float) * nv          # algorithmic bytes per step, per kernel class
+    alg_launch = alg / np.maximum(klaunch, 1)
+    ms_launch = kms / np.maximum(klaunch, 1)
+    gbs = alg_launch / (ms_launch * 1e-3) / 1e9
+    traffic = pmc_traffic(solver.max_batch)
+    fact_alg = float(alg.sum())
+    fact_traffic = None if None in traffic else float(np.dot(traffic, klaunch))
     # triangular solves: 4 passes (L, U, U^T, L^T) over the factors, 16 B per L+U entry
     # per pass per frequency, plus int32 pattern (shared by 64-frequency wavefronts) and vectors
     trsv_bytes = nv * (4 * 16 * st["nnz_lu"] + 4 * 2 * 16 * st["n"])
@@ -156,9 +191,16 @@ def main():
                    "n_dofs": st["n"], "freqs_per_gpu": args.freqs, "chunk": solver.max_batch,
                    "nnz_lu": st["nnz_lu"], "factor_gflop_per_freq": st["factor_flops"] / 1e9,
                    "parallelism": f"frequency shards x{world} + 1 all-reduce/step"},
-        "roofline": {"bound": "mfma", "kernel": "k_factor_level (fp64 vector FMA; MI355X fp64 peak)",
-                     "achieved": fact_tfs, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": fact_tfs / FP64_PEAK_TFLOPS, "traffic": None},
+        "roofline": {"bound": "hbm", "kernel": "k_schur_level", "achieved": gbs[3], "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": gbs[3] / HBM_PEAK_GBS, "traffic": traffic[3],
+                     "alg_bytes_per_launch": alg_launch[3], "avg_launch_ms": ms_launch[3],
+                     "launches_per_step": klaunch[3]},
+        "factor_roofline": {"bound": "hbm", "kernels": list(KERNELS), "ms_per_step": kms.tolist(),
+                            "alg_GBps": gbs.tolist(),
+                            "achieved": fact_alg / (kms.sum() * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": fact_alg / (kms.sum() * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                            "alg_bytes_per_step": fact_alg, "traffic_per_step": fact_traffic,
+                            "fp64_TFLOPs": fact_tfs, "fp64_frac": fact_tfs / FP64_PEAK_TFLOPS},
         "sptrsv_roofline": {"bound": "hbm", "kernel": "k_{l,u,ut,lt}solve_level", "achieved": trsv_gbs,
                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": trsv_gbs / HBM_PEAK_GBS,
                             "traffic": None},

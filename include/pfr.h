@@ -149,6 +149,16 @@ PFR_API int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int
 PFR_API int pfr_set_timing(pfr_solver* s, int32_t enable);
 PFR_API int pfr_last_timings(const pfr_solver* s, double* ms_out /* 5 */);
 
+/* With pfr_set_timing(s, 3) the factorisation additionally brackets every launch with HIP events:
+ * summed device times [ms] of the last call per kernel class (0 = A11 assembly, 1 = A11 LU,
+ * 2 = L21/U12 rows/columns, 3 = Schur complement A22) and their launch counts (NULL allowed). */
+PFR_API int pfr_last_kernel_timings(const pfr_solver* s, double* ms_out /* 4 */, int64_t* launches_out /* 4 */);
+
+/* Algorithmic HBM bytes per frequency of one factorisation, per kernel class as above: complex
+ * entries each class must store plus the entries it must read once (children's update-matrix
+ * entries it gathers, factor blocks it consumes); index data, shared by all frequencies, excluded. */
+PFR_API int pfr_solver_alg_bytes(const pfr_solver* s, int64_t* bytes_out /* 4 */);
+
 #ifdef __cplusplus
 }
 #endif

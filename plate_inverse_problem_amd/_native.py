@@ -70,6 +70,8 @@ _PROTOS = {
     "pfr_sweep": (C.c_int, [_P, C.c_int32, _P, C.c_int32, _P, C.c_double, _P, _P, _P, _P, _P]),
     "pfr_set_timing": (C.c_int, [_P, C.c_int32]),
     "pfr_last_timings": (C.c_int, [_P, _DP]),
+    "pfr_last_kernel_timings": (C.c_int, [_P, _DP, _P]),
+    "pfr_solver_alg_bytes": (C.c_int, [_P, _P]),
 }
 
 _lib = None
@@ -246,10 +248,27 @@ class Solver:
                                int(bool(transpose)), self._stream(y)), "pfr_matvec")
 
     # ---- timing
-    def set_timing(self, on: bool):
-        check(lib().pfr_set_timing(self._h, int(bool(on))), "pfr_set_timing")
+    def set_timing(self, on, kernels: bool = False):
+        """Per-phase HIP-event timing; ``kernels`` also brackets every factorisation launch."""
+        check(lib().pfr_set_timing(self._h, (3 if kernels else 1) if on else 0), "pfr_set_timing")
 
     def last_timings(self) -> np.ndarray:
         out = np.zeros(5)
         check(lib().pfr_last_timings(self._h, out.ctypes.data_as(_DP)), "pfr_last_timings")
+        return out
+
+    KERNEL_CLASSES = ("k_assemble_level", "k_factor_level", "k_offdiag_level", "k_schur_level")
+
+    def last_kernel_timings(self):
+        """(ms, launches) per factorisation kernel class of the last call (needs kernels=True)."""
+        ms = np.zeros(4)
+        n = np.zeros(4, np.int64)
+        check(lib().pfr_last_kernel_timings(self._h, ms.ctypes.data_as(_DP), n.ctypes.data_as(_P)),
+              "pfr_last_kernel_timings")
+        return ms, n
+
+    def alg_bytes(self) -> np.ndarray:
+        """Algorithmic HBM bytes per frequency of one factorisation, per kernel class."""
+        out = np.zeros(4, np.int64)
+        check(lib().pfr_solver_alg_bytes(self._h, out.ctypes.data_as(_P)), "pfr_solver_alg_bytes")
         return out

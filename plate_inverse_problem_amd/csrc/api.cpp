@@ -91,14 +91,20 @@ struct pfr_solver {
   const double* stiff = nullptr;
   int n_stiff = 0;
   pfr::CoefPack e{};
-  // timing
-  bool timing = false;
+  // timing: bit 0 = phases (ev), bit 1 = factorisation kernel classes (kev: 5 per level)
+  int timing = 0;
   hipEvent_t ev[6]{};
   double last_ms[5]{};
+  std::vector<hipEvent_t> kev;
+  double kernel_ms[4]{};                // assemble (A11), diag (A11 LU), offdiag (L21/U12), schur
+  int64_t kernel_launches[4]{};
+  int64_t alg_bytes[4]{};               // algorithmic HBM bytes per frequency of each class (one sweep)
 
   ~pfr_solver() {
     for (void* p : owned) (void)hipFree(p);
     for (auto& x : ev)
+      if (x) (void)hipEventDestroy(x);
+    for (auto& x : kev)
       if (x) (void)hipEventDestroy(x);
   }
   template <class T>
@@ -143,28 +149,58 @@ int finish_timing(pfr_solver* s, const bool* used) {
     if (used[i]) HIP_TRY(hipEventElapsedTime(&ms, s->ev[i], s->ev[i + 1]));
     s->last_ms[i] += used[i] ? ms : 0.0;
   }
+  if ((s->timing & 2) && used[0]) {
+    const int L = (int)s->level_ptr.size() - 1;
+    for (int l = 0; l < L; ++l)
+      for (int c = 0; c < 4; ++c) {
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, s->kev[5 * l + c], s->kev[5 * l + c + 1]));
+        s->kernel_ms[c] += ms;
+        s->kernel_launches[c] += 1;
+      }
+  }
   return PFR_OK;
+}
+
+void reset_timing(pfr_solver* s) {
+  for (double& m : s->last_ms) m = 0;
+  for (double& m : s->kernel_ms) m = 0;
+  for (int64_t& n : s->kernel_launches) n = 0;
 }
 
 int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nvalid, hipStream_t st) {
   const int L = (int)s->level_ptr.size() - 1;
   const int ngroups = (int)(s->Fc / 64);
+  const bool kt = (s->timing & 2) != 0;
+  while (kt && s->kev.size() < (size_t)(5 * L)) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreate(&e));
+    s->kev.push_back(e);
+  }
+  auto mark = [&](int l, int c) {
+    if (kt) (void)hipEventRecord(s->kev[5 * l + c], st);
+  };
   for (int l = 0; l < L; ++l) {
     int nf = s->level_ptr[l + 1] - s->level_ptr[l];
+    mark(l, 0);
     pfr::launch_assemble(mode, s->d_asm + s->asm_ptr[l], s->asm_ptr[l + 1] - s->asm_ptr[l],
                          s->d_asm_xp + s->asm_ptr[l] / 8, s->d_asm_x, ngroups, s->F, s->Fc, s->freqs, s->K, s->M,
                          data, ds, nvalid, st);
+    mark(l, 1);
     // panel: enough workgroups (front x 16 frequencies) to fill the chip -> one wave
     // each (no idle waves at the block barriers); few large fronts -> more waves
     const int64_t wgs = (int64_t)nf * ngroups * 4;
     const int Wp = (int)std::max<int64_t>(1, std::min<int64_t>(s->level_W[l], (4096 + wgs - 1) / wgs));
     pfr::launch_factor(s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st);
+    mark(l, 2);
     pfr::launch_offdiag(mode, s->P, s->d_items + s->item_ptr[l], s->item_ptr[l + 1] - s->item_ptr[l], s->d_orec,
                         s->d_oxp + s->item_ptr[l], s->d_ox, ngroups, s->F, s->Fc, s->freqs, s->K, s->M, data, ds,
                         nvalid, st);
+    mark(l, 3);
     pfr::launch_schur(s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l],
                       s->d_g1 + (int64_t)s->tile_ptr[l] * 64, s->d_gxp + s->tile_ptr[l], s->d_gx, ngroups, s->F,
                       s->Fc, st);
+    mark(l, 4);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -475,6 +511,27 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       s->asm_ptr.push_back((int32_t)av.size());
       s->item_ptr.push_back((int32_t)iv.size());
     }
+    {
+      // algorithmic bytes per frequency (16 B per complex entry; index data is
+      // shared by all frequencies and not counted)
+      int64_t s_ns2 = 0, s_r2 = 0, s_rns = 0, g_a11 = 0, g_off = 0, g_s = 0;
+      for (const Front& F : S.fronts) {
+        const int64_t r = F.f - F.ns;
+        s_ns2 += (int64_t)F.ns * F.ns;
+        s_r2 += r * r;
+        s_rns += 2 * r * F.ns;
+      }
+      for (const int4& a : av) g_a11 += a.z >= 0;
+      for (const int2& o : orec) g_off += o.y >= 0;
+      for (int32_t g : g1) g_s += g >= 0;
+      g_a11 += (int64_t)ax.size();
+      g_off += (int64_t)ox.size();
+      g_s += (int64_t)gxp.back();                          // gx may hold a placeholder
+      s->alg_bytes[0] = 16 * (s_ns2 + g_a11);             // A11 stores + child entries gathered
+      s->alg_bytes[1] = 16 * 2 * s_ns2;                   // A11 read + L11/U11 write
+      s->alg_bytes[2] = 16 * (s_rns + g_off + s_ns2);     // L21/U12 stores + gathered children + L11/U11 read
+      s->alg_bytes[3] = 16 * (s_r2 + g_s + s_rns);        // A22 stores + gathered children + L21/U12 read
+    }
     if (av.empty()) av.assign(8, make_int4(-1, -1, -1, 0));
     if (ax.empty()) ax.push_back(make_int2(0, 0));
     if (iv.empty()) iv.push_back(make_int4(0, 0, 0, 0));
@@ -512,7 +569,22 @@ int32_t pfr_solver_max_batch(const pfr_solver* s) { return s ? (int32_t)s->Fc : 
 
 int pfr_set_timing(pfr_solver* s, int32_t enable) {
   if (!s) return fail(PFR_ERR_ARG, "null solver");
-  s->timing = enable != 0;
+  s->timing = enable == 0 ? 0 : (enable | 1);
+  return PFR_OK;
+}
+
+int pfr_last_kernel_timings(const pfr_solver* s, double* ms, int64_t* launches) {
+  if (!s || !ms) return fail(PFR_ERR_ARG, "null argument");
+  for (int i = 0; i < 4; ++i) {
+    ms[i] = s->kernel_ms[i];
+    if (launches) launches[i] = s->kernel_launches[i];
+  }
+  return PFR_OK;
+}
+
+int pfr_solver_alg_bytes(const pfr_solver* s, int64_t* bytes) {
+  if (!s || !bytes) return fail(PFR_ERR_ARG, "null argument");
+  for (int i = 0; i < 4; ++i) bytes[i] = s->alg_bytes[i];
   return PFR_OK;
 }
 
@@ -619,7 +691,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
   if (reverse && (!s->stiff || !w_dev)) return fail(PFR_ERR_STATE, "reverse pass needs pfr_set_stiffness and w_dev");
   HIP_TRY(hipSetDevice(s->device));
   hipStream_t st = (hipStream_t)stream;
-  for (double& m : s->last_ms) m = 0;
+  reset_timing(s);
   const int64_t Fc = s->Fc;
   const int ngroups = (int)(Fc / 64);
   bool used[5] = {true, true, true, reverse, reverse};
@@ -678,7 +750,7 @@ int pfr_solve(pfr_solver* s, int32_t batch, const double* data_dev, int64_t data
   if (b_stride != 0 && b_stride < s->n) return fail(PFR_ERR_ARG, "b_stride < n");
   HIP_TRY(hipSetDevice(s->device));
   hipStream_t st = (hipStream_t)stream;
-  for (double& m : s->last_ms) m = 0;
+  reset_timing(s);
   const int64_t Fc = s->Fc;
   const double2* data = reinterpret_cast<const double2*>(data_dev);
   const double2* B = reinterpret_cast<const double2*>(b_dev);
