@@ -156,7 +156,9 @@ int finish_timing(pfr_solver* s, const bool* used) {
         float ms = 0;
         HIP_TRY(hipEventElapsedTime(&ms, s->kev[5 * l + c], s->kev[5 * l + c + 1]));
         s->kernel_ms[c] += ms;
-        s->kernel_launches[c] += 1;
+        const int work[4] = {s->asm_ptr[l + 1] - s->asm_ptr[l], s->level_ptr[l + 1] - s->level_ptr[l],
+                             s->item_ptr[l + 1] - s->item_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l]};
+        s->kernel_launches[c] += work[c] > 0;     // empty classes launch nothing
       }
   }
   return PFR_OK;
