@@ -200,7 +200,8 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
                         nvalid, st);
     mark(l, 3);
     pfr::launch_schur(s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l],
-                      s->d_g1 + (int64_t)s->tile_ptr[l] * 64, s->d_gxp + s->tile_ptr[l], s->d_gx, ngroups, s->F,
+                      s->d_g1 + (int64_t)s->tile_ptr[l] * 16 * pfr::SCHUR_SR * pfr::SCHUR_SC, s->d_gxp + s->tile_ptr[l],
+                      s->d_gx, ngroups, s->F,
                       s->Fc, st);
     mark(l, 4);
   }
@@ -399,11 +400,11 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
         // one is stored densely (64 ids per super-tile, -1 = none) so the kernel
         // issues all gather loads at once; the rare further sources go to a
         // per-super-tile overflow list
-        for (int i0 = 0; i0 < r; i0 += 8)
-          for (int j0 = 0; j0 < r; j0 += 8) {
+        for (int i0 = 0; i0 < r; i0 += 4 * pfr::SCHUR_SR)
+          for (int j0 = 0; j0 < r; j0 += 4 * pfr::SCHUR_SC) {
             tv.push_back(make_int4(t, i0, j0, 0));
-            for (int sub = 0; sub < 4; ++sub) {
-              const int ti = i0 / 4 + (sub >> 1), tj = j0 / 4 + (sub & 1);
+            for (int sub = 0; sub < pfr::SCHUR_SR * pfr::SCHUR_SC; ++sub) {
+              const int ti = i0 / 4 + sub / pfr::SCHUR_SC, tj = j0 / 4 + sub % pfr::SCHUR_SC;
               for (int pos = 0; pos < 16; ++pos) {
                 int32_t first = -1;
                 if (ti < ntj && tj < ntj) {

@@ -27,6 +27,11 @@ struct DevPattern {
   int32_t n;
 };
 
+// Schur super-tile: a wavefront = SCHUR_QG frequencies x (SCHUR_SR x SCHUR_SC) lane groups,
+// each lane group one 4 x 4 register tile -> (4 SCHUR_SR) x (4 SCHUR_SC) entries per wave.
+constexpr int SCHUR_SR = 2, SCHUR_SC = 2, SCHUR_QG = 16;
+static_assert(SCHUR_SR * SCHUR_SC * SCHUR_QG == 64, "one wavefront per super-tile");
+
 constexpr int COEF_MAX = 32;
 struct CoefPack {
   double re[COEF_MAX];

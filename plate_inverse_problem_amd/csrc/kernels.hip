@@ -455,9 +455,11 @@ __global__ __launch_bounds__(256) void k_offdiag_level(DevPattern P, const int4*
 // the K loop so every load of a k-step is independent.
 constexpr int TM = 4, TN = 4;
 
-// Lane map: a wavefront = 16 frequencies x 4 sub-tiles; the 4 sub-tiles form a
-// 2 x 2 arrangement of 4 x 4 tiles (an 8 x 8 super-tile), so each L21 row and
-// U12 column value a wave-instruction reads serves two sub-tiles.
+// Lane map: a wavefront = SCHUR_QG (16) frequencies x 4 sub-tiles; the 4 sub-tiles
+// form a 2 x 2 arrangement of 4 x 4 tiles (an 8 x 8 super-tile), so each L21 row
+// and U12 column value a wave-instruction reads serves two sub-tiles.  (8
+// frequencies x 8 sub-tiles as 8 x 16 was measured 22 % slower: eight distinct
+// 128 B lines per wave-instruction instead of four 256 B runs.)
 __global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* __restrict__ tiles, int ntiles,
                                                       const int* __restrict__ g1, const int* __restrict__ gxp,
                                                       const int2* __restrict__ gx, cplx* __restrict__ F, int64_t Fc) {
@@ -468,11 +470,11 @@ __global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* _
   const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
   const int tid = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (tid >= ntiles) return;
-  const int sub = lane >> 4;
-  const int64_t q = (int64_t)by * 16 + (lane & 15);
+  const int sub = lane / SCHUR_QG;
+  const int64_t q = (int64_t)by * SCHUR_QG + lane % SCHUR_QG;
   int4 t = tiles[tid];
-  t.y += 4 * (sub >> 1);
-  t.z += 4 * (sub & 1);
+  t.y += 4 * (sub / SCHUR_SC);
+  t.z += 4 * (sub % SCHUR_SC);
   const Front fr = P.fronts[t.x];
   const int f = fr.f, ns = fr.ns;
   cplx* __restrict__ base = F + fr.off * Fc + q;
@@ -486,7 +488,8 @@ __global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* _
   // loads in flight at once (a missing source reads entry 0 and is dropped)
   cplx acc[TM][TN];
   {
-    const int4* __restrict__ g4 = reinterpret_cast<const int4*>(g1 + (int64_t)tid * 64 + sub * 16);
+    const int4* __restrict__ g4 =
+        reinterpret_cast<const int4*>(g1 + (int64_t)tid * (16 * SCHUR_SR * SCHUR_SC) + sub * 16);
     int src[TM * TN];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -968,7 +971,8 @@ void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPac
 void launch_schur(const DevPattern& P, const int4* tiles, int ntiles, const int* g1, const int* gxp, const int2* gx,
                   int ngroups, double2* F, int64_t Fc, hipStream_t st) {
   if (ntiles <= 0) return;
-  LAUNCH(k_schur_level, dim3((ntiles + 3) / 4, ngroups * 4), dim3(256), st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
+  LAUNCH(k_schur_level, dim3((ntiles + 3) / 4, ngroups * (64 / SCHUR_QG)), dim3(256), st, P, tiles, ntiles, g1, gxp,
+         gx, F, Fc);
 }
 
 void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, const int2* xl, int ngroups, double2* F,
