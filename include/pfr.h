@@ -143,6 +143,20 @@ PFR_API int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int
                       const double* ref_dev, double scale, double* fr_dev, double* loss_dev, double* w_dev,
                       int32_t* flags_dev, void* stream);
 
+/* Exact second derivatives with the factors of the sweep reused (replaces the reference's
+ * forward-over-reverse Hessian, `jax.jacobian(grad)` in Optimizers.py:125-136, whose mode-4
+ * batched solves refactorise per direction, InnerState.h:289-305).  Per frequency: one
+ * factorisation, then x, the adjoint l, and per tangent direction i (n_dir of them, complex
+ * coefficient directions dcoef[i] = d c / d theta_i, host memory, n_dir x n_stiff complex):
+ *   A dx_i = db_i - dA_i x,   A^T dl_i = dG_i(dx_i) - dA_i^T l     (dA_i = sum_k dcoef_ik S_k)
+ * Accumulates loss_dev[0] (may be NULL) and w_dev (n_stiff complex) as pfr_sweep, and
+ *   h_dev[i * n_stiff + k] += sum_f [ -dl_i^T S_k x + e_k dl_i^T b0 - l^T S_k dx_i ]
+ * so that d2L / dtheta_i dtheta_j = Re sum_k ( h_ik dc_kj + w_k d2c_k / dtheta_i dtheta_j ).
+ * loss_type must be one of MSE, RMSE, MSE_AFC, MSE_LOG_AFC. */
+PFR_API int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t loss_type,
+                              const double* ref_dev, double scale, int32_t n_dir, const double* dcoef,
+                              double* loss_dev, double* w_dev, double* h_dev, int32_t* flags_dev, void* stream);
+
 /* Per-phase device times [ms] of the last pfr_sweep/pfr_solve call on this solver, measured with HIP
  * events on the call's stream (0 = factor, 1 = forward solves, 2 = functional, 3 = adjoint solves,
  * 4 = contraction).  Timing is enabled by pfr_set_timing(s, 1). */

@@ -86,7 +86,10 @@ def solve_trust_region_model(B, g, delta, rtol=1e-6, max_iter=100):
 
 
 def optimize_trust_region(f, x_0, N_steps=10, delta_max=1.0, delta=None, eta=0.15, method="newt",
-                          steps_to_stall=10, hessian_rel_step=1e-4):
+                          steps_to_stall=10, hessian_rel_step=1e-4, model=None):
+    """Trust-region Newton (``Optimizers.py:147-232`` of the reference).  ``model(x) -> (f, g, H)``
+    supplies the exact Hessian (``Problem.getLossHessianFunction``: factors reused on the GPU);
+    without it the Hessian is central differences of the adjoint gradient."""
     if delta is None:
         delta = delta_max / 10.0
     if not 0 <= eta <= 0.25:
@@ -102,8 +105,11 @@ def optimize_trust_region(f, x_0, N_steps=10, delta_max=1.0, delta=None, eta=0.1
     k = 0
     for k in range(N_steps):
         if need_model:
-            cur_f, g = vg(x)
-            B = fd_hessian(grad, x, hessian_rel_step)
+            if model is not None:
+                cur_f, g, B = model(x)
+            else:
+                cur_f, g = vg(x)
+                B = fd_hessian(grad, x, hessian_rel_step)
         try:
             sd, lam, pred = solve_trust_region_model(B, g, delta)
         except AssertionError as e:

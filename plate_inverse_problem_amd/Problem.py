@@ -366,6 +366,69 @@ class Problem:
 
         return loss
 
+    def getLossHessianFunction(self, frequencies, reference_fr, func_type: str, scaling_params=None,
+                               *, distributed: bool = False) -> Callable:
+        """``model(params) -> (loss, grad, hessian)`` (numpy) of ``getLossFunction``'s loss.
+
+        Replaces the reference's forward-over-reverse Hessian (``jax.jacobian(grad)``,
+        ``Optimizers.py:125-136``; its mode-4 solves refactorise per direction,
+        ``InnerState.h:289-305``): one GPU sweep factors each frequency once and
+        reuses the factors for the tangent solves ``A dx_i = db_i - dA_i x`` and the
+        second-order adjoints ``A^T dl_i = dG_i - dA_i^T l`` of every parameter
+        direction; the material transform's first and second derivatives come
+        from torch autograd on the host.
+        """
+        frequencies = np.asarray(frequencies)
+        reference_fr = np.asarray(reference_fr)
+        assert frequencies.shape[0] == reference_fr.shape[0]
+        if func_type not in ('MSE', 'RMSE', 'MSE_AFC', 'MSE_LOG_AFC'):
+            raise ValueError(f'Function type "{func_type}" is not supported!')
+        loss_id = _native.LOSS_IDS[func_type]
+        scaling = 1.0 if scaling_params is None else torch.as_tensor(np.array(scaling_params, dtype=np.float64))
+        n_total = frequencies.shape[0]
+        lo, hi, reduce_fn = 0, n_total, None
+        if distributed:
+            from .distributed import shard_range, all_reduce_sum
+            lo, hi = shard_range(n_total)
+            reduce_fn = all_reduce_sum
+        transform = self._transform()
+        f_local = self._freqs(frequencies[lo:hi])
+        ref_local = torch.as_tensor(reference_fr[lo:hi].astype(np.complex128), device=self.device)
+
+        def c_real(p):
+            return torch.view_as_real(_coeffs18(transform, p * scaling)).reshape(-1)      # (36,)
+
+        def model(params):
+            p = torch.as_tensor(np.asarray(params, dtype=np.float64)).detach()
+            n = p.numel()
+            c = _coeffs18(transform, p * scaling).detach().numpy()
+            jac = torch.autograd.functional.jacobian(c_real, p).numpy().reshape(18, 2, n)
+            dc = jac[:, 0] + 1j * jac[:, 1]                                                # (18, n)
+            d2 = np.stack([torch.autograd.functional.hessian(lambda x, m=m: c_real(x)[m], p).numpy()
+                           for m in range(36)]).reshape(18, 2, n, n)
+            d2c = d2[:, 0] + 1j * d2[:, 1]                                                 # (18, n, n)
+            eng = self.engine(max(1, hi - lo))
+            eng.set_coefficients(c)
+            dev = eng.device
+            w = torch.zeros(18, dtype=torch.complex128, device=dev)
+            h = torch.zeros(n, 18, dtype=torch.complex128, device=dev)
+            loss = torch.zeros(1, dtype=torch.float64, device=dev)
+            flags = torch.zeros(f_local.numel(), dtype=torch.int32, device=dev)
+            eng.solver.hessian_sweep(f_local, loss_id, torch.view_as_real(ref_local), 1.0 / n_total, dc.T,
+                                     loss=loss, w=torch.view_as_real(w), h=torch.view_as_real(h), flags=flags)
+            _check_flags(flags)
+            packed = torch.cat([loss.to(torch.complex128), w, h.reshape(-1)])
+            if reduce_fn is not None:
+                packed = reduce_fn(packed)
+            packed = packed.cpu().numpy()
+            val = packed[0].real / n_total
+            w_, h_ = packed[1:19], packed[19:].reshape(n, 18)
+            grad = np.real(w_ @ dc)
+            hess = np.real(h_ @ dc) + np.real(np.einsum('k,kij->ij', w_, d2c))
+            return float(val), grad, 0.5 * (hess + hess.T)
+
+        return model
+
     def solveInverse(self, *args, **kwargs):
         from .inverse import solve_inverse
         return solve_inverse(self, *args, **kwargs)

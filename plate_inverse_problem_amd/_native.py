@@ -68,6 +68,8 @@ _PROTOS = {
     "pfr_set_rhs": (C.c_int, [_P, _DP, C.c_double, C.c_double, C.c_double]),
     "pfr_set_functional": (C.c_int, [_P, C.c_int32, _I32P, _DP, C.c_double]),
     "pfr_sweep": (C.c_int, [_P, C.c_int32, _P, C.c_int32, _P, C.c_double, _P, _P, _P, _P, _P]),
+    "pfr_hessian_sweep": (C.c_int, [_P, C.c_int32, _P, C.c_int32, _P, C.c_double, C.c_int32, _P, _P, _P, _P, _P,
+                                    _P]),
     "pfr_set_timing": (C.c_int, [_P, C.c_int32]),
     "pfr_last_timings": (C.c_int, [_P, _DP]),
     "pfr_last_kernel_timings": (C.c_int, [_P, _DP, _P]),
@@ -237,6 +239,15 @@ class Solver:
     def sweep(self, freqs, loss_type=LOSS_NONE, ref=None, scale=1.0, fr=None, loss=None, w=None, flags=None):
         check(lib().pfr_sweep(self._h, int(freqs.numel()), _ptr(freqs), int(loss_type), _ptr(ref), float(scale),
                               _ptr(fr), _ptr(loss), _ptr(w), _ptr(flags), self._stream(freqs)), "pfr_sweep")
+
+    def hessian_sweep(self, freqs, loss_type, ref, scale, dcoef, loss=None, w=None, h=None, flags=None):
+        """Loss, gradient partials w (18 complex) and second-order partials h (n_dir x 18 complex) with the
+        factors reused for the tangent and second-order adjoint solves; ``dcoef`` (n_dir, n_stiff) complex
+        host array of coefficient directions d c / d theta_i."""
+        d = np.ascontiguousarray(np.asarray(dcoef, dtype=np.complex128))
+        check(lib().pfr_hessian_sweep(self._h, int(freqs.numel()), _ptr(freqs), int(loss_type), _ptr(ref),
+                                      float(scale), int(d.shape[0]), d.ctypes.data_as(_P), _ptr(loss), _ptr(w),
+                                      _ptr(h), _ptr(flags), self._stream(freqs)), "pfr_hessian_sweep")
 
     # ---- InnerState-compatible
     def solve(self, data, data_stride, b, b_stride, x, transpose, batch, flags=None):

@@ -74,6 +74,12 @@ struct pfr_solver {
   int32_t* d_colptr = nullptr;
   int32_t* d_rowind = nullptr;
   double2 *F = nullptr, *WV = nullptr, *X = nullptr, *Y = nullptr, *XA = nullptr, *G = nullptr;
+  // Hessian sweep: permuted matrix by rows and by columns ((ptr, index, nz) each),
+  // tangent solution / adjoint vectors, combined tangent operators (lazily allocated)
+  int32_t *d_rptr = nullptr, *d_ridx = nullptr, *d_rnz = nullptr;
+  int32_t *d_cptr = nullptr, *d_cidx = nullptr, *d_cnz = nullptr;
+  double2 *DX = nullptr, *DL = nullptr, *Kdir = nullptr;
+  int n_kdir = 0;
   double2 *partial = nullptr, *tq = nullptr;
   double *freqs = nullptr, *loss_terms = nullptr;
   int32_t* flags = nullptr;
@@ -547,6 +553,27 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   }
   std::vector<int32_t> cp(colptr, colptr + S.n + 1), ri(rowind, rowind + S.nnz);
   if ((rc = s->up(&s->d_colptr, cp)) || (rc = s->up(&s->d_rowind, ri))) return bail(rc);
+  {
+    // permuted matrix compressed by rows and by columns (Hessian tangent operators)
+    auto compress = [&](const std::vector<int32_t>& key, const std::vector<int32_t>& other, int32_t** dptr,
+                        int32_t** didx, int32_t** dnz) {
+      std::vector<int32_t> ptr(S.n + 1, 0), idx(S.nnz), nz(S.nnz);
+      for (int64_t e = 0; e < S.nnz; ++e) ++ptr[key[e] + 1];
+      for (int i = 0; i < S.n; ++i) ptr[i + 1] += ptr[i];
+      std::vector<int32_t> fill(ptr.begin(), ptr.end() - 1);
+      for (int64_t e = 0; e < S.nnz; ++e) {
+        const int32_t at = fill[key[e]]++;
+        idx[at] = other[e];
+        nz[at] = (int32_t)e;
+      }
+      int r;
+      if ((r = s->up(dptr, ptr)) || (r = s->up(didx, idx)) || (r = s->up(dnz, nz))) return r;
+      return (int)PFR_OK;
+    };
+    if ((rc = compress(S.prow, S.pcol, &s->d_rptr, &s->d_ridx, &s->d_rnz)) ||
+        (rc = compress(S.pcol, S.prow, &s->d_cptr, &s->d_cidx, &s->d_cnz)))
+      return bail(rc);
+  }
   s->P = DevPattern{d_fronts, idx, relpos, rowf, ap, ac, an, ep, es, pm, pr, pc, S.n};
   const int64_t Fc = s->Fc;
   if ((rc = s->alloc(&s->F, S.factor_entries * Fc)) || (rc = s->alloc(&s->WV, S.total_rows * Fc)) ||
@@ -741,6 +768,101 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
     if (flags_dev) pfr::launch_flags_merge(s->flags, nv, flags_dev + q0, st);
     HIP_TRY(hipGetLastError());
     if ((rc = finish_timing(s, used))) return rc;
+  }
+  return PFR_OK;
+}
+
+int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t loss_type, const double* ref_dev,
+                      double scale, int32_t n_dir, const double* dcoef, double* loss_dev, double* w_dev,
+                      double* h_dev, int32_t* flags_dev, void* stream) {
+  if (!s || nfreq <= 0 || !freqs_dev || !ref_dev || !w_dev || !h_dev || n_dir <= 0 || !dcoef)
+    return fail(PFR_ERR_ARG, "bad hessian sweep arguments");
+  if (loss_type < PFR_LOSS_MSE || loss_type > PFR_LOSS_MSE_LOG_AFC)
+    return fail(PFR_ERR_ARG, "hessian sweep needs a loss type (MSE, RMSE, MSE_AFC, MSE_LOG_AFC)");
+  if (!s->K || !s->M) return fail(PFR_ERR_STATE, "operator not set (pfr_set_operator)");
+  if (!s->has_rhs) return fail(PFR_ERR_STATE, "rhs not set (pfr_set_rhs)");
+  if (!s->has_fn) return fail(PFR_ERR_STATE, "functional not set (pfr_set_functional)");
+  if (!s->stiff) return fail(PFR_ERR_STATE, "pfr_set_stiffness not called");
+  HIP_TRY(hipSetDevice(s->device));
+  hipStream_t st = (hipStream_t)stream;
+  reset_timing(s);
+  const int64_t Fc = s->Fc, n = s->n;
+  const int ngroups = (int)(Fc / 64);
+  int rc;
+  if (!s->DX && ((rc = s->alloc(&s->DX, n * Fc)) || (rc = s->alloc(&s->DL, n * Fc)))) return rc;
+  if (s->n_kdir < n_dir) {
+    if ((rc = s->alloc(&s->Kdir, (int64_t)n_dir * s->nnz))) return rc;   // previous block stays owned
+    s->n_kdir = n_dir;
+  }
+  // tangent operators dA_i = sum_k dc_ik S_k and right-hand-side weights beta_i = sum_k dc_ik e_k
+  std::vector<double2> beta(n_dir);
+  pfr::CoefPack zero{};
+  for (int i = 0; i < n_dir; ++i) {
+    pfr::CoefPack c{};
+    double br = 0, bi = 0;
+    for (int k = 0; k < s->n_stiff; ++k) {
+      c.re[k] = dcoef[2 * (i * s->n_stiff + k)];
+      c.im[k] = dcoef[2 * (i * s->n_stiff + k) + 1];
+      br += c.re[k] * s->e.re[k];
+      bi += c.im[k] * s->e.re[k];
+    }
+    beta[i] = make_double2(br, bi);
+    pfr::launch_combine(s->stiff, s->n_stiff, s->nnz, c, s->Kdir + (int64_t)i * s->nnz, st);
+  }
+  double2* H = reinterpret_cast<double2*>(h_dev);
+  for (int64_t q0 = 0; q0 < nfreq; q0 += Fc) {
+    const int nv = (int)std::min<int64_t>(Fc, nfreq - q0);
+    HIP_TRY(hipMemcpyAsync(s->freqs, freqs_dev + q0, nv * sizeof(double), hipMemcpyDeviceToDevice, st));
+    pfr::launch_pad_freqs(s->freqs, nv, Fc, st);
+    HIP_TRY(hipMemsetAsync(s->flags, 0, Fc * sizeof(int32_t), st));
+    if ((rc = factor_all(s, 0, nullptr, 0, nv, st))) return rc;
+    // forward solve, loss, adjoint, gradient partials (as pfr_sweep)
+    pfr::RhsDesc rd;
+    rd.rhsP = s->rhsP;
+    rd.beta_re = s->beta_re;
+    rd.beta_im = s->beta_im;
+    rd.mass_sum = s->mass_sum;
+    rd.freqs = s->freqs;
+    if ((rc = solve_all(s, 0, 0, rd, nullptr, s->Y, st)) || (rc = solve_all(s, 1, 0, rd, s->Y, s->X, st))) return rc;
+    pfr::FunctionalArgs fa = s->fn;
+    fa.loss_type = loss_type;
+    fa.ref = reinterpret_cast<const double2*>(ref_dev);
+    fa.scale = scale;
+    HIP_TRY(hipMemsetAsync(s->G, 0, (size_t)n * Fc * 16, st));
+    pfr::launch_functional(fa, s->X, Fc, nv, q0, nullptr, s->loss_terms, s->G, st);
+    pfr::RhsDesc rg;
+    rg.G = s->G;
+    if ((rc = solve_all(s, 2, 2, rg, nullptr, s->Y, st)) || (rc = solve_all(s, 3, 0, rg, s->Y, s->XA, st))) return rc;
+    pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->XA, s->X, Fc, s->partial, st);
+    pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st);
+    pfr::launch_reduce(s->partial, kContractBlocks, s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
+                       reinterpret_cast<double2*>(w_dev), loss_dev, st);
+    // second order, per direction i (same factors):
+    //   A dx_i = db_i - dA_i x ;  A^T dl_i = dG_i(dx_i) - dA_i^T l
+    //   h_ki += sum_q [ -dl_i^T S_k x + e_k dl_i^T b0 - l^T S_k dx_i ]
+    for (int i = 0; i < n_dir; ++i) {
+      const double2* Kd = s->Kdir + (int64_t)i * s->nnz;
+      pfr::launch_tangent_spmv(s->d_rptr, s->d_ridx, s->d_rnz, (int)n, Kd, s->X, Fc, s->rhsP, beta[i], s->G, 0, st);
+      if ((rc = solve_all(s, 0, 2, rg, nullptr, s->Y, st)) || (rc = solve_all(s, 1, 0, rd, s->Y, s->DX, st)))
+        return rc;
+      HIP_TRY(hipMemsetAsync(s->G, 0, (size_t)n * Fc * 16, st));
+      pfr::launch_functional_tangent(fa, s->X, s->DX, Fc, nv, q0, s->G, st);
+      pfr::launch_tangent_spmv(s->d_cptr, s->d_cidx, s->d_cnz, (int)n, Kd, s->XA, Fc, nullptr, make_double2(0, 0),
+                               s->G, 1, st);
+      if ((rc = solve_all(s, 2, 2, rg, nullptr, s->Y, st)) || (rc = solve_all(s, 3, 0, rg, s->Y, s->DL, st)))
+        return rc;
+      pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->DL, s->X, Fc, s->partial,
+                           st);
+      pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->DL, Fc, s->tq, st);
+      pfr::launch_reduce(s->partial, kContractBlocks, s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
+                         H + (int64_t)i * s->n_stiff, nullptr, st);
+      pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->XA, s->DX, Fc,
+                           s->partial, st);
+      pfr::launch_reduce(s->partial, kContractBlocks, s->n_stiff, s->tq, zero, s->loss_terms, nv, Fc,
+                         H + (int64_t)i * s->n_stiff, nullptr, st);
+    }
+    if (flags_dev) pfr::launch_flags_merge(s->flags, nv, flags_dev + q0, st);
+    HIP_TRY(hipGetLastError());
   }
   return PFR_OK;
 }

@@ -771,6 +771,102 @@ __global__ void k_ltsolve_level(DevPattern P, const int* __restrict__ lvl, const
 #undef V
 }
 
+// ------------------------------------------------------------------ Hessian: tangent operators
+// Y[p] = rhsP[p] * beta - sum_e Kd[nz_e] X[idx_e]        (accumulate = 0; forward tangent
+//        right-hand side  db - dA x, rows of the permuted matrix)
+// Y[p] = Y[p]           - sum_e Kd[nz_e] X[idx_e]        (accumulate = 1; with the column
+//        structure: dG - dA^T lambda)
+// One wavefront per row (64 frequencies); the row's index pairs are wave-uniform.
+__global__ __launch_bounds__(256) void k_tangent_spmv(const int* __restrict__ ptr, const int* __restrict__ idx,
+                                                       const int* __restrict__ nzs, int nrows,
+                                                       const cplx* __restrict__ Kd, const cplx* __restrict__ X,
+                                                       int64_t Fc, const double* __restrict__ rhsP, cplx beta,
+                                                       cplx* __restrict__ Y, int accumulate) {
+  const int p = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  if (p >= nrows) return;
+  const int64_t q = (int64_t)blockIdx.y * 64 + (threadIdx.x & 63);
+  cplx acc;
+  if (accumulate) {
+    acc = Y[(int64_t)p * Fc + q];
+  } else {
+    const double r = rhsP ? rhsP[p] : 0.0;
+    acc = make_double2(r * beta.x, r * beta.y);
+  }
+  const int e1 = ptr[p + 1];
+  int e = ptr[p];
+  for (; e + 4 <= e1; e += 4) {
+    cplx k[4], x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      k[u] = Kd[nzs[e + u]];
+      x[u] = X[(int64_t)idx[e + u] * Fc + q];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = cfms(acc, k[u], x[u]);
+  }
+  for (; e < e1; ++e) acc = cfms(acc, Kd[nzs[e]], X[(int64_t)idx[e] * Fc + q]);
+  Y[(int64_t)p * Fc + q] = acc;
+}
+
+// Directional derivative of the loss cotangent G (k_functional) along dx:
+//   G = s h,  s = scale l'(fr) / fr,  h = ts^2 conj(U) aU + ts^2 conj(V) aV + conj(W) aW
+//   dG = ds h + s dh,  ds = scale (l''(fr) / fr - l'(fr) / fr^2) dfr,
+//   dfr = Re(ts^2 conj(U) dU + ts^2 conj(V) dV + conj(W) dW) / fr
+// (second derivatives of the losses of Problem.py:948-975).  Writes the support entries of G.
+__global__ void k_functional_tangent(FunctionalArgs A, const cplx* __restrict__ X, const cplx* __restrict__ DX,
+                                     int64_t Fc, int nvalid, int64_t q_global0, cplx* __restrict__ G) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Fc) return;
+  cplx U = make_double2(0, 0), V = U, W = U, dU = U, dV = U, dW = U;
+  for (int s = 0; s < A.n_support; ++s) {
+    const int64_t o = (int64_t)A.pidx[s] * Fc + q;
+    const cplx x = X[o], d = DX[o];
+    const double au = A.a[s], av = A.a[A.n_support + s], aw = A.a[2 * A.n_support + s];
+    U.x = fma(au, x.x, U.x); U.y = fma(au, x.y, U.y);
+    V.x = fma(av, x.x, V.x); V.y = fma(av, x.y, V.y);
+    W.x = fma(aw, x.x, W.x); W.y = fma(aw, x.y, W.y);
+    dU.x = fma(au, d.x, dU.x); dU.y = fma(au, d.y, dU.y);
+    dV.x = fma(av, d.x, dV.x); dV.y = fma(av, d.y, dV.y);
+    dW.x = fma(aw, d.x, dW.x); dW.y = fma(aw, d.y, dW.y);
+  }
+  const double ts2 = A.ts * A.ts;
+  const double fr = sqrt(ts2 * (U.x * U.x + U.y * U.y) + ts2 * (V.x * V.x + V.y * V.y) + W.x * W.x + W.y * W.y);
+  double s = 0.0, ds = 0.0;
+  if (q < nvalid && fr > 0.0) {
+    const double dfr =
+        (ts2 * (U.x * dU.x + U.y * dU.y) + ts2 * (V.x * dV.x + V.y * dV.y) + W.x * dW.x + W.y * dW.y) / fr;
+    const cplx r = A.ref[q_global0 + q];
+    const double rabs = sqrt(r.x * r.x + r.y * r.y);
+    double d1 = 0.0, d2 = 0.0;   // l'(fr), l''(fr)
+    switch (A.loss_type) {
+      case PFR_LOSS_MSE: d1 = 2.0 * (fr - r.x); d2 = 2.0; break;
+      case PFR_LOSS_RMSE: d1 = 2.0 * (fr - r.x) / (rabs * rabs); d2 = 2.0 / (rabs * rabs); break;
+      case PFR_LOSS_MSE_AFC: d1 = 2.0 * (fr - rabs); d2 = 2.0; break;
+      case PFR_LOSS_MSE_LOG_AFC: {
+        const double d = log(fr) - log(rabs);
+        d1 = 2.0 * d / fr;
+        d2 = 2.0 * (1.0 - d) / (fr * fr);
+      } break;
+      default: break;
+    }
+    s = A.scale * d1 / fr;
+    ds = A.scale * (d2 / fr - d1 / (fr * fr)) * dfr;
+  }
+  // dG = ds h + s dh, h and dh share the support
+  const cplx hU = make_double2(ts2 * U.x, -ts2 * U.y), hV = make_double2(ts2 * V.x, -ts2 * V.y),
+             hW = make_double2(W.x, -W.y);
+  const cplx kU = make_double2(ts2 * dU.x, -ts2 * dU.y), kV = make_double2(ts2 * dV.x, -ts2 * dV.y),
+             kW = make_double2(dW.x, -dW.y);
+  const cplx cU = make_double2(ds * hU.x + s * kU.x, ds * hU.y + s * kU.y);
+  const cplx cV = make_double2(ds * hV.x + s * kV.x, ds * hV.y + s * kV.y);
+  const cplx cW = make_double2(ds * hW.x + s * kW.x, ds * hW.y + s * kW.y);
+  for (int t = 0; t < A.n_support; ++t) {
+    const double au = A.a[t], av = A.a[A.n_support + t], aw = A.a[2 * A.n_support + t];
+    G[(int64_t)A.pidx[t] * Fc + q] =
+        make_double2(au * cU.x + av * cV.x + aw * cW.x, au * cU.y + av * cV.y + aw * cW.y);
+  }
+}
+
 // ------------------------------------------------------------------ K4: functional + loss cotangent
 // U = aU.x, V = aV.x, W = aW.x; fr = sqrt(ts^2|U|^2 + ts^2|V|^2 + |W|^2)  (Problem.py:454-477)
 // loss terms of Problem.py:948-975; g = dl/fr * (ts^2 conj(U) aU + ts^2 conj(V) aV + conj(W) aW)
@@ -1030,6 +1126,18 @@ void launch_solve(int which, int rhs_mode, const DevPattern& P, const int* lvl, 
       LAUNCH(k_ltsolve_level, g, b, st, P, lvl, F, Fc, WV, Yin, Out);
       break;
   }
+}
+
+void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nrows, const double2* Kd,
+                         const double2* X, int64_t Fc, const double* rhsP, double2 beta, double2* Y, int accumulate,
+                         hipStream_t st) {
+  LAUNCH(k_tangent_spmv, dim3((nrows + 3) / 4, (unsigned)(Fc / 64)), dim3(256), st, ptr, idx, nzs, nrows, Kd, X, Fc,
+         rhsP, beta, Y, accumulate);
+}
+
+void launch_functional_tangent(const FunctionalArgs& A, const double2* X, const double2* DX, int64_t Fc, int nvalid,
+                               int64_t q0, double2* G, hipStream_t st) {
+  LAUNCH(k_functional_tangent, dim3((unsigned)((Fc + 63) / 64)), dim3(64), st, A, X, DX, Fc, nvalid, q0, G);
 }
 
 void launch_functional(const FunctionalArgs& A, const double2* X, int64_t Fc, int nvalid, int64_t q0, double* fr_out,

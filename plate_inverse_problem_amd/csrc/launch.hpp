@@ -31,6 +31,13 @@ void launch_schur(const DevPattern& P, const int4* tiles, int ntiles, const int*
 void launch_solve(int which, int rhs_mode, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups,
                   const double2* F, int64_t Fc, double2* WV, const RhsDesc& rd, const double2* Yin, double2* Out,
                   hipStream_t st);
+// Hessian sweep: tangent right-hand sides (rows of the permuted matrix, or of its
+// transpose with accumulate = 1) and the directional derivative of the loss cotangent
+void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nrows, const double2* Kd,
+                         const double2* X, int64_t Fc, const double* rhsP, double2 beta, double2* Y, int accumulate,
+                         hipStream_t st);
+void launch_functional_tangent(const FunctionalArgs& A, const double2* X, const double2* DX, int64_t Fc, int nvalid,
+                               int64_t q0, double2* G, hipStream_t st);
 void launch_functional(const FunctionalArgs& A, const double2* X, int64_t Fc, int nvalid, int64_t q0, double* fr_out,
                        double* loss_terms, double2* G, hipStream_t st);
 void launch_contract(const DevPattern& P, const double* stiff, int n_stiff, int64_t nnz, int nblk, int ngroups,

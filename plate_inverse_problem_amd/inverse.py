@@ -75,6 +75,11 @@ def solve_inverse(prob, arg0, loss_type: str, optimizer: str, compression=(False
     local = next((fn for names, fn in _LOCAL.items() if optimizer in names), None)
     if local is not None:
         fn, call_x0 = local, x0
+        if local is opt.optimize_trust_region and 'model' not in opt_kwargs and opt_kwargs.get('exact_hessian', True):
+            # exact Hessian from one GPU sweep per model (factors reused per direction)
+            opt_kwargs['model'] = prob.getLossHessianFunction(ref_fr[0], ref_fr[1], loss_type, scaling,
+                                                              distributed=distributed)
+        opt_kwargs.pop('exact_hessian', None)
     elif optimizer in ('de', 'shgo'):
         def np_loss(x):
             return float(loss(torch.as_tensor(np.asarray(x, dtype=np.float64))))

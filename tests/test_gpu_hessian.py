@@ -1,0 +1,53 @@
+"""GPU: exact loss Hessian with the factors reused.
+
+The reference forms the Hessian as ``jax.jacobian(grad)`` (``Optimizers.py:125-136``),
+i.e. forward-over-reverse through the spsolve rules; its exact value is checked here
+against central differences of the adjoint gradient (itself oracle-pinned in
+``test_gpu_parity.py``) and its first-order outputs against ``getLossFunction``.
+"""
+import numpy as np
+import pytest
+
+from helpers import make_problem
+from plate_inverse_problem_amd import Optimizers as opt
+
+pytestmark = pytest.mark.gpu
+
+FREQS = np.linspace(40, 600, 160)
+
+
+def _case(material, loss_type, rel):
+    p = make_problem(material, ny=4, device="cuda:0")
+    ref = p.solveForward(FREQS).astype(np.complex128)
+    theta0 = np.asarray(p.parameters, dtype=np.float64)
+    x = 1.0 + np.asarray(rel[:theta0.size])           # scaled parameters (scaling = theta_true)
+    loss = p.getLossFunction(FREQS, ref, loss_type, theta0)
+    model = p.getLossHessianFunction(FREQS, ref, loss_type, theta0)
+    return loss, model, x
+
+
+@pytest.mark.parametrize("material,loss_type", [("orthotropic", "MSE_LOG_AFC"), ("isotropic", "MSE"),
+                                                ("isotropic", "RMSE"), ("orthotropic_d4", "MSE_AFC")])
+def test_hessian_matches_fd_of_gradient(material, loss_type):
+    loss, model, x = _case(material, loss_type, [0.03, -0.02, 0.04, 0.02, 0.05, 0.01, -0.01, 0.02])
+    f, g, H = model(x)
+    f_ref, g_ref = opt.value_and_grad(loss)(x)
+    assert abs(f - f_ref) <= 1e-12 * abs(f_ref)
+    np.testing.assert_allclose(g, g_ref, rtol=1e-9, atol=1e-12 * np.abs(g_ref).max())
+    H_fd = opt.fd_hessian(lambda y: opt.value_and_grad(loss)(y)[1], x, rel=1e-5)
+    scale = np.abs(H).max()
+    assert np.abs(H - H.T).max() <= 1e-12 * scale
+    err = np.abs(H - H_fd).max() / scale
+    assert err < 2e-5, (err, H, H_fd)
+
+
+def test_trust_region_uses_exact_hessian():
+    """'tr' (reference get_model_newt) with the factor-reusing Hessian recovers theta_true."""
+    p = make_problem("orthotropic", ny=4, device="cuda:0")
+    freq = np.linspace(40, 600, 256)
+    fr = p.solveForward(freq)
+    res = p.solveInverse([0.02, -0.02, 0.03, 0.01, 0.05], 'MSE_LOG_AFC', 'tr', ref_fr=[freq, fr], use_rel=True,
+                         use_scaling=True, log=False, report=False, N_steps=15, delta_max=0.2)
+    rel = np.abs(res.x - p.parameters) / p.parameters
+    assert res.f_history[-1] < 1e-3 * res.f_history[0]
+    assert rel[0] < 1e-3 and rel[2] < 1e-3

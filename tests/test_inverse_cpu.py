@@ -48,6 +48,21 @@ def test_trust_region_converges():
     assert np.allclose(r.x, xs, atol=1e-5)
 
 
+def test_trust_region_with_exact_model():
+    """``model(x) -> (f, g, H)`` (Problem.getLossHessianFunction's contract) replaces the FD Hessian."""
+    f, xs = _quad()
+    A = np.array([[3.0, 0.5, 0.0], [0.5, 2.0, 0.3], [0.0, 0.3, 1.0]])
+    calls = []
+
+    def model(x):
+        calls.append(x.copy())
+        d = x - xs
+        return 0.5 * d @ A @ d, A @ d, A
+
+    r = O.optimize_trust_region(f, np.zeros(3), N_steps=30, delta_max=10.0, model=model)
+    assert np.allclose(r.x, xs, atol=1e-10) and len(calls) >= 1
+
+
 def test_lbfgs_converges():
     f, xs = _quad()
     r = O.optimize_lbfgs(f, np.zeros(3), N_steps=20)
