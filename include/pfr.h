@@ -113,6 +113,16 @@ PFR_API int32_t pfr_solver_max_batch(const pfr_solver* s);
 PFR_API int pfr_solve(pfr_solver* s, int32_t batch, const double* data_dev, int64_t data_stride,
                       const double* b_dev, int64_t b_stride, double* x_dev, int32_t transpose,
                       int32_t* flags_dev, void* stream);
+
+/* Several right-hand sides per matrix on the same factors: the reference's batching mode 4
+ * (data (B, nnz), b (J, B, N), Sparse.py:245-282, used by jax.hessian), which refactorises for every
+ * right-hand side (InnerState.h:289-305).  b of rhs r, item q at b_dev + 2 * (r * b_rhs_stride +
+ * q * b_stride) doubles (b_stride 0 = broadcast); x of rhs r at x_dev + 2 * r * x_rhs_stride
+ * (items contiguous, stride n; x_rhs_stride >= batch * n when nrhs > 1). */
+PFR_API int pfr_solve_multi(pfr_solver* s, int32_t batch, int32_t nrhs, const double* data_dev,
+                            int64_t data_stride, const double* b_dev, int64_t b_stride, int64_t b_rhs_stride,
+                            double* x_dev, int64_t x_rhs_stride, int32_t transpose, int32_t* flags_dev,
+                            void* stream);
 /* pfr_matvec: y[q] = A_q x[q] (or A_q^T x[q]); replaces InnerState::matvec (InnerState.h:310-470). */
 PFR_API int pfr_matvec(pfr_solver* s, int32_t batch, const double* data_dev, int64_t data_stride,
                        const double* x_dev, int64_t x_stride, double* y_dev, int32_t transpose, void* stream);

@@ -108,6 +108,22 @@ def _raw_solve(num, data, b, transpose):
     return x
 
 
+def _raw_solve_multi(num, data, b, transpose):
+    """data (nnz,) or (B, nnz); b (J, B, N) complex; every right-hand side on the same factors."""
+    data, b = data.resolve_conj().contiguous(), b.resolve_conj().contiguous()
+    e = _SOLVER_STATE.entry(num)
+    J, B = b.shape[0], b.shape[1]
+    s = _SOLVER_STATE.solver(num, b.device, B)
+    ds = 0 if data.dim() == 1 else e["nnz"]
+    x = torch.empty_like(b)
+    flags = torch.zeros(B, dtype=torch.int32, device=b.device)
+    s.solve_multi(torch.view_as_real(data), ds, torch.view_as_real(b), e["N"], B * e["N"], torch.view_as_real(x),
+                  B * e["N"], transpose, B, J, flags)
+    if int((flags != 0).sum()):
+        raise _native.NativeError("zero/non-finite static pivot in spsolve (matrix singular in the fixed order)")
+    return x
+
+
 def _raw_matvec(num, data, v, transpose):
     data, v = data.resolve_conj().contiguous(), v.resolve_conj().contiguous()
     e = _SOLVER_STATE.entry(num)
@@ -136,6 +152,30 @@ class _Solve(torch.autograd.Function):
         if ctx.transpose:
             rows, cols = cols, rows
         gA = -(gb[:, rows] * torch.conj(x[:, cols]))
+        if data.dim() == 1:
+            gA = gA.sum(0)
+        return gA, gb, None, None
+
+
+class _SolveMulti(torch.autograd.Function):
+    """Mode 4: b (J, B, N), data (B, nnz) or (nnz,); one factorisation per matrix."""
+
+    @staticmethod
+    def forward(ctx, data, b, num, transpose):
+        x = _raw_solve_multi(num, data, b, transpose)
+        ctx.save_for_backward(data, x)
+        ctx.num, ctx.transpose = num, transpose
+        return x
+
+    @staticmethod
+    def backward(ctx, gx):
+        data, x = ctx.saved_tensors
+        e = _SOLVER_STATE.entry(ctx.num)
+        gb = torch.conj(_raw_solve_multi(ctx.num, data, torch.conj(gx).contiguous(), not ctx.transpose))
+        rows, cols = e["rows"].to(x.device), e["cols"].to(x.device)
+        if ctx.transpose:
+            rows, cols = cols, rows
+        gA = -(gb[:, :, rows] * torch.conj(x[:, :, cols])).sum(0)
         if data.dim() == 1:
             gA = gA.sum(0)
         return gA, gb, None, None
@@ -174,7 +214,10 @@ def _batched(fn, data, b, solver_num, transpose):
     elif v.dim() == 2:                                   # modes 2 / 3
         out = fn(d, v, solver_num, transpose)
     elif v.dim() == 3:                                   # mode 4: b (J, B, N), data (B, nnz)
-        out = torch.stack([fn(d, v[j], solver_num, transpose) for j in range(v.shape[0])])
+        if fn is _Solve.apply:                           # all J right-hand sides on the same factors
+            out = _SolveMulti.apply(d, v.contiguous(), solver_num, transpose)
+        else:
+            out = torch.stack([fn(d, v[j], solver_num, transpose) for j in range(v.shape[0])])
     else:
         raise NotImplementedError(f"Batching of spsolve with arguments shapes: {data.shape=}, {b.shape=}")
     return out.real if real else out

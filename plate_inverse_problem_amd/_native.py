@@ -68,6 +68,8 @@ _PROTOS = {
     "pfr_set_rhs": (C.c_int, [_P, _DP, C.c_double, C.c_double, C.c_double]),
     "pfr_set_functional": (C.c_int, [_P, C.c_int32, _I32P, _DP, C.c_double]),
     "pfr_sweep": (C.c_int, [_P, C.c_int32, _P, C.c_int32, _P, C.c_double, _P, _P, _P, _P, _P]),
+    "pfr_solve_multi": (C.c_int, [_P, C.c_int32, C.c_int32, _P, C.c_int64, _P, C.c_int64, C.c_int64, _P, C.c_int64,
+                                  C.c_int32, _P, _P]),
     "pfr_hessian_sweep": (C.c_int, [_P, C.c_int32, _P, C.c_int32, _P, C.c_double, C.c_int32, _P, _P, _P, _P, _P,
                                     _P]),
     "pfr_set_timing": (C.c_int, [_P, C.c_int32]),
@@ -253,6 +255,12 @@ class Solver:
     def solve(self, data, data_stride, b, b_stride, x, transpose, batch, flags=None):
         check(lib().pfr_solve(self._h, int(batch), _ptr(data), int(data_stride), _ptr(b), int(b_stride), _ptr(x),
                               int(bool(transpose)), _ptr(flags), self._stream(x)), "pfr_solve")
+
+    def solve_multi(self, data, data_stride, b, b_stride, b_rhs_stride, x, x_rhs_stride, transpose, batch, nrhs,
+                    flags=None):
+        check(lib().pfr_solve_multi(self._h, int(batch), int(nrhs), _ptr(data), int(data_stride), _ptr(b),
+                                    int(b_stride), int(b_rhs_stride), _ptr(x), int(x_rhs_stride),
+                                    int(bool(transpose)), _ptr(flags), self._stream(x)), "pfr_solve_multi")
 
     def matvec(self, data, data_stride, x, x_stride, y, transpose, batch):
         check(lib().pfr_matvec(self._h, int(batch), _ptr(data), int(data_stride), _ptr(x), int(x_stride), _ptr(y),

@@ -867,12 +867,15 @@ int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int
   return PFR_OK;
 }
 
-int pfr_solve(pfr_solver* s, int32_t batch, const double* data_dev, int64_t data_stride, const double* b_dev,
-              int64_t b_stride, double* x_dev, int32_t transpose, int32_t* flags_dev, void* stream) {
-  if (!s || batch <= 0 || !data_dev || !b_dev || !x_dev || data_stride < 0 || b_stride < 0)
+int pfr_solve_multi(pfr_solver* s, int32_t batch, int32_t nrhs, const double* data_dev, int64_t data_stride,
+                    const double* b_dev, int64_t b_stride, int64_t b_rhs_stride, double* x_dev, int64_t x_rhs_stride,
+                    int32_t transpose, int32_t* flags_dev, void* stream) {
+  if (!s || batch <= 0 || nrhs <= 0 || !data_dev || !b_dev || !x_dev || data_stride < 0 || b_stride < 0 ||
+      b_rhs_stride < 0 || x_rhs_stride < 0)
     return fail(PFR_ERR_ARG, "bad solve arguments");
   if (data_stride != 0 && data_stride < s->nnz) return fail(PFR_ERR_ARG, "data_stride < nnz");
   if (b_stride != 0 && b_stride < s->n) return fail(PFR_ERR_ARG, "b_stride < n");
+  if (nrhs > 1 && x_rhs_stride < (int64_t)batch * s->n) return fail(PFR_ERR_ARG, "x_rhs_stride < batch * n");
   HIP_TRY(hipSetDevice(s->device));
   hipStream_t st = (hipStream_t)stream;
   reset_timing(s);
@@ -889,28 +892,40 @@ int pfr_solve(pfr_solver* s, int32_t batch, const double* data_dev, int64_t data
     int rc = factor_all(s, 1, data + q0 * data_stride, data_stride, nv, st);
     if (rc) return rc;
     record(s, 1, st);
-    pfr::RhsDesc rd;
-    rd.B = B + q0 * b_stride;
-    rd.b_stride = b_stride;
-    rd.nvalid = nv;
-    if (!transpose) {
-      if ((rc = solve_all(s, 0, 1, rd, nullptr, s->Y, st))) return rc;
-      if ((rc = solve_all(s, 1, 1, rd, s->Y, s->X, st))) return rc;
-    }
-    record(s, 2, st);
-    record(s, 3, st);
-    if (transpose) {
-      if ((rc = solve_all(s, 2, 1, rd, nullptr, s->Y, st))) return rc;
-      if ((rc = solve_all(s, 3, 1, rd, s->Y, s->X, st))) return rc;
+    // every right-hand side of the chunk on the same factors (reference mode 4
+    // refactorises per right-hand side, InnerState.h:289-305)
+    for (int32_t r = 0; r < nrhs; ++r) {
+      pfr::RhsDesc rd;
+      rd.B = B + r * b_rhs_stride + q0 * b_stride;
+      rd.b_stride = b_stride;
+      rd.nvalid = nv;
+      if (!transpose) {
+        if ((rc = solve_all(s, 0, 1, rd, nullptr, s->Y, st))) return rc;
+        if ((rc = solve_all(s, 1, 1, rd, s->Y, s->X, st))) return rc;
+      }
+      if (r == 0) {
+        record(s, 2, st);
+        record(s, 3, st);
+      }
+      if (transpose) {
+        if ((rc = solve_all(s, 2, 1, rd, nullptr, s->Y, st))) return rc;
+        if ((rc = solve_all(s, 3, 1, rd, s->Y, s->X, st))) return rc;
+      }
+      pfr::launch_unpermute(s->P.perm, s->n, s->X, Fc, nv, Xo + r * x_rhs_stride + q0 * s->n, st);
     }
     record(s, 4, st);
-    pfr::launch_unpermute(s->P.perm, s->n, s->X, Fc, nv, Xo + q0 * s->n, st);
     record(s, 5, st);
     if (flags_dev) pfr::launch_flags_merge(s->flags, nv, flags_dev + q0, st);
     HIP_TRY(hipGetLastError());
     if ((rc = finish_timing(s, used))) return rc;
   }
   return PFR_OK;
+}
+
+int pfr_solve(pfr_solver* s, int32_t batch, const double* data_dev, int64_t data_stride, const double* b_dev,
+              int64_t b_stride, double* x_dev, int32_t transpose, int32_t* flags_dev, void* stream) {
+  return pfr_solve_multi(s, batch, 1, data_dev, data_stride, b_dev, b_stride, 0, x_dev, 0, transpose, flags_dev,
+                         stream);
 }
 
 int pfr_matvec(pfr_solver* s, int32_t batch, const double* data_dev, int64_t data_stride, const double* x_dev,
