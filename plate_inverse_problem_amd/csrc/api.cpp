@@ -44,7 +44,7 @@ int upload(T** dst, const std::vector<T>& src) {
 
 int64_t round64(int64_t x) { return (x + 63) / 64 * 64; }
 
-constexpr int kContractBlocks = 64;
+constexpr int kContractBlocks = 256;    // nonzero ranges per frequency group
 }  // namespace
 
 struct pfr_solver {
@@ -632,7 +632,7 @@ int pfr_set_stiffness(pfr_solver* s, int32_t n_stiff, const double* stiff_dev, c
   for (int k = 0; k < n_stiff; ++k) s->e.re[k] = w[k];
   if (!s->partial) {
     HIP_TRY(hipSetDevice(s->device));
-    int rc = s->alloc(&s->partial, (int64_t)kContractBlocks * 18 * s->Fc);
+    int rc = s->alloc(&s->partial, (int64_t)kContractBlocks * 18 * (s->Fc / 64));
     if (rc) return rc;
   }
   return PFR_OK;
@@ -756,10 +756,10 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
       if ((rc = solve_all(s, 2, 2, rg, nullptr, s->Y, st))) return rc;
       if ((rc = solve_all(s, 3, 0, rg, s->Y, s->XA, st))) return rc;
       record(s, 4, st);
-      pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->XA, s->X, Fc, s->partial,
+      pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->XA, s->X, Fc, nv, s->partial,
                            st);
       pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st);
-      pfr::launch_reduce(s->partial, kContractBlocks, s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
+      pfr::launch_reduce(s->partial, kContractBlocks * ngroups, s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
                          reinterpret_cast<double2*>(w_dev), loss_dev, st);
     } else {
       record(s, 4, st);
@@ -833,9 +833,9 @@ int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int
     pfr::RhsDesc rg;
     rg.G = s->G;
     if ((rc = solve_all(s, 2, 2, rg, nullptr, s->Y, st)) || (rc = solve_all(s, 3, 0, rg, s->Y, s->XA, st))) return rc;
-    pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->XA, s->X, Fc, s->partial, st);
+    pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->XA, s->X, Fc, nv, s->partial, st);
     pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st);
-    pfr::launch_reduce(s->partial, kContractBlocks, s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
+    pfr::launch_reduce(s->partial, kContractBlocks * ngroups, s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
                        reinterpret_cast<double2*>(w_dev), loss_dev, st);
     // second order, per direction i (same factors):
     //   A dx_i = db_i - dA_i x ;  A^T dl_i = dG_i(dx_i) - dA_i^T l
@@ -851,14 +851,14 @@ int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int
                                s->G, 1, st);
       if ((rc = solve_all(s, 2, 2, rg, nullptr, s->Y, st)) || (rc = solve_all(s, 3, 0, rg, s->Y, s->DL, st)))
         return rc;
-      pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->DL, s->X, Fc, s->partial,
+      pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->DL, s->X, Fc, nv, s->partial,
                            st);
       pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->DL, Fc, s->tq, st);
-      pfr::launch_reduce(s->partial, kContractBlocks, s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
+      pfr::launch_reduce(s->partial, kContractBlocks * ngroups, s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
                          H + (int64_t)i * s->n_stiff, nullptr, st);
-      pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->XA, s->DX, Fc,
+      pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->XA, s->DX, Fc, nv,
                            s->partial, st);
-      pfr::launch_reduce(s->partial, kContractBlocks, s->n_stiff, s->tq, zero, s->loss_terms, nv, Fc,
+      pfr::launch_reduce(s->partial, kContractBlocks * ngroups, s->n_stiff, s->tq, zero, s->loss_terms, nv, Fc,
                          H + (int64_t)i * s->n_stiff, nullptr, st);
     }
     if (flags_dev) pfr::launch_flags_merge(s->flags, nv, flags_dev + q0, st);

@@ -938,9 +938,10 @@ __global__ void k_functional(FunctionalArgs A, const cplx* __restrict__ X, int64
 // s_{q,k} = sum_nz stiff[nz][k] * Lam[prow] * X[pcol]   (Sparse.py:173-176 matrix cotangent,
 // contracted with the stiffness matrices as JAX's einsum transpose does)
 constexpr int NSTIFF_MAX = 18;
-__global__ void k_contract(DevPattern P, const double* __restrict__ stiff, int n_stiff, int64_t nnz, int64_t nz_per_blk,
-                           const cplx* __restrict__ Lam, const cplx* __restrict__ X, int64_t Fc,
-                           cplx* __restrict__ partial) {
+__global__ __launch_bounds__(64) void k_contract(DevPattern P, const double* __restrict__ stiff, int n_stiff,
+                                                 int64_t nnz, int64_t nz_per_blk, const cplx* __restrict__ Lam,
+                                                 const cplx* __restrict__ X, int64_t Fc, int nvalid,
+                                                 cplx* __restrict__ partial) {
   const int lane = threadIdx.x & 63;
   const int64_t q = (int64_t)blockIdx.y * 64 + lane;
   const int64_t nz0 = (int64_t)blockIdx.x * nz_per_blk;
@@ -948,10 +949,29 @@ __global__ void k_contract(DevPattern P, const double* __restrict__ stiff, int n
   cplx acc[NSTIFF_MAX];
 #pragma unroll
   for (int k = 0; k < NSTIFF_MAX; ++k) acc[k] = make_double2(0, 0);
-  for (int64_t nz = nz0; nz < nz1; ++nz) {
-    const cplx l = Lam[(int64_t)P.prow[nz] * Fc + q];
-    const cplx x = X[(int64_t)P.pcol[nz] * Fc + q];
-    const cplx p = cmul(l, x);
+  int64_t nz = nz0;
+  // 4 nonzeros per step: their 8 vector loads are in flight together
+  for (; nz + 4 <= nz1; nz += 4) {
+    cplx pv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const cplx l = Lam[(int64_t)P.prow[nz + u] * Fc + q];
+      const cplx x = X[(int64_t)P.pcol[nz + u] * Fc + q];
+      pv[u] = cmul(l, x);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const double* s = stiff + (nz + u) * n_stiff;
+#pragma unroll
+      for (int k = 0; k < NSTIFF_MAX; ++k)
+        if (k < n_stiff) {
+          acc[k].x = fma(s[k], pv[u].x, acc[k].x);
+          acc[k].y = fma(s[k], pv[u].y, acc[k].y);
+        }
+    }
+  }
+  for (; nz < nz1; ++nz) {
+    const cplx p = cmul(Lam[(int64_t)P.prow[nz] * Fc + q], X[(int64_t)P.pcol[nz] * Fc + q]);
     const double* s = stiff + nz * n_stiff;
 #pragma unroll
     for (int k = 0; k < NSTIFF_MAX; ++k)
@@ -960,9 +980,19 @@ __global__ void k_contract(DevPattern P, const double* __restrict__ stiff, int n
         acc[k].y = fma(s[k], p.y, acc[k].y);
       }
   }
+  // sum over the wave's frequencies (padded lanes excluded): one partial per block
+  const bool valid = q < nvalid;
 #pragma unroll
   for (int k = 0; k < NSTIFF_MAX; ++k)
-    if (k < n_stiff) partial[((int64_t)blockIdx.x * n_stiff + k) * Fc + q] = acc[k];
+    if (k < n_stiff) {
+      double re = valid ? acc[k].x : 0.0, im = valid ? acc[k].y : 0.0;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        re += __shfl_xor(re, o);
+        im += __shfl_xor(im, o);
+      }
+      if (lane == 0) partial[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * n_stiff + k] = make_double2(re, im);
+    }
 }
 
 // t_q = sum_p Lam[p] * rhsP[p] over the Dirichlet support (d b / d beta)
@@ -981,26 +1011,25 @@ __global__ void k_rhs_dot(const int* __restrict__ sup, const double* __restrict_
 
 // Deterministic reduction over (blocks, valid frequencies):
 //   w[k] += sum_q ( -sum_blk partial[blk][k][q] + e_k * t_q ),  loss += sum_q loss_terms[q]
-__global__ void k_reduce(const cplx* __restrict__ partial, int nblk, int n_stiff, const cplx* __restrict__ t_q,
+__global__ void k_reduce(const cplx* __restrict__ partial, int nparts, int n_stiff, const cplx* __restrict__ t_q,
                          CoefPack e, const double* __restrict__ loss_terms, int nvalid, int64_t Fc,
                          cplx* __restrict__ w_out, double* __restrict__ loss_out) {
   __shared__ double sre[256], sim[256];
   const int k = blockIdx.x;   // 0..n_stiff-1: stiffness; n_stiff: loss
   double re = 0, im = 0;
-  for (int q = threadIdx.x; q < nvalid; q += blockDim.x) {
-    if (k < n_stiff) {
-      double pr = 0, pi = 0;
-      for (int b = 0; b < nblk; ++b) {
-        const cplx v = partial[((int64_t)b * n_stiff + k) * Fc + q];
-        pr += v.x;
-        pi += v.y;
-      }
-      const cplx t = t_q[q];
-      re += -pr + e.re[k] * t.x;
-      im += -pi + e.re[k] * t.y;
-    } else {
-      re += loss_terms[q];
+  if (k < n_stiff) {
+    for (int b = threadIdx.x; b < nparts; b += blockDim.x) {
+      const cplx v = partial[(int64_t)b * n_stiff + k];
+      re -= v.x;
+      im -= v.y;
     }
+    for (int q = threadIdx.x; q < nvalid; q += blockDim.x) {
+      const cplx t = t_q[q];
+      re += e.re[k] * t.x;
+      im += e.re[k] * t.y;
+    }
+  } else {
+    for (int q = threadIdx.x; q < nvalid; q += blockDim.x) re += loss_terms[q];
   }
   sre[threadIdx.x] = re;
   sim[threadIdx.x] = im;
@@ -1146,9 +1175,9 @@ void launch_functional(const FunctionalArgs& A, const double2* X, int64_t Fc, in
 }
 
 void launch_contract(const DevPattern& P, const double* stiff, int n_stiff, int64_t nnz, int nblk, int ngroups,
-                     const double2* Lam, const double2* X, int64_t Fc, double2* partial, hipStream_t st) {
+                     const double2* Lam, const double2* X, int64_t Fc, int nvalid, double2* partial, hipStream_t st) {
   int64_t per = (nnz + nblk - 1) / nblk;
-  LAUNCH(k_contract, dim3(nblk, ngroups), dim3(64), st, P, stiff, n_stiff, nnz, per, Lam, X, Fc, partial);
+  LAUNCH(k_contract, dim3(nblk, ngroups), dim3(64), st, P, stiff, n_stiff, nnz, per, Lam, X, Fc, nvalid, partial);
 }
 
 void launch_rhs_dot(const int* sup, const double* val, int n_sup, const double2* Lam, int64_t Fc, double2* t_out,
@@ -1156,10 +1185,10 @@ void launch_rhs_dot(const int* sup, const double* val, int n_sup, const double2*
   LAUNCH(k_rhs_dot, dim3((unsigned)((Fc + 63) / 64)), dim3(64), st, sup, val, n_sup, Lam, Fc, t_out);
 }
 
-void launch_reduce(const double2* partial, int nblk, int n_stiff, const double2* t_q, const CoefPack& e,
+void launch_reduce(const double2* partial, int nparts, int n_stiff, const double2* t_q, const CoefPack& e,
                    const double* loss_terms, int nvalid, int64_t Fc, double2* w_out, double* loss_out,
                    hipStream_t st) {
-  LAUNCH(k_reduce, dim3(n_stiff + 1), dim3(256), st, partial, nblk, n_stiff, t_q, e, loss_terms, nvalid, Fc, w_out,
+  LAUNCH(k_reduce, dim3(n_stiff + 1), dim3(256), st, partial, nparts, n_stiff, t_q, e, loss_terms, nvalid, Fc, w_out,
          loss_out);
 }
 

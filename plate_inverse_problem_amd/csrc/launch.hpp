@@ -41,10 +41,11 @@ void launch_functional_tangent(const FunctionalArgs& A, const double2* X, const 
 void launch_functional(const FunctionalArgs& A, const double2* X, int64_t Fc, int nvalid, int64_t q0, double* fr_out,
                        double* loss_terms, double2* G, hipStream_t st);
 void launch_contract(const DevPattern& P, const double* stiff, int n_stiff, int64_t nnz, int nblk, int ngroups,
-                     const double2* Lam, const double2* X, int64_t Fc, double2* partial, hipStream_t st);
+                     const double2* Lam, const double2* X, int64_t Fc, int nvalid, double2* partial, hipStream_t st);
 void launch_rhs_dot(const int* sup, const double* val, int n_sup, const double2* Lam, int64_t Fc, double2* t_out,
                     hipStream_t st);
-void launch_reduce(const double2* partial, int nblk, int n_stiff, const double2* t_q, const CoefPack& e,
+// w_out[k] += -sum(partial[., k]) + e_k sum_q t_q ;  loss_out += sum_q loss_terms (q < nvalid)
+void launch_reduce(const double2* partial, int nparts, int n_stiff, const double2* t_q, const CoefPack& e,
                    const double* loss_terms, int nvalid, int64_t Fc, double2* w_out, double* loss_out,
                    hipStream_t st);
 void launch_unpermute(const int* perm, int n, const double2* X, int64_t Fc, int nvalid, double2* out, hipStream_t st);
