@@ -61,7 +61,7 @@ struct pfr_solver {
   int4* d_items = nullptr;              // off-diagonal panel items (front, first row/col, kind, record offset)
   int2* d_orec = nullptr;               // per item x lane group x pivot: (nz, first child source) of the entry
   int32_t* d_oxp = nullptr;             // per item: range of further child sources in d_ox
-  int2* d_ox = nullptr;                 // (pivot * 4 + lane group, element id)
+  int2* d_ox = nullptr;                 // (pivot * 4 OFF_RPL + row slot, element id)
   std::vector<int32_t> item_ptr;
   int32_t* d_g1 = nullptr;              // per super-tile, lane group, position: first child source (or -1)
   int32_t* d_gxp = nullptr;             // per super-tile: range of further sources in d_gx
@@ -497,18 +497,18 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
             if (av.size() % 8 == 0) axp.push_back((int32_t)ax.size());
           }
         for (int kind = 0; kind < 2; ++kind)
-          for (int i0 = ns; i0 < f; i0 += 4) {
+          for (int i0 = ns; i0 < f; i0 += 4 * pfr::OFF_RPL) {
             iv.push_back(make_int4(t, i0, kind, (int32_t)orec.size()));
-            for (int sub = 0; sub < 4; ++sub)
+            for (int slot = 0; slot < 4 * pfr::OFF_RPL; ++slot)   // row i0 + slot = i0 + 4 h + lane group
               for (int c = 0; c < ns; ++c) {
-                const int idx = i0 + sub;
+                const int idx = i0 + slot;
                 if (idx >= f) {
                   orec.push_back(make_int2(-1, -1));
                   continue;
                 }
                 const int a = kind == 0 ? idx : c, b = kind == 0 ? c : idx;
                 orec.push_back(make_int2(nzm[(size_t)a * f + b], s1m[(size_t)a * f + b]));
-                for (int32_t id : extras(a, b)) ox.push_back(make_int2(c * 4 + sub, id));
+                for (int32_t id : extras(a, b)) ox.push_back(make_int2(c * 4 * pfr::OFF_RPL + slot, id));
               }
             oxp.push_back((int32_t)ox.size());
           }

@@ -32,6 +32,9 @@ struct DevPattern {
 constexpr int SCHUR_SR = 2, SCHUR_SC = 2, SCHUR_QG = 16;
 static_assert(SCHUR_SR * SCHUR_SC * SCHUR_QG == 64, "one wavefront per super-tile");
 
+// Off-diagonal panel kernel: rows (columns) per lane; a wave covers 4 OFF_RPL of them.
+constexpr int OFF_RPL = 1;
+
 constexpr int COEF_MAX = 32;
 struct CoefPack {
   double re[COEF_MAX];

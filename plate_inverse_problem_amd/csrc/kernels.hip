@@ -320,19 +320,19 @@ constexpr int OB = 8;
 // kernel and read back): record (nz, first child element) per entry, further
 // child elements in the item's overflow list.
 struct OffSrc {
-  const int2* rec;        // this lane group's records, indexed by pivot
-  const int2* ox;         // overflow (pivot * 4 + lane group, element id)
-  int ox0, ox1, sub;
-  double om2;             // MODE 0: omega^2 of this lane's frequency
+  const int2* rec[OFF_RPL];   // this lane's records per row slot, indexed by pivot
+  const int2* ox;             // overflow (pivot * 4 OFF_RPL + slot, element id)
+  int ox0, ox1, slot0;        // slot of row 0 of this lane: h * 4 + lane group
+  double om2;                 // MODE 0: omega^2 of this lane's frequency
   const cplx* K;
   const double* M;
-  const cplx* dq;         // MODE 1: this lane's explicit matrix values
+  const cplx* dq;             // MODE 1: this lane's explicit matrix values
 };
 
 template <int MODE>
 __device__ __forceinline__ cplx off_source(const OffSrc& S, const cplx* __restrict__ F, int64_t Fc, int64_t q,
-                                           int c) {
-  const int2 g = S.rec[c];
+                                           int h, int c) {
+  const int2 g = S.rec[h][c];
   cplx o;
   if (MODE == 0) {
     const cplx k = S.K[max(g.x, 0)];
@@ -345,58 +345,73 @@ __device__ __forceinline__ cplx off_source(const OffSrc& S, const cplx* __restri
   return cadd(g.x >= 0 ? o : z, g.y >= 0 ? ch : z);
 }
 
-// One chunk of NB consecutive columns (kind 0) / rows (kind 1) c0 .. c0+NB-1.
+// One chunk of NB consecutive columns (kind 0) / rows (kind 1) c0 .. c0+NB-1 of
+// this lane's OFF_RPL rows (columns); the shared L11 / U11 values each step loads
+// serve all of them.
 template <int MODE, int NB>
-__device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, int64_t so, int64_t sc, int64_t sa, int64_t sb,
-                                              bool unit, bool valid, int c0, const OffSrc& S,
-                                              const cplx* __restrict__ F, int64_t Fc, int64_t q) {
-  cplx x[NB];
+__device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int64_t (&so)[OFF_RPL], int64_t sc,
+                                              int64_t sa, int64_t sb, bool unit, const bool (&valid)[OFF_RPL],
+                                              int c0, const OffSrc& S, const cplx* __restrict__ F, int64_t Fc,
+                                              int64_t q) {
+  cplx x[OFF_RPL][NB];
 #pragma unroll
-  for (int j = 0; j < NB; ++j) x[j] = off_source<MODE>(S, F, Fc, q, c0 + j);
+  for (int h = 0; h < OFF_RPL; ++h)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) x[h][j] = off_source<MODE>(S, F, Fc, q, h, c0 + j);
   for (int e = S.ox0; e < S.ox1; ++e) {       // rare: several children cover one entry
     const int2 g = S.ox[e];
-    const int c = (g.x >> 2) - c0;
-    if ((g.x & 3) == S.sub && c >= 0 && c < NB) {
+    const int c = g.x / (4 * OFF_RPL) - c0, slot = g.x % (4 * OFF_RPL);
+    if (c >= 0 && c < NB) {
       const cplx v = F[(int64_t)g.y * Fc + q];
 #pragma unroll
-      for (int j = 0; j < NB; ++j)
-        if (j == c) x[j] = cadd(x[j], v);
+      for (int h = 0; h < OFF_RPL; ++h)
+        if (slot == S.slot0 + 4 * h) {
+#pragma unroll
+          for (int j = 0; j < NB; ++j)
+            if (j == c) x[h][j] = cadd(x[h][j], v);
+        }
     }
   }
   // x -= own(0:c0) * shared(0:c0, c0:c0+NB)
 #pragma unroll 2
   for (int t = 0; t < c0; ++t) {
-    const cplx l = base[(so + (int64_t)t * sc) * Fc];
-    cplx u[NB];
+    cplx l[OFF_RPL], u[NB];
+#pragma unroll
+    for (int h = 0; h < OFF_RPL; ++h) l[h] = base[(so[h] + (int64_t)t * sc) * Fc];
 #pragma unroll
     for (int j = 0; j < NB; ++j) u[j] = base[((int64_t)t * sa + (int64_t)(c0 + j) * sb) * Fc];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) x[j] = cfms(x[j], l, u[j]);
+    for (int h = 0; h < OFF_RPL; ++h)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) x[h][j] = cfms(x[h][j], l[h], u[j]);
   }
-  // triangular block shared(c0:c0+NB, c0:c0+NB)
-  cplx T[NB][NB];
-#pragma unroll
-  for (int a = 0; a < NB; ++a)
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-      if (a < b) T[a][b] = base[((int64_t)(c0 + a) * sa + (int64_t)(c0 + b) * sb) * Fc];
-  if (!unit) {
-#pragma unroll
-    for (int a = 0; a < NB; ++a) T[a][a] = crecip(base[((int64_t)(c0 + a) * (sa + sb)) * Fc]);
-  }
+  // triangular block shared(c0:c0+NB, c0:c0+NB), column by column
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
 #pragma unroll
     for (int a = 0; a < NB; ++a)
-      if (a < j) x[j] = cfms(x[j], x[a], T[a][j]);
-    if (!unit) x[j] = cmul(x[j], T[j][j]);
-  }
-  if (valid) {
+      if (a < j) {
+        const cplx t = base[((int64_t)(c0 + a) * sa + (int64_t)(c0 + j) * sb) * Fc];
 #pragma unroll
-    for (int j = 0; j < NB; ++j) base[(so + (int64_t)(c0 + j) * sc) * Fc] = x[j];
+        for (int h = 0; h < OFF_RPL; ++h) x[h][j] = cfms(x[h][j], x[h][a], t);
+      }
+    if (!unit) {
+      const cplx d = crecip(base[((int64_t)(c0 + j) * (sa + sb)) * Fc]);
+#pragma unroll
+      for (int h = 0; h < OFF_RPL; ++h) x[h][j] = cmul(x[h][j], d);
+    }
   }
+#pragma unroll
+  for (int h = 0; h < OFF_RPL; ++h)
+    if (valid[h]) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) base[(so[h] + (int64_t)(c0 + j) * sc) * Fc] = x[h][j];
+    }
 }
 
+// Item = (front, first row / column, kind, record offset): one wave = 16
+// frequencies x 4 lane groups x OFF_RPL rows (columns) per lane = 4 OFF_RPL
+// consecutive rows (columns); row i0 + 4 h + lane group.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_offdiag_level(DevPattern P, const int4* __restrict__ items, int nitems,
                                                         const int2* __restrict__ orec, const int* __restrict__ oxp,
@@ -414,16 +429,27 @@ __global__ __launch_bounds__(256) void k_offdiag_level(DevPattern P, const int4*
   const int4 it = items[wid];
   const Front fr = P.fronts[it.x];
   const int f = fr.f, ns = fr.ns;
-  const int idx = it.y + sub;
-  const bool valid = idx < f;
-  const int r = min(idx, f - 1);
   cplx* __restrict__ base = F + fr.off * Fc + q;
+  // kind 0: own(c) = E(r, c), shared(a, b) = U(a, b) = E(a, b)
+  // kind 1: own(c) = E(c, r), shared(a, b) = L(b, a) = E(b, a)   (transposed roles)
+  const int64_t sc = it.z == 0 ? 1 : f;
+  const int64_t sa = it.z == 0 ? f : 1, sb = it.z == 0 ? 1 : f;  // shared (a, b) at a * sa + b * sb
+  const bool unit = it.z != 0;                                   // L11 has a unit diagonal
   OffSrc S;
-  S.rec = orec + it.w + (int64_t)sub * ns;
+  int64_t so[OFF_RPL];
+  bool valid[OFF_RPL];
+#pragma unroll
+  for (int h = 0; h < OFF_RPL; ++h) {
+    const int idx = it.y + 4 * h + sub;
+    valid[h] = idx < f;
+    const int r = min(idx, f - 1);
+    so[h] = it.z == 0 ? (int64_t)r * f : r;                      // own element c at so + c * sc
+    S.rec[h] = orec + it.w + (int64_t)(4 * h + sub) * ns;
+  }
   S.ox = ox;
   S.ox0 = oxp[wid];
   S.ox1 = oxp[wid + 1];
-  S.sub = sub;
+  S.slot0 = sub;
   S.om2 = 0.0;
   if (MODE == 0) {
     const double om = 6.283185307179586 * freqs[q];
@@ -432,12 +458,6 @@ __global__ __launch_bounds__(256) void k_offdiag_level(DevPattern P, const int4*
   S.K = K;
   S.M = M;
   S.dq = data + min(q, (int64_t)nvalid - 1) * data_stride;
-  // kind 0: own(c) = E(r, c), shared(a, b) = U(a, b) = E(a, b)
-  // kind 1: own(c) = E(c, r), shared(a, b) = L(b, a) = E(b, a)   (transposed roles)
-  const int64_t so = it.z == 0 ? (int64_t)r * f : r;           // own element c at so + c * sc
-  const int64_t sc = it.z == 0 ? 1 : f;
-  const int64_t sa = it.z == 0 ? f : 1, sb = it.z == 0 ? 1 : f;  // shared (a, b) at a * sa + b * sb
-  const bool unit = it.z != 0;                                   // L11 has a unit diagonal
   int c0 = 0;
   for (; c0 + OB <= ns; c0 += OB) offdiag_chunk<MODE, OB>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q);
   switch (ns - c0) {     // wave-uniform tail width
