@@ -206,7 +206,8 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
                         nvalid, st);
     mark(l, 3);
     pfr::launch_schur(s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l],
-                      s->d_g1 + (int64_t)s->tile_ptr[l] * 16 * pfr::SCHUR_SR * pfr::SCHUR_SC, s->d_gxp + s->tile_ptr[l],
+                      s->d_g1 + (int64_t)s->tile_ptr[l] * pfr::SCHUR_TM * pfr::SCHUR_TN * pfr::SCHUR_SR * pfr::SCHUR_SC,
+                      s->d_gxp + s->tile_ptr[l],
                       s->d_gx, ngroups, s->F,
                       s->Fc, st);
     mark(l, 4);
@@ -385,8 +386,10 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
         const int t = S.level_fronts[e];
         const Front& F = S.fronts[t];
         const int r = F.f - F.ns;
-        const int ntj = (r + 3) / 4;          // 4 x 4 tiles per dimension
-        std::vector<std::vector<int32_t>> lists((size_t)ntj * ntj * 16);
+        // children's update-matrix entries per A22 position: the first densely, the
+        // rare further ones (two or more children covering a position) aside
+        std::vector<int32_t> first((size_t)r * r, -1);
+        std::vector<std::pair<int32_t, int32_t>> more;   // (i * r + j, element id)
         for (int c : kids[t]) {
           const Front& C = S.fronts[c];
           const int32_t* rp = S.relpos.data() + C.row0;
@@ -396,34 +399,35 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
             for (int b = C.ns; b < C.f; ++b) {
               const int j = rp[b] - F.ns;
               if (j < 0) continue;
-              lists[((size_t)(i / 4) * ntj + j / 4) * 16 + (i % 4) * 4 + j % 4].push_back(
-                  (int32_t)(C.off + (int64_t)a * C.f + b));
+              const int32_t id = (int32_t)(C.off + (int64_t)a * C.f + b);
+              int32_t& f1 = first[(size_t)i * r + j];
+              if (f1 < 0)
+                f1 = id;
+              else
+                more.emplace_back(i * r + j, id);
             }
           }
         }
-        // 8 x 8 super-tiles = 2 x 2 arrangement of 4 x 4 tiles (one per lane group).
-        // Almost every position has at most one source (one child covers it): that
-        // one is stored densely (64 ids per super-tile, -1 = none) so the kernel
-        // issues all gather loads at once; the rare further sources go to a
-        // per-super-tile overflow list
-        for (int i0 = 0; i0 < r; i0 += 4 * pfr::SCHUR_SR)
-          for (int j0 = 0; j0 < r; j0 += 4 * pfr::SCHUR_SC) {
+        std::sort(more.begin(), more.end());
+        // super-tiles of (SCHUR_TM SCHUR_SR) x (SCHUR_TN SCHUR_SC): lane group `sub` owns the
+        // SCHUR_TM x SCHUR_TN tile at (TM (sub / SC), TN (sub % SC)); per super-tile the dense
+        // first-source ids (-1 = none), lane group by lane group, then one overflow range
+        constexpr int TM = pfr::SCHUR_TM, TN = pfr::SCHUR_TN, SR = pfr::SCHUR_SR, SC = pfr::SCHUR_SC;
+        for (int i0 = 0; i0 < r; i0 += TM * SR)
+          for (int j0 = 0; j0 < r; j0 += TN * SC) {
             tv.push_back(make_int4(t, i0, j0, 0));
-            for (int sub = 0; sub < pfr::SCHUR_SR * pfr::SCHUR_SC; ++sub) {
-              const int ti = i0 / 4 + sub / pfr::SCHUR_SC, tj = j0 / 4 + sub % pfr::SCHUR_SC;
-              for (int pos = 0; pos < 16; ++pos) {
-                int32_t first = -1;
-                if (ti < ntj && tj < ntj) {
-                  const auto& Lp = lists[((size_t)ti * ntj + tj) * 16 + pos];
-                  for (size_t u = 0; u < Lp.size(); ++u)
-                    if (u == 0)
-                      first = Lp[0];
-                    else
-                      gx.push_back(make_int2(sub * 16 + pos, Lp[u]));
+            for (int sub = 0; sub < SR * SC; ++sub)
+              for (int pos = 0; pos < TM * TN; ++pos) {
+                const int i = i0 + TM * (sub / SC) + pos / TN, j = j0 + TN * (sub % SC) + pos % TN;
+                if (i >= r || j >= r) {
+                  g1.push_back(-1);
+                  continue;
                 }
-                g1.push_back(first);
+                g1.push_back(first[(size_t)i * r + j]);
+                auto lo = std::lower_bound(more.begin(), more.end(), std::make_pair(i * r + j, INT32_MIN));
+                for (; lo != more.end() && lo->first == i * r + j; ++lo)
+                  gx.push_back(make_int2(sub * TM * TN + pos, lo->second));
               }
-            }
             gxp.push_back((int32_t)gx.size());
           }
       }

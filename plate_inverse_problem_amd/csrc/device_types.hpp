@@ -28,8 +28,10 @@ struct DevPattern {
 };
 
 // Schur super-tile: a wavefront = SCHUR_QG frequencies x (SCHUR_SR x SCHUR_SC) lane groups,
-// each lane group one 4 x 4 register tile -> (4 SCHUR_SR) x (4 SCHUR_SC) entries per wave.
+// each lane group one SCHUR_TM x SCHUR_TN register tile -> (SCHUR_TM SCHUR_SR) x
+// (SCHUR_TN SCHUR_SC) entries per wave.
 constexpr int SCHUR_SR = 2, SCHUR_SC = 2, SCHUR_QG = 16;
+constexpr int SCHUR_TM = 4, SCHUR_TN = 4;
 static_assert(SCHUR_SR * SCHUR_SC * SCHUR_QG == 64, "one wavefront per super-tile");
 
 // Off-diagonal panel kernel: rows (columns) per lane; a wave covers 4 OFF_RPL of them.

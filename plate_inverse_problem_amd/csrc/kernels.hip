@@ -473,7 +473,7 @@ __global__ __launch_bounds__(256) void k_offdiag_level(DevPattern P, const int4*
 // A22 -= L21 U12 over all ns pivots of the front: one wavefront per TM x TN tile
 // of A22 (64 lanes = 64 frequencies), accumulators in registers, no stores in
 // the K loop so every load of a k-step is independent.
-constexpr int TM = 4, TN = 4;
+constexpr int TM = SCHUR_TM, TN = SCHUR_TN;
 
 // Lane map: a wavefront = SCHUR_QG (16) frequencies x 4 sub-tiles; the 4 sub-tiles
 // form a 2 x 2 arrangement of 4 x 4 tiles (an 8 x 8 super-tile), so each L21 row
@@ -493,8 +493,8 @@ __global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* _
   const int sub = lane / SCHUR_QG;
   const int64_t q = (int64_t)by * SCHUR_QG + lane % SCHUR_QG;
   int4 t = tiles[tid];
-  t.y += 4 * (sub / SCHUR_SC);
-  t.z += 4 * (sub % SCHUR_SC);
+  t.y += TM * (sub / SCHUR_SC);
+  t.z += TN * (sub % SCHUR_SC);
   const Front fr = P.fronts[t.x];
   const int f = fr.f, ns = fr.ns;
   cplx* __restrict__ base = F + fr.off * Fc + q;
@@ -509,10 +509,10 @@ __global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* _
   cplx acc[TM][TN];
   {
     const int4* __restrict__ g4 =
-        reinterpret_cast<const int4*>(g1 + (int64_t)tid * (16 * SCHUR_SR * SCHUR_SC) + sub * 16);
+        reinterpret_cast<const int4*>(g1 + ((int64_t)tid * (SCHUR_SR * SCHUR_SC) + sub) * (TM * TN));
     int src[TM * TN];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < TM * TN / 4; ++u) {
       const int4 v = g4[u];
       src[4 * u] = v.x;
       src[4 * u + 1] = v.y;
@@ -531,13 +531,13 @@ __global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* _
     const int x1 = gxp[tid + 1];
     for (int x = gxp[tid]; x < x1; ++x) {
       const int2 g = gx[x];
-      if ((g.x >> 4) == sub) {
+      if (g.x / (TM * TN) == sub) {
         const cplx v = F[(int64_t)g.y * Fc + q];
 #pragma unroll
         for (int m = 0; m < TM; ++m)
 #pragma unroll
           for (int n = 0; n < TN; ++n)
-            if ((g.x & 15) == m * TN + n) acc[m][n] = cadd(acc[m][n], v);
+            if (g.x % (TM * TN) == m * TN + n) acc[m][n] = cadd(acc[m][n], v);
       }
     }
   }
