@@ -11,11 +11,17 @@ forward + adjoint (loss + gradient), fp64.
   ``linspace(40, 600, 4096 * N)``); one all-reduce (RCCL) of the loss/gradient
   partials per step;
 * ``value`` = 4096 * N / (max-over-ranks seconds per step);
+* each GPU runs ``lanes`` (default 2) solvers on their own HIP streams over
+  contiguous halves of its frequencies, concurrently (one lane's latency-bound
+  top levels overlap the other's bandwidth-bound ones);
 * ``roofline``: the dominant kernel, ``k_schur_level`` (Schur complement of the
-  multifrontal factorisation; HBM-bound), from HIP events bracketing each of its
-  launches on the sweep's stream: algorithmic bytes per launch (the solver's
-  count: A22 stores + gathered children's entries + L21/U12 read once, 16 B per
-  complex entry) / average launch time; ``traffic`` = measured HBM bytes per
+  multifrontal factorisation; HBM-bound): algorithmic bytes per launch (the
+  solver's count: A22 stores + gathered children's entries + L21/U12 read once,
+  16 B per complex entry) / average launch time, from HIP events that libpfr
+  records around every launch on the lane's stream during one isolated lane-0
+  sweep of a full chunk right after the timed region (inside the timed region the
+  lanes overlap, so a launch's duration there also contains the other lane's
+  work: reported as ``concurrent_*``); ``traffic`` = measured HBM bytes per
   launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes
   (profiles/r01/pmc_traffic.json, gfx950-corrected); the whole factorisation
   (``factor_roofline``) and the triangular solves (``sptrsv_roofline``) beside it;
@@ -120,7 +126,7 @@ def main():
     loss_fn = prob.getLossFunction(freqs, ref, "MSE_LOG_AFC", distributed=world > 1)
     eng = prob.engine()
     solver = eng.solver
-    solver.set_timing(True, kernels=True)
+    eng.set_timing(True, kernels=True)
 
     def step():
         x = torch.tensor(theta, requires_grad=True)
@@ -139,8 +145,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         val, grad = step()
-        phase += solver.last_timings()
-        m, n = solver.last_kernel_timings()
+        phase += eng.last_timings()
+        m, n = eng.last_kernel_timings()
         kms += m
         klaunch += n
     torch.cuda.synchronize()
@@ -154,24 +160,43 @@ def main():
     ms_per_step = 1e3 * elapsed / args.steps
     value = n_total / (elapsed / args.steps)
 
+    from plate_inverse_problem_amd import _native
     st = eng.stats
     nv = hi - lo
-    phase /= args.steps                      # ms per step, per phase
+    phase /= args.steps                      # device ms per step, per phase, summed over lanes
     kms /= args.steps
     klaunch /= args.steps
-    factor_flops = st["factor_flops"] * nv
-    fact_tfs = factor_flops / (phase[0] * 1e-3) / 1e12
-    alg = solver.alg_bytes().astype(float) * nv          # algorithmic bytes per step, per kernel class
-    alg_launch = alg / np.maximum(klaunch, 1)
-    ms_launch = kms / np.maximum(klaunch, 1)
+
+    # Kernel rooflines: one isolated sweep (lane 0 alone, its full chunk, same workload and
+    # theta) right after the timed region, HIP events on lane 0's stream around every launch.
+    # In the timed region the two lanes overlap, so per-launch durations there include the
+    # other lane's kernels sharing the GPU (reported as "concurrent_*").
+    chunk = solver.max_batch
+    f_iso = torch.as_tensor(freqs[lo:lo + min(chunk, nv)], device=device)
+    r_iso = torch.as_tensor(ref[lo:lo + f_iso.numel()], device=device)
+    w_iso = torch.zeros(18, dtype=torch.complex128, device=device)
+    l_iso = torch.zeros(1, dtype=torch.float64, device=device)
+    with torch.cuda.stream(eng.streams[0]):
+        solver.sweep(f_iso, _native.LOSS_MSE_LOG_AFC, ref=torch.view_as_real(r_iso), scale=1.0 / n_total, loss=l_iso,
+                     w=torch.view_as_real(w_iso))
+    torch.cuda.synchronize()
+    iso_phase = solver.last_timings()
+    iso_ms, iso_n = solver.last_kernel_timings()
+    n_iso = f_iso.numel()
+    alg_f = solver.alg_bytes().astype(float)             # algorithmic bytes per frequency, per kernel class
+    alg_launch = alg_f * n_iso / np.maximum(iso_n, 1)
+    ms_launch = iso_ms / np.maximum(iso_n, 1)
     gbs = alg_launch / (ms_launch * 1e-3) / 1e9
-    traffic = pmc_traffic(solver.max_batch)
-    fact_alg = float(alg.sum())
-    fact_traffic = None if None in traffic else float(np.dot(traffic, klaunch))
+    traffic = pmc_traffic(chunk)
+    fact_alg = float(alg_f.sum() * n_iso)
+    fact_ms = float(iso_ms.sum())
+    fact_tfs = st["factor_flops"] * n_iso / (iso_phase[0] * 1e-3) / 1e12
+    fact_traffic = None if None in traffic else float(np.dot(traffic, iso_n))
     # triangular solves: 4 passes (L, U, U^T, L^T) over the factors, 16 B per L+U entry
     # per pass per frequency, plus int32 pattern (shared by 64-frequency wavefronts) and vectors
-    trsv_bytes = nv * (4 * 16 * st["nnz_lu"] + 4 * 2 * 16 * st["n"])
-    trsv_gbs = trsv_bytes / ((phase[1] + phase[3]) * 1e-3) / 1e9
+    trsv_bytes = n_iso * (4 * 16 * st["nnz_lu"] + 4 * 2 * 16 * st["n"])
+    trsv_gbs = trsv_bytes / ((iso_phase[1] + iso_phase[3]) * 1e-3) / 1e9
+    conc_launch = kms / np.maximum(klaunch, 1)
     out = {
         "metric": "freq-solves/sec (forward+adjoint) @20k DOF",
         "value": value,
@@ -188,24 +213,29 @@ def main():
         "config": {"workload": "C3: orthotropic CFRP-like plate, sh_i strip 100x20x2 mm + AP1030, "
                                f"{st['n']} DOF, {args.freqs} freqs/GPU in 40-600 Hz, forward+adjoint, "
                                "loss MSE_LOG_AFC + gradient",
-                   "n_dofs": st["n"], "freqs_per_gpu": args.freqs, "chunk": solver.max_batch,
+                   "n_dofs": st["n"], "freqs_per_gpu": args.freqs, "chunk": chunk,
+                   "lanes": eng.n_lanes,
                    "nnz_lu": st["nnz_lu"], "factor_gflop_per_freq": st["factor_flops"] / 1e9,
-                   "parallelism": f"frequency shards x{world} + 1 all-reduce/step"},
+                   "parallelism": f"frequency shards x{world} + 1 all-reduce/step; {eng.n_lanes} concurrent "
+                                  "solver lanes (HIP streams) per GPU"},
         "roofline": {"bound": "hbm", "kernel": "k_schur_level", "achieved": gbs[3], "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": gbs[3] / HBM_PEAK_GBS, "traffic": traffic[3],
                      "alg_bytes_per_launch": alg_launch[3], "avg_launch_ms": ms_launch[3],
-                     "launches_per_step": klaunch[3]},
-        "factor_roofline": {"bound": "hbm", "kernels": list(KERNELS), "ms_per_step": kms.tolist(),
-                            "alg_GBps": gbs.tolist(),
-                            "achieved": fact_alg / (kms.sum() * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                            "unit": "GB/s", "frac": fact_alg / (kms.sum() * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                            "alg_bytes_per_step": fact_alg, "traffic_per_step": fact_traffic,
-                            "fp64_TFLOPs": fact_tfs, "fp64_frac": fact_tfs / FP64_PEAK_TFLOPS},
+                     "launches": int(iso_n[3]), "measured": f"isolated lane-0 sweep of {n_iso} frequencies "
+                     "(one chunk) after the timed region, HIP events per launch",
+                     "concurrent_avg_launch_ms": conc_launch[3]},
+        "factor_roofline": {"bound": "hbm", "kernels": list(KERNELS), "ms": iso_ms.tolist(),
+                            "alg_GBps": gbs.tolist(), "achieved": fact_alg / (fact_ms * 1e-3) / 1e9,
+                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": fact_alg / (fact_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                            "alg_bytes": fact_alg, "traffic": fact_traffic, "frequencies": n_iso,
+                            "fp64_TFLOPs": fact_tfs, "fp64_frac": fact_tfs / FP64_PEAK_TFLOPS,
+                            "concurrent_ms_per_step": kms.tolist()},
         "sptrsv_roofline": {"bound": "hbm", "kernel": "k_{l,u,ut,lt}solve_level", "achieved": trsv_gbs,
                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": trsv_gbs / HBM_PEAK_GBS,
                             "traffic": None},
         "phase_ms": {"factor": phase[0], "fwd_solves": phase[1], "functional": phase[2],
-                     "adj_solves": phase[3], "contract": phase[4]},
+                     "adj_solves": phase[3], "contract": phase[4], "note": "device ms per step summed over lanes"},
         "loss": val,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -45,9 +45,13 @@ def _default_device():
 
 
 class _Engine:
-    """Device state of one Problem: symbolic analysis, solver, operator data."""
+    """Device state of one Problem: symbolic analysis, operator data and ``lanes``
+    solvers, each with its own workspace and HIP stream.  A sweep splits its
+    frequencies into one contiguous block per lane and runs the lanes
+    concurrently, so one lane's latency-bound levels (few large fronts at the top
+    of the elimination tree) overlap the other's bandwidth-bound ones."""
 
-    def __init__(self, prob: "Problem", device, n_freqs: int, max_batch: int | None):
+    def __init__(self, prob: "Problem", device, n_freqs: int, max_batch: int | None, lanes: int | None = None):
         self.device = device
         mats = prob.mats
         # structural pattern of the matrices that can be non-zero: for a mid-plane
@@ -63,13 +67,21 @@ class _Engine:
         colptr = np.cumsum(colptr).astype(np.int32)
         self.sym = _native.Symbolic(n, colptr, rows.astype(np.int32))
         self.stats = self.sym.stats()
+        if lanes is None:
+            lanes = int(os.environ.get("PFR_LANES", "2"))
+        n_freqs = max(1, n_freqs)
+        self.n_lanes = max(1, min(lanes, -(-n_freqs // 64)))
+        per_lane = -(-n_freqs // self.n_lanes)
         if not max_batch:
-            # as many frequencies per chunk as fit in ~60% of free HBM (multiple of 64, <= 4096)
+            # per lane as many frequencies per chunk as fit in its share of ~85% of free
+            # HBM (multiple of 64, <= 4096), even chunks
             free, _ = torch.cuda.mem_get_info(device)
-            cap = max(64, min(4096, int(0.6 * free / self.sym.workspace_bytes(64)) * 64))
-            n_chunks = -(-max(1, n_freqs) // cap)
-            max_batch = (-(-n_freqs // n_chunks) + 63) // 64 * 64   # even chunks, multiple of 64
-        self.solver = _native.Solver(self.sym, device.index, max_batch)
+            cap = max(64, min(4096, int(0.85 * free / self.n_lanes / self.sym.workspace_bytes(64)) * 64))
+            n_chunks = -(-per_lane // cap)
+            max_batch = (-(-per_lane // n_chunks) + 63) // 64 * 64
+        self.solvers = [_native.Solver(self.sym, device.index, max_batch) for _ in range(self.n_lanes)]
+        self.streams = [torch.cuda.Stream(device) for _ in range(self.n_lanes)]
+        self.solver = self.solvers[0]
         vals = mats[:, self.keep]
         self.stiff = torch.as_tensor(np.ascontiguousarray(vals[:18].T), device=device)       # (nnz, 18)
         I0, I0c, I2, I2c = prob.I0, prob.I0Corr, prob.I2, prob.I2Corr
@@ -79,13 +91,19 @@ class _Engine:
         self.mass_sum = I0 + I0c + I2 + I2c
         self.K = torch.empty(self.keep.size, dtype=torch.complex128, device=device)
         self.e = np.concatenate([np.zeros(12), RHS_WEIGHTS_D])
-        self.solver.set_stiffness(self.stiff, self.e)
-        self.solver.set_operator(torch.view_as_real(self.K), self.mass)
         aU, aV, aW = prob.averaging_vectors()
         sup = np.nonzero((aU != 0) | (aV != 0) | (aW != 0))[0]
-        self.solver.set_functional(sup, np.stack([aU[sup], aV[sup], aW[sup]]), prob.accelerometer.transverse_sensitivity)
+        for sv in self.solvers:
+            sv.set_stiffness(self.stiff, self.e)
+            sv.set_operator(torch.view_as_real(self.K), self.mass)      # K(theta) shared by the lanes
+            sv.set_functional(sup, np.stack([aU[sup], aV[sup], aW[sup]]),
+                              prob.accelerometer.transverse_sensitivity)
         self.rhs = prob.vec
         self._coef_key = None
+
+    @property
+    def max_batch(self) -> int:
+        return self.solver.max_batch
 
     def set_coefficients(self, c: np.ndarray):
         """Precombine K(theta) = sum_k c_k S_k on the device and the rhs scale."""
@@ -94,8 +112,62 @@ class _Engine:
             return
         self.solver.combine(c, torch.view_as_real(self.K))
         beta = complex(self.e @ c)
-        self.solver.set_rhs(self.rhs, beta, self.mass_sum)
+        for sv in self.solvers:
+            sv.set_rhs(self.rhs, beta, self.mass_sum)
         self._coef_key = key
+
+    def _split(self, n):
+        """Contiguous frequency block of each lane (multiples of 64 but the last)."""
+        per = (-(-n // self.n_lanes) + 63) // 64 * 64
+        return [(min(n, i * per), min(n, (i + 1) * per)) for i in range(self.n_lanes)]
+
+    def _run(self, call, n, accum):
+        """``call(solver, lo, hi, bufs)`` on every lane's stream; per-lane ``accum``
+        buffers (zeros like each given tensor) are summed into the given tensors."""
+        cur = torch.cuda.current_stream(self.device)
+        parts = []
+        for sv, st, (lo, hi) in zip(self.solvers, self.streams, self._split(n)):
+            if hi <= lo:
+                continue
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                bufs = [None if a is None else torch.zeros_like(a) for a in accum]
+                call(sv, lo, hi, bufs)
+            parts.append((st, bufs))
+        for st, bufs in parts:
+            cur.wait_stream(st)
+            for a, b in zip(accum, bufs):
+                if a is not None:
+                    b.record_stream(cur)
+                    a.add_(b)
+
+    def sweep(self, freqs, loss_type=_native.LOSS_NONE, ref=None, scale=1.0, fr=None, loss=None, w=None,
+              flags=None):
+        """``Solver.sweep`` over all lanes (fr / flags written in place, loss / w accumulated)."""
+        def call(sv, lo, hi, bufs):
+            sv.sweep(freqs[lo:hi], loss_type, ref=None if ref is None else ref[lo:hi], scale=scale,
+                     fr=None if fr is None else fr[lo:hi], loss=bufs[0], w=bufs[1],
+                     flags=None if flags is None else flags[lo:hi])
+        self._run(call, freqs.numel(), [loss, w])
+
+    def hessian_sweep(self, freqs, loss_type, ref, scale, dcoef, loss=None, w=None, h=None, flags=None):
+        def call(sv, lo, hi, bufs):
+            sv.hessian_sweep(freqs[lo:hi], loss_type, ref[lo:hi], scale, dcoef, loss=bufs[0], w=bufs[1],
+                             h=bufs[2], flags=None if flags is None else flags[lo:hi])
+        self._run(call, freqs.numel(), [loss, w, h])
+
+    # ---- measurement (bench.py)
+    def set_timing(self, on, kernels=False):
+        for sv in self.solvers:
+            sv.set_timing(on, kernels)
+
+    def last_timings(self) -> np.ndarray:
+        """Per-phase device ms of the last call, summed over the lanes (lanes overlap in time)."""
+        return sum(sv.last_timings() for sv in self.solvers)
+
+    def last_kernel_timings(self):
+        ms, n = zip(*(sv.last_kernel_timings() for sv in self.solvers))
+        return sum(ms), sum(n)
 
 
 def _coeffs18(transform, params: torch.Tensor) -> torch.Tensor:
@@ -112,7 +184,7 @@ class _SweepFR(torch.autograd.Function):
         engine.set_coefficients(cn)
         fr = torch.empty(freqs.numel(), dtype=torch.float64, device=engine.device)
         flags = torch.zeros(freqs.numel(), dtype=torch.int32, device=engine.device)
-        engine.solver.sweep(freqs, _native.LOSS_NONE, fr=fr, flags=flags)
+        engine.sweep(freqs, _native.LOSS_NONE, fr=fr, flags=flags)
         _check_flags(flags)
         ctx.engine, ctx.freqs, ctx.cn = engine, freqs, cn
         return fr
@@ -125,8 +197,8 @@ class _SweepFR(torch.autograd.Function):
         ref.real.copy_(grad_fr.to(torch.float64))
         w = torch.zeros(18, dtype=torch.complex128, device=engine.device)
         loss = torch.zeros(1, dtype=torch.float64, device=engine.device)
-        engine.solver.sweep(ctx.freqs, _native.LOSS_COTANGENT, ref=torch.view_as_real(ref), scale=1.0,
-                            loss=loss, w=torch.view_as_real(w))
+        engine.sweep(ctx.freqs, _native.LOSS_COTANGENT, ref=torch.view_as_real(ref), scale=1.0,
+                     loss=loss, w=torch.view_as_real(w))
         return torch.conj(w).to(torch.complex128).cpu(), None, None
 
 
@@ -140,8 +212,8 @@ class _SweepLoss(torch.autograd.Function):
         w = torch.zeros(18, dtype=torch.complex128, device=engine.device)
         loss = torch.zeros(1, dtype=torch.float64, device=engine.device)
         flags = torch.zeros(freqs.numel(), dtype=torch.int32, device=engine.device)
-        engine.solver.sweep(freqs, loss_id, ref=torch.view_as_real(ref), scale=1.0 / n_total,
-                            loss=loss, w=torch.view_as_real(w), flags=flags)
+        engine.sweep(freqs, loss_id, ref=torch.view_as_real(ref), scale=1.0 / n_total,
+                     loss=loss, w=torch.view_as_real(w), flags=flags)
         _check_flags(flags)
         packed = torch.cat([loss.to(torch.complex128), w])
         if reduce_fn is not None:
@@ -414,8 +486,8 @@ class Problem:
             h = torch.zeros(n, 18, dtype=torch.complex128, device=dev)
             loss = torch.zeros(1, dtype=torch.float64, device=dev)
             flags = torch.zeros(f_local.numel(), dtype=torch.int32, device=dev)
-            eng.solver.hessian_sweep(f_local, loss_id, torch.view_as_real(ref_local), 1.0 / n_total, dc.T,
-                                     loss=loss, w=torch.view_as_real(w), h=torch.view_as_real(h), flags=flags)
+            eng.hessian_sweep(f_local, loss_id, torch.view_as_real(ref_local), 1.0 / n_total, dc.T,
+                              loss=loss, w=torch.view_as_real(w), h=torch.view_as_real(h), flags=flags)
             _check_flags(flags)
             packed = torch.cat([loss.to(torch.complex128), w, h.reshape(-1)])
             if reduce_fn is not None:

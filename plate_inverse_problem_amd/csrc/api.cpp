@@ -90,6 +90,7 @@ struct pfr_solver {
   int32_t* rhs_sup = nullptr;
   double* rhs_val = nullptr;
   int n_rhs_sup = 0;
+  std::vector<double> rhs_host;         // last Dirichlet vector uploaded (original order)
   double beta_re = 0, beta_im = 0, mass_sum = 0;
   bool has_rhs = false;
   pfr::FunctionalArgs fn{};
@@ -97,21 +98,28 @@ struct pfr_solver {
   const double* stiff = nullptr;
   int n_stiff = 0;
   pfr::CoefPack e{};
-  // timing: bit 0 = phases (ev), bit 1 = factorisation kernel classes (kev: 5 per level)
+  // timing: bit 0 = phases, bit 1 = factorisation kernel classes (5 events per level).
+  // Events of every chunk of the last call are kept and read only when the caller
+  // asks (pfr_last_timings): no host synchronisation inside a call, so solvers on
+  // different streams overlap.
+  struct ChunkEvents {
+    hipEvent_t ev[6]{};
+    std::vector<hipEvent_t> kev;
+    bool used[5]{};
+  };
   int timing = 0;
-  hipEvent_t ev[6]{};
-  double last_ms[5]{};
-  std::vector<hipEvent_t> kev;
-  double kernel_ms[4]{};                // assemble (A11), diag (A11 LU), offdiag (L21/U12), schur
-  int64_t kernel_launches[4]{};
+  std::vector<ChunkEvents> tev;
+  int n_tev = 0;                        // chunks recorded by the last call
   int64_t alg_bytes[4]{};               // algorithmic HBM bytes per frequency of each class (one sweep)
 
   ~pfr_solver() {
     for (void* p : owned) (void)hipFree(p);
-    for (auto& x : ev)
-      if (x) (void)hipEventDestroy(x);
-    for (auto& x : kev)
-      if (x) (void)hipEventDestroy(x);
+    for (auto& c : tev) {
+      for (auto& x : c.ev)
+        if (x) (void)hipEventDestroy(x);
+      for (auto& x : c.kev)
+        if (x) (void)hipEventDestroy(x);
+    }
   }
   template <class T>
   int alloc(T** p, int64_t count) {
@@ -143,50 +151,43 @@ int64_t workspace_bytes(const Symbolic& S, int64_t Fc) {
 // waves per workgroup for a level whose largest front is maxf
 int waves_for(int maxf) { return std::max(1, std::min(8, (maxf + 23) / 24)); }
 
-void record(pfr_solver* s, int i, hipStream_t st) {
-  if (s->timing) (void)hipEventRecord(s->ev[i], st);
-}
-
-int finish_timing(pfr_solver* s, const bool* used) {
+// start the timing record of a new chunk (events created once per chunk slot)
+int begin_chunk(pfr_solver* s) {
   if (!s->timing) return PFR_OK;
-  HIP_TRY(hipEventSynchronize(s->ev[5]));
-  for (int i = 0; i < 5; ++i) {
-    float ms = 0;
-    if (used[i]) HIP_TRY(hipEventElapsedTime(&ms, s->ev[i], s->ev[i + 1]));
-    s->last_ms[i] += used[i] ? ms : 0.0;
+  if ((int)s->tev.size() <= s->n_tev) {
+    s->tev.emplace_back();
+    for (auto& e : s->tev.back().ev) HIP_TRY(hipEventCreate(&e));
   }
-  if ((s->timing & 2) && used[0]) {
-    const int L = (int)s->level_ptr.size() - 1;
-    for (int l = 0; l < L; ++l)
-      for (int c = 0; c < 4; ++c) {
-        float ms = 0;
-        HIP_TRY(hipEventElapsedTime(&ms, s->kev[5 * l + c], s->kev[5 * l + c + 1]));
-        s->kernel_ms[c] += ms;
-        const int work[4] = {s->asm_ptr[l + 1] - s->asm_ptr[l], s->level_ptr[l + 1] - s->level_ptr[l],
-                             s->item_ptr[l + 1] - s->item_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l]};
-        s->kernel_launches[c] += work[c] > 0;     // empty classes launch nothing
-      }
+  auto& c = s->tev[s->n_tev];
+  const size_t nk = 5 * (s->level_ptr.size() - 1);
+  while ((s->timing & 2) && c.kev.size() < nk) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreate(&e));
+    c.kev.push_back(e);
   }
   return PFR_OK;
 }
 
-void reset_timing(pfr_solver* s) {
-  for (double& m : s->last_ms) m = 0;
-  for (double& m : s->kernel_ms) m = 0;
-  for (int64_t& n : s->kernel_launches) n = 0;
+void record(pfr_solver* s, int i, hipStream_t st) {
+  if (s->timing) (void)hipEventRecord(s->tev[s->n_tev].ev[i], st);
 }
+
+int finish_timing(pfr_solver* s, const bool* used) {
+  if (!s->timing) return PFR_OK;
+  for (int i = 0; i < 5; ++i) s->tev[s->n_tev].used[i] = used[i];
+  ++s->n_tev;
+  return PFR_OK;
+}
+
+void reset_timing(pfr_solver* s) { s->n_tev = 0; }
 
 int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nvalid, hipStream_t st) {
   const int L = (int)s->level_ptr.size() - 1;
   const int ngroups = (int)(s->Fc / 64);
-  const bool kt = (s->timing & 2) != 0;
-  while (kt && s->kev.size() < (size_t)(5 * L)) {
-    hipEvent_t e;
-    HIP_TRY(hipEventCreate(&e));
-    s->kev.push_back(e);
-  }
+  const bool kt = (s->timing & 2) && s->n_tev < (int)s->tev.size() && !s->tev[s->n_tev].kev.empty();
+  hipEvent_t* kev = kt ? s->tev[s->n_tev].kev.data() : nullptr;
   auto mark = [&](int l, int c) {
-    if (kt) (void)hipEventRecord(s->kev[5 * l + c], st);
+    if (kt) (void)hipEventRecord(kev[5 * l + c], st);
   };
   for (int l = 0; l < L; ++l) {
     int nf = s->level_ptr[l + 1] - s->level_ptr[l];
@@ -586,8 +587,6 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       (rc = s->alloc(&s->freqs, Fc)) || (rc = s->alloc(&s->loss_terms, Fc)) || (rc = s->alloc(&s->flags, Fc)) ||
       (rc = s->alloc(&s->tq, Fc)))
     return bail(rc);
-  for (auto& e : s->ev)
-    if (hipEventCreate(&e) != hipSuccess) return bail(fail(PFR_ERR_HIP, "hipEventCreate failed"));
   *out = s;
   return PFR_OK;
 }
@@ -607,11 +606,41 @@ int pfr_set_timing(pfr_solver* s, int32_t enable) {
   return PFR_OK;
 }
 
+int pfr_last_timings(const pfr_solver* s, double* ms) {
+  if (!s || !ms) return fail(PFR_ERR_ARG, "null argument");
+  for (int i = 0; i < 5; ++i) ms[i] = 0.0;
+  if (s->n_tev > 0) HIP_TRY(hipEventSynchronize(s->tev[s->n_tev - 1].ev[5]));
+  for (int c = 0; c < s->n_tev; ++c)
+    for (int i = 0; i < 5; ++i)
+      if (s->tev[c].used[i]) {
+        float m = 0;
+        HIP_TRY(hipEventElapsedTime(&m, s->tev[c].ev[i], s->tev[c].ev[i + 1]));
+        ms[i] += m;
+      }
+  return PFR_OK;
+}
+
 int pfr_last_kernel_timings(const pfr_solver* s, double* ms, int64_t* launches) {
   if (!s || !ms) return fail(PFR_ERR_ARG, "null argument");
   for (int i = 0; i < 4; ++i) {
-    ms[i] = s->kernel_ms[i];
-    if (launches) launches[i] = s->kernel_launches[i];
+    ms[i] = 0.0;
+    if (launches) launches[i] = 0;
+  }
+  if (!(s->timing & 2) || s->n_tev == 0) return PFR_OK;
+  HIP_TRY(hipEventSynchronize(s->tev[s->n_tev - 1].ev[5]));
+  const int L = (int)s->level_ptr.size() - 1;
+  for (int c = 0; c < s->n_tev; ++c) {
+    if (!s->tev[c].used[0]) continue;
+    for (int l = 0; l < L; ++l) {
+      const int work[4] = {s->asm_ptr[l + 1] - s->asm_ptr[l], s->level_ptr[l + 1] - s->level_ptr[l],
+                           s->item_ptr[l + 1] - s->item_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l]};
+      for (int k = 0; k < 4; ++k) {
+        float m = 0;
+        HIP_TRY(hipEventElapsedTime(&m, s->tev[c].kev[5 * l + k], s->tev[c].kev[5 * l + k + 1]));
+        ms[k] += m;
+        if (launches) launches[k] += work[k] > 0;    // empty classes launch nothing
+      }
+    }
   }
   return PFR_OK;
 }
@@ -619,12 +648,6 @@ int pfr_last_kernel_timings(const pfr_solver* s, double* ms, int64_t* launches) 
 int pfr_solver_alg_bytes(const pfr_solver* s, int64_t* bytes) {
   if (!s || !bytes) return fail(PFR_ERR_ARG, "null argument");
   for (int i = 0; i < 4; ++i) bytes[i] = s->alg_bytes[i];
-  return PFR_OK;
-}
-
-int pfr_last_timings(const pfr_solver* s, double* ms) {
-  if (!s || !ms) return fail(PFR_ERR_ARG, "null argument");
-  for (int i = 0; i < 5; ++i) ms[i] = s->last_ms[i];
   return PFR_OK;
 }
 
@@ -665,6 +688,12 @@ int pfr_set_operator(pfr_solver* s, const double* K_dev, const double* M_dev) {
 
 int pfr_set_rhs(pfr_solver* s, const double* rhs, double beta_re, double beta_im, double mass_sum) {
   if (!s || !rhs) return fail(PFR_ERR_ARG, "null argument");
+  s->beta_re = beta_re;
+  s->beta_im = beta_im;
+  s->mass_sum = mass_sum;
+  // the Dirichlet vector rarely changes (only the scale does, per theta): upload it
+  // only when it differs from the last one (no device allocation per call)
+  if (s->has_rhs && std::equal(s->rhs_host.begin(), s->rhs_host.end(), rhs)) return PFR_OK;
   HIP_TRY(hipSetDevice(s->device));
   std::vector<double> rp(s->n);
   std::vector<int32_t> sup;
@@ -677,17 +706,17 @@ int pfr_set_rhs(pfr_solver* s, const double* rhs, double beta_re, double beta_im
     }
   }
   int rc;
-  if (!s->rhsP && (rc = s->alloc(&s->rhsP, s->n))) return rc;
+  if (!s->rhsP) {
+    if ((rc = s->alloc(&s->rhsP, s->n)) || (rc = s->alloc(&s->rhs_sup, s->n)) || (rc = s->alloc(&s->rhs_val, s->n)))
+      return rc;
+  }
   HIP_TRY(hipMemcpy(s->rhsP, rp.data(), s->n * 8, hipMemcpyHostToDevice));
-  s->rhs_sup = nullptr;
-  s->rhs_val = nullptr;
   if (!sup.empty()) {
-    if ((rc = s->up(&s->rhs_sup, sup)) || (rc = s->up(&s->rhs_val, val))) return rc;
+    HIP_TRY(hipMemcpy(s->rhs_sup, sup.data(), sup.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(s->rhs_val, val.data(), val.size() * 8, hipMemcpyHostToDevice));
   }
   s->n_rhs_sup = (int)sup.size();
-  s->beta_re = beta_re;
-  s->beta_im = beta_im;
-  s->mass_sum = mass_sum;
+  s->rhs_host.assign(rhs, rhs + s->n);
   s->has_rhs = true;
   return PFR_OK;
 }
@@ -734,6 +763,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
     HIP_TRY(hipMemcpyAsync(s->freqs, freqs_dev + q0, nv * sizeof(double), hipMemcpyDeviceToDevice, st));
     pfr::launch_pad_freqs(s->freqs, nv, Fc, st);
     HIP_TRY(hipMemsetAsync(s->flags, 0, Fc * sizeof(int32_t), st));
+    if (int rc0 = begin_chunk(s)) return rc0;
     record(s, 0, st);
     int rc = factor_all(s, 0, nullptr, 0, nv, st);
     if (rc) return rc;
@@ -891,6 +921,7 @@ int pfr_solve_multi(pfr_solver* s, int32_t batch, int32_t nrhs, const double* da
   for (int64_t q0 = 0; q0 < batch; q0 += Fc) {
     const int nv = (int)std::min<int64_t>(Fc, batch - q0);
     HIP_TRY(hipMemsetAsync(s->flags, 0, Fc * sizeof(int32_t), st));
+    if (int rc0 = begin_chunk(s)) return rc0;
     record(s, 0, st);
     // padded lanes repeat the last valid item (stride 0 broadcast handled by the kernel's clamp)
     int rc = factor_all(s, 1, data + q0 * data_stride, data_stride, nv, st);
