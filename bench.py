@@ -48,24 +48,27 @@ sys.path.insert(0, REPO)
 FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector/matrix (spec; MI355X_MICROARCH.md lists no fp64 row)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 PMC_FILE = os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")
-KERNELS = ("k_assemble_level<0>", "k_factor_level<true>", "k_offdiag_level<0>", "k_schur_level")
+KERNELS_GENERAL = ("k_assemble_level<0>", "k_factor_level<true>", "k_offdiag_level<0>", "k_schur_level")
+KERNELS_SYM = ("k_assemble_level<0>", "k_factor_level<true>", "k_offdiag_level<0>", "k_schur_sym_level<true>")
 
 
-def pmc_traffic(chunk):
+def pmc_traffic(chunk, kernels):
     """Measured HBM bytes per launch of each factorisation kernel class, scaled to ``chunk``."""
     try:
         d = json.load(open(PMC_FILE))
     except (OSError, ValueError):
         return [None] * 4
     out = []
-    for k in KERNELS:
+    if d.get("factorisation") != ("symmetric" if kernels is KERNELS_SYM else "general"):
+        return [None] * 4
+    for k in kernels:
         e = d["kernels"].get(k)
         out.append(None if e is None else
                    (e["read_bytes"] + e["write_bytes"]) / e["dispatches"] * chunk / d["freqs_per_sweep"])
     return out
 
 
-def build_problem(ny, device):
+def build_problem(ny, device, max_batch=None):
     from plate_inverse_problem_amd.Accelerometer import Accelerometer
     from plate_inverse_problem_amd.Geometry import Geometry, GeometryParams
     from plate_inverse_problem_amd.Material import get_material
@@ -73,7 +76,7 @@ def build_problem(ny, device):
     acc = Accelerometer("AP1030")
     geom = Geometry("sh_i", acc, GeometryParams(100e-3, 20e-3, 2e-3, None, None), ny=ny)
     mat = get_material(1500.0, "orthotropic", E1=120e9, E2=8e9, G12=5e9, nu12=0.3, beta=0.01)
-    return Problem(geom, mat, acc, device=device)
+    return Problem(geom, mat, acc, device=device, max_batch=max_batch)
 
 
 def cpu_baseline(prob, freqs, ref, theta, sample_per_core=128):
@@ -103,6 +106,7 @@ def main():
     ap.add_argument("--freqs", type=int, default=4096, help="frequencies per GPU")
     ap.add_argument("--ny", type=int, default=25, help="mesh cells across the width (25 -> 19,353 DOF)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--chunk", type=int, default=None, help="frequencies per chunk (default: from free HBM)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -113,7 +117,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
 
-    prob = build_problem(args.ny, device)
+    prob = build_problem(args.ny, device, args.chunk)
     n_total = args.freqs * world
     freqs = np.linspace(40.0, 600.0, n_total)
     theta_true = prob.parameters.copy()
@@ -187,14 +191,15 @@ def main():
     alg_launch = alg_f * n_iso / np.maximum(iso_n, 1)
     ms_launch = iso_ms / np.maximum(iso_n, 1)
     gbs = alg_launch / (ms_launch * 1e-3) / 1e9
-    traffic = pmc_traffic(chunk)
+    kernels = KERNELS_SYM if eng.symmetric else KERNELS_GENERAL
+    traffic = pmc_traffic(chunk, kernels)
     fact_alg = float(alg_f.sum() * n_iso)
     fact_ms = float(iso_ms.sum())
     fact_tfs = st["factor_flops"] * n_iso / (iso_phase[0] * 1e-3) / 1e12
     fact_traffic = None if None in traffic else float(np.dot(traffic, iso_n))
-    # triangular solves: 4 passes (L, U, U^T, L^T) over the factors, 16 B per L+U entry
-    # per pass per frequency, plus int32 pattern (shared by 64-frequency wavefronts) and vectors
-    trsv_bytes = n_iso * (4 * 16 * st["nnz_lu"] + 4 * 2 * 16 * st["n"])
+    # each pass reads one triangle: L (L solves) or U (U solves; in symmetric mode U12 is read
+    # as L21), so the four passes read L + U twice: 2 * 16 * nnz(L+U), plus rhs in / solution out
+    trsv_bytes = n_iso * (2 * 16 * st["nnz_lu"] + 4 * 2 * 16 * st["n"])
     trsv_gbs = trsv_bytes / ((iso_phase[1] + iso_phase[3]) * 1e-3) / 1e9
     conc_launch = kms / np.maximum(klaunch, 1)
     out = {
@@ -215,16 +220,18 @@ def main():
                                "loss MSE_LOG_AFC + gradient",
                    "n_dofs": st["n"], "freqs_per_gpu": args.freqs, "chunk": chunk,
                    "lanes": eng.n_lanes,
+                   "factorisation": "symmetric: A = L U, U = diag(U) L^T implicit, Dirichlet nodes decoupled"
+                                    if eng.symmetric else "general: A = L U",
                    "nnz_lu": st["nnz_lu"], "factor_gflop_per_freq": st["factor_flops"] / 1e9,
                    "parallelism": f"frequency shards x{world} + 1 all-reduce/step; {eng.n_lanes} concurrent "
                                   "solver lanes (HIP streams) per GPU"},
-        "roofline": {"bound": "hbm", "kernel": "k_schur_level", "achieved": gbs[3], "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": kernels[3], "achieved": gbs[3], "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": gbs[3] / HBM_PEAK_GBS, "traffic": traffic[3],
                      "alg_bytes_per_launch": alg_launch[3], "avg_launch_ms": ms_launch[3],
                      "launches": int(iso_n[3]), "measured": f"isolated lane-0 sweep of {n_iso} frequencies "
                      "(one chunk) after the timed region, HIP events per launch",
                      "concurrent_avg_launch_ms": conc_launch[3]},
-        "factor_roofline": {"bound": "hbm", "kernels": list(KERNELS), "ms": iso_ms.tolist(),
+        "factor_roofline": {"bound": "hbm", "kernels": list(kernels), "ms": iso_ms.tolist(),
                             "alg_GBps": gbs.tolist(), "achieved": fact_alg / (fact_ms * 1e-3) / 1e9,
                             "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": fact_alg / (fact_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,

@@ -51,6 +51,13 @@ typedef struct pfr_symbolic_options {
   int32_t ordering;    /* 0 nested dissection (default), 1 natural */
   int32_t relax_small, relax_mid, relax_big; /* supernode amalgamation (4, 16, 48) */
   double zrelax_mid, zrelax_big;             /* (0.5, 0.1) */
+  /* 1: symmetric-structure analysis (default 0).  The caller guarantees that the matrices
+   * factorised with it are complex symmetric (A = A^T, non-conjugate) once the Dirichlet
+   * rows -- rows holding only their diagonal entry (tgv = -1 rows, pyFFInterface.py:176) --
+   * and their columns are removed.  Those nodes are decoupled (their column entries move
+   * to the right-hand side / the adjoint's Dirichlet rows), the rest is factorised as
+   * A = L U with U = diag(U) L^T implicit: only L is formed and read. */
+  int32_t symmetric;
 } pfr_symbolic_options;
 
 typedef struct pfr_symbolic_stats {
@@ -63,6 +70,9 @@ typedef struct pfr_symbolic_stats {
   int64_t factor_entries;  /* sum of squared front sizes (dense front storage per frequency) */
   int64_t nnz_lu;          /* entries of L + U (per frequency) */
   double factor_flops;     /* real flops of one numeric factorisation */
+  int32_t symmetric;       /* analysis built with options.symmetric = 1 */
+  int32_t n_dirichlet;     /* symmetric mode: decoupled Dirichlet nodes */
+  int64_t n_coupling;      /* symmetric mode: entries (i, d), i not Dirichlet, d Dirichlet */
 } pfr_symbolic_stats;
 
 /* export ids for pfr_symbolic_export (int32 arrays unless noted) */
@@ -78,6 +88,8 @@ typedef struct pfr_symbolic_stats {
 #define PFR_EXPORT_EA_SRC 9      /* ea_ptr[total_rows] */
 #define PFR_EXPORT_LEVEL_PTR 10  /* n_levels + 1 */
 #define PFR_EXPORT_LEVEL_FRONTS 11 /* n_fronts */
+#define PFR_EXPORT_DIRICHLET 12  /* n_dirichlet x 2: permuted node, CSC index of its diagonal entry */
+#define PFR_EXPORT_COUPLING 13   /* n_coupling x 3: permuted row i, Dirichlet slot, CSC index; by row */
 
 PFR_API const char* pfr_version(void);
 /* Message of the last failed call on this thread ("" if none). */
@@ -109,7 +121,9 @@ PFR_API int32_t pfr_solver_max_batch(const pfr_solver* s);
  * InnerState.h:183-185).  A_q values on the CSC pattern: data_dev + q * data_stride (complex, nnz);
  * data_stride = 0 broadcasts one matrix (modes 0/2 of InnerState::solve, InnerState.h:192-233);
  * b_stride likewise (0 = broadcast b, mode 1).  Batch-major (batch, n) complex output.
- * Replaces InnerState::solve (InnerState.h:164-308).  flags_dev: int32 per batch item (may be NULL). */
+ * Replaces InnerState::solve (InnerState.h:164-308).  flags_dev: int32 per batch item (may be NULL).
+ * Needs a solver on a general analysis (options.symmetric = 0): explicit matrices carry no symmetry
+ * guarantee (PFR_ERR_STATE otherwise). */
 PFR_API int pfr_solve(pfr_solver* s, int32_t batch, const double* data_dev, int64_t data_stride,
                       const double* b_dev, int64_t b_stride, double* x_dev, int32_t transpose,
                       int32_t* flags_dev, void* stream);

@@ -24,6 +24,7 @@ import warnings
 from typing import Callable
 
 import numpy as np
+import scipy.sparse as sp
 import torch
 
 from . import _native
@@ -44,6 +45,27 @@ def _default_device():
     return torch.device("cuda", torch.cuda.current_device())
 
 
+def decoupled_symmetric(rows, cols, vals, n, rtol=1e-10) -> bool:
+    """True when every matrix ``vals[k]`` on the (rows, cols) pattern is complex symmetric
+    once the Dirichlet rows -- rows holding only their diagonal entry, the ``tgv = -1`` rows
+    of pyFFInterface.py:176 -- and their columns are taken out (the condition of the
+    symmetric analysis, include/pfr.h ``pfr_symbolic_options.symmetric``)."""
+    rows = np.asarray(rows, dtype=np.int64)
+    cols = np.asarray(cols, dtype=np.int64)
+    off = rows != cols
+    isdir = np.zeros(n, dtype=bool)
+    isdir[rows[~off]] = True
+    isdir[rows[off]] = False
+    keep = ~isdir[rows] & ~isdir[cols]
+    r, c = rows[keep], cols[keep]
+    for v in np.atleast_2d(vals):
+        A = sp.csr_matrix((np.asarray(v)[keep], (r, c)), shape=(n, n))
+        amax = abs(A).max() if A.nnz else 0.0
+        if amax > 0 and abs(A - A.T).max() > rtol * amax:
+            return False
+    return True
+
+
 class _Engine:
     """Device state of one Problem: symbolic analysis, operator data and ``lanes``
     solvers, each with its own workspace and HIP stream.  A sweep splits its
@@ -51,21 +73,31 @@ class _Engine:
     concurrently, so one lane's latency-bound levels (few large fronts at the top
     of the elimination tree) overlap the other's bandwidth-bound ones."""
 
-    def __init__(self, prob: "Problem", device, n_freqs: int, max_batch: int | None, lanes: int | None = None):
+    def __init__(self, prob: "Problem", device, n_freqs: int, max_batch: int | None, lanes: int | None = None,
+                 symmetric: bool | None = None):
         self.device = device
         mats = prob.mats
         # structural pattern of the matrices that can be non-zero: for a mid-plane
         # symmetric material the B coefficients are identically zero, the KB
         # entries carry exact zeros and are dropped from the factorised pattern.
         active = [k for k in range(26) if not (prob.material.is_mps and KB_SLICE.start <= k < KB_SLICE.stop)]
-        keep = prob.present[active].any(axis=0)
+        # entries that are exactly zero in every active matrix (explicit zeros of the FE layout)
+        # are left out too: they change nothing, and with them out the Dirichlet rows hold
+        # only their diagonal entry
+        keep = prob.present[active].any(axis=0) & (mats[active] != 0).any(axis=0)
         self.keep = np.nonzero(keep)[0]
         rows, cols = prob.rows[self.keep], prob.cols[self.keep]
         n = prob.mat_size
         colptr = np.zeros(n + 1, dtype=np.int64)
         np.add.at(colptr, cols.astype(np.int64) + 1, 1)
         colptr = np.cumsum(colptr).astype(np.int32)
-        self.sym = _native.Symbolic(n, colptr, rows.astype(np.int32))
+        vals = mats[:, self.keep]
+        if symmetric is None:
+            symmetric = os.environ.get("PFR_SYMMETRIC", "1") != "0"
+        # symmetric mode when every matrix is complex symmetric away from the Dirichlet rows
+        # (checked on the values): only L is formed, U = diag(U) L^T (DESIGN.md section 2)
+        self.symmetric = bool(symmetric) and decoupled_symmetric(rows, cols, vals, n)
+        self.sym = _native.Symbolic(n, colptr, rows.astype(np.int32), symmetric=self.symmetric)
         self.stats = self.sym.stats()
         if lanes is None:
             lanes = int(os.environ.get("PFR_LANES", "2"))
@@ -82,7 +114,6 @@ class _Engine:
         self.solvers = [_native.Solver(self.sym, device.index, max_batch) for _ in range(self.n_lanes)]
         self.streams = [torch.cuda.Stream(device) for _ in range(self.n_lanes)]
         self.solver = self.solvers[0]
-        vals = mats[:, self.keep]
         self.stiff = torch.as_tensor(np.ascontiguousarray(vals[:18].T), device=device)       # (nnz, 18)
         I0, I0c, I2, I2c = prob.I0, prob.I0Corr, prob.I2, prob.I2Corr
         mass = I0 * (vals[18] + vals[20] + vals[22]) + I0c * (vals[19] + vals[21] + vals[23]) \

@@ -25,7 +25,7 @@ LOSS_NONE, LOSS_MSE, LOSS_RMSE, LOSS_MSE_AFC, LOSS_MSE_LOG_AFC, LOSS_COTANGENT =
 LOSS_IDS = {"MSE": LOSS_MSE, "RMSE": LOSS_RMSE, "MSE_AFC": LOSS_MSE_AFC, "MSE_LOG_AFC": LOSS_MSE_LOG_AFC}
 
 EXPORT = dict(PERM=0, IPERM=1, FRONTS=2, IDX=3, RELPOS=4, ASM_PTR=5, ASM_COL=6, ASM_NZ=7, EA_PTR=8,
-              EA_SRC=9, LEVEL_PTR=10, LEVEL_FRONTS=11)
+              EA_SRC=9, LEVEL_PTR=10, LEVEL_FRONTS=11, DIRICHLET=12, COUPLING=13)
 
 
 class NativeError(RuntimeError):
@@ -35,13 +35,14 @@ class NativeError(RuntimeError):
 class SymbolicOptions(C.Structure):
     _fields_ = [("leaf_size", C.c_int32), ("ordering", C.c_int32), ("relax_small", C.c_int32),
                 ("relax_mid", C.c_int32), ("relax_big", C.c_int32), ("zrelax_mid", C.c_double),
-                ("zrelax_big", C.c_double)]
+                ("zrelax_big", C.c_double), ("symmetric", C.c_int32)]
 
 
 class SymbolicStats(C.Structure):
     _fields_ = [("n", C.c_int32), ("nnz", C.c_int64), ("n_fronts", C.c_int32), ("n_levels", C.c_int32),
                 ("max_front", C.c_int32), ("total_rows", C.c_int64), ("factor_entries", C.c_int64),
-                ("nnz_lu", C.c_int64), ("factor_flops", C.c_double)]
+                ("nnz_lu", C.c_int64), ("factor_flops", C.c_double), ("symmetric", C.c_int32),
+                ("n_dirichlet", C.c_int32), ("n_coupling", C.c_int64)]
 
 
 _P = C.c_void_p
@@ -133,13 +134,14 @@ def _ptr(t) -> int:
 class Symbolic:
     """Host-only symbolic analysis (nested dissection + supernodal maps)."""
 
-    def __init__(self, n: int, colptr, rowind, *, leaf_size=None, ordering=0, relax=None):
+    def __init__(self, n: int, colptr, rowind, *, leaf_size=None, ordering=0, relax=None, symmetric=False):
         L = lib()
         opt = SymbolicOptions()
         L.pfr_symbolic_options_default(C.byref(opt))
         if leaf_size is not None:
             opt.leaf_size = int(leaf_size)
         opt.ordering = int(ordering)
+        opt.symmetric = int(bool(symmetric))
         if relax is not None:
             opt.relax_small, opt.relax_mid, opt.relax_big = relax
         self.colptr, cp = _i32(colptr)
@@ -167,13 +169,25 @@ class Symbolic:
                  "LEVEL_FRONTS": st["n_fronts"]}
         if what == "EA_SRC":
             size = int(self.export("EA_PTR")[-1])
+        elif what == "DIRICHLET":
+            size = 2 * st["n_dirichlet"]
+        elif what == "COUPLING":
+            size = 3 * st["n_coupling"]
+        elif what in ("ASM_COL", "ASM_NZ"):
+            size = int(self.export("ASM_PTR")[-1])
         else:
             size = sizes[what]
         dtype = np.int64 if what == "FRONTS" else np.int32
         out = np.zeros(size, dtype=dtype)
         check(lib().pfr_symbolic_export(self._h, EXPORT[what], out.ctypes.data_as(_P), out.nbytes),
               "pfr_symbolic_export")
-        return out.reshape(-1, 8) if what == "FRONTS" else out
+        if what == "FRONTS":
+            return out.reshape(-1, 8)
+        if what == "DIRICHLET":
+            return out.reshape(-1, 2)
+        if what == "COUPLING":
+            return out.reshape(-1, 3)
+        return out
 
     def workspace_bytes(self, max_batch: int) -> int:
         return int(lib().pfr_solver_workspace_bytes(self._h, int(max_batch)))

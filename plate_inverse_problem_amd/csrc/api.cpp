@@ -73,6 +73,17 @@ struct pfr_solver {
   std::vector<int32_t> asm_ptr;         // record offset of each level (multiple of 8)
   int32_t* d_colptr = nullptr;
   int32_t* d_rowind = nullptr;
+  // symmetric mode (options.symmetric): U never formed; Dirichlet nodes decoupled
+  bool sym = false;
+  int n_dir = 0, n_crow = 0;
+  int2* d_dir = nullptr;                // per Dirichlet node: (permuted node, diagonal entry)
+  int32_t* d_crow = nullptr;            // coupled rows (permuted)
+  int32_t* d_cptr_dir = nullptr;        // their entry ranges in d_ce
+  int2* d_ce = nullptr;                 // (Dirichlet slot, entry) by coupled row
+  int32_t* d_dptr = nullptr;            // per Dirichlet node: entry range in d_de
+  int2* d_de = nullptr;                 // (permuted row, entry) by Dirichlet node
+  int32_t* d_cslot = nullptr;           // per permuted row: coupled-row slot or -1
+  double2* Bc = nullptr;                // forward right-hand-side corrections (n_crow x Fc)
   double2 *F = nullptr, *WV = nullptr, *X = nullptr, *Y = nullptr, *XA = nullptr, *G = nullptr;
   // Hessian sweep: permuted matrix by rows and by columns ((ptr, index, nz) each),
   // tangent solution / adjoint vectors, combined tangent operators (lazily allocated)
@@ -206,7 +217,7 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
                         s->d_oxp + s->item_ptr[l], s->d_ox, ngroups, s->F, s->Fc, s->freqs, s->K, s->M, data, ds,
                         nvalid, st);
     mark(l, 3);
-    pfr::launch_schur(s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l],
+    pfr::launch_schur(s->sym, s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l],
                       s->d_g1 + (int64_t)s->tile_ptr[l] * pfr::SCHUR_TM * pfr::SCHUR_TN * pfr::SCHUR_SR * pfr::SCHUR_SC,
                       s->d_gxp + s->tile_ptr[l],
                       s->d_gx, ngroups, s->F,
@@ -226,11 +237,58 @@ int solve_all(pfr_solver* s, int which, int rhs_mode, const pfr::RhsDesc& rd, co
   for (int t = 0; t < L; ++t) {
     int l = up ? t : L - 1 - t;
     int nf = s->level_ptr[l + 1] - s->level_ptr[l];
-    pfr::launch_solve(which, rhs_mode, s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_W[l], ngroups, s->F,
+    pfr::launch_solve(which, rhs_mode, s->sym, s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_W[l], ngroups, s->F,
                       s->Fc, s->WV, rd, Yin, Out, st);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
+}
+
+pfr::DirDesc dir_desc(const pfr_solver* s) {
+  pfr::DirDesc d;
+  d.dir = s->d_dir;
+  d.crow = s->d_crow;
+  d.cptr = s->d_cptr_dir;
+  d.ce = s->d_ce;
+  d.dptr = s->d_dptr;
+  d.de = s->d_de;
+  d.K = s->K;
+  d.M = s->M;
+  d.freqs = s->freqs;
+  return d;
+}
+
+// A x = b on the chunk's factors, x -> Out (permuted).  rhs_mode 0: operator right-hand side
+// (rd.rhsP ...); 2: vector rd.G (overwritten in symmetric mode).  Symmetric mode: Dirichlet
+// columns moved to the right-hand side first, then L and U = diag(U) L^T.
+int forward_solve(pfr_solver* s, int rhs_mode, pfr::RhsDesc rd, double2* Out, hipStream_t st) {
+  int rc;
+  if (s->sym) {
+    const pfr::DirDesc dd = dir_desc(s);
+    if (rhs_mode == 0) {
+      pfr::launch_dirichlet_rhs(0, dd, s->n_crow, rd, nullptr, s->Bc, s->Fc, st);
+      rd.cslot = s->d_cslot;
+      rd.Bc = s->Bc;
+      if (s->n_crow > 0) rhs_mode = 3;
+    } else {
+      pfr::launch_dirichlet_rhs(2, dd, s->n_crow, rd, const_cast<double2*>(rd.G), nullptr, s->Fc, st);
+    }
+  }
+  if ((rc = solve_all(s, 0, rhs_mode, rd, nullptr, s->Y, st))) return rc;
+  return solve_all(s, 1, 0, rd, s->Y, Out, st);
+}
+
+// A^T l = g (g = rg.G, permuted), l -> Out.  Symmetric mode: the decoupled matrix is symmetric,
+// so L and U = diag(U) L^T again, then the Dirichlet rows of l are corrected.
+int adjoint_solve(pfr_solver* s, const pfr::RhsDesc& rg, double2* Out, hipStream_t st) {
+  int rc;
+  if (s->sym) {
+    if ((rc = solve_all(s, 0, 2, rg, nullptr, s->Y, st)) || (rc = solve_all(s, 1, 0, rg, s->Y, Out, st))) return rc;
+    pfr::launch_dirichlet_post(dir_desc(s), s->n_dir, Out, s->Fc, st);
+    return PFR_OK;
+  }
+  if ((rc = solve_all(s, 2, 2, rg, nullptr, s->Y, st))) return rc;
+  return solve_all(s, 3, 0, rg, s->Y, Out, st);
 }
 
 }  // namespace
@@ -254,6 +312,7 @@ void pfr_symbolic_options_default(pfr_symbolic_options* o) {
   o->relax_big = d.relax_big;
   o->zrelax_mid = d.zrelax_mid;
   o->zrelax_big = d.zrelax_big;
+  o->symmetric = d.symmetric;
 }
 
 int pfr_symbolic_create(int32_t n, int64_t nnz, const int32_t* colptr, const int32_t* rowind,
@@ -269,6 +328,7 @@ int pfr_symbolic_create(int32_t n, int64_t nnz, const int32_t* colptr, const int
     o.relax_big = opt->relax_big;
     o.zrelax_mid = opt->zrelax_mid;
     o.zrelax_big = opt->zrelax_big;
+    o.symmetric = opt->symmetric;
   }
   auto* sym = new pfr_symbolic();
   if (pfr::analyse(n, nnz, colptr, rowind, o, sym->S) != 0) {
@@ -292,6 +352,9 @@ int pfr_symbolic_stats_get(const pfr_symbolic* sym, pfr_symbolic_stats* o) {
   o->factor_entries = S.factor_entries;
   o->nnz_lu = S.nnz_lu;
   o->factor_flops = S.factor_flops;
+  o->symmetric = S.symmetric;
+  o->n_dirichlet = (int32_t)S.dir_p.size();
+  o->n_coupling = (int64_t)S.cpl_p.size();
   return PFR_OK;
 }
 
@@ -301,6 +364,7 @@ int pfr_symbolic_export(const pfr_symbolic* sym, int32_t what, void* dst, int64_
   const void* src = nullptr;
   int64_t bytes = 0;
   std::vector<int64_t> fr;
+  std::vector<int32_t> tmp;
   auto pick = [&](const std::vector<int32_t>& v) {
     src = v.data();
     bytes = (int64_t)v.size() * 4;
@@ -325,6 +389,14 @@ int pfr_symbolic_export(const pfr_symbolic* sym, int32_t what, void* dst, int64_
     case PFR_EXPORT_EA_SRC: pick(S.ea_src); break;
     case PFR_EXPORT_LEVEL_PTR: pick(S.level_ptr); break;
     case PFR_EXPORT_LEVEL_FRONTS: pick(S.level_fronts); break;
+    case PFR_EXPORT_DIRICHLET:
+      for (size_t d = 0; d < S.dir_p.size(); ++d) tmp.insert(tmp.end(), {S.dir_p[d], S.dir_nz[d]});
+      pick(tmp);
+      break;
+    case PFR_EXPORT_COUPLING:
+      for (size_t c = 0; c < S.cpl_p.size(); ++c) tmp.insert(tmp.end(), {S.cpl_p[c], S.cpl_dir[c], S.cpl_nz[c]});
+      pick(tmp);
+      break;
     default: return fail(PFR_ERR_ARG, "unknown export id");
   }
   if (bytes > cap) return fail(PFR_ERR_ARG, "destination too small");
@@ -373,6 +445,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     // plus, per tile and tile position, the children's update-matrix entries that
     // land there (the extend-add of the Schur block, done as a gather)
     if (S.factor_entries > INT32_MAX) return bail(fail(PFR_ERR_ARG, "front storage exceeds int32 element ids"));
+    const bool sym = S.symmetric != 0;
+    s->sym = sym;
     std::vector<std::vector<int>> kids(S.fronts.size());
     for (size_t t = 0; t < S.fronts.size(); ++t)
       if (S.fronts[t].parent >= 0) kids[S.fronts[t].parent].push_back((int)t);
@@ -399,7 +473,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
             if (i < 0) continue;
             for (int b = C.ns; b < C.f; ++b) {
               const int j = rp[b] - F.ns;
-              if (j < 0) continue;
+              if (j < 0 || (sym && j > i)) continue;   // symmetric: lower triangle only
               const int32_t id = (int32_t)(C.off + (int64_t)a * C.f + b);
               int32_t& f1 = first[(size_t)i * r + j];
               if (f1 < 0)
@@ -414,13 +488,14 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
         // SCHUR_TM x SCHUR_TN tile at (TM (sub / SC), TN (sub % SC)); per super-tile the dense
         // first-source ids (-1 = none), lane group by lane group, then one overflow range
         constexpr int TM = pfr::SCHUR_TM, TN = pfr::SCHUR_TN, SR = pfr::SCHUR_SR, SC = pfr::SCHUR_SC;
+        static_assert(TM * SR == TN * SC, "square super-tiles (symmetric mode keeps j0 <= i0)");
         for (int i0 = 0; i0 < r; i0 += TM * SR)
-          for (int j0 = 0; j0 < r; j0 += TN * SC) {
+          for (int j0 = 0; j0 < r && (!sym || j0 <= i0); j0 += TN * SC) {
             tv.push_back(make_int4(t, i0, j0, 0));
             for (int sub = 0; sub < SR * SC; ++sub)
               for (int pos = 0; pos < TM * TN; ++pos) {
                 const int i = i0 + TM * (sub / SC) + pos / TN, j = j0 + TN * (sub % SC) + pos % TN;
-                if (i >= r || j >= r) {
+                if (i >= r || j >= r || (sym && j > i)) {
                   g1.push_back(-1);
                   continue;
                 }
@@ -477,7 +552,9 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
             for (int b = C.ns; b < C.f; ++b) {
               const int pb = rp[b];
               if (pb >= width) continue;
-              const int32_t id = (int32_t)(C.off + (int64_t)(src - C.row0) * C.f + b);
+              // symmetric: the child's update matrix holds its lower triangle only
+              const int ca = src - C.row0;
+              const int32_t id = (int32_t)(C.off + (sym && ca < b ? (int64_t)b * C.f + ca : (int64_t)ca * C.f + b));
               int32_t& s1 = s1m[(size_t)a * f + pb];
               if (s1 < 0)
                 s1 = id;
@@ -501,7 +578,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
             for (int32_t id : extras(a, b)) ax.push_back(make_int2(k, id));
             if (av.size() % 8 == 0) axp.push_back((int32_t)ax.size());
           }
-        for (int kind = 0; kind < 2; ++kind)
+        for (int kind = 0; kind < (sym ? 1 : 2); ++kind)   // symmetric: U12 = diag(U11) L21^T implicit
           for (int i0 = ns; i0 < f; i0 += 4 * pfr::OFF_RPL) {
             iv.push_back(make_int4(t, i0, kind, (int32_t)orec.size()));
             for (int slot = 0; slot < 4 * pfr::OFF_RPL; ++slot)   // row i0 + slot = i0 + 4 h + lane group
@@ -532,8 +609,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       for (const Front& F : S.fronts) {
         const int64_t r = F.f - F.ns;
         s_ns2 += (int64_t)F.ns * F.ns;
-        s_r2 += r * r;
-        s_rns += 2 * r * F.ns;
+        s_r2 += sym ? r * (r + 1) / 2 : r * r;
+        s_rns += (sym ? 1 : 2) * r * F.ns;
       }
       for (const int4& a : av) g_a11 += a.z >= 0;
       for (const int2& o : orec) g_off += o.y >= 0;
@@ -558,6 +635,36 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   }
   std::vector<int32_t> cp(colptr, colptr + S.n + 1), ri(rowind, rowind + S.nnz);
   if ((rc = s->up(&s->d_colptr, cp)) || (rc = s->up(&s->d_rowind, ri))) return bail(rc);
+  if (s->sym && !S.dir_p.empty()) {
+    // Dirichlet decoupling lists: coupled rows (with their entries), and per Dirichlet node
+    // the entries of its column (adjoint correction); slot of every permuted row
+    std::vector<int2> dir, ce, de;
+    std::vector<int32_t> crow, cptr(1, 0), dptr(1, 0), cslot(S.n, -1);
+    for (size_t d = 0; d < S.dir_p.size(); ++d) dir.push_back(make_int2(S.dir_p[d], S.dir_nz[d]));
+    for (size_t c = 0; c < S.cpl_p.size(); ++c) {
+      if (crow.empty() || crow.back() != S.cpl_p[c]) {
+        if (!crow.empty()) cptr.push_back((int32_t)ce.size());
+        cslot[S.cpl_p[c]] = (int32_t)crow.size();
+        crow.push_back(S.cpl_p[c]);
+      }
+      ce.push_back(make_int2(S.cpl_dir[c], S.cpl_nz[c]));
+    }
+    cptr.push_back((int32_t)ce.size());
+    for (size_t d = 0; d < S.dir_p.size(); ++d) {
+      for (size_t c = 0; c < S.cpl_p.size(); ++c)
+        if (S.cpl_dir[c] == (int32_t)d) de.push_back(make_int2(S.cpl_p[c], S.cpl_nz[c]));
+      dptr.push_back((int32_t)de.size());
+    }
+    if (ce.empty()) ce.push_back(make_int2(0, 0));
+    if (de.empty()) de.push_back(make_int2(0, 0));
+    if (crow.empty()) crow.push_back(0);
+    s->n_dir = (int)S.dir_p.size();
+    s->n_crow = (int)(cptr.size() - 1);
+    if ((rc = s->up(&s->d_dir, dir)) || (rc = s->up(&s->d_crow, crow)) || (rc = s->up(&s->d_cptr_dir, cptr)) ||
+        (rc = s->up(&s->d_ce, ce)) || (rc = s->up(&s->d_dptr, dptr)) || (rc = s->up(&s->d_de, de)) ||
+        (rc = s->up(&s->d_cslot, cslot)) || (rc = s->alloc(&s->Bc, (int64_t)std::max(1, s->n_crow) * s->Fc)))
+      return bail(rc);
+  }
   {
     // permuted matrix compressed by rows and by columns (Hessian tangent operators)
     auto compress = [&](const std::vector<int32_t>& key, const std::vector<int32_t>& other, int32_t** dptr,
@@ -774,8 +881,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
     rd.beta_im = s->beta_im;
     rd.mass_sum = s->mass_sum;
     rd.freqs = s->freqs;
-    if ((rc = solve_all(s, 0, 0, rd, nullptr, s->Y, st))) return rc;
-    if ((rc = solve_all(s, 1, 0, rd, s->Y, s->X, st))) return rc;
+    if ((rc = forward_solve(s, 0, rd, s->X, st))) return rc;
     record(s, 2, st);
     pfr::FunctionalArgs fa = s->fn;
     fa.loss_type = reverse ? loss_type : -1;
@@ -787,8 +893,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
     if (reverse) {
       pfr::RhsDesc rg;
       rg.G = s->G;
-      if ((rc = solve_all(s, 2, 2, rg, nullptr, s->Y, st))) return rc;
-      if ((rc = solve_all(s, 3, 0, rg, s->Y, s->XA, st))) return rc;
+      if ((rc = adjoint_solve(s, rg, s->XA, st))) return rc;
       record(s, 4, st);
       pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->XA, s->X, Fc, nv, s->partial,
                            st);
@@ -857,7 +962,7 @@ int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int
     rd.beta_im = s->beta_im;
     rd.mass_sum = s->mass_sum;
     rd.freqs = s->freqs;
-    if ((rc = solve_all(s, 0, 0, rd, nullptr, s->Y, st)) || (rc = solve_all(s, 1, 0, rd, s->Y, s->X, st))) return rc;
+    if ((rc = forward_solve(s, 0, rd, s->X, st))) return rc;
     pfr::FunctionalArgs fa = s->fn;
     fa.loss_type = loss_type;
     fa.ref = reinterpret_cast<const double2*>(ref_dev);
@@ -866,7 +971,9 @@ int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int
     pfr::launch_functional(fa, s->X, Fc, nv, q0, nullptr, s->loss_terms, s->G, st);
     pfr::RhsDesc rg;
     rg.G = s->G;
-    if ((rc = solve_all(s, 2, 2, rg, nullptr, s->Y, st)) || (rc = solve_all(s, 3, 0, rg, s->Y, s->XA, st))) return rc;
+    rg.rhsP = s->rhsP;
+    rg.freqs = s->freqs;
+    if ((rc = adjoint_solve(s, rg, s->XA, st))) return rc;
     pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->XA, s->X, Fc, nv, s->partial, st);
     pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st);
     pfr::launch_reduce(s->partial, kContractBlocks * ngroups, s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
@@ -877,14 +984,12 @@ int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int
     for (int i = 0; i < n_dir; ++i) {
       const double2* Kd = s->Kdir + (int64_t)i * s->nnz;
       pfr::launch_tangent_spmv(s->d_rptr, s->d_ridx, s->d_rnz, (int)n, Kd, s->X, Fc, s->rhsP, beta[i], s->G, 0, st);
-      if ((rc = solve_all(s, 0, 2, rg, nullptr, s->Y, st)) || (rc = solve_all(s, 1, 0, rd, s->Y, s->DX, st)))
-        return rc;
+      if ((rc = forward_solve(s, 2, rg, s->DX, st))) return rc;
       HIP_TRY(hipMemsetAsync(s->G, 0, (size_t)n * Fc * 16, st));
       pfr::launch_functional_tangent(fa, s->X, s->DX, Fc, nv, q0, s->G, st);
       pfr::launch_tangent_spmv(s->d_cptr, s->d_cidx, s->d_cnz, (int)n, Kd, s->XA, Fc, nullptr, make_double2(0, 0),
                                s->G, 1, st);
-      if ((rc = solve_all(s, 2, 2, rg, nullptr, s->Y, st)) || (rc = solve_all(s, 3, 0, rg, s->Y, s->DL, st)))
-        return rc;
+      if ((rc = adjoint_solve(s, rg, s->DL, st))) return rc;
       pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->DL, s->X, Fc, nv, s->partial,
                            st);
       pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->DL, Fc, s->tq, st);
@@ -910,6 +1015,8 @@ int pfr_solve_multi(pfr_solver* s, int32_t batch, int32_t nrhs, const double* da
   if (data_stride != 0 && data_stride < s->nnz) return fail(PFR_ERR_ARG, "data_stride < nnz");
   if (b_stride != 0 && b_stride < s->n) return fail(PFR_ERR_ARG, "b_stride < n");
   if (nrhs > 1 && x_rhs_stride < (int64_t)batch * s->n) return fail(PFR_ERR_ARG, "x_rhs_stride < batch * n");
+  if (s->sym)
+    return fail(PFR_ERR_STATE, "explicit-matrix solves need a solver on a general analysis (symmetric = 0)");
   HIP_TRY(hipSetDevice(s->device));
   hipStream_t st = (hipStream_t)stream;
   reset_timing(s);

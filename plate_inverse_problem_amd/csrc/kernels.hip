@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "launch.hpp"
 
@@ -480,9 +481,13 @@ constexpr int TM = SCHUR_TM, TN = SCHUR_TN;
 // and U12 column value a wave-instruction reads serves two sub-tiles.  (8
 // frequencies x 8 sub-tiles as 8 x 16 was measured 22 % slower: eight distinct
 // 128 B lines per wave-instruction instead of four 256 B runs.)
-__global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* __restrict__ tiles, int ntiles,
-                                                      const int* __restrict__ g1, const int* __restrict__ gxp,
-                                                      const int2* __restrict__ gx, cplx* __restrict__ F, int64_t Fc) {
+// SYM (symmetric mode): only the lower triangle of A22 is formed; U12 = diag(U11) L21^T is
+// not stored, its entries are made from the L21 rows at load.
+// PF: the next pivot step's loads are issued before the current step's arithmetic.
+template <bool SYM, bool PF>
+__device__ __forceinline__ void schur_tile(const DevPattern& P, const int4* __restrict__ tiles, int ntiles,
+                                           const int* __restrict__ g1, const int* __restrict__ gxp,
+                                           const int2* __restrict__ gx, cplx* __restrict__ F, int64_t Fc) {
   const int lane = threadIdx.x & 63;
   // all super-tiles of one (front, 16 frequencies) on one XCD: the L21 rows and
   // U12 columns they share are fetched into that XCD's L2 once
@@ -541,29 +546,75 @@ __global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* _
       }
     }
   }
+  // row pointers: L21 row r, pivot k at pa[k * Fc]; U12 column c at pb[k * f * Fc] (general) or
+  // L21 row c at pb[k * Fc] times the pivot U(k, k) (symmetric).  All loads of a pivot step are
+  // issued before the arithmetic that uses them.
+  const cplx* pa[TM];
+  const cplx* pb[TN];
+#pragma unroll
+  for (int m = 0; m < TM; ++m) pa[m] = base + (int64_t)ri[m] * f * Fc;
+#pragma unroll
+  for (int n = 0; n < TN; ++n) pb[n] = base + (SYM ? (int64_t)cj[n] * f * Fc : (int64_t)cj[n] * Fc);
+  const int64_t sb = SYM ? Fc : (int64_t)f * Fc, sd = (int64_t)(f + 1) * Fc;
+  cplx a[TM], b[TN], dk = make_double2(1.0, 0.0);
+  auto load = [&](int k, cplx (&aa)[TM], cplx (&bb)[TN], cplx& dd) {
+#pragma unroll
+    for (int m = 0; m < TM; ++m) aa[m] = pa[m][k * Fc];
+#pragma unroll
+    for (int n = 0; n < TN; ++n) bb[n] = pb[n][k * sb];
+    if (SYM) dd = base[k * sd];
+  };
+  if (PF && ns > 0) load(0, a, b, dk);
   for (int k = 0; k < ns; ++k) {
-    cplx a[TM], b[TN];
+    cplx ca[TM], cb[TN], cd;
+    if (PF) {
 #pragma unroll
-    for (int m = 0; m < TM; ++m) a[m] = base[((int64_t)ri[m] * f + k) * Fc];
+      for (int m = 0; m < TM; ++m) ca[m] = a[m];
 #pragma unroll
-    for (int n = 0; n < TN; ++n) b[n] = base[((int64_t)k * f + cj[n]) * Fc];
+      for (int n = 0; n < TN; ++n) cb[n] = b[n];
+      cd = dk;
+      if (k + 1 < ns) load(k + 1, a, b, dk);
+    } else {
+      load(k, ca, cb, cd);
+    }
+    if (SYM) {
+#pragma unroll
+      for (int m = 0; m < TM; ++m) ca[m] = cmul(ca[m], cd);
+    }
 #pragma unroll
     for (int m = 0; m < TM; ++m)
 #pragma unroll
-      for (int n = 0; n < TN; ++n) acc[m][n] = cfms(acc[m][n], a[m], b[n]);
+      for (int n = 0; n < TN; ++n) acc[m][n] = cfms(acc[m][n], ca[m], cb[n]);
   }
 #pragma unroll
   for (int m = 0; m < TM; ++m)
 #pragma unroll
     for (int n = 0; n < TN; ++n)
-      if (ns + t.y + m < f && ns + t.z + n < f)
+      if (ns + t.y + m < f && ns + t.z + n < f && (!SYM || t.y + m >= t.z + n))
         base[((int64_t)(ns + t.y + m) * f + ns + t.z + n) * Fc] = acc[m][n];
+}
+
+__global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* __restrict__ tiles, int ntiles,
+                                                      const int* __restrict__ g1, const int* __restrict__ gxp,
+                                                      const int2* __restrict__ gx, cplx* __restrict__ F, int64_t Fc) {
+  schur_tile<false, false>(P, tiles, ntiles, g1, gxp, gx, F, Fc);
+}
+
+// symmetric mode: register budget of 2 waves per SIMD so that every load of a pivot step
+// (or of two steps with PF) is in flight at once (the default budget serialises them)
+template <bool PF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_schur_sym_level(
+    DevPattern P, const int4* __restrict__ tiles, int ntiles, const int* __restrict__ g1,
+    const int* __restrict__ gxp, const int2* __restrict__ gx, cplx* __restrict__ F, int64_t Fc) {
+  schur_tile<true, PF>(P, tiles, ntiles, g1, gxp, gx, F, Fc);
 }
 
 // ------------------------------------------------------------------ right-hand sides
 // RHS 0: b_p = rhsP[p] * (beta0 - omega^2 * mass_sum)   (Problem.py:447-449)
 // RHS 1: b_p = B[q * b_stride + perm[p]]                 (explicit batch)
 // RHS 2: b_p = G[p * Fc + q]                             (permuted device vector)
+// RHS 3: RHS 0 + Bc[cslot[p] * Fc + q]                   (symmetric mode: Dirichlet columns moved
+//        to the right-hand side, b_i - sum_d A_id b_d / A_dd, k_dirichlet_rhs)
 struct RhsArgs {
   const double* rhsP;     // RHS 0: permuted Dirichlet vector
   double beta_re, beta_im, mass_sum;
@@ -572,15 +623,24 @@ struct RhsArgs {
   int64_t b_stride;
   const cplx* G;          // RHS 2
   int nvalid;             // RHS 1: padded lanes repeat the last valid item
+  const int* cslot;       // RHS 3: coupled-row slot of each permuted row (or -1)
+  const cplx* Bc;         // RHS 3: Dirichlet corrections, slot-major (slot * Fc + q)
 };
 
 template <int RHS>
 __device__ __forceinline__ cplx rhs_value(const DevPattern& P, const RhsArgs& R, int p, int64_t q, int64_t Fc) {
-  if (RHS == 0) {
+  if (RHS == 0 || RHS == 3) {
     const double v = R.rhsP[p];
-    if (v == 0.0) return make_double2(0.0, 0.0);
-    const double om = 6.283185307179586 * R.freqs[q];
-    return make_double2(v * fma(-om * om, R.mass_sum, R.beta_re), v * R.beta_im);
+    cplx b = make_double2(0.0, 0.0);
+    if (v != 0.0) {
+      const double om = 6.283185307179586 * R.freqs[q];
+      b = make_double2(v * fma(-om * om, R.mass_sum, R.beta_re), v * R.beta_im);
+    }
+    if (RHS == 3) {
+      const int c = R.cslot[p];
+      if (c >= 0) b = cadd(b, R.Bc[(int64_t)c * Fc + q]);
+    }
+    return b;
   } else if (RHS == 1) {
     return R.B[min(q, (int64_t)R.nvalid - 1) * R.b_stride + P.perm[p]];
   } else {
@@ -665,6 +725,8 @@ __device__ __forceinline__ cplx offdiag_dot(cplx v, const cplx* __restrict__ e, 
 }
 
 // ------------------------------------------------------------------ K3b: U x = y (top-down)
+// SYM: U12 row a = U(a, a) * (column a of L21)^T (symmetric mode, U12 never formed)
+template <bool SYM>
 __global__ void k_usolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
                                cplx* __restrict__ WV, const cplx* __restrict__ Y, cplx* __restrict__ X) {
   const Ctx c = ctx();
@@ -677,7 +739,12 @@ __global__ void k_usolve_level(DevPattern P, const int* __restrict__ lvl, const 
 #define V(a) wv[(int64_t)(a) * Fc]
   for (int a = c.w; a < ns; a += c.W) {
     cplx v = Y[(int64_t)(fr.col0 + a) * Fc + c.q];
-    v = offdiag_dot(v, &E(a, 0), Fc, X, ix, ns, f, Fc, c.q);
+    if (SYM) {
+      const cplx t = offdiag_dot(make_double2(0.0, 0.0), &E(0, a), (int64_t)f * Fc, X, ix, ns, f, Fc, c.q);
+      v = cadd(v, cmul(E(a, a), t));
+    } else {
+      v = offdiag_dot(v, &E(a, 0), Fc, X, ix, ns, f, Fc, c.q);
+    }
     V(a) = v;
   }
   __syncthreads();
@@ -789,6 +856,79 @@ __global__ void k_ltsolve_level(DevPattern P, const int* __restrict__ lvl, const
   }
 #undef E
 #undef V
+}
+
+// ------------------------------------------------------------------ Dirichlet decoupling (symmetric mode)
+// A Dirichlet row d holds only A_dd; its column entries A_id (i not Dirichlet) are left out
+// of the factorisation, which then sees the decoupled matrix diag(A_DD) + A_rr (A_rr complex
+// symmetric).  Exactly equivalent rewrites of the original systems:
+//   forward  A x = b:       b_i -= sum_d A_id b_d / A_dd        (before the solve)
+//   adjoint  A^T l = g:     l_d -= sum_i A_id l_i / A_dd        (after the solve)
+// A = K - omega^2 M (operator form).  One wave per coupled row / Dirichlet node (64 frequencies).
+struct DirArgs {
+  const int2* dir;        // per Dirichlet node: (permuted node, diagonal entry)
+  const int* crow;        // coupled rows (permuted)
+  const int* cptr;        // entry range of each coupled row in ce
+  const int2* ce;         // (Dirichlet slot, entry)
+  const int* dptr;        // entry range of each Dirichlet node in de
+  const int2* de;         // (permuted row, entry)
+  const cplx* K;
+  const double* M;
+  const double* freqs;
+};
+
+__device__ __forceinline__ cplx op_entry(const DirArgs& D, int nz, double om2) {
+  const cplx k = D.K[nz];
+  return make_double2(fma(-om2, D.M[nz], k.x), k.y);
+}
+
+__device__ __forceinline__ cplx cdiv(cplx a, cplx b) { return cmul(a, crecip(b)); }
+
+// SRC 0: b from the operator right-hand side (RHS 0), corrections into Bc (slot-major);
+// SRC 2: b = G (permuted, frequency-minor), corrected in place
+template <int SRC>
+__global__ __launch_bounds__(64) void k_dirichlet_rhs(DirArgs D, RhsArgs R, cplx* __restrict__ G,
+                                                      cplx* __restrict__ Bc, int64_t Fc) {
+  const int slot = blockIdx.x;
+  const int64_t q = (int64_t)blockIdx.y * 64 + threadIdx.x;
+  const double om = 6.283185307179586 * D.freqs[q];
+  const double om2 = om * om;
+  cplx v = make_double2(0.0, 0.0);
+  const int e1 = D.cptr[slot + 1];
+  for (int e = D.cptr[slot]; e < e1; ++e) {
+    const int2 c = D.ce[e];
+    const int2 d = D.dir[c.x];
+    cplx bd;
+    if (SRC == 0) {
+      const double r = R.rhsP[d.x];
+      bd = make_double2(r * fma(-om2, R.mass_sum, R.beta_re), r * R.beta_im);
+    } else {
+      bd = G[(int64_t)d.x * Fc + q];
+    }
+    v = cfms(v, op_entry(D, c.y, om2), cdiv(bd, op_entry(D, d.y, om2)));
+  }
+  if (SRC == 0) {
+    Bc[(int64_t)slot * Fc + q] = v;
+  } else {
+    cplx* g = G + (int64_t)D.crow[slot] * Fc + q;
+    *g = cadd(*g, v);
+  }
+}
+
+__global__ __launch_bounds__(64) void k_dirichlet_post(DirArgs D, cplx* __restrict__ X, int64_t Fc) {
+  const int slot = blockIdx.x;
+  const int64_t q = (int64_t)blockIdx.y * 64 + threadIdx.x;
+  const double om = 6.283185307179586 * D.freqs[q];
+  const double om2 = om * om;
+  const int2 d = D.dir[slot];
+  cplx s = make_double2(0.0, 0.0);
+  const int e1 = D.dptr[slot + 1];
+  for (int e = D.dptr[slot]; e < e1; ++e) {
+    const int2 c = D.de[e];
+    s = cfms(s, op_entry(D, c.y, om2), X[(int64_t)c.x * Fc + q]);   // -sum A_id l_i
+  }
+  cplx* x = X + (int64_t)d.x * Fc + q;
+  *x = cadd(*x, cdiv(s, op_entry(D, d.y, om2)));
 }
 
 // ------------------------------------------------------------------ Hessian: tangent operators
@@ -1113,11 +1253,17 @@ void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPac
   LAUNCH(k_combine, dim3((unsigned)((nnz + 255) / 256)), dim3(256), st, stiff, n_stiff, nnz, coef, K);
 }
 
-void launch_schur(const DevPattern& P, const int4* tiles, int ntiles, const int* g1, const int* gxp, const int2* gx,
-                  int ngroups, double2* F, int64_t Fc, hipStream_t st) {
+void launch_schur(bool sym, const DevPattern& P, const int4* tiles, int ntiles, const int* g1, const int* gxp,
+                  const int2* gx, int ngroups, double2* F, int64_t Fc, hipStream_t st) {
   if (ntiles <= 0) return;
-  LAUNCH(k_schur_level, dim3((ntiles + 3) / 4, ngroups * (64 / SCHUR_QG)), dim3(256), st, P, tiles, ntiles, g1, gxp,
-         gx, F, Fc);
+  dim3 g((ntiles + 3) / 4, ngroups * (64 / SCHUR_QG)), b(256);
+  static const int pf = [] {
+    const char* e = getenv("PFR_SCHUR_PF");   // tuning knob: 0 = no software prefetch
+    return e ? atoi(e) : 1;
+  }();
+  if (sym && pf) LAUNCH(k_schur_sym_level<true>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
+  else if (sym) LAUNCH(k_schur_sym_level<false>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
+  else LAUNCH(k_schur_level, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
 }
 
 void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, const int2* xl, int ngroups, double2* F,
@@ -1149,10 +1295,11 @@ static RhsArgs make_rhs(const RhsDesc& d) {
   RhsArgs r;
   r.rhsP = d.rhsP; r.beta_re = d.beta_re; r.beta_im = d.beta_im; r.mass_sum = d.mass_sum;
   r.freqs = d.freqs; r.B = d.B; r.b_stride = d.b_stride; r.G = d.G; r.nvalid = d.nvalid;
+  r.cslot = d.cslot; r.Bc = d.Bc;
   return r;
 }
 
-void launch_solve(int which, int rhs_mode, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups,
+void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups,
                   const double2* F, int64_t Fc, double2* WV, const RhsDesc& rd, const double2* Yin, double2* Out,
                   hipStream_t st) {
   dim3 g(nfronts, ngroups), b(64 * W);
@@ -1161,10 +1308,12 @@ void launch_solve(int which, int rhs_mode, const DevPattern& P, const int* lvl, 
     case 0:  // L solve
       if (rhs_mode == 0) LAUNCH(k_lsolve_level<0>, g, b, st, P, lvl, F, Fc, WV, R, Out);
       else if (rhs_mode == 1) LAUNCH(k_lsolve_level<1>, g, b, st, P, lvl, F, Fc, WV, R, Out);
-      else LAUNCH(k_lsolve_level<2>, g, b, st, P, lvl, F, Fc, WV, R, Out);
+      else if (rhs_mode == 2) LAUNCH(k_lsolve_level<2>, g, b, st, P, lvl, F, Fc, WV, R, Out);
+      else LAUNCH(k_lsolve_level<3>, g, b, st, P, lvl, F, Fc, WV, R, Out);
       break;
     case 1:  // U solve
-      LAUNCH(k_usolve_level, g, b, st, P, lvl, F, Fc, WV, Yin, Out);
+      if (sym) LAUNCH(k_usolve_level<true>, g, b, st, P, lvl, F, Fc, WV, Yin, Out);
+      else LAUNCH(k_usolve_level<false>, g, b, st, P, lvl, F, Fc, WV, Yin, Out);
       break;
     case 2:  // U^T solve
       if (rhs_mode == 0) LAUNCH(k_utsolve_level<0>, g, b, st, P, lvl, F, Fc, WV, R, Out);
@@ -1220,6 +1369,26 @@ void launch_matvec(const int* colptr, const int* rowind, int n, const double2* d
                    int64_t xs, double2* y, int transpose, int batch, hipStream_t st) {
   LAUNCH(k_matvec, dim3((n + 255) / 256, batch), dim3(256), st, colptr, rowind, n, data, ds, x, xs, y, transpose,
          batch);
+}
+
+static DirArgs make_dir(const DirDesc& d) {
+  DirArgs a;
+  a.dir = d.dir; a.crow = d.crow; a.cptr = d.cptr; a.ce = d.ce; a.dptr = d.dptr; a.de = d.de;
+  a.K = d.K; a.M = d.M; a.freqs = d.freqs;
+  return a;
+}
+
+void launch_dirichlet_rhs(int src, const DirDesc& d, int n_crow, const RhsDesc& rd, double2* G, double2* Bc,
+                          int64_t Fc, hipStream_t st) {
+  if (n_crow <= 0) return;
+  dim3 g(n_crow, (unsigned)(Fc / 64)), b(64);
+  if (src == 0) LAUNCH(k_dirichlet_rhs<0>, g, b, st, make_dir(d), make_rhs(rd), G, Bc, Fc);
+  else LAUNCH(k_dirichlet_rhs<2>, g, b, st, make_dir(d), make_rhs(rd), G, Bc, Fc);
+}
+
+void launch_dirichlet_post(const DirDesc& d, int n_dir, double2* X, int64_t Fc, hipStream_t st) {
+  if (n_dir <= 0) return;
+  LAUNCH(k_dirichlet_post, dim3(n_dir, (unsigned)(Fc / 64)), dim3(64), st, make_dir(d), X, Fc);
 }
 
 // fill padded frequency slots with the last valid frequency (keeps padded lanes well-posed)

@@ -13,6 +13,21 @@ struct RhsDesc {
   int64_t b_stride = 0;
   const double2* G = nullptr;     // RHS 2: permuted frequency-minor vector (device)
   int nvalid = 1;                 // RHS 1: valid batch items of the chunk
+  const int* cslot = nullptr;     // RHS 3: coupled-row slot per permuted row (symmetric mode)
+  const double2* Bc = nullptr;    // RHS 3: Dirichlet corrections (slot-major)
+};
+
+// Dirichlet decoupling lists of a symmetric-mode solver (device pointers) + operator
+struct DirDesc {
+  const int2* dir = nullptr;
+  const int* crow = nullptr;
+  const int* cptr = nullptr;
+  const int2* ce = nullptr;
+  const int* dptr = nullptr;
+  const int2* de = nullptr;
+  const double2* K = nullptr;
+  const double* M = nullptr;
+  const double* freqs = nullptr;
 };
 
 void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPack& coef, double2* K, hipStream_t st);
@@ -25,10 +40,10 @@ void launch_factor(const DevPattern& P, const int* lvl, int nfronts, int W, int 
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
                     const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,
                     const double* M, const double2* data, int64_t ds, int nvalid, hipStream_t st);
-void launch_schur(const DevPattern& P, const int4* tiles, int ntiles, const int* g1, const int* gxp, const int2* gx,
+void launch_schur(bool sym, const DevPattern& P, const int4* tiles, int ntiles, const int* g1, const int* gxp, const int2* gx,
                   int ngroups, double2* F, int64_t Fc, hipStream_t st);
 // which: 0 = L (bottom-up), 1 = U (top-down), 2 = U^T (bottom-up), 3 = L^T (top-down)
-void launch_solve(int which, int rhs_mode, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups,
+void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups,
                   const double2* F, int64_t Fc, double2* WV, const RhsDesc& rd, const double2* Yin, double2* Out,
                   hipStream_t st);
 // Hessian sweep: tangent right-hand sides (rows of the permuted matrix, or of its
@@ -48,6 +63,11 @@ void launch_rhs_dot(const int* sup, const double* val, int n_sup, const double2*
 void launch_reduce(const double2* partial, int nparts, int n_stiff, const double2* t_q, const CoefPack& e,
                    const double* loss_terms, int nvalid, int64_t Fc, double2* w_out, double* loss_out,
                    hipStream_t st);
+// symmetric mode: forward right-hand-side corrections (src 0: operator rhs -> Bc; src 2: G in
+// place) and the adjoint's Dirichlet rows (X in place)
+void launch_dirichlet_rhs(int src, const DirDesc& d, int n_crow, const RhsDesc& rd, double2* G, double2* Bc,
+                          int64_t Fc, hipStream_t st);
+void launch_dirichlet_post(const DirDesc& d, int n_dir, double2* X, int64_t Fc, hipStream_t st);
 void launch_unpermute(const int* perm, int n, const double2* X, int64_t Fc, int nvalid, double2* out, hipStream_t st);
 void launch_matvec(const int* colptr, const int* rowind, int n, const double2* data, int64_t ds, const double2* x,
                    int64_t xs, double2* y, int transpose, int batch, hipStream_t st);

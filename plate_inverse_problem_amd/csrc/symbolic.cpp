@@ -4,6 +4,7 @@
 #include "symbolic.hpp"
 
 #include <algorithm>
+#include <array>
 #include <cstring>
 #include <numeric>
 #include <stdexcept>
@@ -17,12 +18,13 @@ struct Graph {
   int deg(int v) const { return ptr[v + 1] - ptr[v]; }
 };
 
-Graph symmetric_graph(int n, const int32_t* colptr, const int32_t* rowind) {
+// Adjacency of A + A^T without self loops; edges touching a `cut` node are left out.
+Graph symmetric_graph(int n, const int32_t* colptr, const int32_t* rowind, const std::vector<char>& cut) {
   std::vector<int> cnt(n + 1, 0);
   for (int j = 0; j < n; ++j)
     for (int k = colptr[j]; k < colptr[j + 1]; ++k) {
       int i = rowind[k];
-      if (i == j) continue;
+      if (i == j || cut[i] || cut[j]) continue;
       cnt[i + 1]++;
       cnt[j + 1]++;
     }
@@ -32,7 +34,7 @@ Graph symmetric_graph(int n, const int32_t* colptr, const int32_t* rowind) {
   for (int j = 0; j < n; ++j)
     for (int k = colptr[j]; k < colptr[j + 1]; ++k) {
       int i = rowind[k];
-      if (i == j) continue;
+      if (i == j || cut[i] || cut[j]) continue;
       tmp[pos[i]++] = j;
       tmp[pos[j]++] = i;
     }
@@ -261,7 +263,18 @@ int analyse(int32_t n, int64_t nnz, const int32_t* colptr, const int32_t* rowind
     S = Symbolic();
     S.n = n;
     S.nnz = nnz;
-    Graph g = symmetric_graph(n, colptr, rowind);
+    S.symmetric = opt.symmetric ? 1 : 0;
+    // symmetric mode: Dirichlet nodes (a diagonal entry and no other entry in their row) are
+    // cut out of the graph -- isolated, they become 1 x 1 fronts, and the entries of their
+    // columns are handled outside the factorisation (forward rhs / adjoint corrections)
+    std::vector<char> isdir(n, 0);
+    if (opt.symmetric) {
+      std::vector<char> offd(n, 0), diag(n, 0);
+      for (int j = 0; j < n; ++j)
+        for (int k = colptr[j]; k < colptr[j + 1]; ++k) (rowind[k] == j ? diag : offd)[rowind[k]] = 1;
+      for (int v = 0; v < n; ++v) isdir[v] = diag[v] && !offd[v];
+    }
+    Graph g = symmetric_graph(n, colptr, rowind, isdir);
 
     // ---- ordering
     std::vector<int> perm;
@@ -510,11 +523,25 @@ int analyse(int32_t n, int64_t nnz, const int32_t* colptr, const int32_t* rowind
     S.pcol.resize(nnz);
     std::vector<int32_t> dest(nnz), dcol(nnz);
     std::vector<int32_t> cnt(rows + 1, 0);
+    std::vector<int32_t> dir_slot(n, -1);
+    std::vector<std::array<int32_t, 3>> cpl;   // (row, Dirichlet node, entry)
+    for (int p = 0; p < n; ++p)
+      if (isdir[perm[p]]) {
+        dir_slot[p] = (int32_t)S.dir_p.size();
+        S.dir_p.push_back(p);
+        S.dir_nz.push_back(-1);
+      }
     for (int j = 0; j < n; ++j)
       for (int64_t k = colptr[j]; k < colptr[j + 1]; ++k) {
         int pi = iperm[rowind[k]], pj = iperm[j];
         S.prow[k] = pi;
         S.pcol[k] = pj;
+        if (isdir[j] && rowind[k] == j) S.dir_nz[dir_slot[pj]] = (int32_t)k;
+        if (isdir[j] && rowind[k] != j) {   // column entry of a Dirichlet node: not assembled
+          cpl.push_back({pi, dir_slot[pj], (int32_t)k});
+          dest[k] = -1;
+          continue;
+        }
         int t = front_of_col[std::min(pi, pj)];
         int a = local_pos(t, pi), b = local_pos(t, pj);
         if (a < 0 || b < 0) throw std::runtime_error("entry outside its front (symbolic bug)");
@@ -522,13 +549,22 @@ int analyse(int32_t n, int64_t nnz, const int32_t* colptr, const int32_t* rowind
         dcol[k] = b;
         cnt[dest[k] + 1]++;
       }
+    for (int32_t z : S.dir_nz)
+      if (z < 0) throw std::runtime_error("Dirichlet node without a diagonal entry");
+    std::sort(cpl.begin(), cpl.end());
+    for (const auto& c : cpl) {
+      S.cpl_p.push_back(c[0]);
+      S.cpl_dir.push_back(c[1]);
+      S.cpl_nz.push_back(c[2]);
+    }
     for (int64_t r = 0; r < rows; ++r) cnt[r + 1] += cnt[r];
     S.asm_ptr = cnt;
-    S.asm_col.resize(nnz);
-    S.asm_nz.resize(nnz);
+    S.asm_col.resize(cnt[rows]);
+    S.asm_nz.resize(cnt[rows]);
     {
       std::vector<int32_t> pos(cnt.begin(), cnt.end() - 1);
       for (int64_t k = 0; k < nnz; ++k) {
+        if (dest[k] < 0) continue;
         int32_t p = pos[dest[k]]++;
         S.asm_col[p] = dcol[k];
         S.asm_nz[p] = (int32_t)k;

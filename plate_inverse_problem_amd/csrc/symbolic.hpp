@@ -24,6 +24,7 @@ struct SymbolicOptions {
   double zrelax_mid = 0.5;
   double zrelax_big = 0.1;
   int ordering = 0;          // 0 = nested dissection, 1 = natural (tests)
+  int symmetric = 0;         // 1 = symmetric-structure analysis with decoupled Dirichlet nodes
 };
 
 struct Front {
@@ -62,6 +63,12 @@ struct Symbolic {
   int64_t nnz_lu = 0;           // sum (2 ns f - ns^2)
   double factor_flops = 0.0;    // real flops of the numeric factorisation (complex MAC = 8)
   int32_t max_front = 0;
+  // symmetric mode (options.symmetric): Dirichlet nodes d (rows holding only their diagonal)
+  // are decoupled 1 x 1 fronts; the entries (i, d) of their columns are not assembled into
+  // any front but listed here (forward right-hand-side and adjoint corrections)
+  int symmetric = 0;
+  std::vector<int32_t> dir_p, dir_nz;            // per Dirichlet node: permuted index, diagonal entry
+  std::vector<int32_t> cpl_p, cpl_dir, cpl_nz;   // coupling entries sorted by permuted row: row, dir slot, entry
   std::string error;
 };
 

@@ -106,3 +106,48 @@ class MFModel:
         out = np.zeros(self.n, dtype=complex)
         out[self.perm] = X
         return out
+
+    # ---------------------------------------------------------------- symmetric mode
+    def solve_sym(self, F, b, sym, data, transpose=False):
+        """Symmetric-mode solve (pfr_symbolic_options.symmetric = 1), as libpfr runs it:
+        the factorisation is of the decoupled matrix (Dirichlet columns left out); the
+        U solve uses U12 = diag(U11) L21^T (U12 never formed).  forward: Dirichlet columns
+        moved to the right-hand side first; transpose: Dirichlet rows of the solution
+        corrected after the solve (kernels.hip k_dirichlet_rhs / k_dirichlet_post)."""
+        dirs = sym.export("DIRICHLET")
+        cpl = sym.export("COUPLING")
+        bp = b[self.perm].astype(complex)
+        if not transpose:
+            for p_i, ds, nz in cpl:
+                p_d, nz_dd = dirs[ds]
+                bp[p_i] -= data[nz] * bp[p_d] / data[nz_dd]
+        WV = np.zeros(int(self.fr[:, 1].sum()), dtype=complex)
+        Y = np.zeros(self.n, dtype=complex)
+        X = np.zeros(self.n, dtype=complex)
+        for lvl in self.levels():
+            for t in lvl:
+                ns, f, row0, col0 = (int(v) for v in self.fr[t, :4])
+                w = self._gather(F, WV, t, bp)
+                A = F[t]
+                for k in range(ns):
+                    w[k + 1:] -= A[k + 1:, k] * w[k]
+                WV[row0:row0 + f] = w
+                Y[col0:col0 + ns] = w[:ns]
+        for lvl in self.levels(reverse=True):
+            for t in lvl:
+                ns, f, row0, col0 = (int(v) for v in self.fr[t, :4])
+                A = F[t]
+                xr = X[self.idx[row0 + ns:row0 + f]]
+                U12 = np.diag(A)[:ns, None] * A[ns:, :ns].T
+                v = Y[col0:col0 + ns] - U12 @ xr
+                for k in range(ns - 1, -1, -1):
+                    v[k] /= A[k, k]
+                    v[:k] -= A[:k, k] * v[k]
+                X[col0:col0 + ns] = v
+        if transpose:
+            for p_i, ds, nz in cpl:
+                p_d, nz_dd = dirs[ds]
+                X[p_d] -= data[nz] * X[p_i] / data[nz_dd]
+        out = np.zeros(self.n, dtype=complex)
+        out[self.perm] = X
+        return out

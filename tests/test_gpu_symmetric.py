@@ -1,0 +1,84 @@
+"""GPU: symmetric mode (pfr_symbolic_options.symmetric) against the general LU path and the oracle.
+
+Every FE matrix of the reference model is complex symmetric once the Dirichlet rows (only a
+diagonal entry, tgv = -1, pyFFInterface.py:176) and their columns are taken out, so the
+engine factorises A = L diag(U) L^T-style (U never formed, Dirichlet columns moved to the
+right-hand side / the adjoint's Dirichlet rows).  Both paths must meet
+the parity tolerances of test_gpu_parity.py; PFR_SYMMETRIC=0 selects the general path.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import make_problem, oracle_for
+
+pytestmark = pytest.mark.gpu
+
+FR_RTOL = 1e-8
+GRAD_RTOL = 1e-6
+
+
+def _rel(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+@pytest.mark.parametrize("material", ["isotropic", "orthotropic", "orthotropic_d4", "sol", "sol_sym", "symm_sol"])
+def test_symmetric_mode_selected(material):
+    p = make_problem(material, ny=3, device="cuda:0")
+    eng = p.engine()
+    assert eng.symmetric
+    st = eng.sym.stats()
+    assert st["symmetric"] == 1 and st["n_dirichlet"] > 0
+
+
+@pytest.mark.parametrize("mode", ["symmetric", "general"])
+@pytest.mark.parametrize("material,loss_type", [("orthotropic", "MSE_LOG_AFC"), ("sol", "MSE_AFC")])
+def test_both_modes_match_oracle(mode, material, loss_type, monkeypatch):
+    from oracle.plate_oracle import loss_and_grad
+    monkeypatch.setenv("PFR_SYMMETRIC", "1" if mode == "symmetric" else "0")
+    p = make_problem(material, ny=5, device="cuda:0")
+    assert p.engine().symmetric == (mode == "symmetric")
+    freqs = np.linspace(40.0, 600.0, 90)
+    orc = oracle_for(p)
+    fr = p.solveForward(freqs)
+    assert _rel(fr, orc.fr(freqs, p.parameters)) < FR_RTOL
+    ref = fr * np.exp(0.1j) * 1.02
+    theta = p.parameters * 1.04
+    x = torch.tensor(theta, requires_grad=True)
+    val = p.getLossFunction(freqs, ref, loss_type)(x)
+    val.backward()
+    lo, go = loss_and_grad(orc, freqs, ref, loss_type, theta)
+    assert abs(val.item() - lo) / abs(lo) < FR_RTOL
+    assert _rel(x.grad.numpy(), go) < GRAD_RTOL
+
+
+def test_general_mode_hessian_matches_symmetric(monkeypatch):
+    """The exact Hessian (tangent and second-order adjoint solves with the Dirichlet
+    corrections) agrees between the two factorisations."""
+    freqs = np.linspace(40, 600, 96)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("PFR_SYMMETRIC", mode)
+        p = make_problem("orthotropic", ny=4, device="cuda:0")
+        ref = p.solveForward(freqs).astype(np.complex128)
+        theta0 = np.asarray(p.parameters, dtype=np.float64)
+        model = p.getLossHessianFunction(freqs, ref * 1.03, "MSE_LOG_AFC", theta0)
+        out[mode] = model(np.array([1.03, 0.98, 1.04, 1.02, 1.05]))
+    f1, g1, H1 = out["1"]
+    f0, g0, H0 = out["0"]
+    assert abs(f1 - f0) <= 1e-9 * abs(f0)
+    assert _rel(g1, g0) < 1e-7
+    assert _rel(H1, H0) < 1e-6
+
+
+def test_explicit_solve_refused_on_symmetric_solver():
+    from plate_inverse_problem_amd import _native
+    p = make_problem("isotropic", ny=3, device="cuda:0")
+    eng = p.engine()
+    n, nnz = p.mat_size, eng.keep.size
+    data = torch.zeros((1, nnz), dtype=torch.complex128, device="cuda:0")
+    b = torch.zeros((1, n), dtype=torch.complex128, device="cuda:0")
+    x = torch.zeros_like(b)
+    with pytest.raises(_native.NativeError, match="general analysis"):
+        eng.solver.solve(torch.view_as_real(data), nnz, torch.view_as_real(b), n, torch.view_as_real(x), False, 1)

@@ -37,7 +37,8 @@ def test_bad_arguments_return_status():
 
 
 def _active_pattern(p):
-    keep = p.present[[k for k in range(26) if not (p.material.is_mps and 6 <= k < 12)]].any(0)
+    active = [k for k in range(26) if not (p.material.is_mps and 6 <= k < 12)]
+    keep = p.present[active].any(0) & (p.mats[active] != 0).any(0)     # as Problem._Engine
     idx = np.nonzero(keep)[0]
     rows, cols = p.rows[idx], p.cols[idx]
     colptr = np.zeros(p.mat_size + 1, np.int64)
@@ -102,3 +103,52 @@ def test_workspace_estimate_scales_with_batch():
     sym = _native.Symbolic(p.mat_size, colptr, rowind)
     assert sym.workspace_bytes(128) == 2 * sym.workspace_bytes(64)
     assert sym.workspace_bytes(65) == sym.workspace_bytes(128)
+
+
+@pytest.mark.parametrize("material", ["isotropic", "orthotropic", "sol", "symm_sol"])
+def test_symmetric_mode_model_matches_dense(material):
+    """Symmetric analysis: Dirichlet nodes decoupled, U = diag(U) L^T implicit, forward and
+    transpose solves (with the Dirichlet corrections) == dense solves of the ORIGINAL matrix."""
+    from plate_inverse_problem_amd.Problem import decoupled_symmetric
+    p = make_problem(material, ny=3)
+    idx, colptr, rowind = _active_pattern(p)
+    cols = np.repeat(np.arange(p.mat_size), np.diff(colptr))
+    assert decoupled_symmetric(rowind, cols, p.mats[:, idx], p.mat_size)
+    sym = _native.Symbolic(p.mat_size, colptr, rowind, leaf_size=16, symmetric=True)
+    st = sym.stats()
+    assert st["symmetric"] == 1 and st["n_dirichlet"] > 0 and st["n_coupling"] > 0
+    dirs, cpl = sym.export("DIRICHLET"), sym.export("COUPLING")
+    asm_nz = sym.export("ASM_NZ")
+    # every entry is assembled once, or is a Dirichlet column entry
+    assert np.array_equal(np.sort(np.concatenate([asm_nz, cpl[:, 2]])), np.arange(rowind.size))
+    fr = sym.export("FRONTS")
+    perm = sym.export("PERM")
+    for p_d, nz in dirs:          # decoupled 1 x 1 fronts, diagonal entry
+        t = np.nonzero((fr[:, 3] <= p_d) & (p_d < fr[:, 3] + fr[:, 0]))[0][0]
+        assert fr[t, 0] == 1 and fr[t, 1] == 1
+        assert rowind[nz] == perm[p_d] and cols[nz] == perm[p_d]
+    orc = oracle_for(p)
+    c = orc.coefficients(p.parameters)
+    data = (orc.mass_values() * -(2 * np.pi * 317.0) ** 2 + c @ p.mats[:18])[idx]
+    A = sp.csc_matrix((data, rowind, colptr), shape=(p.mat_size,) * 2).toarray()
+    rng = np.random.default_rng(1)
+    b = rng.standard_normal(p.mat_size) + 1j * rng.standard_normal(p.mat_size)
+    mf = MFModel(sym)
+    F = mf.factor(data)
+    for tr in (False, True):
+        x = mf.solve_sym(F, b, sym, data, transpose=tr)
+        xd = np.linalg.solve(A.T if tr else A, b)
+        assert np.linalg.norm(x - xd) / np.linalg.norm(xd) < 1e-10, tr
+
+
+def test_symmetric_detection_rejects_unsymmetric():
+    from plate_inverse_problem_amd.Problem import decoupled_symmetric
+    rows = np.array([0, 1, 0, 1, 2, 2])
+    cols = np.array([0, 0, 1, 1, 1, 2])
+    v = np.array([[2.0, 1.0, 1.0, 3.0, 0.5, 1.0]])     # row 2 couples to column 1: not Dirichlet
+    assert not decoupled_symmetric(rows, cols, v, 3)
+    rows2, cols2 = np.array([0, 1, 0, 1, 2, 1]), np.array([0, 0, 1, 1, 2, 2])
+    v2 = np.array([[2.0, 1.0, 1.0, 3.0, 1.0, 0.5]])    # row 2 Dirichlet; (1, 2) is its column entry
+    assert decoupled_symmetric(rows2, cols2, v2, 3)
+    v3 = np.array([[2.0, 1.0, 1.5, 3.0, 1.0, 0.5]])
+    assert not decoupled_symmetric(rows2, cols2, v3, 3)

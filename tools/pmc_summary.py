@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--json")
     ap.add_argument("--freqs", type=int, default=2048, help="frequencies of the profiled sweep (one chunk)")
     ap.add_argument("--note", default="")
+    ap.add_argument("--factorisation", default="symmetric", choices=["symmetric", "general"])
     a = ap.parse_args()
     fr, wr = load(a.fetch), load(a.write)
     if a.last_sweep:
@@ -60,7 +61,7 @@ def main():
         print(f"{k:34s} {n:5d} {r/1e9:9.3f} {w/1e9:9.3f} {dt/1e6:8.2f} {gbs:8.0f}")
         out[k] = {"dispatches": n, "read_bytes": r, "write_bytes": w, "ns": dt}
     if a.json:
-        json.dump({"freqs_per_sweep": a.freqs, "note": a.note,
+        json.dump({"freqs_per_sweep": a.freqs, "note": a.note, "factorisation": a.factorisation,
                    "correction": "FETCH_SIZE x2 (gfx950 16 B/lane streaming reads); WRITE_SIZE as is",
                    "kernels": out}, open(a.json, "w"), indent=1)
 
