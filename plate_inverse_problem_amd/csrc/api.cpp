@@ -84,6 +84,13 @@ struct pfr_solver {
   int2* d_de = nullptr;                 // (permuted row, entry) by Dirichlet node
   int32_t* d_cslot = nullptr;           // per permuted row: coupled-row slot or -1
   double2* Bc = nullptr;                // forward right-hand-side corrections (n_crow x Fc)
+  // right-hand-side reach (0 = forward operator rhs, 1 = loss adjoint on the functional support):
+  // the fronts holding a support row and their elimination-tree ancestors -- the only fronts
+  // whose bottom-up solve can be non-zero (per-front flags + the fronts level by level)
+  std::vector<int32_t> front_of_col, front_parent, level_fronts_host;
+  int32_t* d_reach[2] = {nullptr, nullptr};
+  int32_t* d_reach_fronts[2] = {nullptr, nullptr};
+  std::vector<int32_t> reach_ptr[2];
   double2 *F = nullptr, *WV = nullptr, *X = nullptr, *Y = nullptr, *XA = nullptr, *G = nullptr;
   // Hessian sweep: permuted matrix by rows and by columns ((ptr, index, nz) each),
   // tangent solution / adjoint vectors, combined tangent operators (lazily allocated)
@@ -229,16 +236,24 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
 }
 
 // which: 0 L, 1 U, 2 U^T, 3 L^T ; bottom-up for 0/2, top-down for 1/3
+// subset (0 forward rhs, 1 loss adjoint, -1 none): bottom-up passes visit only the reached
+// fronts; top-down passes treat the pivot values of unreached fronts as zero
 int solve_all(pfr_solver* s, int which, int rhs_mode, const pfr::RhsDesc& rd, const double2* Yin, double2* Out,
-              hipStream_t st) {
+              hipStream_t st, int subset = -1) {
   const int L = (int)s->level_ptr.size() - 1;
   const int ngroups = (int)(s->Fc / 64);
   const bool up = (which == 0 || which == 2);
+  const int* reach = subset >= 0 ? s->d_reach[subset] : nullptr;
   for (int t = 0; t < L; ++t) {
     int l = up ? t : L - 1 - t;
+    const int32_t* lvl = s->d_level_fronts + s->level_ptr[l];
     int nf = s->level_ptr[l + 1] - s->level_ptr[l];
-    pfr::launch_solve(which, rhs_mode, s->sym, s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_W[l], ngroups, s->F,
-                      s->Fc, s->WV, rd, Yin, Out, st);
+    if (up && subset >= 0) {
+      lvl = s->d_reach_fronts[subset] + s->reach_ptr[subset][l];
+      nf = s->reach_ptr[subset][l + 1] - s->reach_ptr[subset][l];
+    }
+    pfr::launch_solve(which, rhs_mode, s->sym, s->P, lvl, nf, s->level_W[l], ngroups, s->F, s->Fc, s->WV, rd, Yin, Out,
+                      reach, st);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -261,7 +276,7 @@ pfr::DirDesc dir_desc(const pfr_solver* s) {
 // A x = b on the chunk's factors, x -> Out (permuted).  rhs_mode 0: operator right-hand side
 // (rd.rhsP ...); 2: vector rd.G (overwritten in symmetric mode).  Symmetric mode: Dirichlet
 // columns moved to the right-hand side first, then L and U = diag(U) L^T.
-int forward_solve(pfr_solver* s, int rhs_mode, pfr::RhsDesc rd, double2* Out, hipStream_t st) {
+int forward_solve(pfr_solver* s, int rhs_mode, pfr::RhsDesc rd, double2* Out, hipStream_t st, int subset = -1) {
   int rc;
   if (s->sym) {
     const pfr::DirDesc dd = dir_desc(s);
@@ -274,21 +289,43 @@ int forward_solve(pfr_solver* s, int rhs_mode, pfr::RhsDesc rd, double2* Out, hi
       pfr::launch_dirichlet_rhs(2, dd, s->n_crow, rd, const_cast<double2*>(rd.G), nullptr, s->Fc, st);
     }
   }
-  if ((rc = solve_all(s, 0, rhs_mode, rd, nullptr, s->Y, st))) return rc;
-  return solve_all(s, 1, 0, rd, s->Y, Out, st);
+  if ((rc = solve_all(s, 0, rhs_mode, rd, nullptr, s->Y, st, subset))) return rc;
+  return solve_all(s, 1, 0, rd, s->Y, Out, st, subset);
 }
 
 // A^T l = g (g = rg.G, permuted), l -> Out.  Symmetric mode: the decoupled matrix is symmetric,
 // so L and U = diag(U) L^T again, then the Dirichlet rows of l are corrected.
-int adjoint_solve(pfr_solver* s, const pfr::RhsDesc& rg, double2* Out, hipStream_t st) {
+int adjoint_solve(pfr_solver* s, const pfr::RhsDesc& rg, double2* Out, hipStream_t st, int subset = -1) {
   int rc;
   if (s->sym) {
-    if ((rc = solve_all(s, 0, 2, rg, nullptr, s->Y, st)) || (rc = solve_all(s, 1, 0, rg, s->Y, Out, st))) return rc;
+    if ((rc = solve_all(s, 0, 2, rg, nullptr, s->Y, st, subset)) || (rc = solve_all(s, 1, 0, rg, s->Y, Out, st, subset)))
+      return rc;
     pfr::launch_dirichlet_post(dir_desc(s), s->n_dir, Out, s->Fc, st);
     return PFR_OK;
   }
-  if ((rc = solve_all(s, 2, 2, rg, nullptr, s->Y, st))) return rc;
-  return solve_all(s, 3, 0, rg, s->Y, Out, st);
+  if ((rc = solve_all(s, 2, 2, rg, nullptr, s->Y, st, subset))) return rc;
+  return solve_all(s, 3, 0, rg, s->Y, Out, st, subset);
+}
+
+// Mark the fronts holding the given permuted rows and all their ancestors; upload the flags and
+// the marked fronts level by level (level_fronts order kept).
+int set_reach(pfr_solver* s, int which, const std::vector<int32_t>& prows) {
+  const int nf = (int)s->front_parent.size();
+  std::vector<int32_t> mark(nf, 0);
+  for (int32_t p : prows)
+    for (int t = s->front_of_col[p]; t >= 0 && !mark[t]; t = s->front_parent[t]) mark[t] = 1;
+  const int L = (int)s->level_ptr.size() - 1;
+  std::vector<int32_t> lf(s->level_fronts_host.size());
+  std::vector<int32_t> list;
+  s->reach_ptr[which].assign(1, 0);
+  for (int l = 0; l < L; ++l) {
+    for (int e = s->level_ptr[l]; e < s->level_ptr[l + 1]; ++e)
+      if (mark[s->level_fronts_host[e]]) list.push_back(s->level_fronts_host[e]);
+    s->reach_ptr[which].push_back((int32_t)list.size());
+  }
+  HIP_TRY(hipMemcpy(s->d_reach[which], mark.data(), nf * 4, hipMemcpyHostToDevice));
+  if (!list.empty()) HIP_TRY(hipMemcpy(s->d_reach_fronts[which], list.data(), list.size() * 4, hipMemcpyHostToDevice));
+  return PFR_OK;
 }
 
 }  // namespace
@@ -687,6 +724,21 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       return bail(rc);
   }
   s->P = DevPattern{d_fronts, idx, relpos, rowf, ap, ac, an, ep, es, pm, pr, pc, S.n};
+  {
+    const int nf = (int)S.fronts.size();
+    s->front_of_col.assign(S.n, -1);
+    s->front_parent.resize(nf);
+    for (int t = 0; t < nf; ++t) {
+      const Front& F = S.fronts[t];
+      s->front_parent[t] = F.parent;
+      for (int a = 0; a < F.ns; ++a) s->front_of_col[F.col0 + a] = t;
+    }
+    s->level_fronts_host = S.level_fronts;
+    for (int w = 0; w < 2; ++w) {
+      if ((rc = s->alloc(&s->d_reach[w], nf)) || (rc = s->alloc(&s->d_reach_fronts[w], nf))) return bail(rc);
+      if ((rc = set_reach(s, w, {}))) return bail(rc);
+    }
+  }
   const int64_t Fc = s->Fc;
   if ((rc = s->alloc(&s->F, S.factor_entries * Fc)) || (rc = s->alloc(&s->WV, S.total_rows * Fc)) ||
       (rc = s->alloc(&s->X, (int64_t)S.n * Fc)) || (rc = s->alloc(&s->Y, (int64_t)S.n * Fc)) ||
@@ -823,6 +875,16 @@ int pfr_set_rhs(pfr_solver* s, const double* rhs, double beta_re, double beta_im
     HIP_TRY(hipMemcpy(s->rhs_val, val.data(), val.size() * 8, hipMemcpyHostToDevice));
   }
   s->n_rhs_sup = (int)sup.size();
+  {
+    // forward reach: rhs support (+ rows coupled to Dirichlet columns in symmetric mode)
+    std::vector<int32_t> rows(sup);
+    std::vector<int32_t> crow(std::max(1, s->n_crow));
+    if (s->sym && s->n_crow > 0) {
+      HIP_TRY(hipMemcpy(crow.data(), s->d_crow, s->n_crow * 4, hipMemcpyDeviceToHost));
+      rows.insert(rows.end(), crow.begin(), crow.begin() + s->n_crow);
+    }
+    if ((rc = set_reach(s, 0, rows))) return rc;
+  }
   s->rhs_host.assign(rhs, rhs + s->n);
   s->has_rhs = true;
   return PFR_OK;
@@ -841,6 +903,7 @@ int pfr_set_functional(pfr_solver* s, int32_t n_support, const int32_t* index, c
   double* d_a;
   int rc;
   if ((rc = s->up(&d_idx, pidx)) || (rc = s->up(&d_a, av))) return rc;
+  if ((rc = set_reach(s, 1, pidx))) return rc;        // loss adjoint reach: functional support
   s->fn.n_support = n_support;
   s->fn.pidx = d_idx;
   s->fn.a = d_a;
@@ -881,7 +944,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
     rd.beta_im = s->beta_im;
     rd.mass_sum = s->mass_sum;
     rd.freqs = s->freqs;
-    if ((rc = forward_solve(s, 0, rd, s->X, st))) return rc;
+    if ((rc = forward_solve(s, 0, rd, s->X, st, 0))) return rc;
     record(s, 2, st);
     pfr::FunctionalArgs fa = s->fn;
     fa.loss_type = reverse ? loss_type : -1;
@@ -893,7 +956,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
     if (reverse) {
       pfr::RhsDesc rg;
       rg.G = s->G;
-      if ((rc = adjoint_solve(s, rg, s->XA, st))) return rc;
+      if ((rc = adjoint_solve(s, rg, s->XA, st, 1))) return rc;
       record(s, 4, st);
       pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->XA, s->X, Fc, nv, s->partial,
                            st);
@@ -962,7 +1025,7 @@ int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int
     rd.beta_im = s->beta_im;
     rd.mass_sum = s->mass_sum;
     rd.freqs = s->freqs;
-    if ((rc = forward_solve(s, 0, rd, s->X, st))) return rc;
+    if ((rc = forward_solve(s, 0, rd, s->X, st, 0))) return rc;
     pfr::FunctionalArgs fa = s->fn;
     fa.loss_type = loss_type;
     fa.ref = reinterpret_cast<const double2*>(ref_dev);
@@ -973,7 +1036,7 @@ int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int
     rg.G = s->G;
     rg.rhsP = s->rhsP;
     rg.freqs = s->freqs;
-    if ((rc = adjoint_solve(s, rg, s->XA, st))) return rc;
+    if ((rc = adjoint_solve(s, rg, s->XA, st, 1))) return rc;
     pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->XA, s->X, Fc, nv, s->partial, st);
     pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st);
     pfr::launch_reduce(s->partial, kContractBlocks * ngroups, s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,

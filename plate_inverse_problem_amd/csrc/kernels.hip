@@ -649,23 +649,35 @@ __device__ __forceinline__ cplx rhs_value(const DevPattern& P, const RhsArgs& R,
 }
 
 // Gather the frontal vector: pivot rows from the rhs, plus children's update vectors.
+// reach (per front, may be NULL): fronts whose update vector can be non-zero for this right-hand
+// side (the RHS support and its elimination-tree ancestors); others' stale vectors are skipped.
 template <int RHS>
 __device__ __forceinline__ void gather_frontal(const DevPattern& P, const Front& fr, const RhsArgs& R,
-                                               cplx* __restrict__ WV, int64_t Fc, const Ctx& c) {
+                                               cplx* __restrict__ WV, int64_t Fc, const Ctx& c,
+                                               const int* __restrict__ reach) {
   for (int a = c.w; a < fr.f; a += c.W) {
     const int r = fr.row0 + a;
     cplx v = make_double2(0.0, 0.0);
     if (a < fr.ns) v = rhs_value<RHS>(P, R, P.idx[r], c.q, Fc);
     const int x1 = P.ea_ptr[r + 1];
-    for (int e = P.ea_ptr[r]; e < x1; ++e) v = cadd(v, WV[(int64_t)P.ea_src[e] * Fc + c.q]);
+    for (int e = P.ea_ptr[r]; e < x1; ++e) {
+      const int src = P.ea_src[e];
+      if (!reach || reach[P.row_front[src]]) v = cadd(v, WV[(int64_t)src * Fc + c.q]);
+    }
     WV[(int64_t)r * Fc + c.q] = v;
   }
 }
 
 // ------------------------------------------------------------------ K3a: L y = b (bottom-up)
+// Workgroup = (front, 64 frequencies), W waves.  Pivot rows: blocks of KBS pivots, the
+// diagonal block solved by wave 0 in registers (its loads independent of the chain), the
+// later pivot rows updated by all waves.  Update rows: V(i) -= L21(i, :) y in ONE
+// read-modify-write per row, SRB rows per wave, y in chunks of SKC.
+constexpr int SRB = 4, SKC = 8;
+
 template <int RHS>
-__global__ void k_lsolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
-                               cplx* __restrict__ WV, RhsArgs R, cplx* __restrict__ Y) {
+__global__ __launch_bounds__(512) void k_lsolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
+                               cplx* __restrict__ WV, RhsArgs R, cplx* __restrict__ Y, const int* __restrict__ reach) {
   const Ctx c = ctx();
   const Front fr = P.fronts[lvl[blockIdx.x]];
   const int f = fr.f, ns = fr.ns;
@@ -673,28 +685,59 @@ __global__ void k_lsolve_level(DevPattern P, const int* __restrict__ lvl, const 
   cplx* __restrict__ wv = WV + (int64_t)fr.row0 * Fc + c.q;
 #define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
 #define V(a) wv[(int64_t)(a) * Fc]
-  gather_frontal<RHS>(P, fr, R, WV, Fc, c);
+  gather_frontal<RHS>(P, fr, R, WV, Fc, c, reach);
   __syncthreads();
   for (int k0 = 0; k0 < ns; k0 += KBS) {
     const int kb = min(KBS, ns - k0), k1 = k0 + kb;
-    if (c.w == 0)
-      for (int k = k0; k < k1; ++k) {
-        const cplx z = V(k);
-        for (int i = k + 1; i < k1; ++i) V(i) = cfms(V(i), E(i, k), z);
-      }
-    __syncthreads();
-    cplx z[KBS];
+    if (c.w == 0) {
+      cplx v[KBS];
 #pragma unroll
-    for (int t = 0; t < KBS; ++t)
-      if (t < kb) z[t] = V(k0 + t);
-    for (int i = k1 + c.w; i < f; i += c.W) {
-      cplx v = V(i);
+      for (int t = 0; t < KBS; ++t) v[t] = t < kb ? V(k0 + t) : make_double2(0.0, 0.0);
+#pragma unroll
+      for (int k = 0; k < KBS; ++k)
+#pragma unroll
+        for (int i = k + 1; i < KBS; ++i)
+          if (i < kb) v[i] = cfms(v[i], E(k0 + i, k0 + k), v[k]);
 #pragma unroll
       for (int t = 0; t < KBS; ++t)
-        if (t < kb) v = cfms(v, E(i, k0 + t), z[t]);
-      V(i) = v;
+        if (t < kb) V(k0 + t) = v[t];
     }
     __syncthreads();
+    if (k1 < ns) {
+      cplx z[KBS];
+#pragma unroll
+      for (int t = 0; t < KBS; ++t)
+        if (t < kb) z[t] = V(k0 + t);
+      for (int i = k1 + c.w; i < ns; i += c.W) {
+        cplx v = V(i);
+#pragma unroll
+        for (int t = 0; t < KBS; ++t)
+          if (t < kb) v = cfms(v, E(i, k0 + t), z[t]);
+        V(i) = v;
+      }
+      __syncthreads();
+    }
+  }
+  for (int i0 = ns + SRB * c.w; i0 < f; i0 += SRB * c.W) {
+    int ri[SRB];
+    cplx acc[SRB];
+#pragma unroll
+    for (int r = 0; r < SRB; ++r) {
+      ri[r] = min(i0 + r, f - 1);
+      acc[r] = V(ri[r]);
+    }
+    for (int k0 = 0; k0 < ns; k0 += SKC) {
+      cplx y[SKC];
+#pragma unroll
+      for (int u = 0; u < SKC; ++u) y[u] = k0 + u < ns ? V(k0 + u) : make_double2(0.0, 0.0);
+#pragma unroll
+      for (int r = 0; r < SRB; ++r)
+#pragma unroll
+        for (int u = 0; u < SKC; ++u) acc[r] = cfms(acc[r], E(ri[r], min(k0 + u, ns - 1)), y[u]);
+    }
+#pragma unroll
+    for (int r = 0; r < SRB; ++r)
+      if (i0 + r < f) V(i0 + r) = acc[r];
   }
   for (int a = c.w; a < ns; a += c.W) Y[(int64_t)(fr.col0 + a) * Fc + c.q] = V(a);
 #undef E
@@ -725,10 +768,14 @@ __device__ __forceinline__ cplx offdiag_dot(cplx v, const cplx* __restrict__ e, 
 }
 
 // ------------------------------------------------------------------ K3b: U x = y (top-down)
-// SYM: U12 row a = U(a, a) * (column a of L21)^T (symmetric mode, U12 never formed)
+// Pivot rows first take the update-row solution: v_a = y_a - U12(a, :) x_upd, SRB pivot rows
+// per wave sharing each gathered x value (SYM: U12(a, b) = U(a, a) L21(b, a), read from L21);
+// then U11 backward in KBS blocks, the diagonal block by wave 0 in registers.
 template <bool SYM>
-__global__ void k_usolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
-                               cplx* __restrict__ WV, const cplx* __restrict__ Y, cplx* __restrict__ X) {
+__global__ __launch_bounds__(512) void k_usolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
+                               cplx* __restrict__ WV, const cplx* __restrict__ Y, cplx* __restrict__ X,
+                               const int* __restrict__ reach) {
+  const bool live = !reach || reach[lvl[blockIdx.x]];   // unreached front: y = 0
   const Ctx c = ctx();
   const Front fr = P.fronts[lvl[blockIdx.x]];
   const int f = fr.f, ns = fr.ns;
@@ -737,39 +784,74 @@ __global__ void k_usolve_level(DevPattern P, const int* __restrict__ lvl, const 
   const int* __restrict__ ix = P.idx + fr.row0;
 #define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
 #define V(a) wv[(int64_t)(a) * Fc]
-  for (int a = c.w; a < ns; a += c.W) {
-    cplx v = Y[(int64_t)(fr.col0 + a) * Fc + c.q];
-    if (SYM) {
-      const cplx t = offdiag_dot(make_double2(0.0, 0.0), &E(0, a), (int64_t)f * Fc, X, ix, ns, f, Fc, c.q);
-      v = cadd(v, cmul(E(a, a), t));
-    } else {
-      v = offdiag_dot(v, &E(a, 0), Fc, X, ix, ns, f, Fc, c.q);
+  for (int a0 = SRB * c.w; a0 < ns; a0 += SRB * c.W) {
+    int ra[SRB];
+    cplx acc[SRB];
+#pragma unroll
+    for (int r = 0; r < SRB; ++r) {
+      ra[r] = min(a0 + r, ns - 1);
+      acc[r] = make_double2(0.0, 0.0);
     }
-    V(a) = v;
+    for (int b0 = ns; b0 < f; b0 += SKC) {
+      int iv[SKC];
+      cplx xv[SKC];
+#pragma unroll
+      for (int u = 0; u < SKC; ++u) iv[u] = ix[min(b0 + u, f - 1)];
+#pragma unroll
+      for (int u = 0; u < SKC; ++u)
+        xv[u] = b0 + u < f ? X[(int64_t)iv[u] * Fc + c.q] : make_double2(0.0, 0.0);
+#pragma unroll
+      for (int r = 0; r < SRB; ++r)
+#pragma unroll
+        for (int u = 0; u < SKC; ++u) {
+          const int b = min(b0 + u, f - 1);
+          acc[r] = cfms(acc[r], SYM ? E(b, ra[r]) : E(ra[r], b), xv[u]);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < SRB; ++r)
+      if (a0 + r < ns) {
+        const cplx y = live ? Y[(int64_t)(fr.col0 + a0 + r) * Fc + c.q] : make_double2(0.0, 0.0);
+        V(a0 + r) = SYM ? cadd(y, cmul(E(ra[r], ra[r]), acc[r])) : cadd(y, acc[r]);
+      }
   }
   __syncthreads();
   for (int k1 = ns; k1 > 0; k1 -= KBS) {
     const int k0 = max(0, k1 - KBS), kb = k1 - k0;
-    if (c.w == 0)
-      for (int k = k1 - 1; k >= k0; --k) {
-        const cplx x = cmul(V(k), crecip(E(k, k)));
-        V(k) = x;
-        X[(int64_t)(fr.col0 + k) * Fc + c.q] = x;
-        for (int i = k0; i < k; ++i) V(i) = cfms(V(i), E(i, k), x);
-      }
-    __syncthreads();
-    cplx x[KBS];
+    if (c.w == 0) {
+      cplx v[KBS];
 #pragma unroll
-    for (int t = 0; t < KBS; ++t)
-      if (t < kb) x[t] = V(k0 + t);
-    for (int i = c.w; i < k0; i += c.W) {
-      cplx v = V(i);
+      for (int t = 0; t < KBS; ++t) v[t] = t < kb ? V(k0 + t) : make_double2(0.0, 0.0);
+#pragma unroll
+      for (int k = KBS - 1; k >= 0; --k)
+        if (k < kb) {
+          v[k] = cmul(v[k], crecip(E(k0 + k, k0 + k)));
+#pragma unroll
+          for (int i = 0; i < KBS; ++i)
+            if (i < k) v[i] = cfms(v[i], E(k0 + i, k0 + k), v[k]);
+        }
 #pragma unroll
       for (int t = 0; t < KBS; ++t)
-        if (t < kb) v = cfms(v, E(i, k0 + t), x[t]);
-      V(i) = v;
+        if (t < kb) {
+          V(k0 + t) = v[t];
+          X[(int64_t)(fr.col0 + k0 + t) * Fc + c.q] = v[t];
+        }
     }
     __syncthreads();
+    if (k0 > 0) {
+      cplx x[KBS];
+#pragma unroll
+      for (int t = 0; t < KBS; ++t)
+        if (t < kb) x[t] = V(k0 + t);
+      for (int i = c.w; i < k0; i += c.W) {
+        cplx v = V(i);
+#pragma unroll
+        for (int t = 0; t < KBS; ++t)
+          if (t < kb) v = cfms(v, E(i, k0 + t), x[t]);
+        V(i) = v;
+      }
+      __syncthreads();
+    }
   }
 #undef E
 #undef V
@@ -777,8 +859,8 @@ __global__ void k_usolve_level(DevPattern P, const int* __restrict__ lvl, const 
 
 // ------------------------------------------------------------------ K3c: U^T y = g (bottom-up)
 template <int RHS>
-__global__ void k_utsolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
-                                cplx* __restrict__ WV, RhsArgs R, cplx* __restrict__ Y) {
+__global__ __launch_bounds__(512) void k_utsolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
+                                cplx* __restrict__ WV, RhsArgs R, cplx* __restrict__ Y, const int* __restrict__ reach) {
   const Ctx c = ctx();
   const Front fr = P.fronts[lvl[blockIdx.x]];
   const int f = fr.f, ns = fr.ns;
@@ -786,7 +868,7 @@ __global__ void k_utsolve_level(DevPattern P, const int* __restrict__ lvl, const
   cplx* __restrict__ wv = WV + (int64_t)fr.row0 * Fc + c.q;
 #define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
 #define V(a) wv[(int64_t)(a) * Fc]
-  gather_frontal<RHS>(P, fr, R, WV, Fc, c);
+  gather_frontal<RHS>(P, fr, R, WV, Fc, c, reach);
   __syncthreads();
   for (int k0 = 0; k0 < ns; k0 += KBS) {
     const int kb = min(KBS, ns - k0), k1 = k0 + kb;
@@ -816,8 +898,10 @@ __global__ void k_utsolve_level(DevPattern P, const int* __restrict__ lvl, const
 }
 
 // ------------------------------------------------------------------ K3d: L^T x = y (top-down)
-__global__ void k_ltsolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
-                                cplx* __restrict__ WV, const cplx* __restrict__ Y, cplx* __restrict__ X) {
+__global__ __launch_bounds__(512) void k_ltsolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
+                                cplx* __restrict__ WV, const cplx* __restrict__ Y, cplx* __restrict__ X,
+                               const int* __restrict__ reach) {
+  const bool live = !reach || reach[lvl[blockIdx.x]];   // unreached front: y = 0
   const Ctx c = ctx();
   const Front fr = P.fronts[lvl[blockIdx.x]];
   const int f = fr.f, ns = fr.ns;
@@ -827,7 +911,7 @@ __global__ void k_ltsolve_level(DevPattern P, const int* __restrict__ lvl, const
 #define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
 #define V(a) wv[(int64_t)(a) * Fc]
   for (int a = c.w; a < ns; a += c.W) {
-    cplx v = Y[(int64_t)(fr.col0 + a) * Fc + c.q];
+    cplx v = live ? Y[(int64_t)(fr.col0 + a) * Fc + c.q] : make_double2(0.0, 0.0);
     v = offdiag_dot(v, &E(0, a), (int64_t)f * Fc, X, ix, ns, f, Fc, c.q);
     V(a) = v;
   }
@@ -1301,27 +1385,28 @@ static RhsArgs make_rhs(const RhsDesc& d) {
 
 void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups,
                   const double2* F, int64_t Fc, double2* WV, const RhsDesc& rd, const double2* Yin, double2* Out,
-                  hipStream_t st) {
+                  const int* reach, hipStream_t st) {
+  if (nfronts <= 0) return;
   dim3 g(nfronts, ngroups), b(64 * W);
   RhsArgs R = make_rhs(rd);
   switch (which) {
     case 0:  // L solve
-      if (rhs_mode == 0) LAUNCH(k_lsolve_level<0>, g, b, st, P, lvl, F, Fc, WV, R, Out);
-      else if (rhs_mode == 1) LAUNCH(k_lsolve_level<1>, g, b, st, P, lvl, F, Fc, WV, R, Out);
-      else if (rhs_mode == 2) LAUNCH(k_lsolve_level<2>, g, b, st, P, lvl, F, Fc, WV, R, Out);
-      else LAUNCH(k_lsolve_level<3>, g, b, st, P, lvl, F, Fc, WV, R, Out);
+      if (rhs_mode == 0) LAUNCH(k_lsolve_level<0>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach);
+      else if (rhs_mode == 1) LAUNCH(k_lsolve_level<1>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach);
+      else if (rhs_mode == 2) LAUNCH(k_lsolve_level<2>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach);
+      else LAUNCH(k_lsolve_level<3>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach);
       break;
     case 1:  // U solve
-      if (sym) LAUNCH(k_usolve_level<true>, g, b, st, P, lvl, F, Fc, WV, Yin, Out);
-      else LAUNCH(k_usolve_level<false>, g, b, st, P, lvl, F, Fc, WV, Yin, Out);
+      if (sym) LAUNCH(k_usolve_level<true>, g, b, st, P, lvl, F, Fc, WV, Yin, Out, reach);
+      else LAUNCH(k_usolve_level<false>, g, b, st, P, lvl, F, Fc, WV, Yin, Out, reach);
       break;
     case 2:  // U^T solve
-      if (rhs_mode == 0) LAUNCH(k_utsolve_level<0>, g, b, st, P, lvl, F, Fc, WV, R, Out);
-      else if (rhs_mode == 1) LAUNCH(k_utsolve_level<1>, g, b, st, P, lvl, F, Fc, WV, R, Out);
-      else LAUNCH(k_utsolve_level<2>, g, b, st, P, lvl, F, Fc, WV, R, Out);
+      if (rhs_mode == 0) LAUNCH(k_utsolve_level<0>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach);
+      else if (rhs_mode == 1) LAUNCH(k_utsolve_level<1>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach);
+      else LAUNCH(k_utsolve_level<2>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach);
       break;
     default:  // L^T solve
-      LAUNCH(k_ltsolve_level, g, b, st, P, lvl, F, Fc, WV, Yin, Out);
+      LAUNCH(k_ltsolve_level, g, b, st, P, lvl, F, Fc, WV, Yin, Out, reach);
       break;
   }
 }
