@@ -484,7 +484,7 @@ constexpr int TM = SCHUR_TM, TN = SCHUR_TN;
 // SYM (symmetric mode): only the lower triangle of A22 is formed; U12 = diag(U11) L21^T is
 // not stored, its entries are made from the L21 rows at load.
 // PF: the next pivot step's loads are issued before the current step's arithmetic.
-template <bool SYM, bool PF>
+template <bool SYM, bool PF, int KU>
 __device__ __forceinline__ void schur_tile(const DevPattern& P, const int4* __restrict__ tiles, int ntiles,
                                            const int* __restrict__ g1, const int* __restrict__ gxp,
                                            const int2* __restrict__ gx, cplx* __restrict__ F, int64_t Fc) {
@@ -556,35 +556,51 @@ __device__ __forceinline__ void schur_tile(const DevPattern& P, const int4* __re
 #pragma unroll
   for (int n = 0; n < TN; ++n) pb[n] = base + (SYM ? (int64_t)cj[n] * f * Fc : (int64_t)cj[n] * Fc);
   const int64_t sb = SYM ? Fc : (int64_t)f * Fc, sd = (int64_t)(f + 1) * Fc;
-  cplx a[TM], b[TN], dk = make_double2(1.0, 0.0);
-  auto load = [&](int k, cplx (&aa)[TM], cplx (&bb)[TN], cplx& dd) {
+  // KU pivot steps per iteration; with PF the next KU steps' loads are issued before this
+  // iteration's arithmetic.  Steps past ns load the last pivot and contribute zero.
+  cplx a[KU][TM], b[KU][TN], d[KU];
+  auto load = [&](int k0, cplx (&aa)[KU][TM], cplx (&bb)[KU][TN], cplx (&dd)[KU]) {
 #pragma unroll
-    for (int m = 0; m < TM; ++m) aa[m] = pa[m][k * Fc];
+    for (int u = 0; u < KU; ++u) {
+      const int k = min(k0 + u, ns - 1);
 #pragma unroll
-    for (int n = 0; n < TN; ++n) bb[n] = pb[n][k * sb];
-    if (SYM) dd = base[k * sd];
+      for (int m = 0; m < TM; ++m) aa[u][m] = pa[m][k * Fc];
+#pragma unroll
+      for (int n = 0; n < TN; ++n) bb[u][n] = pb[n][k * sb];
+      if (SYM) dd[u] = base[k * sd];
+    }
   };
-  if (PF && ns > 0) load(0, a, b, dk);
-  for (int k = 0; k < ns; ++k) {
-    cplx ca[TM], cb[TN], cd;
+  if (PF && ns > 0) load(0, a, b, d);
+  for (int k0 = 0; k0 < ns; k0 += KU) {
+    cplx ca[KU][TM], cb[KU][TN], cd[KU];
     if (PF) {
 #pragma unroll
-      for (int m = 0; m < TM; ++m) ca[m] = a[m];
+      for (int u = 0; u < KU; ++u) {
 #pragma unroll
-      for (int n = 0; n < TN; ++n) cb[n] = b[n];
-      cd = dk;
-      if (k + 1 < ns) load(k + 1, a, b, dk);
+        for (int m = 0; m < TM; ++m) ca[u][m] = a[u][m];
+#pragma unroll
+        for (int n = 0; n < TN; ++n) cb[u][n] = b[u][n];
+        cd[u] = d[u];
+      }
+      if (k0 + KU < ns) load(k0 + KU, a, b, d);
     } else {
-      load(k, ca, cb, cd);
-    }
-    if (SYM) {
-#pragma unroll
-      for (int m = 0; m < TM; ++m) ca[m] = cmul(ca[m], cd);
+      load(k0, ca, cb, cd);
     }
 #pragma unroll
-    for (int m = 0; m < TM; ++m)
+    for (int u = 0; u < KU; ++u) {
+      if (SYM) {
+        const cplx du = k0 + u < ns ? cd[u] : make_double2(0.0, 0.0);
 #pragma unroll
-      for (int n = 0; n < TN; ++n) acc[m][n] = cfms(acc[m][n], ca[m], cb[n]);
+        for (int m = 0; m < TM; ++m) ca[u][m] = cmul(ca[u][m], du);
+      } else if (k0 + u >= ns) {
+#pragma unroll
+        for (int m = 0; m < TM; ++m) ca[u][m] = make_double2(0.0, 0.0);
+      }
+#pragma unroll
+      for (int m = 0; m < TM; ++m)
+#pragma unroll
+        for (int n = 0; n < TN; ++n) acc[m][n] = cfms(acc[m][n], ca[u][m], cb[u][n]);
+    }
   }
 #pragma unroll
   for (int m = 0; m < TM; ++m)
@@ -597,16 +613,16 @@ __device__ __forceinline__ void schur_tile(const DevPattern& P, const int4* __re
 __global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* __restrict__ tiles, int ntiles,
                                                       const int* __restrict__ g1, const int* __restrict__ gxp,
                                                       const int2* __restrict__ gx, cplx* __restrict__ F, int64_t Fc) {
-  schur_tile<false, false>(P, tiles, ntiles, g1, gxp, gx, F, Fc);
+  schur_tile<false, false, 1>(P, tiles, ntiles, g1, gxp, gx, F, Fc);
 }
 
 // symmetric mode: register budget of 2 waves per SIMD so that every load of a pivot step
 // (or of two steps with PF) is in flight at once (the default budget serialises them)
-template <bool PF>
+template <int KU>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_schur_sym_level(
     DevPattern P, const int4* __restrict__ tiles, int ntiles, const int* __restrict__ g1,
     const int* __restrict__ gxp, const int2* __restrict__ gx, cplx* __restrict__ F, int64_t Fc) {
-  schur_tile<true, PF>(P, tiles, ntiles, g1, gxp, gx, F, Fc);
+  schur_tile<true, true, KU>(P, tiles, ntiles, g1, gxp, gx, F, Fc);
 }
 
 // ------------------------------------------------------------------ right-hand sides
@@ -1341,12 +1357,13 @@ void launch_schur(bool sym, const DevPattern& P, const int4* tiles, int ntiles, 
                   const int2* gx, int ngroups, double2* F, int64_t Fc, hipStream_t st) {
   if (ntiles <= 0) return;
   dim3 g((ntiles + 3) / 4, ngroups * (64 / SCHUR_QG)), b(256);
-  static const int pf = [] {
-    const char* e = getenv("PFR_SCHUR_PF");   // tuning knob: 0 = no software prefetch
-    return e ? atoi(e) : 1;
+  static const int ku = [] {
+    const char* e = getenv("PFR_SCHUR_KU");   // tuning knob: pivot steps per prefetched batch
+    return e ? atoi(e) : 2;
   }();
-  if (sym && pf) LAUNCH(k_schur_sym_level<true>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
-  else if (sym) LAUNCH(k_schur_sym_level<false>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
+  if (sym && ku == 3) LAUNCH(k_schur_sym_level<3>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
+  else if (sym && ku == 2) LAUNCH(k_schur_sym_level<2>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
+  else if (sym) LAUNCH(k_schur_sym_level<1>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
   else LAUNCH(k_schur_level, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
 }
 

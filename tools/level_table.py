@@ -29,12 +29,14 @@ def main(d):
         wr = wd.get(int(r["Dispatch_Id"]), 0)
         t = tot.setdefault(n, [0, 0, 0])
         t[0] += dt; t[1] += rd; t[2] += wr
-        if any(k in n for k in ["schur", "offdiag", "factor", "assemble"]):
+        if ALL or any(k in n for k in ["schur", "offdiag", "factor", "assemble"]):
             print("%-24s %5d %8.3f %8.2f %8.2f %7.2f" % (n[:24], lvl, dt, rd / 1e9, wr / 1e9, (rd + wr) / dt / 1e9))
     print()
     for n, (dt, rd, wr) in sorted(tot.items(), key=lambda kv: -kv[1][0]):
         print("%-40s %8.2f ms %8.2f GB rd %8.2f GB wr" % (n[:40], dt, rd / 1e9, wr / 1e9))
 
+
+ALL = "--all" in sys.argv
 
 if __name__ == "__main__":
     main(sys.argv[1])
