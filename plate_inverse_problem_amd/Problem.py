@@ -97,7 +97,13 @@ class _Engine:
         # symmetric mode when every matrix is complex symmetric away from the Dirichlet rows
         # (checked on the values): only L is formed, U = diag(U) L^T
         self.symmetric = bool(symmetric) and decoupled_symmetric(rows, cols, vals, n)
-        self.sym = _native.Symbolic(n, colptr, rows.astype(np.int32), symmetric=self.symmetric)
+        # tuning knobs of the symbolic analysis (defaults in include/pfr.h): PFR_LEAF_SIZE and
+        # PFR_RELAX="small,mid,big" (supernode amalgamation pivot limits)
+        leaf = os.environ.get("PFR_LEAF_SIZE")
+        relax = os.environ.get("PFR_RELAX")
+        self.sym = _native.Symbolic(n, colptr, rows.astype(np.int32), symmetric=self.symmetric,
+                                    leaf_size=int(leaf) if leaf else None,
+                                    relax=tuple(int(v) for v in relax.split(",")) if relax else None)
         self.stats = self.sym.stats()
         if lanes is None:
             lanes = int(os.environ.get("PFR_LANES", "2"))

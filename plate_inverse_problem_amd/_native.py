@@ -16,7 +16,7 @@ import re
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libpfr.so")
+LIB_PATH = os.environ.get("PFR_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libpfr.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "pfr.h")
 
 PFR_OK = 0

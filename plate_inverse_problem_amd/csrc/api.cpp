@@ -52,7 +52,7 @@ struct pfr_solver {
   int n = 0;
   int64_t nnz = 0;
   int64_t Fc = 0;  // frequencies per chunk (multiple of 64)
-  std::vector<int32_t> level_ptr, level_maxf, level_W, perm, iperm;
+  std::vector<int32_t> level_ptr, level_maxf, level_maxns, level_W, perm, iperm;
   DevPattern P{};
   // owned device arrays
   std::vector<void*> owned;
@@ -224,7 +224,7 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
                         s->d_oxp + s->item_ptr[l], s->d_ox, ngroups, s->F, s->Fc, s->freqs, s->K, s->M, data, ds,
                         nvalid, st);
     mark(l, 3);
-    pfr::launch_schur(s->sym, s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l],
+    pfr::launch_schur(s->sym, s->level_maxns[l], s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l],
                       s->d_g1 + (int64_t)s->tile_ptr[l] * pfr::SCHUR_TM * pfr::SCHUR_TN * pfr::SCHUR_SR * pfr::SCHUR_SC,
                       s->d_gxp + s->tile_ptr[l],
                       s->d_gx, ngroups, s->F,
@@ -467,6 +467,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->perm = S.perm;
   s->iperm = S.iperm;
   for (int m : S.level_maxf) s->level_W.push_back(waves_for(m));
+  s->level_maxns.assign(S.level_maxf.size(), 0);
+  for (const Front& F : S.fronts) s->level_maxns[F.level] = std::max(s->level_maxns[F.level], F.ns);
   Front* d_fronts = nullptr;
   int rc = PFR_OK;
   std::vector<Front> fv(S.fronts);

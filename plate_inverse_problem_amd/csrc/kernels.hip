@@ -618,6 +618,14 @@ __global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* _
 
 // symmetric mode: register budget of 2 waves per SIMD so that every load of a pivot step
 // (or of two steps with PF) is in flight at once (the default budget serialises them)
+// symmetric mode, levels with few pivots (short pivot loops, latency of the children's gather
+// dominates): no prefetch, register budget of 4 waves per SIMD
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_schur_sym_small(
+    DevPattern P, const int4* __restrict__ tiles, int ntiles, const int* __restrict__ g1,
+    const int* __restrict__ gxp, const int2* __restrict__ gx, cplx* __restrict__ F, int64_t Fc) {
+  schur_tile<true, false, 1>(P, tiles, ntiles, g1, gxp, gx, F, Fc);
+}
+
 template <int KU>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_schur_sym_level(
     DevPattern P, const int4* __restrict__ tiles, int ntiles, const int* __restrict__ g1,
@@ -788,7 +796,7 @@ __device__ __forceinline__ cplx offdiag_dot(cplx v, const cplx* __restrict__ e, 
 // per wave sharing each gathered x value (SYM: U12(a, b) = U(a, a) L21(b, a), read from L21);
 // then U11 backward in KBS blocks, the diagonal block by wave 0 in registers.
 template <bool SYM>
-__global__ __launch_bounds__(512) void k_usolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_usolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
                                cplx* __restrict__ WV, const cplx* __restrict__ Y, cplx* __restrict__ X,
                                const int* __restrict__ reach) {
   const bool live = !reach || reach[lvl[blockIdx.x]];   // unreached front: y = 0
@@ -808,21 +816,33 @@ __global__ __launch_bounds__(512) void k_usolve_level(DevPattern P, const int* _
       ra[r] = min(a0 + r, ns - 1);
       acc[r] = make_double2(0.0, 0.0);
     }
+    // U12(a, b) of pivot row a at pu[a][b * su] (SYM: column a of L21); update-row solution
+    // values gathered through wave-uniform (scalar) indices; every load of a chunk issued first
+    const cplx* pu[SRB];
+#pragma unroll
+    for (int r = 0; r < SRB; ++r) pu[r] = base + (SYM ? (int64_t)ra[r] : (int64_t)ra[r] * f) * Fc;
+    const int64_t su = SYM ? (int64_t)f * Fc : Fc;
+    const cplx* __restrict__ xq = X + c.q;
     for (int b0 = ns; b0 < f; b0 += SKC) {
       int iv[SKC];
-      cplx xv[SKC];
+      cplx xv[SKC], ev[SRB][SKC];
 #pragma unroll
-      for (int u = 0; u < SKC; ++u) iv[u] = ix[min(b0 + u, f - 1)];
+      for (int u = 0; u < SKC; ++u) iv[u] = ix[__builtin_amdgcn_readfirstlane(min(b0 + u, f - 1))];
 #pragma unroll
-      for (int u = 0; u < SKC; ++u)
-        xv[u] = b0 + u < f ? X[(int64_t)iv[u] * Fc + c.q] : make_double2(0.0, 0.0);
+      for (int u = 0; u < SKC; ++u) xv[u] = xq[(int64_t)iv[u] * Fc];
 #pragma unroll
       for (int r = 0; r < SRB; ++r)
 #pragma unroll
-        for (int u = 0; u < SKC; ++u) {
-          const int b = min(b0 + u, f - 1);
-          acc[r] = cfms(acc[r], SYM ? E(b, ra[r]) : E(ra[r], b), xv[u]);
-        }
+        for (int u = 0; u < SKC; ++u) ev[r][u] = pu[r][min(b0 + u, f - 1) * su];
+      __builtin_amdgcn_sched_group_barrier(0x020, SKC * (SRB + 1), 0);   // all vector loads first
+      __builtin_amdgcn_sched_group_barrier(0x002, 4 * SKC * SRB + 8, 0);
+#pragma unroll
+      for (int u = 0; u < SKC; ++u)
+        if (b0 + u >= f) xv[u] = make_double2(0.0, 0.0);
+#pragma unroll
+      for (int r = 0; r < SRB; ++r)
+#pragma unroll
+        for (int u = 0; u < SKC; ++u) acc[r] = cfms(acc[r], ev[r][u], xv[u]);
     }
 #pragma unroll
     for (int r = 0; r < SRB; ++r)
@@ -1353,15 +1373,20 @@ void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPac
   LAUNCH(k_combine, dim3((unsigned)((nnz + 255) / 256)), dim3(256), st, stiff, n_stiff, nnz, coef, K);
 }
 
-void launch_schur(bool sym, const DevPattern& P, const int4* tiles, int ntiles, const int* g1, const int* gxp,
-                  const int2* gx, int ngroups, double2* F, int64_t Fc, hipStream_t st) {
+void launch_schur(bool sym, int maxns, const DevPattern& P, const int4* tiles, int ntiles, const int* g1,
+                  const int* gxp, const int2* gx, int ngroups, double2* F, int64_t Fc, hipStream_t st) {
   if (ntiles <= 0) return;
   dim3 g((ntiles + 3) / 4, ngroups * (64 / SCHUR_QG)), b(256);
   static const int ku = [] {
     const char* e = getenv("PFR_SCHUR_KU");   // tuning knob: pivot steps per prefetched batch
     return e ? atoi(e) : 2;
   }();
-  if (sym && ku == 3) LAUNCH(k_schur_sym_level<3>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
+  static const int small_ns = [] {
+    const char* e = getenv("PFR_SCHUR_SMALL_NS");   // tuning knob: levels with few pivots
+    return e ? atoi(e) : 0;
+  }();
+  if (sym && maxns <= small_ns) LAUNCH(k_schur_sym_small, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
+  else if (sym && ku == 3) LAUNCH(k_schur_sym_level<3>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
   else if (sym && ku == 2) LAUNCH(k_schur_sym_level<2>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
   else if (sym) LAUNCH(k_schur_sym_level<1>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
   else LAUNCH(k_schur_level, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
