@@ -53,6 +53,7 @@ struct pfr_solver {
   int64_t nnz = 0;
   int64_t Fc = 0;  // frequencies per chunk (multiple of 64)
   std::vector<int32_t> level_ptr, level_maxf, level_maxns, level_W, perm, iperm;
+  std::vector<char> level_lds;          // symmetric Schur of the level: LDS-staged 16 x 16 blocks
   DevPattern P{};
   // owned device arrays
   std::vector<void*> owned;
@@ -224,7 +225,7 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
                         s->d_oxp + s->item_ptr[l], s->d_ox, ngroups, s->F, s->Fc, s->freqs, s->K, s->M, data, ds,
                         nvalid, st);
     mark(l, 3);
-    pfr::launch_schur(s->sym, s->level_maxns[l], s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l],
+    pfr::launch_schur(s->sym, s->level_lds[l], s->level_maxns[l], s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l],
                       s->d_g1 + (int64_t)s->tile_ptr[l] * pfr::SCHUR_TM * pfr::SCHUR_TN * pfr::SCHUR_SR * pfr::SCHUR_SC,
                       s->d_gxp + s->tile_ptr[l],
                       s->d_gx, ngroups, s->F,
@@ -468,7 +469,18 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->iperm = S.iperm;
   for (int m : S.level_maxf) s->level_W.push_back(waves_for(m));
   s->level_maxns.assign(S.level_maxf.size(), 0);
-  for (const Front& F : S.fronts) s->level_maxns[F.level] = std::max(s->level_maxns[F.level], F.ns);
+  std::vector<int32_t> level_maxr(S.level_maxf.size(), 0);
+  for (const Front& F : S.fronts) {
+    s->level_maxns[F.level] = std::max(s->level_maxns[F.level], F.ns);
+    level_maxr[F.level] = std::max(level_maxr[F.level], F.f - F.ns);
+  }
+  {
+    // the LDS-staged Schur pays off once update blocks are large (measured per level at C3:
+    // better from max r ~ 64 on, worse on the small leaf fronts where 16 x 16 blocks waste waves)
+    const char* e = getenv("PFR_SCHUR_LDS_MINR");   // tuning knob
+    const int minr = e ? atoi(e) : 80;
+    for (size_t l = 0; l < level_maxr.size(); ++l) s->level_lds.push_back(S.symmetric && level_maxr[l] >= minr);
+  }
   Front* d_fronts = nullptr;
   int rc = PFR_OK;
   std::vector<Front> fv(S.fronts);
@@ -528,8 +540,22 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
         // first-source ids (-1 = none), lane group by lane group, then one overflow range
         constexpr int TM = pfr::SCHUR_TM, TN = pfr::SCHUR_TN, SR = pfr::SCHUR_SR, SC = pfr::SCHUR_SC;
         static_assert(TM * SR == TN * SC, "square super-tiles (symmetric mode keeps j0 <= i0)");
-        for (int i0 = 0; i0 < r; i0 += TM * SR)
-          for (int j0 = 0; j0 < r && (!sym || j0 <= i0); j0 += TN * SC) {
+        // symmetric mode: super-tiles in blocks of 2 x 2 (k_schur_sym_lds stages each block's L21
+        // rows in LDS once for its four waves); the upper super-tile of a diagonal block and
+        // super-tiles past the edge carry no sources and store nothing
+        constexpr int ST = TM * SR, BL = 2 * ST;
+        std::vector<std::pair<int, int>> order;
+        if (sym && s->level_lds[l]) {
+          for (int b0 = 0; b0 < r; b0 += BL)
+            for (int c0 = 0; c0 <= b0; c0 += BL)
+              for (int w = 0; w < 4; ++w) order.emplace_back(b0 + ST * (w / 2), c0 + ST * (w % 2));
+        } else {
+          for (int i0 = 0; i0 < r; i0 += ST)
+            for (int j0 = 0; j0 < r && (!sym || j0 <= i0); j0 += ST) order.emplace_back(i0, j0);
+        }
+        for (const auto& ij : order) {
+          const int i0 = ij.first, j0 = ij.second;
+          {
             tv.push_back(make_int4(t, i0, j0, 0));
             for (int sub = 0; sub < SR * SC; ++sub)
               for (int pos = 0; pos < TM * TN; ++pos) {
@@ -545,6 +571,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
               }
             gxp.push_back((int32_t)gx.size());
           }
+        }
       }
       s->tile_ptr.push_back((int32_t)tv.size());
     }

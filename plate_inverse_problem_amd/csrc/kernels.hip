@@ -618,6 +618,250 @@ __global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* _
 
 // symmetric mode: register budget of 2 waves per SIMD so that every load of a pivot step
 // (or of two steps with PF) is in flight at once (the default budget serialises them)
+// symmetric mode, LDS-staged: workgroup = one 16 x 16 block of A22 (2 x 2 super-tiles, one
+// per wave) x 16 frequencies.  Per chunk of LKC pivots the block's 16 row + 16 column L21 rows
+// (and the pivots U(k, k)) are loaded ONCE for the four waves -- every global load a distinct
+// 256 B run -- into LDS, from where each wave reads its 4 x 4 register tiles' operands.  The
+// next chunk's loads are in flight (registers) while the current one is computed.
+constexpr int LKC = 8;                       // pivots per LDS chunk
+constexpr int LROWS = 4 * SCHUR_TM * SCHUR_SR;   // 16 block rows + 16 block columns
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_schur_sym_lds(
+    DevPattern P, const int4* __restrict__ tiles, int ntiles, const int* __restrict__ g1,
+    const int* __restrict__ gxp, const int2* __restrict__ gx, cplx* __restrict__ F, int64_t Fc) {
+  __shared__ cplx sh[LKC][LROWS][SCHUR_QG];
+  __shared__ cplx shd[LKC][SCHUR_QG];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t nblk = (int64_t)gridDim.x;
+  const int64_t lid = xcd_swizzle(blockIdx.x + nblk * blockIdx.y, nblk * gridDim.y);
+  const int blk = (int)(lid % nblk), by = (int)(lid / nblk);
+  if (4 * blk >= ntiles) return;                    // whole workgroup
+  const int tid = 4 * blk + w;
+  const int sub = lane / SCHUR_QG, fq = lane % SCHUR_QG;
+  const int64_t q = (int64_t)by * SCHUR_QG + fq;
+  const int4 t0 = tiles[4 * blk];                   // block origin (front, i0, j0)
+  int4 t = tiles[tid];
+  const bool upper = t.z > t.y;                     // upper super-tile of a diagonal block
+  t.y += TM * (sub / SCHUR_SC);
+  t.z += TN * (sub % SCHUR_SC);
+  const Front fr = P.fronts[t0.x];
+  const int f = fr.f, ns = fr.ns;
+  cplx* __restrict__ base = F + fr.off * Fc + q;
+  cplx acc[TM][TN];
+  {
+    const int4* __restrict__ g4 =
+        reinterpret_cast<const int4*>(g1 + ((int64_t)tid * (SCHUR_SR * SCHUR_SC) + sub) * (TM * TN));
+    int src[TM * TN];
+#pragma unroll
+    for (int u = 0; u < TM * TN / 4; ++u) {
+      const int4 v = g4[u];
+      src[4 * u] = v.x;
+      src[4 * u + 1] = v.y;
+      src[4 * u + 2] = v.z;
+      src[4 * u + 3] = v.w;
+    }
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int n = 0; n < TN; ++n) {
+        const int e = src[m * TN + n];
+        const cplx v = F[(int64_t)max(e, 0) * Fc + q];
+        acc[m][n] = e >= 0 ? v : make_double2(0.0, 0.0);
+      }
+    const int x1 = gxp[tid + 1];
+    for (int x = gxp[tid]; x < x1; ++x) {
+      const int2 g = gx[x];
+      if (g.x / (TM * TN) == sub) {
+        const cplx v = F[(int64_t)g.y * Fc + q];
+#pragma unroll
+        for (int m = 0; m < TM; ++m)
+#pragma unroll
+          for (int n = 0; n < TN; ++n)
+            if (g.x % (TM * TN) == m * TN + n) acc[m][n] = cadd(acc[m][n], v);
+      }
+    }
+  }
+  // staging map: thread (g = threadIdx.x >> 4, frequency threadIdx.x & 15) loads block row g and
+  // block column g (L21 rows t0.y + g and t0.z + g) for every pivot of the chunk
+  const int g = threadIdx.x >> 4;
+  const cplx* __restrict__ bq = F + fr.off * Fc + (int64_t)by * SCHUR_QG + (threadIdx.x & 15);
+  const cplx* __restrict__ rowa = bq + (int64_t)min(ns + t0.y + g, f - 1) * f * Fc;
+  const cplx* __restrict__ rowb = bq + (int64_t)min(ns + t0.z + g, f - 1) * f * Fc;
+  // this lane's operands: a rows (block rows), b rows (block columns) of its 4 x 4 tile
+  const int ar = t.y - t0.y, bc = LROWS / 2 + t.z - t0.z;
+  for (int k0 = 0; k0 < ns; k0 += LKC) {
+#pragma unroll
+    for (int u = 0; u < LKC; ++u) {
+      const int64_t o = (int64_t)min(k0 + u, ns - 1) * Fc;
+      sh[u][g][threadIdx.x & 15] = rowa[o];
+      sh[u][LROWS / 2 + g][threadIdx.x & 15] = rowb[o];
+    }
+    if (threadIdx.x < LKC * SCHUR_QG)
+      shd[g][threadIdx.x & 15] = bq[(int64_t)min(k0 + g, ns - 1) * (f + 1) * Fc];
+    __syncthreads();
+    if (!upper) {
+#pragma unroll
+      for (int kk = 0; kk < LKC; ++kk) {
+        if (k0 + kk < ns) {
+          const cplx dk = shd[kk][fq];
+          cplx a[TM], b[TN];
+#pragma unroll
+          for (int m = 0; m < TM; ++m) a[m] = cmul(sh[kk][ar + m][fq], dk);
+#pragma unroll
+          for (int n = 0; n < TN; ++n) b[n] = sh[kk][bc + n][fq];
+#pragma unroll
+          for (int m = 0; m < TM; ++m)
+#pragma unroll
+            for (int n = 0; n < TN; ++n) acc[m][n] = cfms(acc[m][n], a[m], b[n]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (upper) return;
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int n = 0; n < TN; ++n)
+      if (ns + t.y + m < f && ns + t.z + n < f && t.y + m >= t.z + n)
+        base[((int64_t)(ns + t.y + m) * f + ns + t.z + n) * Fc] = acc[m][n];
+}
+
+// As k_schur_sym_lds, with the chunks brought in by LDS-DMA (global_load_lds_dwordx4, no
+// registers) into two LDS buffers: chunk c + 1 is in flight while chunk c is computed.  One
+// wave-instruction = 4 staged values (same pivot, 4 consecutive block rows) of 16 frequencies.
+constexpr int GKC = 4;                              // pivots per chunk
+constexpr int GINS = GKC * LROWS / 4 / 4;           // LDS-DMA instructions per wave per chunk (+1 pivots, wave 0)
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_schur_sym_glds(
+    DevPattern P, const int4* __restrict__ tiles, int ntiles, const int* __restrict__ g1,
+    const int* __restrict__ gxp, const int2* __restrict__ gx, cplx* __restrict__ F, int64_t Fc) {
+  __shared__ cplx sh[2][GKC][LROWS][SCHUR_QG];
+  __shared__ cplx shd[2][GKC][SCHUR_QG];
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nblk = (int64_t)gridDim.x;
+  const int64_t lid = xcd_swizzle(blockIdx.x + nblk * blockIdx.y, nblk * gridDim.y);
+  const int blk = (int)(lid % nblk), by = (int)(lid / nblk);
+  if (4 * blk >= ntiles) return;                    // whole workgroup
+  const int tid = 4 * blk + w;
+  const int sub = lane / SCHUR_QG, fq = lane % SCHUR_QG;
+  const int64_t q = (int64_t)by * SCHUR_QG + fq;
+  const int4 t0 = tiles[4 * blk];
+  int4 t = tiles[tid];
+  const bool upper = t.z > t.y;
+  t.y += TM * (sub / SCHUR_SC);
+  t.z += TN * (sub % SCHUR_SC);
+  const Front fr = P.fronts[t0.x];
+  const int f = fr.f, ns = fr.ns;
+  cplx* __restrict__ base = F + fr.off * Fc + q;
+  // chunk staging: instruction j of wave w = values 4 i .. 4 i + 3, i = w + 4 j (pivot i / 8, block
+  // rows 4 (i % 8) ..), lane -> value 4 i + sub; row pointers of this lane for its GINS values
+  const cplx* __restrict__ bq = F + fr.off * Fc + (int64_t)by * SCHUR_QG + fq;
+  const cplx* srcp[GINS];
+  int srck[GINS];
+#pragma unroll
+  for (int j = 0; j < GINS; ++j) {
+    const int v = 4 * (w + 4 * j) + sub;
+    const int kk = v / LROWS, r = v % LROWS;
+    const int br = r < LROWS / 2 ? t0.y + r : t0.z + r - LROWS / 2;
+    srcp[j] = bq + (int64_t)min(ns + br, f - 1) * f * Fc;
+    srck[j] = kk;
+  }
+  auto issue = [&](int k0, int buf) {
+#pragma unroll
+    for (int j = 0; j < GINS; ++j) {
+      const cplx* src = srcp[j] + (int64_t)min(k0 + srck[j], ns - 1) * Fc;
+      __builtin_amdgcn_global_load_lds(src, &sh[buf][0][0][0] + 64 * (w + 4 * j), 16, 0, 0);
+    }
+    if (w == 0) {
+      const cplx* src = bq + (int64_t)min(k0 + sub, ns - 1) * (f + 1) * Fc;
+      __builtin_amdgcn_global_load_lds(src, &shd[buf][0][0], 16, 0, 0);
+    }
+  };
+  cplx acc[TM][TN];
+  {
+    const int4* __restrict__ g4 =
+        reinterpret_cast<const int4*>(g1 + ((int64_t)tid * (SCHUR_SR * SCHUR_SC) + sub) * (TM * TN));
+    int src[TM * TN];
+#pragma unroll
+    for (int u = 0; u < TM * TN / 4; ++u) {
+      const int4 v = g4[u];
+      src[4 * u] = v.x;
+      src[4 * u + 1] = v.y;
+      src[4 * u + 2] = v.z;
+      src[4 * u + 3] = v.w;
+    }
+#pragma unroll
+    for (int m = 0; m < TM; ++m)
+#pragma unroll
+      for (int n = 0; n < TN; ++n) {
+        const int e = src[m * TN + n];
+        const cplx v = F[(int64_t)max(e, 0) * Fc + q];
+        acc[m][n] = e >= 0 ? v : make_double2(0.0, 0.0);
+      }
+    const int x1 = gxp[tid + 1];
+    for (int x = gxp[tid]; x < x1; ++x) {
+      const int2 g = gx[x];
+      if (g.x / (TM * TN) == sub) {
+        const cplx v = F[(int64_t)g.y * Fc + q];
+#pragma unroll
+        for (int m = 0; m < TM; ++m)
+#pragma unroll
+          for (int n = 0; n < TN; ++n)
+            if (g.x % (TM * TN) == m * TN + n) acc[m][n] = cadd(acc[m][n], v);
+      }
+    }
+  }
+  wait_vm<0>();     // the gather is complete before any LDS-DMA is counted
+  const int ar = t.y - t0.y, bc = LROWS / 2 + t.z - t0.z;
+  const int nch = (ns + GKC - 1) / GKC;
+  if (nch > 0) issue(0, 0);
+  for (int c = 0; c < nch; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < nch) {
+      issue((c + 1) * GKC, buf ^ 1);
+      if (w == 0) wait_vm<GINS + 1>();
+      else wait_vm<GINS>();
+    } else {
+      wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (!upper) {
+#pragma unroll
+      for (int kk = 0; kk < GKC; ++kk) {
+        if (c * GKC + kk < ns) {
+          const cplx dk = shd[buf][kk][fq];
+          cplx a[TM], b[TN];
+#pragma unroll
+          for (int m = 0; m < TM; ++m) a[m] = cmul(sh[buf][kk][ar + m][fq], dk);
+#pragma unroll
+          for (int n = 0; n < TN; ++n) b[n] = sh[buf][kk][bc + n][fq];
+#pragma unroll
+          for (int m = 0; m < TM; ++m)
+#pragma unroll
+            for (int n = 0; n < TN; ++n) acc[m][n] = cfms(acc[m][n], a[m], b[n]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  if (upper) return;
+#pragma unroll
+  for (int m = 0; m < TM; ++m)
+#pragma unroll
+    for (int n = 0; n < TN; ++n)
+      if (ns + t.y + m < f && ns + t.z + n < f && t.y + m >= t.z + n)
+        base[((int64_t)(ns + t.y + m) * f + ns + t.z + n) * Fc] = acc[m][n];
+}
+
 // symmetric mode, levels with few pivots (short pivot loops, latency of the children's gather
 // dominates): no prefetch, register budget of 4 waves per SIMD
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_schur_sym_small(
@@ -1373,7 +1617,7 @@ void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPac
   LAUNCH(k_combine, dim3((unsigned)((nnz + 255) / 256)), dim3(256), st, stiff, n_stiff, nnz, coef, K);
 }
 
-void launch_schur(bool sym, int maxns, const DevPattern& P, const int4* tiles, int ntiles, const int* g1,
+void launch_schur(bool sym, bool lds_level, int maxns, const DevPattern& P, const int4* tiles, int ntiles, const int* g1,
                   const int* gxp, const int2* gx, int ngroups, double2* F, int64_t Fc, hipStream_t st) {
   if (ntiles <= 0) return;
   dim3 g((ntiles + 3) / 4, ngroups * (64 / SCHUR_QG)), b(256);
@@ -1385,6 +1629,18 @@ void launch_schur(bool sym, int maxns, const DevPattern& P, const int4* tiles, i
     const char* e = getenv("PFR_SCHUR_SMALL_NS");   // tuning knob: levels with few pivots
     return e ? atoi(e) : 0;
   }();
+  static const int lds = [] {
+    const char* e = getenv("PFR_SCHUR_LDS");   // tuning knob: LDS-staged symmetric Schur
+    return e ? atoi(e) : 1;
+  }();
+  if (sym && lds_level && lds == 2) {
+    LAUNCH(k_schur_sym_glds, dim3(ntiles / 4, ngroups * (64 / SCHUR_QG)), b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
+    return;
+  }
+  if (sym && lds_level && lds) {
+    LAUNCH(k_schur_sym_lds, dim3(ntiles / 4, ngroups * (64 / SCHUR_QG)), b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
+    return;
+  }
   if (sym && maxns <= small_ns) LAUNCH(k_schur_sym_small, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
   else if (sym && ku == 3) LAUNCH(k_schur_sym_level<3>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
   else if (sym && ku == 2) LAUNCH(k_schur_sym_level<2>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
