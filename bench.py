@@ -48,23 +48,27 @@ sys.path.insert(0, REPO)
 FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector/matrix (spec; MI355X_MICROARCH.md lists no fp64 row)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 PMC_FILE = os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")
-KERNELS_GENERAL = ("k_assemble_level<0>", "k_factor_level<true>", "k_offdiag_level<0>", "k_schur_level")
-KERNELS_SYM = ("k_assemble_level<0>", "k_factor_level<true>", "k_offdiag_level<0>", "k_schur_sym_level<true>")
+# kernel classes of the factorisation (libpfr per-class HIP-event timings); the rocprof kernel names
+# of a class start with its prefix (the Schur class has per-level variants)
+KERNELS = ("k_assemble_level", "k_factor_level", "k_offdiag_level", "k_schur")
 
 
-def pmc_traffic(chunk, kernels):
+def pmc_traffic(chunk, symmetric):
     """Measured HBM bytes per launch of each factorisation kernel class, scaled to ``chunk``."""
     try:
         d = json.load(open(PMC_FILE))
     except (OSError, ValueError):
         return [None] * 4
     out = []
-    if d.get("factorisation") != ("symmetric" if kernels is KERNELS_SYM else "general"):
+    if d.get("factorisation") != ("symmetric" if symmetric else "general"):
         return [None] * 4
-    for k in kernels:
-        e = d["kernels"].get(k)
-        out.append(None if e is None else
-                   (e["read_bytes"] + e["write_bytes"]) / e["dispatches"] * chunk / d["freqs_per_sweep"])
+    for k in KERNELS:
+        es = [e for name, e in d["kernels"].items() if name.startswith(k)]
+        if not es:
+            out.append(None)
+            continue
+        byts = sum(e["read_bytes"] + e["write_bytes"] for e in es)
+        out.append(byts / sum(e["dispatches"] for e in es) * chunk / d["freqs_per_sweep"])
     return out
 
 
@@ -191,15 +195,15 @@ def main():
     alg_launch = alg_f * n_iso / np.maximum(iso_n, 1)
     ms_launch = iso_ms / np.maximum(iso_n, 1)
     gbs = alg_launch / (ms_launch * 1e-3) / 1e9
-    kernels = KERNELS_SYM if eng.symmetric else KERNELS_GENERAL
-    traffic = pmc_traffic(chunk, kernels)
+    kernels = KERNELS
+    traffic = pmc_traffic(chunk, eng.symmetric)
     fact_alg = float(alg_f.sum() * n_iso)
     fact_ms = float(iso_ms.sum())
     fact_tfs = st["factor_flops"] * n_iso / (iso_phase[0] * 1e-3) / 1e12
     fact_traffic = None if None in traffic else float(np.dot(traffic, iso_n))
-    # each pass reads one triangle: L (L solves) or U (U solves; in symmetric mode U12 is read
-    # as L21), so the four passes read L + U twice: 2 * 16 * nnz(L+U), plus rhs in / solution out
-    trsv_bytes = n_iso * (2 * 16 * st["nnz_lu"] + 4 * 2 * 16 * st["n"])
+    # solve pairs: bottom-up pass over the fronts the rhs support reaches + full top-down pass
+    # (libpfr's count of factor entries read once, 16 B each, plus rhs in / solution out)
+    trsv_bytes = n_iso * float(solver.solve_bytes().sum())
     trsv_gbs = trsv_bytes / ((iso_phase[1] + iso_phase[3]) * 1e-3) / 1e9
     conc_launch = kms / np.maximum(klaunch, 1)
     out = {
@@ -238,7 +242,8 @@ def main():
                             "alg_bytes": fact_alg, "traffic": fact_traffic, "frequencies": n_iso,
                             "fp64_TFLOPs": fact_tfs, "fp64_frac": fact_tfs / FP64_PEAK_TFLOPS,
                             "concurrent_ms_per_step": kms.tolist()},
-        "sptrsv_roofline": {"bound": "hbm", "kernel": "k_{l,u,ut,lt}solve_level", "achieved": trsv_gbs,
+        "sptrsv_roofline": {"bound": "hbm", "kernel": "k_lsolve_level + k_usolve_level (forward and adjoint pairs)",
+                            "achieved": trsv_gbs, "alg_bytes": trsv_bytes,
                             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": trsv_gbs / HBM_PEAK_GBS,
                             "traffic": None},
         "phase_ms": {"factor": phase[0], "fwd_solves": phase[1], "functional": phase[2],

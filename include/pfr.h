@@ -197,6 +197,11 @@ PFR_API int pfr_last_kernel_timings(const pfr_solver* s, double* ms_out /* 4 */,
  * entries it gathers, factor blocks it consumes); index data, shared by all frequencies, excluded. */
 PFR_API int pfr_solver_alg_bytes(const pfr_solver* s, int64_t* bytes_out /* 4 */);
 
+/* Algorithmic HBM bytes per frequency of the triangular solves of one pfr_sweep: [0] forward pair
+ * (bottom-up pass over the fronts the rhs reaches + full top-down pass), [1] adjoint pair (reach of the
+ * functional support + full pass): factor entries read once (16 B each) plus rhs in / solution out. */
+PFR_API int pfr_solver_solve_bytes(const pfr_solver* s, int64_t* bytes_out /* 2 */);
+
 #ifdef __cplusplus
 }
 #endif

@@ -77,6 +77,7 @@ _PROTOS = {
     "pfr_last_timings": (C.c_int, [_P, _DP]),
     "pfr_last_kernel_timings": (C.c_int, [_P, _DP, _P]),
     "pfr_solver_alg_bytes": (C.c_int, [_P, _P]),
+    "pfr_solver_solve_bytes": (C.c_int, [_P, _P]),
 }
 
 _lib = None
@@ -304,4 +305,10 @@ class Solver:
         """Algorithmic HBM bytes per frequency of one factorisation, per kernel class."""
         out = np.zeros(4, np.int64)
         check(lib().pfr_solver_alg_bytes(self._h, out.ctypes.data_as(_P)), "pfr_solver_alg_bytes")
+        return out
+
+    def solve_bytes(self) -> np.ndarray:
+        """Algorithmic HBM bytes per frequency of the forward and the adjoint solve pair of a sweep."""
+        out = np.zeros(2, np.int64)
+        check(lib().pfr_solver_solve_bytes(self._h, out.ctypes.data_as(_P)), "pfr_solver_solve_bytes")
         return out

@@ -88,7 +88,8 @@ struct pfr_solver {
   // right-hand-side reach (0 = forward operator rhs, 1 = loss adjoint on the functional support):
   // the fronts holding a support row and their elimination-tree ancestors -- the only fronts
   // whose bottom-up solve can be non-zero (per-front flags + the fronts level by level)
-  std::vector<int32_t> front_of_col, front_parent, level_fronts_host;
+  std::vector<int32_t> front_of_col, front_parent, level_fronts_host, front_ns, front_f;
+  std::vector<char> reach_host[2];
   int32_t* d_reach[2] = {nullptr, nullptr};
   int32_t* d_reach_fronts[2] = {nullptr, nullptr};
   std::vector<int32_t> reach_ptr[2];
@@ -324,6 +325,7 @@ int set_reach(pfr_solver* s, int which, const std::vector<int32_t>& prows) {
       if (mark[s->level_fronts_host[e]]) list.push_back(s->level_fronts_host[e]);
     s->reach_ptr[which].push_back((int32_t)list.size());
   }
+  s->reach_host[which].assign(mark.begin(), mark.end());
   HIP_TRY(hipMemcpy(s->d_reach[which], mark.data(), nf * 4, hipMemcpyHostToDevice));
   if (!list.empty()) HIP_TRY(hipMemcpy(s->d_reach_fronts[which], list.data(), list.size() * 4, hipMemcpyHostToDevice));
   return PFR_OK;
@@ -760,6 +762,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     for (int t = 0; t < nf; ++t) {
       const Front& F = S.fronts[t];
       s->front_parent[t] = F.parent;
+      s->front_ns.push_back(F.ns);
+      s->front_f.push_back(F.f);
       for (int a = 0; a < F.ns; ++a) s->front_of_col[F.col0 + a] = t;
     }
     s->level_fronts_host = S.level_fronts;
@@ -836,6 +840,20 @@ int pfr_last_kernel_timings(const pfr_solver* s, double* ms, int64_t* launches) 
 int pfr_solver_alg_bytes(const pfr_solver* s, int64_t* bytes) {
   if (!s || !bytes) return fail(PFR_ERR_ARG, "null argument");
   for (int i = 0; i < 4; ++i) bytes[i] = s->alg_bytes[i];
+  return PFR_OK;
+}
+
+int pfr_solver_solve_bytes(const pfr_solver* s, int64_t* bytes) {
+  if (!s || !bytes) return fail(PFR_ERR_ARG, "null argument");
+  for (int w = 0; w < 2; ++w) {
+    int64_t lower = 0, upper = 0;
+    for (size_t t = 0; t < s->front_ns.size(); ++t) {
+      const int64_t ns = s->front_ns[t], r = s->front_f[t] - ns;
+      upper += ns * (ns + 1) / 2 + r * ns;                      // U11 + U12 (symmetric: L21)
+      if (s->reach_host[w][t]) lower += ns * (ns - 1) / 2 + r * ns;   // L11 + L21, reached fronts
+    }
+    bytes[w] = 16 * (lower + upper) + 2 * 16 * (int64_t)s->n;
+  }
   return PFR_OK;
 }
 
