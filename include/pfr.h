@@ -49,7 +49,7 @@ typedef struct pfr_solver pfr_solver;
 typedef struct pfr_symbolic_options {
   int32_t leaf_size;   /* nested-dissection leaf size (default 96) */
   int32_t ordering;    /* 0 nested dissection (default), 1 natural */
-  int32_t relax_small, relax_mid, relax_big; /* supernode amalgamation (4, 16, 48) */
+  int32_t relax_small, relax_mid, relax_big; /* supernode amalgamation (4, 8, 24) */
   double zrelax_mid, zrelax_big;             /* (0.5, 0.1) */
   /* 1: symmetric-structure analysis (default 0).  The caller guarantees that the matrices
    * factorised with it are complex symmetric (A = A^T, non-conjugate) once the Dirichlet
@@ -58,6 +58,12 @@ typedef struct pfr_symbolic_options {
    * to the right-hand side / the adjoint's Dirichlet rows), the rest is factorised as
    * A = L U with U = diag(U) L^T implicit: only L is formed and read. */
   int32_t symmetric;
+  /* Nodes to be eliminated last, together (default none): ordered after every other node, they
+   * form the root front.  The engine passes the loss functional's support, so that the adjoint's
+   * bottom-up solve stays inside the root and both top-down solves run as one pass. */
+  int32_t n_last;
+  const int32_t* last;
+  int32_t max_ns;      /* > 0: fundamental supernodes split into pieces of at most max_ns pivots (default 0) */
 } pfr_symbolic_options;
 
 typedef struct pfr_symbolic_stats {

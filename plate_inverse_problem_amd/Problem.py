@@ -97,13 +97,15 @@ class _Engine:
         # symmetric mode when every matrix is complex symmetric away from the Dirichlet rows
         # (checked on the values): only L is formed, U = diag(U) L^T
         self.symmetric = bool(symmetric) and decoupled_symmetric(rows, cols, vals, n)
-        # tuning knobs of the symbolic analysis (defaults in include/pfr.h): PFR_LEAF_SIZE and
-        # PFR_RELAX="small,mid,big" (supernode amalgamation pivot limits)
+        # tuning knobs of the symbolic analysis (defaults in include/pfr.h): PFR_LEAF_SIZE,
+        # PFR_RELAX="small,mid,big" (supernode amalgamation pivot limits), PFR_MAX_NS
         leaf = os.environ.get("PFR_LEAF_SIZE")
         relax = os.environ.get("PFR_RELAX")
+        max_ns = os.environ.get("PFR_MAX_NS")
         self.sym = _native.Symbolic(n, colptr, rows.astype(np.int32), symmetric=self.symmetric,
                                     leaf_size=int(leaf) if leaf else None,
-                                    relax=tuple(int(v) for v in relax.split(",")) if relax else None)
+                                    relax=tuple(int(v) for v in relax.split(",")) if relax else None,
+                                    max_ns=int(max_ns) if max_ns else None)
         self.stats = self.sym.stats()
         if lanes is None:
             lanes = int(os.environ.get("PFR_LANES", "2"))

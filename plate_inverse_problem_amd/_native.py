@@ -35,7 +35,8 @@ class NativeError(RuntimeError):
 class SymbolicOptions(C.Structure):
     _fields_ = [("leaf_size", C.c_int32), ("ordering", C.c_int32), ("relax_small", C.c_int32),
                 ("relax_mid", C.c_int32), ("relax_big", C.c_int32), ("zrelax_mid", C.c_double),
-                ("zrelax_big", C.c_double), ("symmetric", C.c_int32)]
+                ("zrelax_big", C.c_double), ("symmetric", C.c_int32), ("n_last", C.c_int32),
+                ("last", C.POINTER(C.c_int32)), ("max_ns", C.c_int32)]
 
 
 class SymbolicStats(C.Structure):
@@ -135,7 +136,8 @@ def _ptr(t) -> int:
 class Symbolic:
     """Host-only symbolic analysis (nested dissection + supernodal maps)."""
 
-    def __init__(self, n: int, colptr, rowind, *, leaf_size=None, ordering=0, relax=None, symmetric=False):
+    def __init__(self, n: int, colptr, rowind, *, leaf_size=None, ordering=0, relax=None, symmetric=False,
+                 last=None, max_ns=None):
         L = lib()
         opt = SymbolicOptions()
         L.pfr_symbolic_options_default(C.byref(opt))
@@ -143,6 +145,12 @@ class Symbolic:
             opt.leaf_size = int(leaf_size)
         opt.ordering = int(ordering)
         opt.symmetric = int(bool(symmetric))
+        if max_ns is not None:
+            opt.max_ns = int(max_ns)
+        if last is not None and len(last):
+            self.last, lp = _i32(last)
+            opt.n_last = int(self.last.size)
+            opt.last = lp
         if relax is not None:
             opt.relax_small, opt.relax_mid, opt.relax_big = relax
         self.colptr, cp = _i32(colptr)

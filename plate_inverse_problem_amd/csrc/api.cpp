@@ -353,6 +353,9 @@ void pfr_symbolic_options_default(pfr_symbolic_options* o) {
   o->zrelax_mid = d.zrelax_mid;
   o->zrelax_big = d.zrelax_big;
   o->symmetric = d.symmetric;
+  o->n_last = 0;
+  o->last = nullptr;
+  o->max_ns = d.max_ns;
 }
 
 int pfr_symbolic_create(int32_t n, int64_t nnz, const int32_t* colptr, const int32_t* rowind,
@@ -369,6 +372,11 @@ int pfr_symbolic_create(int32_t n, int64_t nnz, const int32_t* colptr, const int
     o.zrelax_mid = opt->zrelax_mid;
     o.zrelax_big = opt->zrelax_big;
     o.symmetric = opt->symmetric;
+    o.max_ns = opt->max_ns;
+    if (opt->n_last > 0) {
+      if (!opt->last) return fail(PFR_ERR_ARG, "n_last > 0 without last nodes");
+      o.last.assign(opt->last, opt->last + opt->n_last);
+    }
   }
   auto* sym = new pfr_symbolic();
   if (pfr::analyse(n, nnz, colptr, rowind, o, sym->S) != 0) {

@@ -281,9 +281,26 @@ int analyse(int32_t n, int64_t nnz, const int32_t* colptr, const int32_t* rowind
     if (opt.ordering == 1) {
       perm.resize(n);
       std::iota(perm.begin(), perm.end(), 0);
-    } else {
+    } else if (opt.last.empty()) {
       NestedDissection nd(g, opt);
       perm = nd.run();
+    } else {
+      // nodes required last (e.g. the loss functional's support, so that one top-down solve
+      // pass can serve the forward and the adjoint right-hand sides): ordered by nested
+      // dissection with their edges cut, then moved to the end of the order
+      std::vector<char> islast(n, 0);
+      for (int v : opt.last) {
+        if (v < 0 || v >= n) throw std::runtime_error("last node out of range");
+        islast[v] = 1;
+      }
+      std::vector<char> cut2(isdir);
+      for (int v = 0; v < n; ++v) cut2[v] = cut2[v] || islast[v];
+      Graph g2 = symmetric_graph(n, colptr, rowind, cut2);
+      NestedDissection nd(g2, opt);
+      for (int v : nd.run())
+        if (!islast[v]) perm.push_back(v);
+      for (int v = 0; v < n; ++v)
+        if (islast[v]) perm.push_back(v);
     }
     if ((int)perm.size() != n) throw std::runtime_error("ordering lost nodes");
     std::vector<int> iperm(n, -1);
@@ -378,7 +395,8 @@ int analyse(int32_t n, int64_t nnz, const int32_t* colptr, const int32_t* rowind
     std::vector<int> sn_first, sn_last;  // inclusive column ranges
     for (int j = 0; j < n; ++j) {
       bool extend = j > 0 && parent[j - 1] == j && nchild[j] == 1 &&
-                    cs[j - 1].size() == cs[j].size() + 1;
+                    cs[j - 1].size() == cs[j].size() + 1 &&
+                    (opt.max_ns <= 0 || j - sn_first.back() < opt.max_ns);
       if (extend) sn_last.back() = j;
       else {
         sn_first.push_back(j);
