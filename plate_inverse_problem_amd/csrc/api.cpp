@@ -52,8 +52,7 @@ struct pfr_solver {
   int n = 0;
   int64_t nnz = 0;
   int64_t Fc = 0;  // frequencies per chunk (multiple of 64)
-  std::vector<int32_t> level_ptr, level_maxf, level_maxns, level_W, perm, iperm;
-  std::vector<char> level_lds;          // symmetric Schur of the level: LDS-staged 16 x 16 blocks
+  std::vector<int32_t> level_ptr, level_maxf, level_W, perm, iperm;
   DevPattern P{};
   // owned device arrays
   std::vector<void*> owned;
@@ -62,7 +61,7 @@ struct pfr_solver {
   int4* d_items = nullptr;              // off-diagonal panel items (front, first row/col, kind, record offset)
   int2* d_orec = nullptr;               // per item x lane group x pivot: (nz, first child source) of the entry
   int32_t* d_oxp = nullptr;             // per item: range of further child sources in d_ox
-  int2* d_ox = nullptr;                 // (pivot * 4 OFF_RPL + row slot, element id)
+  int2* d_ox = nullptr;                 // (pivot * OFF_G OFF_RPL + row slot, element id)
   std::vector<int32_t> item_ptr;
   int32_t* d_g1 = nullptr;              // per super-tile, lane group, position: first child source (or -1)
   int32_t* d_gxp = nullptr;             // per super-tile: range of further sources in d_gx
@@ -218,7 +217,7 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     mark(l, 1);
     // panel: enough workgroups (front x 16 frequencies) to fill the chip -> one wave
     // each (no idle waves at the block barriers); few large fronts -> more waves
-    const int64_t wgs = (int64_t)nf * ngroups * 4;
+    const int64_t wgs = (int64_t)nf * ngroups * pfr::FAC_G;
     const int Wp = (int)std::max<int64_t>(1, std::min<int64_t>(s->level_W[l], (4096 + wgs - 1) / wgs));
     pfr::launch_factor(s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st);
     mark(l, 2);
@@ -226,7 +225,7 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
                         s->d_oxp + s->item_ptr[l], s->d_ox, ngroups, s->F, s->Fc, s->freqs, s->K, s->M, data, ds,
                         nvalid, st);
     mark(l, 3);
-    pfr::launch_schur(s->sym, s->level_lds[l], s->level_maxns[l], s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l],
+    pfr::launch_schur(s->sym, s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l],
                       s->d_g1 + (int64_t)s->tile_ptr[l] * pfr::SCHUR_TM * pfr::SCHUR_TN * pfr::SCHUR_SR * pfr::SCHUR_SC,
                       s->d_gxp + s->tile_ptr[l],
                       s->d_gx, ngroups, s->F,
@@ -478,19 +477,6 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->perm = S.perm;
   s->iperm = S.iperm;
   for (int m : S.level_maxf) s->level_W.push_back(waves_for(m));
-  s->level_maxns.assign(S.level_maxf.size(), 0);
-  std::vector<int32_t> level_maxr(S.level_maxf.size(), 0);
-  for (const Front& F : S.fronts) {
-    s->level_maxns[F.level] = std::max(s->level_maxns[F.level], F.ns);
-    level_maxr[F.level] = std::max(level_maxr[F.level], F.f - F.ns);
-  }
-  {
-    // the LDS-staged Schur pays off once update blocks are large (measured per level at C3:
-    // better from max r ~ 64 on, worse on the small leaf fronts where 16 x 16 blocks waste waves)
-    const char* e = getenv("PFR_SCHUR_LDS_MINR");   // tuning knob
-    const int minr = e ? atoi(e) : 80;
-    for (size_t l = 0; l < level_maxr.size(); ++l) s->level_lds.push_back(S.symmetric && level_maxr[l] >= minr);
-  }
   Front* d_fronts = nullptr;
   int rc = PFR_OK;
   std::vector<Front> fv(S.fronts);
@@ -550,19 +536,10 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
         // first-source ids (-1 = none), lane group by lane group, then one overflow range
         constexpr int TM = pfr::SCHUR_TM, TN = pfr::SCHUR_TN, SR = pfr::SCHUR_SR, SC = pfr::SCHUR_SC;
         static_assert(TM * SR == TN * SC, "square super-tiles (symmetric mode keeps j0 <= i0)");
-        // symmetric mode: super-tiles in blocks of 2 x 2 (k_schur_sym_lds stages each block's L21
-        // rows in LDS once for its four waves); the upper super-tile of a diagonal block and
-        // super-tiles past the edge carry no sources and store nothing
-        constexpr int ST = TM * SR, BL = 2 * ST;
-        std::vector<std::pair<int, int>> order;
-        if (sym && s->level_lds[l]) {
-          for (int b0 = 0; b0 < r; b0 += BL)
-            for (int c0 = 0; c0 <= b0; c0 += BL)
-              for (int w = 0; w < 4; ++w) order.emplace_back(b0 + ST * (w / 2), c0 + ST * (w % 2));
-        } else {
-          for (int i0 = 0; i0 < r; i0 += ST)
-            for (int j0 = 0; j0 < r && (!sym || j0 <= i0); j0 += ST) order.emplace_back(i0, j0);
-        }
+        constexpr int ST = TM * SR;
+        std::vector<std::pair<int, int>> order;   // super-tiles (symmetric: lower triangle)
+        for (int i0 = 0; i0 < r; i0 += ST)
+          for (int j0 = 0; j0 < r && (!sym || j0 <= i0); j0 += ST) order.emplace_back(i0, j0);
         for (const auto& ij : order) {
           const int i0 = ij.first, j0 = ij.second;
           {
@@ -655,9 +632,9 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
             if (av.size() % 8 == 0) axp.push_back((int32_t)ax.size());
           }
         for (int kind = 0; kind < (sym ? 1 : 2); ++kind)   // symmetric: U12 = diag(U11) L21^T implicit
-          for (int i0 = ns; i0 < f; i0 += 4 * pfr::OFF_RPL) {
+          for (int i0 = ns; i0 < f; i0 += pfr::OFF_G * pfr::OFF_RPL) {
             iv.push_back(make_int4(t, i0, kind, (int32_t)orec.size()));
-            for (int slot = 0; slot < 4 * pfr::OFF_RPL; ++slot)   // row i0 + slot = i0 + 4 h + lane group
+            for (int slot = 0; slot < pfr::OFF_G * pfr::OFF_RPL; ++slot)   // row i0 + slot = i0 + OFF_G h + lane group
               for (int c = 0; c < ns; ++c) {
                 const int idx = i0 + slot;
                 if (idx >= f) {
@@ -666,7 +643,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
                 }
                 const int a = kind == 0 ? idx : c, b = kind == 0 ? c : idx;
                 orec.push_back(make_int2(nzm[(size_t)a * f + b], s1m[(size_t)a * f + b]));
-                for (int32_t id : extras(a, b)) ox.push_back(make_int2(c * 4 * pfr::OFF_RPL + slot, id));
+                for (int32_t id : extras(a, b)) ox.push_back(make_int2(c * pfr::OFF_G * pfr::OFF_RPL + slot, id));
               }
             oxp.push_back((int32_t)ox.size());
           }

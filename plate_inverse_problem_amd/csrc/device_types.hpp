@@ -30,12 +30,31 @@ struct DevPattern {
 // Schur super-tile: a wavefront = SCHUR_QG frequencies x (SCHUR_SR x SCHUR_SC) lane groups,
 // each lane group one SCHUR_TM x SCHUR_TN register tile -> (SCHUR_TM SCHUR_SR) x
 // (SCHUR_TN SCHUR_SC) entries per wave.
-constexpr int SCHUR_SR = 2, SCHUR_SC = 2, SCHUR_QG = 16;
-constexpr int SCHUR_TM = 4, SCHUR_TN = 4;
+#ifndef PFR_SCHUR_SR
+#define PFR_SCHUR_SR 1
+#endif
+#ifndef PFR_SCHUR_TM
+#define PFR_SCHUR_TM 4
+#endif
+constexpr int SCHUR_SR = PFR_SCHUR_SR, SCHUR_SC = PFR_SCHUR_SR, SCHUR_QG = 64 / (SCHUR_SR * SCHUR_SC);
+constexpr int SCHUR_TM = PFR_SCHUR_TM, SCHUR_TN = PFR_SCHUR_TM;
 static_assert(SCHUR_SR * SCHUR_SC * SCHUR_QG == 64, "one wavefront per super-tile");
 
-// Off-diagonal panel kernel: rows (columns) per lane; a wave covers 4 OFF_RPL of them.
-constexpr int OFF_RPL = 1;
+// Off-diagonal panel kernel: a wave = OFF_G lane groups of 64 / OFF_G frequencies, OFF_RPL rows
+// (columns) per lane: OFF_G OFF_RPL rows per wave.
+#ifndef PFR_OFF_G
+#define PFR_OFF_G 1
+#endif
+#ifndef PFR_OFF_RPL
+#define PFR_OFF_RPL 2
+#endif
+constexpr int OFF_G = PFR_OFF_G;
+// A11 factorisation kernel: lane groups per wave (64 / FAC_G frequencies each, one front row each)
+#ifndef PFR_FAC_G
+#define PFR_FAC_G 2
+#endif
+constexpr int FAC_G = PFR_FAC_G;
+constexpr int OFF_RPL = PFR_OFF_RPL;
 
 constexpr int COEF_MAX = 32;
 struct CoefPack {

@@ -205,10 +205,10 @@ __device__ __forceinline__ void col_solve(const cplx* __restrict__ rd, cplx* __r
   }
 }
 
-// Panel kernel lane map: a wavefront covers 16 frequencies x 4 front rows
-// (lane = 16 * sub + frequency), so every wave-instruction advances four rows
-// (or four columns) at once and the pivot-row values it reads are shared by
-// the four row groups; workgroup = (front, 16 frequencies), W waves.
+// Panel kernel lane map: a wavefront covers 64 / FAC_G frequencies x FAC_G front rows
+// (lane = (64 / FAC_G) * sub + frequency; FAC_G = 2 measured best of 1, 2, 4), so every
+// wave-instruction advances FAC_G rows (or columns) at once and the pivot-row values it
+// reads are shared by the row groups; workgroup = (front, 64 / FAC_G frequencies), W waves.
 // DIAG = true: only the diagonal block A11 = L11 U11 (rows and columns < ns);
 // L21 and U12 are then formed row / column-wise by k_offdiag_level.
 template <bool DIAG>
@@ -219,8 +219,9 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
   c.lane = threadIdx.x & 63;
   c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   c.W = blockDim.x >> 6;
-  c.q = (int64_t)blockIdx.y * 16 + (c.lane & 15);
-  const int sub = c.lane >> 4;
+  constexpr int QG = 64 / FAC_G;     // frequencies per lane group
+  c.q = (int64_t)blockIdx.y * QG + c.lane % QG;
+  const int sub = c.lane / QG;
   const Front fr = P.fronts[lvl[blockIdx.x]];
   const int f = fr.f, ns = fr.ns;
   const int lim = DIAG ? ns : f;     // rows / pivot-row columns handled here
@@ -267,7 +268,7 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
 #pragma unroll
         for (int j = 0; j < KB; ++j)
           if (j < i && i < kb) L[i][j] = E(k0 + i, k0 + j);
-      col_solve(base, base, (int64_t)k0 * f, f, Fc, k1 + 4 * c.w + sub, lim, 4 * c.W, kb, L);
+      col_solve(base, base, (int64_t)k0 * f, f, Fc, k1 + FAC_G * c.w + sub, lim, FAC_G * c.W, kb, L);
     }
     __syncthreads();
     // rows >= k1: l = A(i, block) U11^{-1}; then update
@@ -283,7 +284,7 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
 #pragma unroll
       for (int i = 0; i < KB; ++i)
         if (i < kb) Dinv[i] = crecip(E(k0 + i, k0 + i));
-      for (int i = k1 + 4 * c.w + sub; i < lim; i += 4 * c.W) {
+      for (int i = k1 + FAC_G * c.w + sub; i < lim; i += FAC_G * c.W) {
         cplx l[KB];
 #pragma unroll
         for (int t = 0; t < KB; ++t)
@@ -322,7 +323,7 @@ constexpr int OB = 8;
 // child elements in the item's overflow list.
 struct OffSrc {
   const int2* rec[OFF_RPL];   // this lane's records per row slot, indexed by pivot
-  const int2* ox;             // overflow (pivot * 4 OFF_RPL + slot, element id)
+  const int2* ox;             // overflow (pivot * OFF_G OFF_RPL + slot, element id)
   int ox0, ox1, slot0;        // slot of row 0 of this lane: h * 4 + lane group
   double om2;                 // MODE 0: omega^2 of this lane's frequency
   const cplx* K;
@@ -361,12 +362,12 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
     for (int j = 0; j < NB; ++j) x[h][j] = off_source<MODE>(S, F, Fc, q, h, c0 + j);
   for (int e = S.ox0; e < S.ox1; ++e) {       // rare: several children cover one entry
     const int2 g = S.ox[e];
-    const int c = g.x / (4 * OFF_RPL) - c0, slot = g.x % (4 * OFF_RPL);
+    const int c = g.x / (OFF_G * OFF_RPL) - c0, slot = g.x % (OFF_G * OFF_RPL);
     if (c >= 0 && c < NB) {
       const cplx v = F[(int64_t)g.y * Fc + q];
 #pragma unroll
       for (int h = 0; h < OFF_RPL; ++h)
-        if (slot == S.slot0 + 4 * h) {
+        if (slot == S.slot0 + OFF_G * h) {
 #pragma unroll
           for (int j = 0; j < NB; ++j)
             if (j == c) x[h][j] = cadd(x[h][j], v);
@@ -410,9 +411,11 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
     }
 }
 
-// Item = (front, first row / column, kind, record offset): one wave = 16
-// frequencies x 4 lane groups x OFF_RPL rows (columns) per lane = 4 OFF_RPL
-// consecutive rows (columns); row i0 + 4 h + lane group.
+// Item = (front, first row / column, kind, record offset): one wave = 64 / OFF_G
+// frequencies x OFF_G lane groups x OFF_RPL rows (columns) per lane = OFF_G OFF_RPL
+// consecutive rows (columns); row i0 + OFF_G h + lane group.  Default: lane = frequency
+// (OFF_G = 1), 2 rows per lane: every load a 1 KiB run, each U11 value serving two rows
+// (measured 26 % faster than 16 frequencies x 4 rows).
 template <int MODE>
 __global__ __launch_bounds__(256) void k_offdiag_level(DevPattern P, const int4* __restrict__ items, int nitems,
                                                         const int2* __restrict__ orec, const int* __restrict__ oxp,
@@ -425,8 +428,9 @@ __global__ __launch_bounds__(256) void k_offdiag_level(DevPattern P, const int4*
   const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
   const int wid = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (wid >= nitems) return;
-  const int sub = lane >> 4;
-  const int64_t q = (int64_t)by * 16 + (lane & 15);
+  constexpr int QG = 64 / OFF_G;                  // frequencies per lane group
+  const int sub = lane / QG;
+  const int64_t q = (int64_t)by * QG + lane % QG;
   const int4 it = items[wid];
   const Front fr = P.fronts[it.x];
   const int f = fr.f, ns = fr.ns;
@@ -441,11 +445,11 @@ __global__ __launch_bounds__(256) void k_offdiag_level(DevPattern P, const int4*
   bool valid[OFF_RPL];
 #pragma unroll
   for (int h = 0; h < OFF_RPL; ++h) {
-    const int idx = it.y + 4 * h + sub;
+    const int idx = it.y + OFF_G * h + sub;
     valid[h] = idx < f;
     const int r = min(idx, f - 1);
     so[h] = it.z == 0 ? (int64_t)r * f : r;                      // own element c at so + c * sc
-    S.rec[h] = orec + it.w + (int64_t)(4 * h + sub) * ns;
+    S.rec[h] = orec + it.w + (int64_t)(OFF_G * h + sub) * ns;
   }
   S.ox = ox;
   S.ox0 = oxp[wid];
@@ -476,11 +480,11 @@ __global__ __launch_bounds__(256) void k_offdiag_level(DevPattern P, const int4*
 // the K loop so every load of a k-step is independent.
 constexpr int TM = SCHUR_TM, TN = SCHUR_TN;
 
-// Lane map: a wavefront = SCHUR_QG (16) frequencies x 4 sub-tiles; the 4 sub-tiles
-// form a 2 x 2 arrangement of 4 x 4 tiles (an 8 x 8 super-tile), so each L21 row
-// and U12 column value a wave-instruction reads serves two sub-tiles.  (8
-// frequencies x 8 sub-tiles as 8 x 16 was measured 22 % slower: eight distinct
-// 128 B lines per wave-instruction instead of four 256 B runs.)
+// Lane map: a wavefront = SCHUR_QG frequencies x SCHUR_SR x SCHUR_SC sub-tiles of
+// SCHUR_TM x SCHUR_TN.  Default (device_types.hpp): lane = frequency, one 4 x 4 tile per
+// wave, every operand load one 1 KiB run of 64 frequencies -- measured 10 % faster than 16
+// frequencies x a 2 x 2 arrangement of 4 x 4 tiles (four 256 B runs per load, each loaded
+// value shared by two sub-tiles).
 // SYM (symmetric mode): only the lower triangle of A22 is formed; U12 = diag(U11) L21^T is
 // not stored, its entries are made from the L21 rows at load.
 // PF: the next pivot step's loads are issued before the current step's arithmetic.
@@ -618,258 +622,6 @@ __global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* _
 
 // symmetric mode: register budget of 2 waves per SIMD so that every load of a pivot step
 // (or of two steps with PF) is in flight at once (the default budget serialises them)
-// symmetric mode, LDS-staged: workgroup = one 16 x 16 block of A22 (2 x 2 super-tiles, one
-// per wave) x 16 frequencies.  Per chunk of LKC pivots the block's 16 row + 16 column L21 rows
-// (and the pivots U(k, k)) are loaded ONCE for the four waves -- every global load a distinct
-// 256 B run -- into LDS, from where each wave reads its 4 x 4 register tiles' operands.  The
-// next chunk's loads are in flight (registers) while the current one is computed.
-constexpr int LKC = 8;                       // pivots per LDS chunk
-constexpr int LROWS = 4 * SCHUR_TM * SCHUR_SR;   // 16 block rows + 16 block columns
-
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_schur_sym_lds(
-    DevPattern P, const int4* __restrict__ tiles, int ntiles, const int* __restrict__ g1,
-    const int* __restrict__ gxp, const int2* __restrict__ gx, cplx* __restrict__ F, int64_t Fc) {
-  __shared__ cplx sh[LKC][LROWS][SCHUR_QG];
-  __shared__ cplx shd[LKC][SCHUR_QG];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t nblk = (int64_t)gridDim.x;
-  const int64_t lid = xcd_swizzle(blockIdx.x + nblk * blockIdx.y, nblk * gridDim.y);
-  const int blk = (int)(lid % nblk), by = (int)(lid / nblk);
-  if (4 * blk >= ntiles) return;                    // whole workgroup
-  const int tid = 4 * blk + w;
-  const int sub = lane / SCHUR_QG, fq = lane % SCHUR_QG;
-  const int64_t q = (int64_t)by * SCHUR_QG + fq;
-  const int4 t0 = tiles[4 * blk];                   // block origin (front, i0, j0)
-  int4 t = tiles[tid];
-  const bool upper = t.z > t.y;                     // upper super-tile of a diagonal block
-  t.y += TM * (sub / SCHUR_SC);
-  t.z += TN * (sub % SCHUR_SC);
-  const Front fr = P.fronts[t0.x];
-  const int f = fr.f, ns = fr.ns;
-  cplx* __restrict__ base = F + fr.off * Fc + q;
-  cplx acc[TM][TN];
-  {
-    const int4* __restrict__ g4 =
-        reinterpret_cast<const int4*>(g1 + ((int64_t)tid * (SCHUR_SR * SCHUR_SC) + sub) * (TM * TN));
-    int src[TM * TN];
-#pragma unroll
-    for (int u = 0; u < TM * TN / 4; ++u) {
-      const int4 v = g4[u];
-      src[4 * u] = v.x;
-      src[4 * u + 1] = v.y;
-      src[4 * u + 2] = v.z;
-      src[4 * u + 3] = v.w;
-    }
-#pragma unroll
-    for (int m = 0; m < TM; ++m)
-#pragma unroll
-      for (int n = 0; n < TN; ++n) {
-        const int e = src[m * TN + n];
-        const cplx v = F[(int64_t)max(e, 0) * Fc + q];
-        acc[m][n] = e >= 0 ? v : make_double2(0.0, 0.0);
-      }
-    const int x1 = gxp[tid + 1];
-    for (int x = gxp[tid]; x < x1; ++x) {
-      const int2 g = gx[x];
-      if (g.x / (TM * TN) == sub) {
-        const cplx v = F[(int64_t)g.y * Fc + q];
-#pragma unroll
-        for (int m = 0; m < TM; ++m)
-#pragma unroll
-          for (int n = 0; n < TN; ++n)
-            if (g.x % (TM * TN) == m * TN + n) acc[m][n] = cadd(acc[m][n], v);
-      }
-    }
-  }
-  // staging map: thread (g = threadIdx.x >> 4, frequency threadIdx.x & 15) loads block row g and
-  // block column g (L21 rows t0.y + g and t0.z + g) for every pivot of the chunk
-  const int g = threadIdx.x >> 4;
-  const cplx* __restrict__ bq = F + fr.off * Fc + (int64_t)by * SCHUR_QG + (threadIdx.x & 15);
-  const cplx* __restrict__ rowa = bq + (int64_t)min(ns + t0.y + g, f - 1) * f * Fc;
-  const cplx* __restrict__ rowb = bq + (int64_t)min(ns + t0.z + g, f - 1) * f * Fc;
-  // this lane's operands: a rows (block rows), b rows (block columns) of its 4 x 4 tile
-  const int ar = t.y - t0.y, bc = LROWS / 2 + t.z - t0.z;
-  for (int k0 = 0; k0 < ns; k0 += LKC) {
-#pragma unroll
-    for (int u = 0; u < LKC; ++u) {
-      const int64_t o = (int64_t)min(k0 + u, ns - 1) * Fc;
-      sh[u][g][threadIdx.x & 15] = rowa[o];
-      sh[u][LROWS / 2 + g][threadIdx.x & 15] = rowb[o];
-    }
-    if (threadIdx.x < LKC * SCHUR_QG)
-      shd[g][threadIdx.x & 15] = bq[(int64_t)min(k0 + g, ns - 1) * (f + 1) * Fc];
-    __syncthreads();
-    if (!upper) {
-#pragma unroll
-      for (int kk = 0; kk < LKC; ++kk) {
-        if (k0 + kk < ns) {
-          const cplx dk = shd[kk][fq];
-          cplx a[TM], b[TN];
-#pragma unroll
-          for (int m = 0; m < TM; ++m) a[m] = cmul(sh[kk][ar + m][fq], dk);
-#pragma unroll
-          for (int n = 0; n < TN; ++n) b[n] = sh[kk][bc + n][fq];
-#pragma unroll
-          for (int m = 0; m < TM; ++m)
-#pragma unroll
-            for (int n = 0; n < TN; ++n) acc[m][n] = cfms(acc[m][n], a[m], b[n]);
-        }
-      }
-    }
-    __syncthreads();
-  }
-  if (upper) return;
-#pragma unroll
-  for (int m = 0; m < TM; ++m)
-#pragma unroll
-    for (int n = 0; n < TN; ++n)
-      if (ns + t.y + m < f && ns + t.z + n < f && t.y + m >= t.z + n)
-        base[((int64_t)(ns + t.y + m) * f + ns + t.z + n) * Fc] = acc[m][n];
-}
-
-// As k_schur_sym_lds, with the chunks brought in by LDS-DMA (global_load_lds_dwordx4, no
-// registers) into two LDS buffers: chunk c + 1 is in flight while chunk c is computed.  One
-// wave-instruction = 4 staged values (same pivot, 4 consecutive block rows) of 16 frequencies.
-constexpr int GKC = 4;                              // pivots per chunk
-constexpr int GINS = GKC * LROWS / 4 / 4;           // LDS-DMA instructions per wave per chunk (+1 pivots, wave 0)
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_schur_sym_glds(
-    DevPattern P, const int4* __restrict__ tiles, int ntiles, const int* __restrict__ g1,
-    const int* __restrict__ gxp, const int2* __restrict__ gx, cplx* __restrict__ F, int64_t Fc) {
-  __shared__ cplx sh[2][GKC][LROWS][SCHUR_QG];
-  __shared__ cplx shd[2][GKC][SCHUR_QG];
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t nblk = (int64_t)gridDim.x;
-  const int64_t lid = xcd_swizzle(blockIdx.x + nblk * blockIdx.y, nblk * gridDim.y);
-  const int blk = (int)(lid % nblk), by = (int)(lid / nblk);
-  if (4 * blk >= ntiles) return;                    // whole workgroup
-  const int tid = 4 * blk + w;
-  const int sub = lane / SCHUR_QG, fq = lane % SCHUR_QG;
-  const int64_t q = (int64_t)by * SCHUR_QG + fq;
-  const int4 t0 = tiles[4 * blk];
-  int4 t = tiles[tid];
-  const bool upper = t.z > t.y;
-  t.y += TM * (sub / SCHUR_SC);
-  t.z += TN * (sub % SCHUR_SC);
-  const Front fr = P.fronts[t0.x];
-  const int f = fr.f, ns = fr.ns;
-  cplx* __restrict__ base = F + fr.off * Fc + q;
-  // chunk staging: instruction j of wave w = values 4 i .. 4 i + 3, i = w + 4 j (pivot i / 8, block
-  // rows 4 (i % 8) ..), lane -> value 4 i + sub; row pointers of this lane for its GINS values
-  const cplx* __restrict__ bq = F + fr.off * Fc + (int64_t)by * SCHUR_QG + fq;
-  const cplx* srcp[GINS];
-  int srck[GINS];
-#pragma unroll
-  for (int j = 0; j < GINS; ++j) {
-    const int v = 4 * (w + 4 * j) + sub;
-    const int kk = v / LROWS, r = v % LROWS;
-    const int br = r < LROWS / 2 ? t0.y + r : t0.z + r - LROWS / 2;
-    srcp[j] = bq + (int64_t)min(ns + br, f - 1) * f * Fc;
-    srck[j] = kk;
-  }
-  auto issue = [&](int k0, int buf) {
-#pragma unroll
-    for (int j = 0; j < GINS; ++j) {
-      const cplx* src = srcp[j] + (int64_t)min(k0 + srck[j], ns - 1) * Fc;
-      __builtin_amdgcn_global_load_lds(src, &sh[buf][0][0][0] + 64 * (w + 4 * j), 16, 0, 0);
-    }
-    if (w == 0) {
-      const cplx* src = bq + (int64_t)min(k0 + sub, ns - 1) * (f + 1) * Fc;
-      __builtin_amdgcn_global_load_lds(src, &shd[buf][0][0], 16, 0, 0);
-    }
-  };
-  cplx acc[TM][TN];
-  {
-    const int4* __restrict__ g4 =
-        reinterpret_cast<const int4*>(g1 + ((int64_t)tid * (SCHUR_SR * SCHUR_SC) + sub) * (TM * TN));
-    int src[TM * TN];
-#pragma unroll
-    for (int u = 0; u < TM * TN / 4; ++u) {
-      const int4 v = g4[u];
-      src[4 * u] = v.x;
-      src[4 * u + 1] = v.y;
-      src[4 * u + 2] = v.z;
-      src[4 * u + 3] = v.w;
-    }
-#pragma unroll
-    for (int m = 0; m < TM; ++m)
-#pragma unroll
-      for (int n = 0; n < TN; ++n) {
-        const int e = src[m * TN + n];
-        const cplx v = F[(int64_t)max(e, 0) * Fc + q];
-        acc[m][n] = e >= 0 ? v : make_double2(0.0, 0.0);
-      }
-    const int x1 = gxp[tid + 1];
-    for (int x = gxp[tid]; x < x1; ++x) {
-      const int2 g = gx[x];
-      if (g.x / (TM * TN) == sub) {
-        const cplx v = F[(int64_t)g.y * Fc + q];
-#pragma unroll
-        for (int m = 0; m < TM; ++m)
-#pragma unroll
-          for (int n = 0; n < TN; ++n)
-            if (g.x % (TM * TN) == m * TN + n) acc[m][n] = cadd(acc[m][n], v);
-      }
-    }
-  }
-  wait_vm<0>();     // the gather is complete before any LDS-DMA is counted
-  const int ar = t.y - t0.y, bc = LROWS / 2 + t.z - t0.z;
-  const int nch = (ns + GKC - 1) / GKC;
-  if (nch > 0) issue(0, 0);
-  for (int c = 0; c < nch; ++c) {
-    const int buf = c & 1;
-    if (c + 1 < nch) {
-      issue((c + 1) * GKC, buf ^ 1);
-      if (w == 0) wait_vm<GINS + 1>();
-      else wait_vm<GINS>();
-    } else {
-      wait_vm<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    if (!upper) {
-#pragma unroll
-      for (int kk = 0; kk < GKC; ++kk) {
-        if (c * GKC + kk < ns) {
-          const cplx dk = shd[buf][kk][fq];
-          cplx a[TM], b[TN];
-#pragma unroll
-          for (int m = 0; m < TM; ++m) a[m] = cmul(sh[buf][kk][ar + m][fq], dk);
-#pragma unroll
-          for (int n = 0; n < TN; ++n) b[n] = sh[buf][kk][bc + n][fq];
-#pragma unroll
-          for (int m = 0; m < TM; ++m)
-#pragma unroll
-            for (int n = 0; n < TN; ++n) acc[m][n] = cfms(acc[m][n], a[m], b[n]);
-        }
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  }
-  if (upper) return;
-#pragma unroll
-  for (int m = 0; m < TM; ++m)
-#pragma unroll
-    for (int n = 0; n < TN; ++n)
-      if (ns + t.y + m < f && ns + t.z + n < f && t.y + m >= t.z + n)
-        base[((int64_t)(ns + t.y + m) * f + ns + t.z + n) * Fc] = acc[m][n];
-}
-
-// symmetric mode, levels with few pivots (short pivot loops, latency of the children's gather
-// dominates): no prefetch, register budget of 4 waves per SIMD
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_schur_sym_small(
-    DevPattern P, const int4* __restrict__ tiles, int ntiles, const int* __restrict__ g1,
-    const int* __restrict__ gxp, const int2* __restrict__ gx, cplx* __restrict__ F, int64_t Fc) {
-  schur_tile<true, false, 1>(P, tiles, ntiles, g1, gxp, gx, F, Fc);
-}
-
 template <int KU>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_schur_sym_level(
     DevPattern P, const int4* __restrict__ tiles, int ntiles, const int* __restrict__ g1,
@@ -1617,34 +1369,16 @@ void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPac
   LAUNCH(k_combine, dim3((unsigned)((nnz + 255) / 256)), dim3(256), st, stiff, n_stiff, nnz, coef, K);
 }
 
-void launch_schur(bool sym, bool lds_level, int maxns, const DevPattern& P, const int4* tiles, int ntiles, const int* g1,
-                  const int* gxp, const int2* gx, int ngroups, double2* F, int64_t Fc, hipStream_t st) {
+void launch_schur(bool sym, const DevPattern& P, const int4* tiles, int ntiles, const int* g1, const int* gxp,
+                  const int2* gx, int ngroups, double2* F, int64_t Fc, hipStream_t st) {
   if (ntiles <= 0) return;
   dim3 g((ntiles + 3) / 4, ngroups * (64 / SCHUR_QG)), b(256);
   static const int ku = [] {
     const char* e = getenv("PFR_SCHUR_KU");   // tuning knob: pivot steps per prefetched batch
     return e ? atoi(e) : 2;
   }();
-  static const int small_ns = [] {
-    const char* e = getenv("PFR_SCHUR_SMALL_NS");   // tuning knob: levels with few pivots
-    return e ? atoi(e) : 0;
-  }();
-  static const int lds = [] {
-    const char* e = getenv("PFR_SCHUR_LDS");   // tuning knob: LDS-staged symmetric Schur
-    return e ? atoi(e) : 1;
-  }();
-  if (sym && lds_level && lds == 2) {
-    LAUNCH(k_schur_sym_glds, dim3(ntiles / 4, ngroups * (64 / SCHUR_QG)), b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
-    return;
-  }
-  if (sym && lds_level && lds) {
-    LAUNCH(k_schur_sym_lds, dim3(ntiles / 4, ngroups * (64 / SCHUR_QG)), b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
-    return;
-  }
-  if (sym && maxns <= small_ns) LAUNCH(k_schur_sym_small, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
-  else if (sym && ku == 3) LAUNCH(k_schur_sym_level<3>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
-  else if (sym && ku == 2) LAUNCH(k_schur_sym_level<2>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
-  else if (sym) LAUNCH(k_schur_sym_level<1>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
+  if (sym && ku == 1) LAUNCH(k_schur_sym_level<1>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
+  else if (sym) LAUNCH(k_schur_sym_level<2>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
   else LAUNCH(k_schur_level, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
 }
 
@@ -1659,14 +1393,14 @@ void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, cons
 
 void launch_factor(const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F, int64_t Fc,
                    int* flags, hipStream_t st) {
-  LAUNCH(k_factor_level<true>, dim3(nfronts, ngroups * 4), dim3(64 * W), st, P, lvl, F, Fc, flags);
+  LAUNCH(k_factor_level<true>, dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
 }
 
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
                     const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,
                     const double* M, const double2* data, int64_t ds, int nvalid, hipStream_t st) {
   if (nitems <= 0) return;
-  dim3 g((nitems + 3) / 4, ngroups * 4), b(256);
+  dim3 g((nitems + 3) / 4, ngroups * OFF_G), b(256);
   if (mode == 0)
     LAUNCH(k_offdiag_level<0>, g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid);
   else

@@ -40,8 +40,8 @@ void launch_factor(const DevPattern& P, const int* lvl, int nfronts, int W, int 
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
                     const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,
                     const double* M, const double2* data, int64_t ds, int nvalid, hipStream_t st);
-void launch_schur(bool sym, bool lds_level, int maxns, const DevPattern& P, const int4* tiles, int ntiles, const int* g1,
-                  const int* gxp, const int2* gx, int ngroups, double2* F, int64_t Fc, hipStream_t st);
+void launch_schur(bool sym, const DevPattern& P, const int4* tiles, int ntiles, const int* g1, const int* gxp,
+                  const int2* gx, int ngroups, double2* F, int64_t Fc, hipStream_t st);
 // which: 0 = L (bottom-up), 1 = U (top-down), 2 = U^T (bottom-up), 3 = L^T (top-down)
 void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups,
                   const double2* F, int64_t Fc, double2* WV, const RhsDesc& rd, const double2* Yin, double2* Out,
