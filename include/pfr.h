@@ -63,7 +63,8 @@ typedef struct pfr_symbolic_options {
    * bottom-up solve stays inside the root and both top-down solves run as one pass. */
   int32_t n_last;
   const int32_t* last;
-  int32_t max_ns;      /* > 0: fundamental supernodes split into pieces of at most max_ns pivots (default 0) */
+  int32_t max_ns;      /* fundamental supernodes split into pieces of at most max_ns pivots (default 256;
+                        * 0 = no split) */
 } pfr_symbolic_options;
 
 typedef struct pfr_symbolic_stats {

@@ -468,6 +468,10 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     delete s;
     return rc;
   };
+  if (S.max_front > pfr::MAX_FRONT) {
+    delete s;
+    return fail(PFR_ERR_ARG, "front larger than MAX_FRONT (device_types.hpp)");
+  }
   s->device = device;
   s->n = S.n;
   s->nnz = S.nnz;
@@ -535,11 +539,10 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
         // SCHUR_TM x SCHUR_TN tile at (TM (sub / SC), TN (sub % SC)); per super-tile the dense
         // first-source ids (-1 = none), lane group by lane group, then one overflow range
         constexpr int TM = pfr::SCHUR_TM, TN = pfr::SCHUR_TN, SR = pfr::SCHUR_SR, SC = pfr::SCHUR_SC;
-        static_assert(TM * SR == TN * SC, "square super-tiles (symmetric mode keeps j0 <= i0)");
-        constexpr int ST = TM * SR;
-        std::vector<std::pair<int, int>> order;   // super-tiles (symmetric: lower triangle)
-        for (int i0 = 0; i0 < r; i0 += ST)
-          for (int j0 = 0; j0 < r && (!sym || j0 <= i0); j0 += ST) order.emplace_back(i0, j0);
+        constexpr int STR = TM * SR, STC = TN * SC;
+        std::vector<std::pair<int, int>> order;   // super-tiles (symmetric: those touching the lower triangle)
+        for (int i0 = 0; i0 < r; i0 += STR)
+          for (int j0 = 0; j0 < r && (!sym || j0 <= i0 + STR - 1); j0 += STC) order.emplace_back(i0, j0);
         for (const auto& ij : order) {
           const int i0 = ij.first, j0 = ij.second;
           {

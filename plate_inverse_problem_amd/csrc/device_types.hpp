@@ -37,7 +37,10 @@ struct DevPattern {
 #define PFR_SCHUR_TM 4
 #endif
 constexpr int SCHUR_SR = PFR_SCHUR_SR, SCHUR_SC = PFR_SCHUR_SR, SCHUR_QG = 64 / (SCHUR_SR * SCHUR_SC);
-constexpr int SCHUR_TM = PFR_SCHUR_TM, SCHUR_TN = PFR_SCHUR_TM;
+#ifndef PFR_SCHUR_TN
+#define PFR_SCHUR_TN PFR_SCHUR_TM
+#endif
+constexpr int SCHUR_TM = PFR_SCHUR_TM, SCHUR_TN = PFR_SCHUR_TN;
 static_assert(SCHUR_SR * SCHUR_SC * SCHUR_QG == 64, "one wavefront per super-tile");
 
 // Off-diagonal panel kernel: a wave = OFF_G lane groups of 64 / OFF_G frequencies, OFF_RPL rows
@@ -55,6 +58,9 @@ constexpr int OFF_G = PFR_OFF_G;
 #endif
 constexpr int FAC_G = PFR_FAC_G;
 constexpr int OFF_RPL = PFR_OFF_RPL;
+
+// Largest front the solve kernels stage index lists for in LDS (checked at solver creation)
+constexpr int MAX_FRONT = 1024;
 
 constexpr int COEF_MAX = 32;
 struct CoefPack {

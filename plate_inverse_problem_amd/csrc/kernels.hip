@@ -801,7 +801,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
   const int f = fr.f, ns = fr.ns;
   const cplx* __restrict__ base = F + fr.off * Fc + c.q;
   cplx* __restrict__ wv = WV + (int64_t)fr.row0 * Fc + c.q;
-  const int* __restrict__ ix = P.idx + fr.row0;
+  // the front's row indices, staged in LDS once: the solution gathers of every pivot row read
+  // them there instead of through dependent global loads
+  __shared__ int six[MAX_FRONT];
+  for (int a = threadIdx.x; a < f; a += blockDim.x) six[a] = P.idx[fr.row0 + a];
+  __syncthreads();
+  const int* ix = six;
 #define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
 #define V(a) wv[(int64_t)(a) * Fc]
   for (int a0 = SRB * c.w; a0 < ns; a0 += SRB * c.W) {
@@ -823,7 +828,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
       int iv[SKC];
       cplx xv[SKC], ev[SRB][SKC];
 #pragma unroll
-      for (int u = 0; u < SKC; ++u) iv[u] = ix[__builtin_amdgcn_readfirstlane(min(b0 + u, f - 1))];
+      for (int u = 0; u < SKC; ++u) iv[u] = __builtin_amdgcn_readfirstlane(ix[min(b0 + u, f - 1)]);
 #pragma unroll
       for (int u = 0; u < SKC; ++u) xv[u] = xq[(int64_t)iv[u] * Fc];
 #pragma unroll

@@ -26,7 +26,7 @@ struct SymbolicOptions {
   int ordering = 0;          // 0 = nested dissection, 1 = natural (tests)
   int symmetric = 0;         // 1 = symmetric-structure analysis with decoupled Dirichlet nodes
   std::vector<int> last;     // nodes eliminated last, together (they form the root front)
-  int max_ns = 0;            // > 0: fundamental supernodes are split into pieces of at most this many pivots
+  int max_ns = 256;          // > 0: fundamental supernodes are split into pieces of at most this many pivots
 };
 
 struct Front {
