@@ -437,7 +437,7 @@ int analyse(int32_t n, int64_t nnz, const int32_t* colptr, const int32_t* rowind
       bool merge = ns_new <= opt.relax_small ||
                    (ns_new <= opt.relax_mid && zfrac < opt.zrelax_mid) ||
                    (ns_new <= opt.relax_big && zfrac < opt.zrelax_big);
-      if (!merge) continue;
+      if (!merge || (opt.max_ns > 0 && ns_new > opt.max_ns)) continue;
       rep[s] = p;
       first[p] = first[s];
       true_nz[p] += true_nz[s];

@@ -152,3 +152,32 @@ def test_symmetric_detection_rejects_unsymmetric():
     assert decoupled_symmetric(rows2, cols2, v2, 3)
     v3 = np.array([[2.0, 1.0, 1.5, 3.0, 1.0, 0.5]])
     assert not decoupled_symmetric(rows2, cols2, v3, 3)
+
+
+def test_last_nodes_and_max_ns_options():
+    """Nodes required last form the root front(s); max_ns caps every supernode."""
+    p = make_problem("orthotropic", ny=4)
+    idx, colptr, rowind = _active_pattern(p)
+    aU, aV, aW = p.averaging_vectors()
+    sup = np.nonzero((aU != 0) | (aV != 0) | (aW != 0))[0]
+    sym = _native.Symbolic(p.mat_size, colptr, rowind, symmetric=True, last=sup, max_ns=8)
+    iperm = sym.export("IPERM")
+    fr = sym.export("FRONTS")
+    assert fr[:, 0].max() <= 8                                # no supernode above max_ns
+    # the support nodes sit at the top of their elimination trees: every ancestor front of a
+    # front holding a support node holds support nodes too
+    owner = np.repeat(np.arange(len(fr)), fr[:, 0])           # pivot column -> front
+    sfr = set(owner[iperm[sup]])
+    for t in sfr:
+        par = fr[t, 4]
+        assert par < 0 or par in sfr
+    assert fr[:, 0].sum() == p.mat_size
+    # the factorisation through the exported maps still solves the system
+    orc = oracle_for(p)
+    c = orc.coefficients(p.parameters)
+    data = (orc.mass_values() * -(2 * np.pi * 211.0) ** 2 + c @ p.mats[:18])[idx]
+    A = sp.csc_matrix((data, rowind, colptr), shape=(p.mat_size,) * 2).toarray()
+    b = np.random.default_rng(2).standard_normal(p.mat_size) + 0j
+    mf = MFModel(sym)
+    x = mf.solve_sym(mf.factor(data), b, sym, data)
+    assert np.linalg.norm(x - np.linalg.solve(A, b)) / np.linalg.norm(x) < 1e-10
