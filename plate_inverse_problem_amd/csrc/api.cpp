@@ -92,7 +92,7 @@ struct pfr_solver {
   int32_t* d_reach[2] = {nullptr, nullptr};
   int32_t* d_reach_fronts[2] = {nullptr, nullptr};
   std::vector<int32_t> reach_ptr[2];
-  double2 *F = nullptr, *WV = nullptr, *X = nullptr, *Y = nullptr, *XA = nullptr, *G = nullptr;
+  double2 *F = nullptr, *WV = nullptr, *X = nullptr, *Y = nullptr, *XA = nullptr, *G = nullptr, *Y2 = nullptr;
   // Hessian sweep: permuted matrix by rows and by columns ((ptr, index, nz) each),
   // tangent solution / adjoint vectors, combined tangent operators (lazily allocated)
   int32_t *d_rptr = nullptr, *d_ridx = nullptr, *d_rnz = nullptr;
@@ -162,7 +162,7 @@ int64_t workspace_bytes(const Symbolic& S, int64_t Fc) {
   int64_t b = 0;
   b += S.factor_entries * Fc * 16;   // F
   b += S.total_rows * Fc * 16;       // WV
-  b += 4 * (int64_t)S.n * Fc * 16;   // X, Y, XA, G
+  b += 5 * (int64_t)S.n * Fc * 16;   // X, Y, XA, G, Y2
   b += Fc * (8 + 8 + 4 + 16);        // freqs, loss terms, flags, tq
   return b;
 }
@@ -306,6 +306,34 @@ int adjoint_solve(pfr_solver* s, const pfr::RhsDesc& rg, double2* Out, hipStream
   }
   if ((rc = solve_all(s, 2, 2, rg, nullptr, s->Y, st, subset))) return rc;
   return solve_all(s, 3, 0, rg, s->Y, Out, st, subset);
+}
+
+// Symmetric mode, loss + gradient: the forward top-down pass first over the fronts the loss
+// support reaches only (they hold every support row), then -- once the loss cotangent is known
+// and its bottom-up pass (same fronts) done -- ONE top-down pass computes the adjoint on every
+// front and the forward solution on the rest, each factor value loaded once for both.
+int sym_top_down_support(pfr_solver* s, const pfr::RhsDesc& rd, hipStream_t st) {
+  const int L = (int)s->level_ptr.size() - 1;
+  const int ngroups = (int)(s->Fc / 64);
+  for (int l = L - 1; l >= 0; --l) {
+    const int nf = s->reach_ptr[1][l + 1] - s->reach_ptr[1][l];
+    pfr::launch_solve(1, 0, true, s->P, s->d_reach_fronts[1] + s->reach_ptr[1][l], nf, s->level_W[l], ngroups, s->F,
+                      s->Fc, s->WV, rd, s->Y, s->X, s->d_reach[0], st);
+  }
+  HIP_TRY(hipGetLastError());
+  return PFR_OK;
+}
+
+int sym_top_down_pair(pfr_solver* s, hipStream_t st) {
+  const int L = (int)s->level_ptr.size() - 1;
+  const int ngroups = (int)(s->Fc / 64);
+  for (int l = L - 1; l >= 0; --l) {
+    const int nf = s->level_ptr[l + 1] - s->level_ptr[l];
+    pfr::launch_usolve2(true, s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_W[l], ngroups, s->F, s->Fc, s->Y,
+                        s->X, s->d_reach[0], s->d_reach[1], s->Y2, s->XA, s->d_reach[1], st);
+  }
+  HIP_TRY(hipGetLastError());
+  return PFR_OK;
 }
 
 // Mark the fronts holding the given permuted rows and all their ancestors; upload the flags and
@@ -764,6 +792,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   if ((rc = s->alloc(&s->F, S.factor_entries * Fc)) || (rc = s->alloc(&s->WV, S.total_rows * Fc)) ||
       (rc = s->alloc(&s->X, (int64_t)S.n * Fc)) || (rc = s->alloc(&s->Y, (int64_t)S.n * Fc)) ||
       (rc = s->alloc(&s->XA, (int64_t)S.n * Fc)) || (rc = s->alloc(&s->G, (int64_t)S.n * Fc)) ||
+      (rc = s->alloc(&s->Y2, (int64_t)S.n * Fc)) ||
       (rc = s->alloc(&s->freqs, Fc)) || (rc = s->alloc(&s->loss_terms, Fc)) || (rc = s->alloc(&s->flags, Fc)) ||
       (rc = s->alloc(&s->tq, Fc)))
     return bail(rc);
@@ -979,7 +1008,19 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
     rd.beta_im = s->beta_im;
     rd.mass_sum = s->mass_sum;
     rd.freqs = s->freqs;
-    if ((rc = forward_solve(s, 0, rd, s->X, st, 0))) return rc;
+    // symmetric loss + gradient: forward top-down only over the loss support's fronts, then one
+    // combined top-down pass (sym_top_down_pair); otherwise the full forward solve first
+    const bool paired = s->sym && reverse;
+    if (paired) {
+      pfr::RhsDesc rf = rd;
+      pfr::launch_dirichlet_rhs(0, dir_desc(s), s->n_crow, rd, nullptr, s->Bc, s->Fc, st);
+      rf.cslot = s->d_cslot;
+      rf.Bc = s->Bc;
+      if ((rc = solve_all(s, 0, s->n_crow > 0 ? 3 : 0, rf, nullptr, s->Y, st, 0))) return rc;
+      if ((rc = sym_top_down_support(s, rf, st))) return rc;
+    } else if ((rc = forward_solve(s, 0, rd, s->X, st, 0))) {
+      return rc;
+    }
     record(s, 2, st);
     pfr::FunctionalArgs fa = s->fn;
     fa.loss_type = reverse ? loss_type : -1;
@@ -991,7 +1032,12 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
     if (reverse) {
       pfr::RhsDesc rg;
       rg.G = s->G;
-      if ((rc = adjoint_solve(s, rg, s->XA, st, 1))) return rc;
+      if (paired) {
+        if ((rc = solve_all(s, 0, 2, rg, nullptr, s->Y2, st, 1)) || (rc = sym_top_down_pair(s, st))) return rc;
+        pfr::launch_dirichlet_post(dir_desc(s), s->n_dir, s->XA, s->Fc, st);
+      } else if ((rc = adjoint_solve(s, rg, s->XA, st, 1))) {
+        return rc;
+      }
       record(s, 4, st);
       pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->XA, s->X, Fc, nv, s->partial,
                            st);

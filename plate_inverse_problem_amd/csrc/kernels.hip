@@ -894,6 +894,134 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
 #undef V
 }
 
+// ------------------------------------------------------------------ K3b': two top-down solves in one pass
+// U x = y for two right-hand sides on the same factors (symmetric mode: the forward solution x
+// and the adjoint lambda), each L21 / U11 value loaded once for both.  Vector v is computed on
+// the fronts where act = !skip[front] (the forward pass is skipped on the fronts it was already
+// solved on, those the loss support reaches); its y is zero on fronts outside reach.  X itself
+// is the scratch of a front's pivot values.
+struct UPair {
+  const cplx* Y;
+  cplx* X;
+  const int* reach;   // y non-zero only on these fronts (NULL = all)
+  const int* skip;    // fronts this vector is not computed on (NULL = none)
+};
+
+template <bool SYM>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_usolve2_level(
+    DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc, UPair A, UPair B) {
+  const int ft = lvl[blockIdx.x];
+  const bool act[2] = {!A.skip || !A.skip[ft], !B.skip || !B.skip[ft]};
+  const bool live[2] = {!A.reach || A.reach[ft], !B.reach || B.reach[ft]};
+  const cplx* Ys[2] = {A.Y, B.Y};
+  cplx* Xs[2] = {A.X, B.X};
+  const Ctx c = ctx();
+  const Front fr = P.fronts[ft];
+  const int f = fr.f, ns = fr.ns;
+  const cplx* __restrict__ base = F + fr.off * Fc + c.q;
+  __shared__ int six[MAX_FRONT];
+  for (int a = threadIdx.x; a < f; a += blockDim.x) six[a] = P.idx[fr.row0 + a];
+  __syncthreads();
+#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+#define XV(v, a) Xs[v][(int64_t)(fr.col0 + (a)) * Fc + c.q]
+  for (int a0 = SRB * c.w; a0 < ns; a0 += SRB * c.W) {
+    int ra[SRB];
+    cplx acc[2][SRB];
+#pragma unroll
+    for (int r = 0; r < SRB; ++r) {
+      ra[r] = min(a0 + r, ns - 1);
+      acc[0][r] = acc[1][r] = make_double2(0.0, 0.0);
+    }
+    const cplx* pu[SRB];
+#pragma unroll
+    for (int r = 0; r < SRB; ++r) pu[r] = base + (SYM ? (int64_t)ra[r] : (int64_t)ra[r] * f) * Fc;
+    const int64_t su = SYM ? (int64_t)f * Fc : Fc;
+    for (int b0 = ns; b0 < f; b0 += SKC) {
+      int iv[SKC];
+      cplx xv[2][SKC], ev[SRB][SKC];
+#pragma unroll
+      for (int u = 0; u < SKC; ++u) iv[u] = __builtin_amdgcn_readfirstlane(six[min(b0 + u, f - 1)]);
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int u = 0; u < SKC; ++u) xv[v][u] = Xs[v][(int64_t)iv[u] * Fc + c.q];   // inactive: unused
+#pragma unroll
+      for (int r = 0; r < SRB; ++r)
+#pragma unroll
+        for (int u = 0; u < SKC; ++u) ev[r][u] = pu[r][min(b0 + u, f - 1) * su];
+      __builtin_amdgcn_sched_group_barrier(0x020, SKC * (SRB + 2), 0);   // all vector loads first
+      __builtin_amdgcn_sched_group_barrier(0x002, 8 * SKC * SRB + 16, 0);
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int u = 0; u < SKC; ++u)
+          if (b0 + u >= f) xv[v][u] = make_double2(0.0, 0.0);
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int r = 0; r < SRB; ++r)
+#pragma unroll
+          for (int u = 0; u < SKC; ++u) acc[v][r] = cfms(acc[v][r], ev[r][u], xv[v][u]);
+    }
+#pragma unroll
+    for (int r = 0; r < SRB; ++r)
+      if (a0 + r < ns) {
+        const cplx urr = SYM ? E(ra[r], ra[r]) : make_double2(1.0, 0.0);
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+          if (act[v]) {
+            const cplx y = live[v] ? Ys[v][(int64_t)(fr.col0 + a0 + r) * Fc + c.q] : make_double2(0.0, 0.0);
+            XV(v, a0 + r) = SYM ? cadd(y, cmul(urr, acc[v][r])) : cadd(y, acc[v][r]);
+          }
+      }
+  }
+  __syncthreads();
+  for (int k1 = ns; k1 > 0; k1 -= KBS) {
+    const int k0 = max(0, k1 - KBS), kb = k1 - k0;
+    if (c.w == 0) {
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+        if (act[v]) {
+          cplx x[KBS];
+#pragma unroll
+          for (int t = 0; t < KBS; ++t) x[t] = t < kb ? XV(v, k0 + t) : make_double2(0.0, 0.0);
+#pragma unroll
+          for (int k = KBS - 1; k >= 0; --k)
+            if (k < kb) {
+              x[k] = cmul(x[k], crecip(E(k0 + k, k0 + k)));
+#pragma unroll
+              for (int i = 0; i < KBS; ++i)
+                if (i < k) x[i] = cfms(x[i], E(k0 + i, k0 + k), x[k]);
+            }
+#pragma unroll
+          for (int t = 0; t < KBS; ++t)
+            if (t < kb) XV(v, k0 + t) = x[t];
+        }
+    }
+    __syncthreads();
+    if (k0 > 0) {
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+        if (act[v]) {
+          cplx x[KBS];
+#pragma unroll
+          for (int t = 0; t < KBS; ++t)
+            if (t < kb) x[t] = XV(v, k0 + t);
+          for (int i = c.w; i < k0; i += c.W) {
+            cplx y = XV(v, i);
+#pragma unroll
+            for (int t = 0; t < KBS; ++t)
+              if (t < kb) y = cfms(y, E(i, k0 + t), x[t]);
+            XV(v, i) = y;
+          }
+        }
+      __syncthreads();
+    }
+  }
+#undef E
+#undef XV
+}
+
 // ------------------------------------------------------------------ K3c: U^T y = g (bottom-up)
 template <int RHS>
 __global__ __launch_bounds__(512) void k_utsolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
@@ -1446,6 +1574,16 @@ void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const 
       LAUNCH(k_ltsolve_level, g, b, st, P, lvl, F, Fc, WV, Yin, Out, reach);
       break;
   }
+}
+
+void launch_usolve2(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, const double2* F,
+                    int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0, const double2* Y1,
+                    double2* X1, const int* reach1, hipStream_t st) {
+  if (nfronts <= 0) return;
+  UPair a{Y0, X0, reach0, skip0}, b{Y1, X1, reach1, nullptr};
+  dim3 g(nfronts, ngroups), bl(64 * W);
+  if (sym) LAUNCH(k_usolve2_level<true>, g, bl, st, P, lvl, F, Fc, a, b);
+  else LAUNCH(k_usolve2_level<false>, g, bl, st, P, lvl, F, Fc, a, b);
 }
 
 void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nrows, const double2* Kd,
