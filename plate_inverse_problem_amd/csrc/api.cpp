@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -89,6 +90,11 @@ struct pfr_solver {
   // whose bottom-up solve can be non-zero (per-front flags + the fronts level by level)
   std::vector<int32_t> front_of_col, front_parent, level_fronts_host, front_ns, front_f;
   std::vector<char> reach_host[2];
+  // side stream for the forward bottom-up solve over the rhs reach, overlapped with the
+  // factorisation level by level (symmetric loss + gradient sweeps)
+  hipStream_t aux = nullptr;
+  std::vector<hipEvent_t> lev_ev;
+  hipEvent_t aux_start = nullptr, aux_done = nullptr;
   int32_t* d_reach[2] = {nullptr, nullptr};
   int32_t* d_reach_fronts[2] = {nullptr, nullptr};
   std::vector<int32_t> reach_ptr[2];
@@ -132,6 +138,10 @@ struct pfr_solver {
   int64_t alg_bytes[4]{};               // algorithmic HBM bytes per frequency of each class (one sweep)
 
   ~pfr_solver() {
+    for (auto e : lev_ev) (void)hipEventDestroy(e);
+    if (aux_start) (void)hipEventDestroy(aux_start);
+    if (aux_done) (void)hipEventDestroy(aux_done);
+    if (aux) (void)hipStreamDestroy(aux);
     for (void* p : owned) (void)hipFree(p);
     for (auto& c : tev) {
       for (auto& x : c.ev)
@@ -200,7 +210,9 @@ int finish_timing(pfr_solver* s, const bool* used) {
 
 void reset_timing(pfr_solver* s) { s->n_tev = 0; }
 
-int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nvalid, hipStream_t st) {
+// after_panel(l): called once level l's L21 panel is launched (its L factor complete in stream order)
+int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nvalid, hipStream_t st,
+               const std::function<void(int)>& after_panel = nullptr) {
   const int L = (int)s->level_ptr.size() - 1;
   const int ngroups = (int)(s->Fc / 64);
   const bool kt = (s->timing & 2) && s->n_tev < (int)s->tev.size() && !s->tev[s->n_tev].kev.empty();
@@ -224,6 +236,7 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     pfr::launch_offdiag(mode, s->P, s->d_items + s->item_ptr[l], s->item_ptr[l + 1] - s->item_ptr[l], s->d_orec,
                         s->d_oxp + s->item_ptr[l], s->d_ox, ngroups, s->F, s->Fc, s->freqs, s->K, s->M, data, ds,
                         nvalid, st);
+    if (after_panel) after_panel(l);
     mark(l, 3);
     pfr::launch_schur(s->sym, s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l],
                       s->d_g1 + (int64_t)s->tile_ptr[l] * pfr::SCHUR_TM * pfr::SCHUR_TN * pfr::SCHUR_SR * pfr::SCHUR_SC,
@@ -796,6 +809,16 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       (rc = s->alloc(&s->freqs, Fc)) || (rc = s->alloc(&s->loss_terms, Fc)) || (rc = s->alloc(&s->flags, Fc)) ||
       (rc = s->alloc(&s->tq, Fc)))
     return bail(rc);
+  // PFR_AUX=1: run the forward sparse L-solve on a side stream, level by level behind the
+  // factorisation (+2% with one solver lane; with two lanes the extra queues cost more than it saves)
+  const char* aux_env = getenv("PFR_AUX");
+  if (s->sym && aux_env && atoi(aux_env) == 1) {
+    HIP_TRY(hipStreamCreateWithFlags(&s->aux, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&s->aux_start, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&s->aux_done, hipEventDisableTiming));
+    s->lev_ev.resize(s->level_ptr.size() - 1);
+    for (auto& e : s->lev_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
   *out = s;
   return PFR_OK;
 }
@@ -999,24 +1022,50 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
     HIP_TRY(hipMemsetAsync(s->flags, 0, Fc * sizeof(int32_t), st));
     if (int rc0 = begin_chunk(s)) return rc0;
     record(s, 0, st);
-    int rc = factor_all(s, 0, nullptr, 0, nv, st);
-    if (rc) return rc;
-    record(s, 1, st);
     pfr::RhsDesc rd;
     rd.rhsP = s->rhsP;
     rd.beta_re = s->beta_re;
     rd.beta_im = s->beta_im;
     rd.mass_sum = s->mass_sum;
     rd.freqs = s->freqs;
-    // symmetric loss + gradient: forward top-down only over the loss support's fronts, then one
-    // combined top-down pass (sym_top_down_pair); otherwise the full forward solve first
     const bool paired = s->sym && reverse;
-    if (paired) {
-      pfr::RhsDesc rf = rd;
+    pfr::RhsDesc rf = rd;
+    int rc;
+    if (paired && !s->aux) {
       pfr::launch_dirichlet_rhs(0, dir_desc(s), s->n_crow, rd, nullptr, s->Bc, s->Fc, st);
       rf.cslot = s->d_cslot;
       rf.Bc = s->Bc;
+      if ((rc = factor_all(s, 0, nullptr, 0, nv, st))) return rc;
       if ((rc = solve_all(s, 0, s->n_crow > 0 ? 3 : 0, rf, nullptr, s->Y, st, 0))) return rc;
+    } else if (paired) {
+      // forward bottom-up solve over the rhs reach on the side stream, level l as soon as level
+      // l's L factor is formed (it needs nothing else), overlapping the factorisation
+      const int ngroups_ = ngroups;
+      HIP_TRY(hipEventRecord(s->aux_start, st));
+      HIP_TRY(hipStreamWaitEvent(s->aux, s->aux_start, 0));
+      pfr::launch_dirichlet_rhs(0, dir_desc(s), s->n_crow, rd, nullptr, s->Bc, s->Fc, s->aux);
+      rf.cslot = s->d_cslot;
+      rf.Bc = s->Bc;
+      const int rmode = s->n_crow > 0 ? 3 : 0;
+      auto hook = [&](int l) {
+        (void)hipEventRecord(s->lev_ev[l], st);
+        (void)hipStreamWaitEvent(s->aux, s->lev_ev[l], 0);
+        const int nf = s->reach_ptr[0][l + 1] - s->reach_ptr[0][l];
+        pfr::launch_solve(0, rmode, true, s->P, s->d_reach_fronts[0] + s->reach_ptr[0][l], nf, s->level_W[l], ngroups_,
+                          s->F, s->Fc, s->WV, rf, nullptr, s->Y, s->d_reach[0], s->aux);
+      };
+      rc = factor_all(s, 0, nullptr, 0, nv, st, hook);
+      if (rc) return rc;
+      HIP_TRY(hipEventRecord(s->aux_done, s->aux));
+      HIP_TRY(hipStreamWaitEvent(st, s->aux_done, 0));
+    } else {
+      rc = factor_all(s, 0, nullptr, 0, nv, st);
+      if (rc) return rc;
+    }
+    record(s, 1, st);
+    // symmetric loss + gradient: forward top-down only over the loss support's fronts, then one
+    // combined top-down pass (sym_top_down_pair); otherwise the full forward solve first
+    if (paired) {
       if ((rc = sym_top_down_support(s, rf, st))) return rc;
     } else if ((rc = forward_solve(s, 0, rd, s->X, st, 0))) {
       return rc;
