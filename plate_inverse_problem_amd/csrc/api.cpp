@@ -231,7 +231,7 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     // each (no idle waves at the block barriers); few large fronts -> more waves
     const int64_t wgs = (int64_t)nf * ngroups * pfr::FAC_G;
     const int Wp = (int)std::max<int64_t>(1, std::min<int64_t>(s->level_W[l], (4096 + wgs - 1) / wgs));
-    pfr::launch_factor(s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st);
+    pfr::launch_factor(s->sym, s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st);
     mark(l, 2);
     pfr::launch_offdiag(mode, s->P, s->d_items + s->item_ptr[l], s->item_ptr[l + 1] - s->item_ptr[l], s->d_orec,
                         s->d_oxp + s->item_ptr[l], s->d_ox, ngroups, s->F, s->Fc, s->freqs, s->K, s->M, data, ds,

@@ -211,7 +211,10 @@ __device__ __forceinline__ void col_solve(const cplx* __restrict__ rd, cplx* __r
 // reads are shared by the row groups; workgroup = (front, 64 / FAC_G frequencies), W waves.
 // DIAG = true: only the diagonal block A11 = L11 U11 (rows and columns < ns);
 // L21 and U12 are then formed row / column-wise by k_offdiag_level.
-template <bool DIAG>
+// SYM (symmetric mode, DIAG only): A11 is symmetric, so only its lower triangle is kept up
+// to date -- the trailing updates cover j <= i (half the work and traffic of the LU) -- and
+// U11 = diag(U11) L11^T is written from each L row as it is formed (no pivot-row solves).
+template <bool DIAG, bool SYM>
 __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* __restrict__ lvl,
                                                        cplx* __restrict__ F, int64_t Fc,
                                                        int* __restrict__ flags) {
@@ -237,7 +240,10 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
 #pragma unroll
       for (int i = 0; i < KB; ++i)
 #pragma unroll
-        for (int j = 0; j < KB; ++j) D[i][j] = E(k0 + min(i, kb - 1), k0 + min(j, kb - 1));
+        for (int j = 0; j < KB; ++j) {
+          const int a = k0 + min(i, kb - 1), b = k0 + min(j, kb - 1);
+          D[i][j] = SYM ? E(max(a, b), min(a, b)) : E(a, b);
+        }
 #pragma unroll
       for (int k = 0; k < KB; ++k) {
         if (k < kb) {
@@ -260,6 +266,49 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
       }
     }
     __syncthreads();
+    if (SYM) {
+      // rows i >= k1 of the block columns: L(i, blk) = A(i, blk) U_blk^{-1}, U(blk, i) = diag L(i, blk)^T
+      cplx U[KB][KB];
+      cplx Dg[KB], Dinv[KB];
+#pragma unroll
+      for (int i = 0; i < KB; ++i)
+#pragma unroll
+        for (int j = 0; j < KB; ++j)
+          if (i < j && j < kb) U[i][j] = E(k0 + i, k0 + j);
+#pragma unroll
+      for (int i = 0; i < KB; ++i)
+        if (i < kb) {
+          Dg[i] = E(k0 + i, k0 + i);
+          Dinv[i] = crecip(Dg[i]);
+        }
+      for (int i = k1 + FAC_G * c.w + sub; i < ns; i += FAC_G * c.W) {
+        cplx l[KB];
+#pragma unroll
+        for (int t = 0; t < KB; ++t)
+          if (t < kb) l[t] = E(i, k0 + t);
+#pragma unroll
+        for (int t = 0; t < KB; ++t)
+          if (t < kb) {
+#pragma unroll
+            for (int s = 0; s < KB; ++s)
+              if (s < t) l[t] = cfms(l[t], l[s], U[s][t]);
+            l[t] = cmul(l[t], Dinv[t]);
+            E(i, k0 + t) = l[t];
+            E(k0 + t, i) = cmul(Dg[t], l[t]);
+          }
+      }
+      __syncthreads();
+      // trailing lower triangle: A(i, j) -= L(i, blk) U(blk, j), k1 <= j <= i
+      for (int i = k1 + FAC_G * c.w + sub; i < ns; i += FAC_G * c.W) {
+        cplx l[KB];
+#pragma unroll
+        for (int t = 0; t < KB; ++t)
+          if (t < kb) l[t] = E(i, k0 + t);
+        row_update(base, base, (int64_t)i * f, (int64_t)k0 * f, f, Fc, k1, i + 1, kb, l);
+      }
+      __syncthreads();
+      continue;
+    }
     // pivot rows of the block, columns >= k1:  L11^{-1} A12 (columns over waves)
     {
       cplx L[KB][KB];
@@ -1527,9 +1576,10 @@ void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, cons
   else LAUNCH(k_assemble_level<1>, g, b, st, recs, nrec, xptr, xl, F, Fc, freqs, K, M, data, ds, nvalid);
 }
 
-void launch_factor(const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F, int64_t Fc,
-                   int* flags, hipStream_t st) {
-  LAUNCH(k_factor_level<true>, dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
+void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F,
+                   int64_t Fc, int* flags, hipStream_t st) {
+  if (sym) LAUNCH((k_factor_level<true, true>), dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
+  else LAUNCH((k_factor_level<true, false>), dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
 }
 
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,

@@ -34,7 +34,7 @@ void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPac
 void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, const int2* xl, int ngroups, double2* F,
                      int64_t Fc, const double* freqs, const double2* K, const double* M, const double2* data,
                      int64_t ds, int nvalid, hipStream_t st);
-void launch_factor(const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F, int64_t Fc,
+void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F, int64_t Fc,
                    int* flags, hipStream_t st);
 // Schur complement A22 -= L21 U12 for a level's tile list (TM x TN = 4 x 4 tiles)
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
