@@ -668,7 +668,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
           return out;
         };
         for (int a = 0; a < ns; ++a)
-          for (int b = 0; b < ns; ++b) {
+          for (int b = 0; b < (sym ? a + 1 : ns); ++b) {   // symmetric: A11's lower triangle only
             const int k = (int)(av.size() % 8);
             av.push_back(make_int4((int32_t)(F.off + (int64_t)a * f + b), nzm[(size_t)a * f + b],
                                    s1m[(size_t)a * f + b], 0));
@@ -702,10 +702,11 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     {
       // algorithmic bytes per frequency (16 B per complex entry; index data is
       // shared by all frequencies and not counted)
-      int64_t s_ns2 = 0, s_r2 = 0, s_rns = 0, g_a11 = 0, g_off = 0, g_s = 0;
+      int64_t s_ns2 = 0, s_a11 = 0, s_r2 = 0, s_rns = 0, g_a11 = 0, g_off = 0, g_s = 0;
       for (const Front& F : S.fronts) {
         const int64_t r = F.f - F.ns;
         s_ns2 += (int64_t)F.ns * F.ns;
+        s_a11 += sym ? (int64_t)F.ns * (F.ns + 1) / 2 : (int64_t)F.ns * F.ns;
         s_r2 += sym ? r * (r + 1) / 2 : r * r;
         s_rns += (sym ? 1 : 2) * r * F.ns;
       }
@@ -715,8 +716,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       g_a11 += (int64_t)ax.size();
       g_off += (int64_t)ox.size();
       g_s += (int64_t)gxp.back();                          // gx may hold a placeholder
-      s->alg_bytes[0] = 16 * (s_ns2 + g_a11);             // A11 stores + child entries gathered
-      s->alg_bytes[1] = 16 * 2 * s_ns2;                   // A11 read + L11/U11 write
+      s->alg_bytes[0] = 16 * (s_a11 + g_a11);             // A11 (symmetric: lower) stores + child entries gathered
+      s->alg_bytes[1] = 16 * (s_a11 + s_ns2);             // A11 read + L11/U11 write
       s->alg_bytes[2] = 16 * (s_rns + g_off + s_ns2);     // L21/U12 stores + gathered children + L11/U11 read
       s->alg_bytes[3] = 16 * (s_r2 + g_s + s_rns);        // A22 stores + gathered children + L21/U12 read
     }
