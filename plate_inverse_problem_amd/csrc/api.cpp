@@ -68,6 +68,12 @@ struct pfr_solver {
   int32_t* d_gxp = nullptr;             // per super-tile: range of further sources in d_gx
   int2* d_gx = nullptr;                 // (lane group * 16 + position, element id) of the rare extra sources
   std::vector<int32_t> tile_ptr;
+  // symmetric mode, fronts with large update blocks: 16 x 16 Schur blocks (k_schur_sym_blk)
+  int4* d_blocks = nullptr;             // (front, i0, j0, 0), grouped by level
+  int32_t* d_bg1 = nullptr;             // per block, wave, position: first child source (or -1)
+  int32_t* d_bgxp = nullptr;            // per block: range of further sources in d_bgx
+  int2* d_bgx = nullptr;                // (wave * 16 + position, element id)
+  std::vector<int32_t> blk_ptr;
   int4* d_asm = nullptr;                // panel-entry assembly records (dst, nz, first child source, 0), by level
   int32_t* d_asm_xp = nullptr;          // per 8-record chunk: range of further child sources in d_asm_x
   int2* d_asm_x = nullptr;              // (record within chunk, child element id)
@@ -243,6 +249,9 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
                       s->d_gxp + s->tile_ptr[l],
                       s->d_gx, ngroups, s->F,
                       s->Fc, st);
+    pfr::launch_schur_blk(s->P, s->d_blocks + s->blk_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
+                          s->d_bg1 + (int64_t)s->blk_ptr[l] * 256, s->d_bgxp + s->blk_ptr[l], s->d_bgx, ngroups, s->F,
+                          s->Fc, st);
     mark(l, 4);
   }
   HIP_TRY(hipGetLastError());
@@ -547,6 +556,13 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     std::vector<int32_t> g1, gxp(1, 0);
     std::vector<int2> gx;
     s->tile_ptr.assign(1, 0);
+    std::vector<int4> bv;
+    std::vector<int32_t> bg1, bgxp(1, 0);
+    std::vector<int2> bgx;
+    s->blk_ptr.assign(1, 0);
+    // update blocks of at least this many rows go to the 16 x 16 block kernel (symmetric mode)
+    const char* be = getenv("PFR_SCHUR_BLK_MIN");
+    const int blk_min = be ? atoi(be) : 32;
     const int L = (int)S.level_ptr.size() - 1;
     for (int l = 0; l < L; ++l) {
       for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
@@ -576,6 +592,28 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
           }
         }
         std::sort(more.begin(), more.end());
+        if (sym && blk_min > 0 && r >= blk_min) {
+          // 16 x 16 blocks touching the lower triangle; wave w owns the 4 x 4 tile (w / 4, w % 4)
+          constexpr int B = pfr::SCHUR_BLK;
+          for (int i0 = 0; i0 < r; i0 += B)
+            for (int j0 = 0; j0 <= i0; j0 += B) {
+              bv.push_back(make_int4(t, i0, j0, 0));
+              for (int w = 0; w < 16; ++w)
+                for (int pos = 0; pos < 16; ++pos) {
+                  const int i = i0 + 4 * (w / 4) + pos / 4, j = j0 + 4 * (w % 4) + pos % 4;
+                  if (i >= r || j > i) {
+                    bg1.push_back(-1);
+                    continue;
+                  }
+                  bg1.push_back(first[(size_t)i * r + j]);
+                  auto lo = std::lower_bound(more.begin(), more.end(), std::make_pair(i * r + j, INT32_MIN));
+                  for (; lo != more.end() && lo->first == i * r + j; ++lo)
+                    bgx.push_back(make_int2(w * 16 + pos, lo->second));
+                }
+              bgxp.push_back((int32_t)bgx.size());
+            }
+          continue;
+        }
         // super-tiles of (SCHUR_TM SCHUR_SR) x (SCHUR_TN SCHUR_SC): lane group `sub` owns the
         // SCHUR_TM x SCHUR_TN tile at (TM (sub / SC), TN (sub % SC)); per super-tile the dense
         // first-source ids (-1 = none), lane group by lane group, then one overflow range
@@ -605,10 +643,15 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
         }
       }
       s->tile_ptr.push_back((int32_t)tv.size());
+      s->blk_ptr.push_back((int32_t)bv.size());
     }
     if (gx.empty()) gx.push_back(make_int2(0, 0));   // keep the buffers non-null
+    if (bv.empty()) bv.push_back(make_int4(0, 0, 0, 0));
+    if (bg1.empty()) bg1.push_back(-1);
+    if (bgx.empty()) bgx.push_back(make_int2(0, 0));
     if ((rc = s->up(&s->d_tiles, tv)) || (rc = s->up(&s->d_g1, g1)) || (rc = s->up(&s->d_gxp, gxp)) ||
-        (rc = s->up(&s->d_gx, gx)))
+        (rc = s->up(&s->d_gx, gx)) || (rc = s->up(&s->d_blocks, bv)) || (rc = s->up(&s->d_bg1, bg1)) ||
+        (rc = s->up(&s->d_bgxp, bgxp)) || (rc = s->up(&s->d_bgx, bgx)))
       return bail(rc);
     // assembly of the panel region (pivot rows: all columns; update rows: pivot
     // columns) as a gather: one record per entry = original matrix entry (or -1)
@@ -713,6 +756,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       for (const int4& a : av) g_a11 += a.z >= 0;
       for (const int2& o : orec) g_off += o.y >= 0;
       for (int32_t g : g1) g_s += g >= 0;
+      for (int32_t g : bg1) g_s += g >= 0;
+      g_s += (int64_t)bgxp.back();
       g_a11 += (int64_t)ax.size();
       g_off += (int64_t)ox.size();
       g_s += (int64_t)gxp.back();                          // gx may hold a placeholder
@@ -866,7 +911,8 @@ int pfr_last_kernel_timings(const pfr_solver* s, double* ms, int64_t* launches) 
     if (!s->tev[c].used[0]) continue;
     for (int l = 0; l < L; ++l) {
       const int work[4] = {s->asm_ptr[l + 1] - s->asm_ptr[l], s->level_ptr[l + 1] - s->level_ptr[l],
-                           s->item_ptr[l + 1] - s->item_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l]};
+                           s->item_ptr[l + 1] - s->item_ptr[l],
+                           s->tile_ptr[l + 1] - s->tile_ptr[l] + s->blk_ptr[l + 1] - s->blk_ptr[l]};
       for (int k = 0; k < 4; ++k) {
         float m = 0;
         HIP_TRY(hipEventElapsedTime(&m, s->tev[c].kev[5 * l + k], s->tev[c].kev[5 * l + k + 1]));

@@ -61,6 +61,7 @@ constexpr int OFF_RPL = PFR_OFF_RPL;
 
 // Largest front the solve kernels stage index lists for in LDS (checked at solver creation)
 constexpr int MAX_FRONT = 1024;
+constexpr int SCHUR_BLK = 16;   // k_schur_sym_blk block edge (16 waves x 4 x 4 tiles)
 
 constexpr int COEF_MAX = 32;
 struct CoefPack {

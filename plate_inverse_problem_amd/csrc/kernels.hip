@@ -681,6 +681,145 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PFR_SCHUR_W
   schur_tile<true, true, KU>(P, tiles, ntiles, g1, gxp, gx, F, Fc);
 }
 
+// Symmetric mode, large update blocks (r >= PFR_SCHUR_BLK_MIN rows): a workgroup = 16 waves
+// forms one 16 x 16 block of A22's lower triangle for 64 frequencies (lane = frequency), wave w
+// the 4 x 4 tile (w / 4, w % 4).  Per stage of BKC pivots the block's 16 row operands L21(i, k),
+// 16 column operands L21(j, k) and the pivots U(k, k) are copied once into LDS by global->LDS
+// loads (no staging registers), double-buffered: stage s + 1 is in flight while stage s is
+// multiplied.  Per pivot step that is 33 1-KiB loads for the block instead of 16 x 9 for 16
+// independent 4 x 4 tiles -- the tile kernel is bound by its L2 operand traffic, not by HBM.
+constexpr int BROWS = 2 * SCHUR_BLK + 1;     // rows per pivot: 16 row operands, 16 column operands, U(k, k)
+
+// global -> LDS copy of one 1 KiB row (lane l's 16 B to lds_row + 16 l), issued as inline asm so
+// that the compiler's wait insertion does not see it: with the builtin it waits vmcnt(0) before
+// every LDS read of the staging array (the copies in flight might alias), which serialises the
+// pipeline.  Every wait on these copies is therefore explicit (PFR_WAIT_VM).
+__device__ __forceinline__ void glds16(const cplx* g, cplx* lds_row) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds_row);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(dst)
+               : "memory");
+}
+
+// s_waitcnt vmcnt(n) alone (expcnt / lgkmcnt left at their no-wait maxima; gfx9 encoding)
+#define PFR_WAIT_VM(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | (7 << 4) | (15 << 8))
+
+// NB LDS buffers of KC pivots each.  NB = 2: plain double buffering, one __syncthreads per
+// stage (it drains the next stage's copies).  NB >= 3: the copies of NB - 1 stages ahead stay in
+// flight across a raw s_barrier, each stage retired by a counted vmcnt.
+template <int NB, int KC>
+__global__ __launch_bounds__(1024) void k_schur_sym_blk(DevPattern P, const int4* __restrict__ blocks, int nblocks,
+                                                         const int* __restrict__ bg1, const int* __restrict__ bgxp,
+                                                         const int2* __restrict__ bgx, cplx* __restrict__ F,
+                                                         int64_t Fc) {
+  __shared__ cplx sop[NB][KC][BROWS][64];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
+  const int bid = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
+  if (bid >= nblocks) return;                // whole workgroup: uniform
+  const int64_t q = (int64_t)by * 64 + lane;
+  const int4 bk = blocks[bid];
+  const Front fr = P.fronts[bk.x];
+  const int f = fr.f, ns = fr.ns, r = f - ns;
+  cplx* __restrict__ base = F + fr.off * Fc + q;
+  const int ti = 4 * (w >> 2), tj = 4 * (w & 3);
+  // the tile holds a lower-triangle entry inside the update block
+  const bool active = bk.y + ti < r && bk.y + ti + 3 >= bk.z + tj;
+  cplx acc[4][4];
+  if (active) {
+    const int4* __restrict__ g4 = reinterpret_cast<const int4*>(bg1 + ((int64_t)bid * 16 + w) * 16);
+    int src[16];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int4 v = g4[u];
+      src[4 * u] = v.x;
+      src[4 * u + 1] = v.y;
+      src[4 * u + 2] = v.z;
+      src[4 * u + 3] = v.w;
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int e = src[m * 4 + n];
+        const cplx v = F[(int64_t)max(e, 0) * Fc + q];
+        acc[m][n] = e >= 0 ? v : make_double2(0.0, 0.0);
+      }
+    const int x1 = bgxp[bid + 1];
+    for (int x = bgxp[bid]; x < x1; ++x) {
+      const int2 g = bgx[x];
+      if (g.x / 16 == w) {
+        const cplx v = F[(int64_t)g.y * Fc + q];
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int n = 0; n < 4; ++n)
+            if (g.x % 16 == m * 4 + n) acc[m][n] = cadd(acc[m][n], v);
+      }
+    }
+  }
+  // stage copy: row slot rho of pivot u: rho < 16 -> L21 row i0 + rho, rho < 32 -> L21 row
+  // j0 + rho - 16, rho = 32 -> U(k, k); wave w copies slots w and w + 16 of every pivot, wave u
+  // the pivot of step u.  Rows past the block and pivots past ns read clamped (valid) addresses.
+  const cplx* ra = base + ((int64_t)(ns + min(bk.y + w, r - 1)) * f) * Fc;
+  const cplx* rb = base + ((int64_t)(ns + min(bk.z + w, r - 1)) * f) * Fc;
+  auto stage = [&](int buf, int k0) {
+#pragma unroll
+    for (int u = 0; u < KC; ++u) {
+      const int k = max(min(k0 + u, ns - 1), 0);
+      if (w == u) glds16(base + (int64_t)k * (f + 1) * Fc, &sop[buf][u][2 * SCHUR_BLK][0]);
+      glds16(ra + (int64_t)k * Fc, &sop[buf][u][w][0]);
+      glds16(rb + (int64_t)k * Fc, &sop[buf][u][SCHUR_BLK + w][0]);
+    }
+  };
+  auto compute = [&](int buf, int k0) {
+    if (!active) return;
+#pragma unroll
+    for (int u = 0; u < KC; ++u) {
+      if (k0 + u < ns) {
+        const cplx d = sop[buf][u][2 * SCHUR_BLK][lane];
+        cplx a[4], b[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) a[m] = cmul(sop[buf][u][ti + m][lane], d);
+#pragma unroll
+        for (int n = 0; n < 4; ++n) b[n] = sop[buf][u][SCHUR_BLK + tj + n][lane];
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int n = 0; n < 4; ++n) acc[m][n] = cfms(acc[m][n], a[m], b[n]);
+      }
+    }
+  };
+  const int nst = (ns + KC - 1) / KC;
+  PFR_WAIT_VM(0);                      // the gathers above (ordinary loads) out of the count
+  // prologue: stages 0 .. NB - 2 in flight (stages past nst copy clamped rows, never read)
+#pragma unroll
+  for (int p = 0; p < NB - 1; ++p) stage(p, p * KC);
+  for (int st = 0; st < nst; ++st) {
+    // retire stage st: NB - 2 later stages may stay in flight (2 KC copies per wave and stage;
+    // waves 0 .. KC-1 issue their pivot copy first and one more per stage, so they wait for a
+    // copy or two more than needed)
+    PFR_WAIT_VM((NB - 2) * 2 * KC);
+    __builtin_amdgcn_s_barrier();   // stage st visible to all; everyone done with stage st - 1
+    stage((st + NB - 1) % NB, (st + NB - 1) * KC);
+    compute(st % NB, st * KC);
+  }
+  PFR_WAIT_VM(0);
+  if (active) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int i = bk.y + ti + m, j = bk.z + tj + n;
+        if (i < r && j <= i) base[((int64_t)(ns + i) * f + ns + j) * Fc] = acc[m][n];
+      }
+  }
+}
+
 // ------------------------------------------------------------------ right-hand sides
 // RHS 0: b_p = rhsP[p] * (beta0 - omega^2 * mass_sum)   (Problem.py:447-449)
 // RHS 1: b_p = B[q * b_stride + perm[p]]                 (explicit batch)
@@ -1565,6 +1704,20 @@ void launch_schur(bool sym, const DevPattern& P, const int4* tiles, int ntiles, 
   if (sym && ku == 1) LAUNCH(k_schur_sym_level<1>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
   else if (sym) LAUNCH(k_schur_sym_level<2>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
   else LAUNCH(k_schur_level, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
+}
+
+void launch_schur_blk(const DevPattern& P, const int4* blocks, int nblocks, const int* bg1, const int* bgxp,
+                      const int2* bgx, int ngroups, double2* F, int64_t Fc, hipStream_t st) {
+  if (nblocks <= 0) return;
+  static const int cfg = [] {
+    const char* e = getenv("PFR_SCHUR_BLK_CFG");   // tuning knob: buffers x 10 + pivots per stage
+    return e ? atoi(e) : 41;
+  }();
+  const dim3 g(nblocks, ngroups), b(1024);
+  if (cfg == 31) LAUNCH((k_schur_sym_blk<3, 1>), g, b, st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
+  else if (cfg == 41) LAUNCH((k_schur_sym_blk<4, 1>), g, b, st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
+  else if (cfg == 21) LAUNCH((k_schur_sym_blk<2, 1>), g, b, st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
+  else LAUNCH((k_schur_sym_blk<2, 2>), g, b, st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
 }
 
 void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, const int2* xl, int ngroups, double2* F,
