@@ -562,7 +562,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     s->blk_ptr.assign(1, 0);
     // update blocks of at least this many rows go to the 16 x 16 block kernel (symmetric mode)
     const char* be = getenv("PFR_SCHUR_BLK_MIN");
-    const int blk_min = be ? atoi(be) : 32;
+    const int blk_min = be ? atoi(be) : 24;
     const int L = (int)S.level_ptr.size() - 1;
     for (int l = 0; l < L; ++l) {
       for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {

@@ -82,3 +82,14 @@ def test_explicit_solve_refused_on_symmetric_solver():
     x = torch.zeros_like(b)
     with pytest.raises(_native.NativeError, match="general analysis"):
         eng.solver.solve(torch.view_as_real(data), nnz, torch.view_as_real(b), n, torch.view_as_real(x), False, 1)
+
+
+@pytest.mark.parametrize("blk_min", ["0", "4", "24"])
+def test_schur_kernel_split_matches_oracle(blk_min, monkeypatch):
+    """Symmetric Schur complement through the 4 x 4 tile kernel alone (PFR_SCHUR_BLK_MIN=0),
+    the 16 x 16 LDS block kernel for almost every front (4) and the default split (24)."""
+    monkeypatch.setenv("PFR_SCHUR_BLK_MIN", blk_min)
+    p = make_problem("orthotropic", ny=6, device="cuda:0")
+    freqs = np.linspace(40.0, 600.0, 130)
+    fr = p.solveForward(freqs)
+    assert _rel(fr, oracle_for(p).fr(freqs, p.parameters)) < FR_RTOL
