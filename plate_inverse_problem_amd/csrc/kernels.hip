@@ -862,20 +862,79 @@ __device__ __forceinline__ cplx rhs_value(const DevPattern& P, const RhsArgs& R,
 // Gather the frontal vector: pivot rows from the rhs, plus children's update vectors.
 // reach (per front, may be NULL): fronts whose update vector can be non-zero for this right-hand
 // side (the RHS support and its elimination-tree ancestors); others' stale vectors are skipped.
+// The index chains (row -> child entries -> child front -> reach; row -> permuted index -> rhs
+// scalars) are resolved first by all threads at once into LDS, so the row loop issues only the
+// value loads (each row's chain walked by one wave cost several dependent memory round trips).
+constexpr int GATHER_CAP = 4096;    // child entries per front staged in LDS (more: direct path)
+
+template <int RHS>
+__device__ __forceinline__ cplx rhs_staged(const RhsArgs& R, int p, double rv, int cs, double om2, int64_t q,
+                                           int64_t Fc) {
+  if (RHS == 0 || RHS == 3) {
+    cplx b = make_double2(0.0, 0.0);
+    if (rv != 0.0) b = make_double2(rv * fma(-om2, R.mass_sum, R.beta_re), rv * R.beta_im);
+    if (RHS == 3 && cs >= 0) b = cadd(b, R.Bc[(int64_t)cs * Fc + q]);
+    return b;
+  } else if (RHS == 1) {
+    return R.B[min(q, (int64_t)R.nvalid - 1) * R.b_stride + p];    // p = perm[idx] here
+  } else {
+    return R.G[(int64_t)p * Fc + q];
+  }
+}
+
 template <int RHS>
 __device__ __forceinline__ void gather_frontal(const DevPattern& P, const Front& fr, const RhsArgs& R,
                                                cplx* __restrict__ WV, int64_t Fc, const Ctx& c,
                                                const int* __restrict__ reach) {
-  for (int a = c.w; a < fr.f; a += c.W) {
-    const int r = fr.row0 + a;
-    cplx v = make_double2(0.0, 0.0);
-    if (a < fr.ns) v = rhs_value<RHS>(P, R, P.idx[r], c.q, Fc);
-    const int x1 = P.ea_ptr[r + 1];
-    for (int e = P.ea_ptr[r]; e < x1; ++e) {
-      const int src = P.ea_src[e];
-      if (!reach || reach[P.row_front[src]]) v = cadd(v, WV[(int64_t)src * Fc + c.q]);
+  __shared__ int s_ptr[MAX_FRONT + 1];
+  __shared__ int s_src[GATHER_CAP];
+  __shared__ int s_p[MAX_FRONT];
+  __shared__ double s_rv[MAX_FRONT];
+  __shared__ int s_cs[MAX_FRONT];
+  const int f = fr.f, ns = fr.ns;
+  const int E0 = P.ea_ptr[fr.row0], nE = P.ea_ptr[fr.row0 + f] - E0;
+  if (nE > GATHER_CAP) {
+    for (int a = c.w; a < f; a += c.W) {
+      const int r = fr.row0 + a;
+      cplx v = make_double2(0.0, 0.0);
+      if (a < fr.ns) v = rhs_value<RHS>(P, R, P.idx[r], c.q, Fc);
+      const int x1 = P.ea_ptr[r + 1];
+      for (int e = P.ea_ptr[r]; e < x1; ++e) {
+        const int src = P.ea_src[e];
+        if (!reach || reach[P.row_front[src]]) v = cadd(v, WV[(int64_t)src * Fc + c.q]);
+      }
+      WV[(int64_t)r * Fc + c.q] = v;
     }
-    WV[(int64_t)r * Fc + c.q] = v;
+    return;
+  }
+  for (int t = threadIdx.x; t <= f; t += blockDim.x) s_ptr[t] = P.ea_ptr[fr.row0 + t] - E0;
+  for (int t = threadIdx.x; t < nE; t += blockDim.x) {
+    const int src = P.ea_src[E0 + t];
+    s_src[t] = (!reach || reach[P.row_front[src]]) ? src : -1;
+  }
+  for (int t = threadIdx.x; t < ns; t += blockDim.x) {
+    const int p = P.idx[fr.row0 + t];
+    s_p[t] = RHS == 1 ? P.perm[p] : p;
+    if (RHS == 0 || RHS == 3) s_rv[t] = R.rhsP[p];
+    if (RHS == 3) s_cs[t] = R.cslot[p];
+  }
+  double om2 = 0.0;
+  if (RHS == 0 || RHS == 3) {
+    const double om = 6.283185307179586 * R.freqs[c.q];
+    om2 = om * om;
+  }
+  __syncthreads();
+  for (int a = c.w; a < f; a += c.W) {
+    cplx v = make_double2(0.0, 0.0);
+    if (a < ns)
+      v = rhs_staged<RHS>(R, __builtin_amdgcn_readfirstlane(s_p[a]), s_rv[a], __builtin_amdgcn_readfirstlane(s_cs[a]),
+                          om2, c.q, Fc);
+    const int x0 = __builtin_amdgcn_readfirstlane(s_ptr[a]), x1 = __builtin_amdgcn_readfirstlane(s_ptr[a + 1]);
+    for (int e = x0; e < x1; ++e) {
+      const int src = __builtin_amdgcn_readfirstlane(s_src[e]);
+      if (src >= 0) v = cadd(v, WV[(int64_t)src * Fc + c.q]);
+    }
+    WV[(int64_t)(fr.row0 + a) * Fc + c.q] = v;
   }
 }
 
