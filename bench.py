@@ -14,10 +14,11 @@ forward + adjoint (loss + gradient), fp64.
 * each GPU runs ``lanes`` (default 2) solvers on their own HIP streams over
   contiguous halves of its frequencies, concurrently (one lane's latency-bound
   top levels overlap the other's bandwidth-bound ones);
-* ``roofline``: the dominant kernel, ``k_schur_level`` (Schur complement of the
-  multifrontal factorisation; HBM-bound): algorithmic bytes per launch (the
-  solver's count: A22 stores + gathered children's entries + L21/U12 read once,
-  16 B per complex entry) / average launch time, from HIP events that libpfr
+* ``roofline``: the dominant kernel class by device time -- at C3 ``k_schur_sym_blk``
+  (Schur complement of the large update blocks of the multifrontal factorisation;
+  HBM-bound): algorithmic bytes per launch (the solver's count: A22 stores +
+  gathered children's entries + L21 read once, 16 B per complex entry) / average
+  launch time, from HIP events that libpfr
   records around every launch on the lane's stream during one isolated lane-0
   sweep of a full chunk right after the timed region (inside the timed region the
   lanes overlap, so a launch's duration there also contains the other lane's
@@ -48,9 +49,12 @@ sys.path.insert(0, REPO)
 FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector/matrix (spec; MI355X_MICROARCH.md lists no fp64 row)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 PMC_FILE = os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")
-# kernel classes of the factorisation (libpfr per-class HIP-event timings); the rocprof kernel names
-# of a class start with its prefix (the Schur class has per-level variants)
-KERNELS = ("k_assemble_level", "k_factor_level", "k_offdiag_level", "k_schur")
+# kernel classes of the factorisation (libpfr per-class HIP-event timings, pfr_last_kernel_timings
+# order); the rocprof names of a class's kernels start with one of its prefixes
+KERNELS = (("k_assemble_level",), ("k_factor_level",), ("k_offdiag_level",), ("k_schur_sym_blk",),
+           ("k_schur_level", "k_schur_sym_level"))
+KERNEL_NAMES = ("k_assemble_level", "k_factor_level", "k_offdiag_level", "k_schur_sym_blk",
+                "k_schur_sym_level / k_schur_level")
 
 
 def pmc_traffic(chunk, symmetric):
@@ -58,10 +62,10 @@ def pmc_traffic(chunk, symmetric):
     try:
         d = json.load(open(PMC_FILE))
     except (OSError, ValueError):
-        return [None] * 4
+        return [None] * len(KERNELS)
     out = []
     if d.get("factorisation") != ("symmetric" if symmetric else "general"):
-        return [None] * 4
+        return [None] * len(KERNELS)
     for k in KERNELS:
         es = [e for name, e in d["kernels"].items() if name.startswith(k)]
         if not es:
@@ -148,8 +152,8 @@ def main():
     if world > 1:
         dist.barrier()
     phase = np.zeros(5)
-    kms = np.zeros(4)
-    klaunch = np.zeros(4)
+    kms = np.zeros(len(KERNELS))
+    klaunch = np.zeros(len(KERNELS))
     t0 = time.perf_counter()
     for _ in range(args.steps):
         val, grad = step()
@@ -195,12 +199,14 @@ def main():
     alg_launch = alg_f * n_iso / np.maximum(iso_n, 1)
     ms_launch = iso_ms / np.maximum(iso_n, 1)
     gbs = alg_launch / (ms_launch * 1e-3) / 1e9
-    kernels = KERNELS
+    kernels = KERNEL_NAMES
     traffic = pmc_traffic(chunk, eng.symmetric)
+    dom = int(np.argmax(iso_ms))                         # the dominant kernel class
     fact_alg = float(alg_f.sum() * n_iso)
     fact_ms = float(iso_ms.sum())
     fact_tfs = st["factor_flops"] * n_iso / (iso_phase[0] * 1e-3) / 1e12
-    fact_traffic = None if None in traffic else float(np.dot(traffic, iso_n))
+    fact_traffic = None if any(t is None and n > 0 for t, n in zip(traffic, iso_n)) else \
+        float(sum(t * n for t, n in zip(traffic, iso_n) if n > 0))
     # solve pairs: bottom-up pass over the fronts the rhs support reaches + full top-down pass
     # (libpfr's count of factor entries read once, 16 B each, plus rhs in / solution out)
     trsv_bytes = n_iso * float(solver.solve_bytes().sum())
@@ -229,12 +235,12 @@ def main():
                    "nnz_lu": st["nnz_lu"], "factor_gflop_per_freq": st["factor_flops"] / 1e9,
                    "parallelism": f"frequency shards x{world} + 1 all-reduce/step; {eng.n_lanes} concurrent "
                                   "solver lanes (HIP streams) per GPU"},
-        "roofline": {"bound": "hbm", "kernel": kernels[3], "achieved": gbs[3], "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": gbs[3] / HBM_PEAK_GBS, "traffic": traffic[3],
-                     "alg_bytes_per_launch": alg_launch[3], "avg_launch_ms": ms_launch[3],
-                     "launches": int(iso_n[3]), "measured": f"isolated lane-0 sweep of {n_iso} frequencies "
+        "roofline": {"bound": "hbm", "kernel": kernels[dom], "achieved": gbs[dom], "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": gbs[dom] / HBM_PEAK_GBS, "traffic": traffic[dom],
+                     "alg_bytes_per_launch": alg_launch[dom], "avg_launch_ms": ms_launch[dom],
+                     "launches": int(iso_n[dom]), "measured": f"isolated lane-0 sweep of {n_iso} frequencies "
                      "(one chunk) after the timed region, HIP events per launch",
-                     "concurrent_avg_launch_ms": conc_launch[3]},
+                     "concurrent_avg_launch_ms": conc_launch[dom]},
         "factor_roofline": {"bound": "hbm", "kernels": list(kernels), "ms": iso_ms.tolist(),
                             "alg_GBps": gbs.tolist(), "achieved": fact_alg / (fact_ms * 1e-3) / 1e9,
                             "peak": HBM_PEAK_GBS, "unit": "GB/s",

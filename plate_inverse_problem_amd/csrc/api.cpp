@@ -141,7 +141,7 @@ struct pfr_solver {
   int timing = 0;
   std::vector<ChunkEvents> tev;
   int n_tev = 0;                        // chunks recorded by the last call
-  int64_t alg_bytes[4]{};               // algorithmic HBM bytes per frequency of each class (one sweep)
+  int64_t alg_bytes[5]{};               // algorithmic HBM bytes per frequency of each class (one sweep)
 
   ~pfr_solver() {
     for (auto e : lev_ev) (void)hipEventDestroy(e);
@@ -194,7 +194,7 @@ int begin_chunk(pfr_solver* s) {
     for (auto& e : s->tev.back().ev) HIP_TRY(hipEventCreate(&e));
   }
   auto& c = s->tev[s->n_tev];
-  const size_t nk = 5 * (s->level_ptr.size() - 1);
+  const size_t nk = 6 * (s->level_ptr.size() - 1);
   while ((s->timing & 2) && c.kev.size() < nk) {
     hipEvent_t e;
     HIP_TRY(hipEventCreate(&e));
@@ -224,7 +224,7 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
   const bool kt = (s->timing & 2) && s->n_tev < (int)s->tev.size() && !s->tev[s->n_tev].kev.empty();
   hipEvent_t* kev = kt ? s->tev[s->n_tev].kev.data() : nullptr;
   auto mark = [&](int l, int c) {
-    if (kt) (void)hipEventRecord(kev[5 * l + c], st);
+    if (kt) (void)hipEventRecord(kev[6 * l + c], st);
   };
   for (int l = 0; l < L; ++l) {
     int nf = s->level_ptr[l + 1] - s->level_ptr[l];
@@ -244,15 +244,16 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
                         nvalid, st);
     if (after_panel) after_panel(l);
     mark(l, 3);
+    pfr::launch_schur_blk(s->P, s->d_blocks + s->blk_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
+                          s->d_bg1 + (int64_t)s->blk_ptr[l] * 256, s->d_bgxp + s->blk_ptr[l], s->d_bgx, ngroups, s->F,
+                          s->Fc, st);
+    mark(l, 4);
     pfr::launch_schur(s->sym, s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l],
                       s->d_g1 + (int64_t)s->tile_ptr[l] * pfr::SCHUR_TM * pfr::SCHUR_TN * pfr::SCHUR_SR * pfr::SCHUR_SC,
                       s->d_gxp + s->tile_ptr[l],
                       s->d_gx, ngroups, s->F,
                       s->Fc, st);
-    pfr::launch_schur_blk(s->P, s->d_blocks + s->blk_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
-                          s->d_bg1 + (int64_t)s->blk_ptr[l] * 256, s->d_bgxp + s->blk_ptr[l], s->d_bgx, ngroups, s->F,
-                          s->Fc, st);
-    mark(l, 4);
+    mark(l, 5);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -541,6 +542,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       (rc = s->up(&ep, S.ea_ptr)) || (rc = s->up(&es, S.ea_src)) || (rc = s->up(&pm, S.perm)) ||
       (rc = s->up(&pr, S.prow)) || (rc = s->up(&pc, S.pcol)) || (rc = s->up(&s->d_level_fronts, S.level_fronts)))
     return bail(rc);
+  std::vector<char> blk_front(S.fronts.size(), 0);   // front's Schur complement by the block kernel
   {
     // Schur-complement tiles (4 x 4) of every front's update block, level by level
     // plus, per tile and tile position, the children's update-matrix entries that
@@ -612,6 +614,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
                 }
               bgxp.push_back((int32_t)bgx.size());
             }
+          blk_front[t] = 1;
           continue;
         }
         // super-tiles of (SCHUR_TM SCHUR_SR) x (SCHUR_TN SCHUR_SC): lane group `sub` owns the
@@ -745,26 +748,31 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     {
       // algorithmic bytes per frequency (16 B per complex entry; index data is
       // shared by all frequencies and not counted)
-      int64_t s_ns2 = 0, s_a11 = 0, s_r2 = 0, s_rns = 0, g_a11 = 0, g_off = 0, g_s = 0;
-      for (const Front& F : S.fronts) {
+      int64_t s_ns2 = 0, s_a11 = 0, s_r2[2] = {0, 0}, s_rns = 0, s_rns2[2] = {0, 0}, g_a11 = 0, g_off = 0;
+      int64_t g_s[2] = {0, 0};   // [0] block kernel, [1] tile kernel
+      for (size_t t = 0; t < S.fronts.size(); ++t) {
+        const Front& F = S.fronts[t];
         const int64_t r = F.f - F.ns;
+        const int k = blk_front[t] ? 0 : 1;
         s_ns2 += (int64_t)F.ns * F.ns;
         s_a11 += sym ? (int64_t)F.ns * (F.ns + 1) / 2 : (int64_t)F.ns * F.ns;
-        s_r2 += sym ? r * (r + 1) / 2 : r * r;
+        s_r2[k] += sym ? r * (r + 1) / 2 : r * r;
         s_rns += (sym ? 1 : 2) * r * F.ns;
+        s_rns2[k] += (sym ? 1 : 2) * r * F.ns;
       }
       for (const int4& a : av) g_a11 += a.z >= 0;
       for (const int2& o : orec) g_off += o.y >= 0;
-      for (int32_t g : g1) g_s += g >= 0;
-      for (int32_t g : bg1) g_s += g >= 0;
-      g_s += (int64_t)bgxp.back();
+      for (int32_t g : g1) g_s[1] += g >= 0;
+      for (int32_t g : bg1) g_s[0] += g >= 0;
+      g_s[0] += (int64_t)bgxp.back();
       g_a11 += (int64_t)ax.size();
       g_off += (int64_t)ox.size();
-      g_s += (int64_t)gxp.back();                          // gx may hold a placeholder
+      g_s[1] += (int64_t)gxp.back();                       // gx may hold a placeholder
       s->alg_bytes[0] = 16 * (s_a11 + g_a11);             // A11 (symmetric: lower) stores + child entries gathered
       s->alg_bytes[1] = 16 * (s_a11 + s_ns2);             // A11 read + L11/U11 write
       s->alg_bytes[2] = 16 * (s_rns + g_off + s_ns2);     // L21/U12 stores + gathered children + L11/U11 read
-      s->alg_bytes[3] = 16 * (s_r2 + g_s + s_rns);        // A22 stores + gathered children + L21/U12 read
+      for (int k = 0; k < 2; ++k)                         // A22 stores + gathered children + L21/U12 read
+        s->alg_bytes[3 + k] = 16 * (s_r2[k] + g_s[k] + s_rns2[k]);
     }
     if (av.empty()) av.assign(8, make_int4(-1, -1, -1, 0));
     if (ax.empty()) ax.push_back(make_int2(0, 0));
@@ -900,7 +908,7 @@ int pfr_last_timings(const pfr_solver* s, double* ms) {
 
 int pfr_last_kernel_timings(const pfr_solver* s, double* ms, int64_t* launches) {
   if (!s || !ms) return fail(PFR_ERR_ARG, "null argument");
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 5; ++i) {
     ms[i] = 0.0;
     if (launches) launches[i] = 0;
   }
@@ -910,12 +918,12 @@ int pfr_last_kernel_timings(const pfr_solver* s, double* ms, int64_t* launches) 
   for (int c = 0; c < s->n_tev; ++c) {
     if (!s->tev[c].used[0]) continue;
     for (int l = 0; l < L; ++l) {
-      const int work[4] = {s->asm_ptr[l + 1] - s->asm_ptr[l], s->level_ptr[l + 1] - s->level_ptr[l],
-                           s->item_ptr[l + 1] - s->item_ptr[l],
-                           s->tile_ptr[l + 1] - s->tile_ptr[l] + s->blk_ptr[l + 1] - s->blk_ptr[l]};
-      for (int k = 0; k < 4; ++k) {
+      const int work[5] = {s->asm_ptr[l + 1] - s->asm_ptr[l], s->level_ptr[l + 1] - s->level_ptr[l],
+                           s->item_ptr[l + 1] - s->item_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
+                           s->tile_ptr[l + 1] - s->tile_ptr[l]};
+      for (int k = 0; k < 5; ++k) {
         float m = 0;
-        HIP_TRY(hipEventElapsedTime(&m, s->tev[c].kev[5 * l + k], s->tev[c].kev[5 * l + k + 1]));
+        HIP_TRY(hipEventElapsedTime(&m, s->tev[c].kev[6 * l + k], s->tev[c].kev[6 * l + k + 1]));
         ms[k] += m;
         if (launches) launches[k] += work[k] > 0;    // empty classes launch nothing
       }
@@ -926,7 +934,7 @@ int pfr_last_kernel_timings(const pfr_solver* s, double* ms, int64_t* launches) 
 
 int pfr_solver_alg_bytes(const pfr_solver* s, int64_t* bytes) {
   if (!s || !bytes) return fail(PFR_ERR_ARG, "null argument");
-  for (int i = 0; i < 4; ++i) bytes[i] = s->alg_bytes[i];
+  for (int i = 0; i < 5; ++i) bytes[i] = s->alg_bytes[i];
   return PFR_OK;
 }
 

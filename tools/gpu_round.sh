@@ -1,6 +1,6 @@
 # Round measurement on one MI355X: GPU tests, PMC traffic passes (lanes = 1), the default bench
 # (reads the fresh traffic), and a rocprofv3 kernel-trace --stats profile of the bench with lanes = 1
-# (so per-launch durations are those of the isolated sweep the bench's roofline uses).
+# and 2,048-frequency chunks (so per-launch durations are those of the isolated sweep the bench roofline uses).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -15,5 +15,5 @@ python3 tools/pmc_summary.py $O/fetch $O/write --last-sweep --freqs 2048 --json 
 cp $O/pmc_traffic.json profiles/r01/pmc_traffic.json
 timeout -k 10 400 python -u bench.py > $O/bench.json 2> $O/bench.err || exit 1
 cat $O/bench.json
-PFR_LANES=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python3 bench.py --no-cpu-baseline > $O/bench_prof_l1.json 2> $O/stats.err || exit 1
+PFR_LANES=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python3 bench.py --no-cpu-baseline --chunk 2048 > $O/bench_prof_l1.json 2> $O/stats.err || exit 1
 echo DONE
