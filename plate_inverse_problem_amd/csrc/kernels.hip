@@ -44,7 +44,7 @@ __device__ __forceinline__ void pivot_check(cplx p, int* flags, int64_t q) {
 }
 
 constexpr int KB = 4;    // factorisation pivot block
-constexpr int KBS = 16;  // triangular-solve block
+constexpr int KBS = 8;   // triangular-solve block (its lower triangle: 28 loads, all in flight)
 
 // ------------------------------------------------------------------ helpers
 // XCD-aware workgroup order: the dispatcher deals workgroups round-robin over
@@ -945,6 +945,13 @@ __device__ __forceinline__ void gather_frontal(const DevPattern& P, const Front&
 // read-modify-write per row, SRB rows per wave, y in chunks of SKC.
 constexpr int SRB = 4, SKC = 8;
 
+// Pivot blocks of the solves: every load unconditional (indices clamped into the block) and the
+// entries past the block masked arithmetically.  A load under a runtime condition -- even a
+// wave-uniform one like `t < kb` -- becomes a branch around that load followed by vmcnt(0), so a
+// 16-pivot block cost ~130 dependent memory round trips (~85 us) instead of a few.
+__device__ __forceinline__ cplx cscale(cplx a, double m) { return make_double2(a.x * m, a.y * m); }
+
+
 template <int RHS>
 __global__ __launch_bounds__(512) void k_lsolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
                                cplx* __restrict__ WV, RhsArgs R, cplx* __restrict__ Y, const int* __restrict__ reach) {
@@ -960,14 +967,17 @@ __global__ __launch_bounds__(512) void k_lsolve_level(DevPattern P, const int* _
   for (int k0 = 0; k0 < ns; k0 += KBS) {
     const int kb = min(KBS, ns - k0), k1 = k0 + kb;
     if (c.w == 0) {
+      // row-oriented forward substitution; rows past the block compute garbage that no row of
+      // the block reads
       cplx v[KBS];
 #pragma unroll
-      for (int t = 0; t < KBS; ++t) v[t] = t < kb ? V(k0 + t) : make_double2(0.0, 0.0);
+      for (int t = 0; t < KBS; ++t) v[t] = V(k0 + min(t, kb - 1));
 #pragma unroll
-      for (int k = 0; k < KBS; ++k)
+      for (int i = 1; i < KBS; ++i) {
+        const int ri = k0 + min(i, kb - 1);
 #pragma unroll
-        for (int i = k + 1; i < KBS; ++i)
-          if (i < kb) v[i] = cfms(v[i], E(k0 + i, k0 + k), v[k]);
+        for (int k = 0; k < i; ++k) v[i] = cfms(v[i], E(ri, k0 + min(k, kb - 1)), v[k]);
+      }
 #pragma unroll
       for (int t = 0; t < KBS; ++t)
         if (t < kb) V(k0 + t) = v[t];
@@ -976,13 +986,11 @@ __global__ __launch_bounds__(512) void k_lsolve_level(DevPattern P, const int* _
     if (k1 < ns) {
       cplx z[KBS];
 #pragma unroll
-      for (int t = 0; t < KBS; ++t)
-        if (t < kb) z[t] = V(k0 + t);
+      for (int t = 0; t < KBS; ++t) z[t] = cscale(V(k0 + min(t, kb - 1)), t < kb ? 1.0 : 0.0);
       for (int i = k1 + c.w; i < ns; i += c.W) {
         cplx v = V(i);
 #pragma unroll
-        for (int t = 0; t < KBS; ++t)
-          if (t < kb) v = cfms(v, E(i, k0 + t), z[t]);
+        for (int t = 0; t < KBS; ++t) v = cfms(v, E(i, k0 + min(t, kb - 1)), z[t]);
         V(i) = v;
       }
       __syncthreads();
@@ -1106,17 +1114,17 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
   for (int k1 = ns; k1 > 0; k1 -= KBS) {
     const int k0 = max(0, k1 - KBS), kb = k1 - k0;
     if (c.w == 0) {
+      // row-oriented backward substitution; rows past the block are forced to zero
       cplx v[KBS];
 #pragma unroll
-      for (int t = 0; t < KBS; ++t) v[t] = t < kb ? V(k0 + t) : make_double2(0.0, 0.0);
+      for (int t = 0; t < KBS; ++t) v[t] = V(k0 + min(t, kb - 1));
 #pragma unroll
-      for (int k = KBS - 1; k >= 0; --k)
-        if (k < kb) {
-          v[k] = cmul(v[k], crecip(E(k0 + k, k0 + k)));
+      for (int i = KBS - 1; i >= 0; --i) {
+        const int ri = k0 + min(i, kb - 1);
 #pragma unroll
-          for (int i = 0; i < KBS; ++i)
-            if (i < k) v[i] = cfms(v[i], E(k0 + i, k0 + k), v[k]);
-        }
+        for (int k = i + 1; k < KBS; ++k) v[i] = cfms(v[i], E(ri, k0 + min(k, kb - 1)), v[k]);
+        v[i] = cscale(cmul(v[i], crecip(E(ri, ri))), i < kb ? 1.0 : 0.0);
+      }
 #pragma unroll
       for (int t = 0; t < KBS; ++t)
         if (t < kb) {
@@ -1128,13 +1136,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     if (k0 > 0) {
       cplx x[KBS];
 #pragma unroll
-      for (int t = 0; t < KBS; ++t)
-        if (t < kb) x[t] = V(k0 + t);
+      for (int t = 0; t < KBS; ++t) x[t] = cscale(V(k0 + min(t, kb - 1)), t < kb ? 1.0 : 0.0);
       for (int i = c.w; i < k0; i += c.W) {
         cplx v = V(i);
 #pragma unroll
-        for (int t = 0; t < KBS; ++t)
-          if (t < kb) v = cfms(v, E(i, k0 + t), x[t]);
+        for (int t = 0; t < KBS; ++t) v = cfms(v, E(i, k0 + min(t, kb - 1)), x[t]);
         V(i) = v;
       }
       __syncthreads();
@@ -1234,15 +1240,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
         if (act[v]) {
           cplx x[KBS];
 #pragma unroll
-          for (int t = 0; t < KBS; ++t) x[t] = t < kb ? XV(v, k0 + t) : make_double2(0.0, 0.0);
+          for (int t = 0; t < KBS; ++t) x[t] = XV(v, k0 + min(t, kb - 1));
 #pragma unroll
-          for (int k = KBS - 1; k >= 0; --k)
-            if (k < kb) {
-              x[k] = cmul(x[k], crecip(E(k0 + k, k0 + k)));
+          for (int i = KBS - 1; i >= 0; --i) {
+            const int ri = k0 + min(i, kb - 1);
 #pragma unroll
-              for (int i = 0; i < KBS; ++i)
-                if (i < k) x[i] = cfms(x[i], E(k0 + i, k0 + k), x[k]);
-            }
+            for (int k = i + 1; k < KBS; ++k) x[i] = cfms(x[i], E(ri, k0 + min(k, kb - 1)), x[k]);
+            x[i] = cscale(cmul(x[i], crecip(E(ri, ri))), i < kb ? 1.0 : 0.0);
+          }
 #pragma unroll
           for (int t = 0; t < KBS; ++t)
             if (t < kb) XV(v, k0 + t) = x[t];
@@ -1255,13 +1260,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
         if (act[v]) {
           cplx x[KBS];
 #pragma unroll
-          for (int t = 0; t < KBS; ++t)
-            if (t < kb) x[t] = XV(v, k0 + t);
+          for (int t = 0; t < KBS; ++t) x[t] = cscale(XV(v, k0 + min(t, kb - 1)), t < kb ? 1.0 : 0.0);
           for (int i = c.w; i < k0; i += c.W) {
             cplx y = XV(v, i);
 #pragma unroll
-            for (int t = 0; t < KBS; ++t)
-              if (t < kb) y = cfms(y, E(i, k0 + t), x[t]);
+            for (int t = 0; t < KBS; ++t) y = cfms(y, E(i, k0 + min(t, kb - 1)), x[t]);
             XV(v, i) = y;
           }
         }
