@@ -33,6 +33,7 @@ __device__ __forceinline__ cplx cmul(cplx a, cplx b) {
 __device__ __forceinline__ cplx cfms(cplx c, cplx a, cplx b) {
   return make_double2(fma(-a.x, b.x, fma(a.y, b.y, c.x)), fma(-a.x, b.y, fma(-a.y, b.x, c.y)));
 }
+__device__ __forceinline__ cplx cscale(cplx a, double m) { return make_double2(a.x * m, a.y * m); }
 __device__ __forceinline__ cplx crecip(cplx b) {
   double d = fma(b.x, b.x, b.y * b.y);
   double inv = 1.0 / d;
@@ -166,14 +167,14 @@ __device__ __forceinline__ void row_update(const cplx* __restrict__ rd, cplx* __
       const int j = min(jb + jj, jend - 1);
       v[jj] = rd[(row_i + j) * Fc];
 #pragma unroll
-      for (int t = 0; t < KB; ++t)
-        if (t < kb) u[t][jj] = rd[(row_k0 + (int64_t)t * f + j) * Fc];
+      for (int t = 0; t < KB; ++t) u[t][jj] = rd[(row_k0 + (int64_t)min(t, kb - 1) * f + j) * Fc];
     }
+    // l[t] = 0 for t >= kb (callers), so the clamped rows add nothing; no load sits under a
+    // runtime test (that compiles to a branch + vmcnt(0) per load)
 #pragma unroll
     for (int jj = 0; jj < JB; ++jj)
 #pragma unroll
-      for (int t = 0; t < KB; ++t)
-        if (t < kb) v[jj] = cfms(v[jj], l[t], u[t][jj]);
+      for (int t = 0; t < KB; ++t) v[jj] = cfms(v[jj], l[t], u[t][jj]);
 #pragma unroll
     for (int jj = 0; jj < JB; ++jj)
       if (jb + jj < jend) wr[(row_i + jb + jj) * Fc] = v[jj];
@@ -274,18 +275,16 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
       for (int i = 0; i < KB; ++i)
 #pragma unroll
         for (int j = 0; j < KB; ++j)
-          if (i < j && j < kb) U[i][j] = E(k0 + i, k0 + j);
+          if (i < j) U[i][j] = E(k0 + min(i, kb - 1), k0 + min(j, kb - 1));
 #pragma unroll
-      for (int i = 0; i < KB; ++i)
-        if (i < kb) {
-          Dg[i] = E(k0 + i, k0 + i);
-          Dinv[i] = crecip(Dg[i]);
-        }
+      for (int i = 0; i < KB; ++i) {
+        Dg[i] = E(k0 + min(i, kb - 1), k0 + min(i, kb - 1));
+        Dinv[i] = crecip(Dg[i]);
+      }
       for (int i = k1 + FAC_G * c.w + sub; i < ns; i += FAC_G * c.W) {
         cplx l[KB];
 #pragma unroll
-        for (int t = 0; t < KB; ++t)
-          if (t < kb) l[t] = E(i, k0 + t);
+        for (int t = 0; t < KB; ++t) l[t] = E(i, k0 + min(t, kb - 1));
 #pragma unroll
         for (int t = 0; t < KB; ++t)
           if (t < kb) {
@@ -302,8 +301,7 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
       for (int i = k1 + FAC_G * c.w + sub; i < ns; i += FAC_G * c.W) {
         cplx l[KB];
 #pragma unroll
-        for (int t = 0; t < KB; ++t)
-          if (t < kb) l[t] = E(i, k0 + t);
+        for (int t = 0; t < KB; ++t) l[t] = cscale(E(i, k0 + min(t, kb - 1)), t < kb ? 1.0 : 0.0);
         row_update(base, base, (int64_t)i * f, (int64_t)k0 * f, f, Fc, k1, i + 1, kb, l);
       }
       __syncthreads();
@@ -336,8 +334,7 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
       for (int i = k1 + FAC_G * c.w + sub; i < lim; i += FAC_G * c.W) {
         cplx l[KB];
 #pragma unroll
-        for (int t = 0; t < KB; ++t)
-          if (t < kb) l[t] = E(i, k0 + t);
+        for (int t = 0; t < KB; ++t) l[t] = cscale(E(i, k0 + min(t, kb - 1)), t < kb ? 1.0 : 0.0);
 #pragma unroll
         for (int t = 0; t < KB; ++t)
           if (t < kb) {
@@ -949,7 +946,6 @@ constexpr int SRB = 4, SKC = 8;
 // entries past the block masked arithmetically.  A load under a runtime condition -- even a
 // wave-uniform one like `t < kb` -- becomes a branch around that load followed by vmcnt(0), so a
 // 16-pivot block cost ~130 dependent memory round trips (~85 us) instead of a few.
-__device__ __forceinline__ cplx cscale(cplx a, double m) { return make_double2(a.x * m, a.y * m); }
 
 
 template <int RHS>
