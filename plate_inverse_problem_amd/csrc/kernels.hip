@@ -353,6 +353,29 @@ __global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* _
 #undef E
 }
 
+// global -> LDS copy of one 1 KiB row (lane l's 16 B to lds_row + 16 l), issued as inline asm so
+// that the compiler's wait insertion does not see it: with the builtin it waits vmcnt(0) before
+// every LDS read of the staging array (the copies in flight might alias), which serialises the
+// pipeline.  Every wait on these copies is therefore explicit (PFR_WAIT_VM).
+__device__ __forceinline__ void glds16(const cplx* g, cplx* lds_row) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds_row);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(g), "s"(dst)
+               : "memory");
+}
+
+// Workgroup barrier for the LDS-staged kernels: LDS reads retired (lgkmcnt(0)), then s_barrier,
+// as one asm statement with a memory clobber so that the compiler moves no LDS access across it
+// (the builtin s_barrier is no compiler fence: reads of a buffer were sunk below the barrier after
+// which other waves overwrite it).  Global->LDS copies in flight are NOT waited for here.
+#define PFR_BARRIER() asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory")
+
+// s_waitcnt vmcnt(n) alone (expcnt / lgkmcnt left at their no-wait maxima; gfx9 encoding)
+#define PFR_WAIT_VM(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | (7 << 4) | (15 << 8))
+
 // Off-diagonal panel blocks once A11 = L11 U11 is factored, every row of L21 and
 // every column of U12 independently (read once, written once):
 //   kind 0, row i >= ns:     L(i, :ns) = A(i, :ns) U11^{-1}
@@ -389,8 +412,8 @@ __device__ __forceinline__ cplx off_source(const OffSrc& S, const cplx* __restri
     o = S.dq[max(g.x, 0)];
   }
   const cplx ch = F[(int64_t)max(g.y, 0) * Fc + q];
-  const cplx z = make_double2(0.0, 0.0);
-  return cadd(g.x >= 0 ? o : z, g.y >= 0 ? ch : z);
+  // masks as multipliers: with a select the load is sunk under a branch and waited for at once
+  return cadd(cscale(o, g.x >= 0 ? 1.0 : 0.0), cscale(ch, g.y >= 0 ? 1.0 : 0.0));
 }
 
 // One chunk of NB consecutive columns (kind 0) / rows (kind 1) c0 .. c0+NB-1 of
@@ -687,23 +710,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PFR_SCHUR_W
 // independent 4 x 4 tiles -- the tile kernel is bound by its L2 operand traffic, not by HBM.
 constexpr int BROWS = 2 * SCHUR_BLK + 1;     // rows per pivot: 16 row operands, 16 column operands, U(k, k)
 
-// global -> LDS copy of one 1 KiB row (lane l's 16 B to lds_row + 16 l), issued as inline asm so
-// that the compiler's wait insertion does not see it: with the builtin it waits vmcnt(0) before
-// every LDS read of the staging array (the copies in flight might alias), which serialises the
-// pipeline.  Every wait on these copies is therefore explicit (PFR_WAIT_VM).
-__device__ __forceinline__ void glds16(const cplx* g, cplx* lds_row) {
-  const uint32_t dst = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds_row);
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(g), "s"(dst)
-               : "memory");
-}
-
-// s_waitcnt vmcnt(n) alone (expcnt / lgkmcnt left at their no-wait maxima; gfx9 encoding)
-#define PFR_WAIT_VM(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | (7 << 4) | (15 << 8))
-
 // NB LDS buffers of KC pivots each.  NB = 2: plain double buffering, one __syncthreads per
 // stage (it drains the next stage's copies).  NB >= 3: the copies of NB - 1 stages ahead stay in
 // flight across a raw s_barrier, each stage retired by a counted vmcnt.
@@ -801,7 +807,7 @@ __global__ __launch_bounds__(1024) void k_schur_sym_blk(DevPattern P, const int4
     // waves 0 .. KC-1 issue their pivot copy first and one more per stage, so they wait for a
     // copy or two more than needed)
     PFR_WAIT_VM((NB - 2) * 2 * KC);
-    __builtin_amdgcn_s_barrier();   // stage st visible to all; everyone done with stage st - 1
+    PFR_BARRIER();   // stage st visible to all; everyone done with stage st - 1
     stage((st + NB - 1) % NB, (st + NB - 1) * KC);
     compute(st % NB, st * KC);
   }
