@@ -235,8 +235,16 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     mark(l, 1);
     // panel: enough workgroups (front x 16 frequencies) to fill the chip -> one wave
     // each (no idle waves at the block barriers); few large fronts -> more waves
+    // (symmetric kernel: up to 16 waves -- the top levels' few fronts are latency-bound, every
+    // wave more takes rows off each wave's serial chain)
+    static const int fac_wmax = [] {
+      const char* e = getenv("PFR_FAC_WMAX");   // tuning knob
+      return e ? atoi(e) : 16;
+    }();
     const int64_t wgs = (int64_t)nf * ngroups * pfr::FAC_G;
-    const int Wp = (int)std::max<int64_t>(1, std::min<int64_t>(s->level_W[l], (4096 + wgs - 1) / wgs));
+    const int64_t wfill = (4096 + wgs - 1) / wgs;
+    const int Wp = (int)std::max<int64_t>(
+        1, s->sym ? std::min<int64_t>(fac_wmax, wfill) : std::min<int64_t>(s->level_W[l], wfill));
     pfr::launch_factor(s->sym, s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st);
     mark(l, 2);
     pfr::launch_offdiag(mode, s->P, s->d_items + s->item_ptr[l], s->item_ptr[l + 1] - s->item_ptr[l], s->d_orec,
@@ -352,7 +360,8 @@ int sym_top_down_pair(pfr_solver* s, hipStream_t st) {
   const int ngroups = (int)(s->Fc / 64);
   for (int l = L - 1; l >= 0; --l) {
     const int nf = s->level_ptr[l + 1] - s->level_ptr[l];
-    pfr::launch_usolve2(true, s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_W[l], ngroups, s->F, s->Fc, s->Y,
+    pfr::launch_usolve2(true, s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_W[l], s->level_maxf[l], ngroups,
+                        s->F, s->Fc, s->Y,
                         s->X, s->d_reach[0], s->d_reach[1], s->Y2, s->XA, s->d_reach[1], st);
   }
   HIP_TRY(hipGetLastError());

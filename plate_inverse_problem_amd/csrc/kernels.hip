@@ -216,7 +216,7 @@ __device__ __forceinline__ void col_solve(const cplx* __restrict__ rd, cplx* __r
 // to date -- the trailing updates cover j <= i (half the work and traffic of the LU) -- and
 // U11 = diag(U11) L11^T is written from each L row as it is formed (no pivot-row solves).
 template <bool DIAG, bool SYM>
-__global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* __restrict__ lvl,
+__global__ __launch_bounds__(SYM ? 1024 : 512) void k_factor_level(DevPattern P, const int* __restrict__ lvl,
                                                        cplx* __restrict__ F, int64_t Fc,
                                                        int* __restrict__ flags) {
   Ctx c;
@@ -1165,8 +1165,11 @@ struct UPair {
   const int* skip;    // fronts this vector is not computed on (NULL = none)
 };
 
-template <bool SYM>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_usolve2_level(
+// SR pivot rows per wave sharing each gathered solution value, SK values per chunk, WPE waves per
+// SIMD: (4, 8, 2) for the levels of large fronts; (2, 4, 4) for levels of small fronts, where the
+// many tiny workgroups are latency-bound and occupancy, not per-wave reuse, hides it.
+template <bool SYM, int SR, int SK, int WPE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void k_usolve2_level(
     DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc, UPair A, UPair B) {
   const int ft = lvl[blockIdx.x];
   const bool act[2] = {!A.skip || !A.skip[ft], !B.skip || !B.skip[ft]};
@@ -1182,47 +1185,47 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
   __syncthreads();
 #define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
 #define XV(v, a) Xs[v][(int64_t)(fr.col0 + (a)) * Fc + c.q]
-  for (int a0 = SRB * c.w; a0 < ns; a0 += SRB * c.W) {
-    int ra[SRB];
-    cplx acc[2][SRB];
+  for (int a0 = SR * c.w; a0 < ns; a0 += SR * c.W) {
+    int ra[SR];
+    cplx acc[2][SR];
 #pragma unroll
-    for (int r = 0; r < SRB; ++r) {
+    for (int r = 0; r < SR; ++r) {
       ra[r] = min(a0 + r, ns - 1);
       acc[0][r] = acc[1][r] = make_double2(0.0, 0.0);
     }
-    const cplx* pu[SRB];
+    const cplx* pu[SR];
 #pragma unroll
-    for (int r = 0; r < SRB; ++r) pu[r] = base + (SYM ? (int64_t)ra[r] : (int64_t)ra[r] * f) * Fc;
+    for (int r = 0; r < SR; ++r) pu[r] = base + (SYM ? (int64_t)ra[r] : (int64_t)ra[r] * f) * Fc;
     const int64_t su = SYM ? (int64_t)f * Fc : Fc;
-    for (int b0 = ns; b0 < f; b0 += SKC) {
-      int iv[SKC];
-      cplx xv[2][SKC], ev[SRB][SKC];
+    for (int b0 = ns; b0 < f; b0 += SK) {
+      int iv[SK];
+      cplx xv[2][SK], ev[SR][SK];
 #pragma unroll
-      for (int u = 0; u < SKC; ++u) iv[u] = __builtin_amdgcn_readfirstlane(six[min(b0 + u, f - 1)]);
-#pragma unroll
-      for (int v = 0; v < 2; ++v)
-#pragma unroll
-        for (int u = 0; u < SKC; ++u) xv[v][u] = Xs[v][(int64_t)iv[u] * Fc + c.q];   // inactive: unused
-#pragma unroll
-      for (int r = 0; r < SRB; ++r)
-#pragma unroll
-        for (int u = 0; u < SKC; ++u) ev[r][u] = pu[r][min(b0 + u, f - 1) * su];
-      __builtin_amdgcn_sched_group_barrier(0x020, SKC * (SRB + 2), 0);   // all vector loads first
-      __builtin_amdgcn_sched_group_barrier(0x002, 8 * SKC * SRB + 16, 0);
+      for (int u = 0; u < SK; ++u) iv[u] = __builtin_amdgcn_readfirstlane(six[min(b0 + u, f - 1)]);
 #pragma unroll
       for (int v = 0; v < 2; ++v)
 #pragma unroll
-        for (int u = 0; u < SKC; ++u)
+        for (int u = 0; u < SK; ++u) xv[v][u] = Xs[v][(int64_t)iv[u] * Fc + c.q];   // inactive: unused
+#pragma unroll
+      for (int r = 0; r < SR; ++r)
+#pragma unroll
+        for (int u = 0; u < SK; ++u) ev[r][u] = pu[r][min(b0 + u, f - 1) * su];
+      __builtin_amdgcn_sched_group_barrier(0x020, SK * (SR + 2), 0);   // all vector loads first
+      __builtin_amdgcn_sched_group_barrier(0x002, 8 * SK * SR + 16, 0);
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int u = 0; u < SK; ++u)
           if (b0 + u >= f) xv[v][u] = make_double2(0.0, 0.0);
 #pragma unroll
       for (int v = 0; v < 2; ++v)
 #pragma unroll
-        for (int r = 0; r < SRB; ++r)
+        for (int r = 0; r < SR; ++r)
 #pragma unroll
-          for (int u = 0; u < SKC; ++u) acc[v][r] = cfms(acc[v][r], ev[r][u], xv[v][u]);
+          for (int u = 0; u < SK; ++u) acc[v][r] = cfms(acc[v][r], ev[r][u], xv[v][u]);
     }
 #pragma unroll
-    for (int r = 0; r < SRB; ++r)
+    for (int r = 0; r < SR; ++r)
       if (a0 + r < ns) {
         const cplx urr = SYM ? E(ra[r], ra[r]) : make_double2(1.0, 0.0);
 #pragma unroll
@@ -1846,14 +1849,21 @@ void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const 
   }
 }
 
-void launch_usolve2(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, const double2* F,
-                    int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0, const double2* Y1,
-                    double2* X1, const int* reach1, hipStream_t st) {
+void launch_usolve2(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int maxf, int ngroups,
+                    const double2* F, int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0,
+                    const double2* Y1, double2* X1, const int* reach1, hipStream_t st) {
   if (nfronts <= 0) return;
   UPair a{Y0, X0, reach0, skip0}, b{Y1, X1, reach1, nullptr};
   dim3 g(nfronts, ngroups), bl(64 * W);
-  if (sym) LAUNCH(k_usolve2_level<true>, g, bl, st, P, lvl, F, Fc, a, b);
-  else LAUNCH(k_usolve2_level<false>, g, bl, st, P, lvl, F, Fc, a, b);
+  static const int small_max = [] {
+    const char* e = getenv("PFR_US2_SMALL");   // tuning knob: largest front of a "small-front" level
+    return e ? atoi(e) : 110;
+  }();
+  const bool small = maxf <= small_max;
+  if (sym && small) LAUNCH((k_usolve2_level<true, 2, 4, 4>), g, bl, st, P, lvl, F, Fc, a, b);
+  else if (sym) LAUNCH((k_usolve2_level<true, 4, 8, 2>), g, bl, st, P, lvl, F, Fc, a, b);
+  else if (small) LAUNCH((k_usolve2_level<false, 2, 4, 4>), g, bl, st, P, lvl, F, Fc, a, b);
+  else LAUNCH((k_usolve2_level<false, 4, 8, 2>), g, bl, st, P, lvl, F, Fc, a, b);
 }
 
 void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nrows, const double2* Kd,

@@ -50,9 +50,9 @@ void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const 
                   const double2* F, int64_t Fc, double2* WV, const RhsDesc& rd, const double2* Yin, double2* Out,
                   const int* reach, hipStream_t st);
 // two top-down U solves in one pass (vector 0 skipped on the fronts flagged in skip0)
-void launch_usolve2(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, const double2* F,
-                    int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0, const double2* Y1,
-                    double2* X1, const int* reach1, hipStream_t st);
+void launch_usolve2(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int maxf, int ngroups,
+                    const double2* F, int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0,
+                    const double2* Y1, double2* X1, const int* reach1, hipStream_t st);
 // Hessian sweep: tangent right-hand sides (rows of the permuted matrix, or of its
 // transpose with accumulate = 1) and the directional derivative of the loss cotangent
 void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nrows, const double2* Kd,
