@@ -798,10 +798,17 @@ __global__ __launch_bounds__(1024) void k_schur_sym_blk(DevPattern P, const int4
     }
   };
   const int nst = (ns + KC - 1) / KC;
-  PFR_WAIT_VM(0);                      // the gathers above (ordinary loads) out of the count
-  // prologue: stages 0 .. NB - 2 in flight (stages past nst copy clamped rows, never read)
+  // prologue: stages 0 .. NB - 2 in flight (stages past nst copy clamped rows, never read).  The
+  // children's entries gathered above are older than these copies, so the first counted wait
+  // retires them together with stage 0: one memory round trip for both.
 #pragma unroll
   for (int p = 0; p < NB - 1; ++p) stage(p, p * KC);
+  // the gathered values are needed from here on: tie them down once (otherwise the compiler waits
+  // for them -- vmcnt(0), copies in flight included -- inside the loop, every step)
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) asm volatile("" : "+v"(acc[m][n].x), "+v"(acc[m][n].y));
   for (int st = 0; st < nst; ++st) {
     // retire stage st: NB - 2 later stages may stay in flight (2 KC copies per wave and stage;
     // waves 0 .. KC-1 issue their pivot copy first and one more per stage, so they wait for a
