@@ -212,11 +212,8 @@ __device__ __forceinline__ void col_solve(const cplx* __restrict__ rd, cplx* __r
 // reads are shared by the row groups; workgroup = (front, 64 / FAC_G frequencies), W waves.
 // DIAG = true: only the diagonal block A11 = L11 U11 (rows and columns < ns);
 // L21 and U12 are then formed row / column-wise by k_offdiag_level.
-// SYM (symmetric mode, DIAG only): A11 is symmetric, so only its lower triangle is kept up
-// to date -- the trailing updates cover j <= i (half the work and traffic of the LU) -- and
-// U11 = diag(U11) L11^T is written from each L row as it is formed (no pivot-row solves).
-template <bool DIAG, bool SYM>
-__global__ __launch_bounds__(SYM ? 1024 : 512) void k_factor_level(DevPattern P, const int* __restrict__ lvl,
+template <bool DIAG>
+__global__ __launch_bounds__(512) void k_factor_level(DevPattern P, const int* __restrict__ lvl,
                                                        cplx* __restrict__ F, int64_t Fc,
                                                        int* __restrict__ flags) {
   Ctx c;
@@ -243,7 +240,7 @@ __global__ __launch_bounds__(SYM ? 1024 : 512) void k_factor_level(DevPattern P,
 #pragma unroll
         for (int j = 0; j < KB; ++j) {
           const int a = k0 + min(i, kb - 1), b = k0 + min(j, kb - 1);
-          D[i][j] = SYM ? E(max(a, b), min(a, b)) : E(a, b);
+          D[i][j] = E(a, b);
         }
 #pragma unroll
       for (int k = 0; k < KB; ++k) {
@@ -267,46 +264,6 @@ __global__ __launch_bounds__(SYM ? 1024 : 512) void k_factor_level(DevPattern P,
       }
     }
     __syncthreads();
-    if (SYM) {
-      // rows i >= k1 of the block columns: L(i, blk) = A(i, blk) U_blk^{-1}, U(blk, i) = diag L(i, blk)^T
-      cplx U[KB][KB];
-      cplx Dg[KB], Dinv[KB];
-#pragma unroll
-      for (int i = 0; i < KB; ++i)
-#pragma unroll
-        for (int j = 0; j < KB; ++j)
-          if (i < j) U[i][j] = E(k0 + min(i, kb - 1), k0 + min(j, kb - 1));
-#pragma unroll
-      for (int i = 0; i < KB; ++i) {
-        Dg[i] = E(k0 + min(i, kb - 1), k0 + min(i, kb - 1));
-        Dinv[i] = crecip(Dg[i]);
-      }
-      for (int i = k1 + FAC_G * c.w + sub; i < ns; i += FAC_G * c.W) {
-        cplx l[KB];
-#pragma unroll
-        for (int t = 0; t < KB; ++t) l[t] = E(i, k0 + min(t, kb - 1));
-#pragma unroll
-        for (int t = 0; t < KB; ++t)
-          if (t < kb) {
-#pragma unroll
-            for (int s = 0; s < KB; ++s)
-              if (s < t) l[t] = cfms(l[t], l[s], U[s][t]);
-            l[t] = cmul(l[t], Dinv[t]);
-            E(i, k0 + t) = l[t];
-            E(k0 + t, i) = cmul(Dg[t], l[t]);
-          }
-      }
-      __syncthreads();
-      // trailing lower triangle: A(i, j) -= L(i, blk) U(blk, j), k1 <= j <= i
-      for (int i = k1 + FAC_G * c.w + sub; i < ns; i += FAC_G * c.W) {
-        cplx l[KB];
-#pragma unroll
-        for (int t = 0; t < KB; ++t) l[t] = cscale(E(i, k0 + min(t, kb - 1)), t < kb ? 1.0 : 0.0);
-        row_update(base, base, (int64_t)i * f, (int64_t)k0 * f, f, Fc, k1, i + 1, kb, l);
-      }
-      __syncthreads();
-      continue;
-    }
     // pivot rows of the block, columns >= k1:  L11^{-1} A12 (columns over waves)
     {
       cplx L[KB][KB];
@@ -375,6 +332,156 @@ __device__ __forceinline__ void glds16(const cplx* g, cplx* lds_row) {
 
 // s_waitcnt vmcnt(n) alone (expcnt / lgkmcnt left at their no-wait maxima; gfx9 encoding)
 #define PFR_WAIT_VM(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | (7 << 4) | (15 << 8))
+
+// Symmetric mode: A11 is symmetric, so only its lower triangle is kept up to date (trailing
+// updates over j <= i: half the LU's work and traffic) and U11 = diag(U11) L11^T is written from
+// each L row as it is formed (no pivot-row solves).  Pivots in super-blocks of 8 = two 4-pivot
+// blocks A, B with lookahead: A's diagonal block and L rows, B's columns updated by A alone, B's
+// diagonal block and L rows, then ONE rank-8 update of the trailing lower triangle -- which is
+// read and written once per 8 pivots instead of once per 4 (the dominant traffic of this kernel).
+// Lane map as k_factor_level; up to 16 waves per front.
+template <int JBU>
+__device__ __forceinline__ void row_update8(const cplx* __restrict__ rd, cplx* __restrict__ wr, int64_t row_i,
+                                            int64_t row_k0, int f, int64_t Fc, int j0, int jend, int kb8,
+                                            const cplx (&l)[2 * KB]) {
+#pragma unroll 2
+  for (int jb = j0; jb < jend; jb += JBU) {
+    cplx u[2 * KB][JBU], v[JBU];
+#pragma unroll
+    for (int jj = 0; jj < JBU; ++jj) {
+      const int j = min(jb + jj, jend - 1);
+      v[jj] = rd[(row_i + j) * Fc];
+#pragma unroll
+      for (int t = 0; t < 2 * KB; ++t) u[t][jj] = rd[(row_k0 + (int64_t)min(t, kb8 - 1) * f + j) * Fc];
+    }
+#pragma unroll
+    for (int jj = 0; jj < JBU; ++jj)
+#pragma unroll
+      for (int t = 0; t < 2 * KB; ++t) v[jj] = cfms(v[jj], l[t], u[t][jj]);   // l[t] = 0 for t >= kb8
+#pragma unroll
+    for (int jj = 0; jj < JBU; ++jj)
+      if (jb + jj < jend) wr[(row_i + jb + jj) * Fc] = v[jj];
+  }
+}
+
+#ifndef PFR_FAC_JBU
+#define PFR_FAC_JBU 2
+#endif
+#ifndef PFR_FAC_LB
+#define PFR_FAC_LB 1024
+#endif
+
+__global__ __launch_bounds__(PFR_FAC_LB) void k_factor_sym(DevPattern P, const int* __restrict__ lvl, cplx* __restrict__ F,
+                                                     int64_t Fc, int* __restrict__ flags) {
+  Ctx c;
+  c.lane = threadIdx.x & 63;
+  c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  c.W = blockDim.x >> 6;
+  constexpr int QG = 64 / FAC_G;     // frequencies per lane group
+  c.q = (int64_t)blockIdx.y * QG + c.lane % QG;
+  const int sub = c.lane / QG;
+  const Front fr = P.fronts[lvl[blockIdx.x]];
+  const int f = fr.f, ns = fr.ns;
+  cplx* __restrict__ base = F + fr.off * Fc + c.q;
+  const int r0 = FAC_G * c.w + sub, rs = FAC_G * c.W;   // this lane's first row offset, row stride
+#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+  // 4-pivot diagonal block at k0 (kb pivots): one load burst from the lower triangle, LU in
+  // registers (U = diag(U) L^T up to rounding), one store burst
+  auto diag = [&](int k0, int kb) {
+    if (c.w != 0) return;
+    cplx D[KB][KB];
+#pragma unroll
+    for (int i = 0; i < KB; ++i)
+#pragma unroll
+      for (int j = 0; j < KB; ++j) {
+        const int a = k0 + min(i, kb - 1), b = k0 + min(j, kb - 1);
+        D[i][j] = E(max(a, b), min(a, b));
+      }
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      if (k < kb) {
+        pivot_check(D[k][k], flags, c.q);
+        const cplx inv = crecip(D[k][k]);
+#pragma unroll
+        for (int i = k + 1; i < KB; ++i) {
+          D[i][k] = cmul(D[i][k], inv);
+#pragma unroll
+          for (int j = k + 1; j < KB; ++j) D[i][j] = cfms(D[i][j], D[i][k], D[k][j]);
+        }
+      }
+    }
+    if (sub == 0) {
+#pragma unroll
+      for (int i = 0; i < KB; ++i)
+#pragma unroll
+        for (int j = 0; j < KB; ++j)
+          if (i < kb && j < kb) E(k0 + i, k0 + j) = D[i][j];
+    }
+  };
+  // rows i >= i0 of the block's columns: L(i, blk) = A(i, blk) U_blk^{-1}, U(blk, i) = diag L(i, blk)^T
+  auto rows = [&](int k0, int kb, int i0) {
+    cplx U[KB][KB];
+    cplx Dg[KB], Dinv[KB];
+#pragma unroll
+    for (int i = 0; i < KB; ++i)
+#pragma unroll
+      for (int j = 0; j < KB; ++j)
+        if (i < j) U[i][j] = E(k0 + min(i, kb - 1), k0 + min(j, kb - 1));
+#pragma unroll
+    for (int i = 0; i < KB; ++i) {
+      Dg[i] = E(k0 + min(i, kb - 1), k0 + min(i, kb - 1));
+      Dinv[i] = crecip(Dg[i]);
+    }
+    for (int i = i0 + r0; i < ns; i += rs) {
+      cplx l[KB];
+#pragma unroll
+      for (int t = 0; t < KB; ++t) l[t] = E(i, k0 + min(t, kb - 1));
+#pragma unroll
+      for (int t = 0; t < KB; ++t)
+        if (t < kb) {
+#pragma unroll
+          for (int s = 0; s < KB; ++s)
+            if (s < t) l[t] = cfms(l[t], l[s], U[s][t]);
+          l[t] = cmul(l[t], Dinv[t]);
+          E(i, k0 + t) = l[t];
+          E(k0 + t, i) = cmul(Dg[t], l[t]);
+        }
+    }
+  };
+  for (int k0 = 0; k0 < ns; k0 += 2 * KB) {
+    const int kb8 = min(2 * KB, ns - k0), kbA = min(KB, kb8), kbB = kb8 - kbA;
+    diag(k0, kbA);
+    __syncthreads();
+    rows(k0, kbA, k0 + kbA);
+    __syncthreads();
+    if (kbB > 0) {
+      // block B's columns (lower part) updated by block A: rank kbA
+      for (int i = k0 + KB + r0; i < ns; i += rs) {
+        cplx l[KB];
+#pragma unroll
+        for (int t = 0; t < KB; ++t) l[t] = cscale(E(i, k0 + min(t, kbA - 1)), t < kbA ? 1.0 : 0.0);
+        row_update(base, base, (int64_t)i * f, (int64_t)k0 * f, f, Fc, k0 + KB, min(k0 + KB + kbB, i + 1), kbA, l);
+      }
+      __syncthreads();
+      diag(k0 + KB, kbB);
+      __syncthreads();
+      rows(k0 + KB, kbB, k0 + kb8);
+      __syncthreads();
+    }
+    const int k1 = k0 + kb8;
+    if (k1 < ns) {
+      // trailing lower triangle: A(i, j) -= L(i, k0:k1) U(k0:k1, j), k1 <= j <= i, rank kb8
+      for (int i = k1 + r0; i < ns; i += rs) {
+        cplx l[2 * KB];
+#pragma unroll
+        for (int t = 0; t < 2 * KB; ++t) l[t] = cscale(E(i, k0 + min(t, kb8 - 1)), t < kb8 ? 1.0 : 0.0);
+        row_update8<PFR_FAC_JBU>(base, base, (int64_t)i * f, (int64_t)k0 * f, f, Fc, k1, i + 1, kb8, l);
+      }
+      __syncthreads();
+    }
+  }
+#undef E
+}
 
 // Off-diagonal panel blocks once A11 = L11 U11 is factored, every row of L21 and
 // every column of U12 independently (read once, written once):
@@ -1805,8 +1912,8 @@ void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, cons
 
 void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F,
                    int64_t Fc, int* flags, hipStream_t st) {
-  if (sym) LAUNCH((k_factor_level<true, true>), dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
-  else LAUNCH((k_factor_level<true, false>), dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
+  if (sym) LAUNCH(k_factor_sym, dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
+  else LAUNCH(k_factor_level<true>, dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
 }
 
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
