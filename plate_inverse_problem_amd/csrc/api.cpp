@@ -74,6 +74,7 @@ struct pfr_solver {
   int32_t* d_bgxp = nullptr;            // per block: range of further sources in d_bgx
   int2* d_bgx = nullptr;                // (wave * 16 + position, element id)
   std::vector<int32_t> blk_ptr;
+  int schur_bc = 16;                    // block columns (16: 16 waves per block, 8: 8 waves)
   int4* d_asm = nullptr;                // panel-entry assembly records (dst, nz, first child source, 0), by level
   int32_t* d_asm_xp = nullptr;          // per 8-record chunk: range of further child sources in d_asm_x
   int2* d_asm_x = nullptr;              // (record within chunk, child element id)
@@ -252,8 +253,8 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
                         nvalid, st);
     if (after_panel) after_panel(l);
     mark(l, 3);
-    pfr::launch_schur_blk(s->P, s->d_blocks + s->blk_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
-                          s->d_bg1 + (int64_t)s->blk_ptr[l] * 256, s->d_bgxp + s->blk_ptr[l], s->d_bgx, ngroups, s->F,
+    pfr::launch_schur_blk(s->schur_bc, s->P, s->d_blocks + s->blk_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
+                          s->d_bg1 + (int64_t)s->blk_ptr[l] * 16 * s->schur_bc, s->d_bgxp + s->blk_ptr[l], s->d_bgx, ngroups, s->F,
                           s->Fc, st);
     mark(l, 4);
     pfr::launch_schur(s->sym, s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l],
@@ -572,6 +573,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     std::vector<int2> bgx;
     s->blk_ptr.assign(1, 0);
     // update blocks of at least this many rows go to the 16 x 16 block kernel (symmetric mode)
+    const char* bce = getenv("PFR_SCHUR_BC");   // tuning knob: Schur block columns (16 or 8)
+    s->schur_bc = bce && atoi(bce) == 8 ? 8 : 16;
     const char* be = getenv("PFR_SCHUR_BLK_MIN");
     const int blk_min = be ? atoi(be) : 24;
     const int L = (int)S.level_ptr.size() - 1;
@@ -604,14 +607,15 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
         }
         std::sort(more.begin(), more.end());
         if (sym && blk_min > 0 && r >= blk_min) {
-          // 16 x 16 blocks touching the lower triangle; wave w owns the 4 x 4 tile (w / 4, w % 4)
+          // 16 x BC blocks touching the lower triangle; wave w owns the 4 x 4 tile (w / tcw, w % tcw)
           constexpr int B = pfr::SCHUR_BLK;
+          const int BC = s->schur_bc, tcw = BC / 4;
           for (int i0 = 0; i0 < r; i0 += B)
-            for (int j0 = 0; j0 <= i0; j0 += B) {
+            for (int j0 = 0; j0 < i0 + B; j0 += BC) {
               bv.push_back(make_int4(t, i0, j0, 0));
-              for (int w = 0; w < 16; ++w)
+              for (int w = 0; w < BC; ++w)
                 for (int pos = 0; pos < 16; ++pos) {
-                  const int i = i0 + 4 * (w / 4) + pos / 4, j = j0 + 4 * (w % 4) + pos % 4;
+                  const int i = i0 + 4 * (w / tcw) + pos / 4, j = j0 + 4 * (w % tcw) + pos % 4;
                   if (i >= r || j > i) {
                     bg1.push_back(-1);
                     continue;

@@ -815,16 +815,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PFR_SCHUR_W
 // loads (no staging registers), double-buffered: stage s + 1 is in flight while stage s is
 // multiplied.  Per pivot step that is 33 1-KiB loads for the block instead of 16 x 9 for 16
 // independent 4 x 4 tiles -- the tile kernel is bound by its L2 operand traffic, not by HBM.
-constexpr int BROWS = 2 * SCHUR_BLK + 1;     // rows per pivot: 16 row operands, 16 column operands, U(k, k)
+// BC = 16: 16 x 16 blocks, 16 waves; BC = 8: 16 x 8 blocks, 8 waves (half the LDS and waves per
+// workgroup, so two blocks share a CU and one's barriers and prologue overlap the other's work).
 
 // NB LDS buffers of KC pivots each.  NB = 2: plain double buffering, one __syncthreads per
 // stage (it drains the next stage's copies).  NB >= 3: the copies of NB - 1 stages ahead stay in
 // flight across a raw s_barrier, each stage retired by a counted vmcnt.
-template <int NB, int KC>
-__global__ __launch_bounds__(1024) void k_schur_sym_blk(DevPattern P, const int4* __restrict__ blocks, int nblocks,
+template <int NB, int KC, int BC>
+__global__ __launch_bounds__(64 * BC) void k_schur_sym_blk(DevPattern P, const int4* __restrict__ blocks, int nblocks,
                                                          const int* __restrict__ bg1, const int* __restrict__ bgxp,
                                                          const int2* __restrict__ bgx, cplx* __restrict__ F,
                                                          int64_t Fc) {
+  constexpr int BR = SCHUR_BLK, NW = BC, TCW = BC / 4;   // block rows, waves, tile columns
+  constexpr int BROWS = BR + BC + 1;      // LDS rows per pivot: row operands, column operands, U(k, k)
   __shared__ cplx sop[NB][KC][BROWS][64];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -836,12 +839,12 @@ __global__ __launch_bounds__(1024) void k_schur_sym_blk(DevPattern P, const int4
   const Front fr = P.fronts[bk.x];
   const int f = fr.f, ns = fr.ns, r = f - ns;
   cplx* __restrict__ base = F + fr.off * Fc + q;
-  const int ti = 4 * (w >> 2), tj = 4 * (w & 3);
+  const int ti = 4 * (w / TCW), tj = 4 * (w % TCW);
   // the tile holds a lower-triangle entry inside the update block
   const bool active = bk.y + ti < r && bk.y + ti + 3 >= bk.z + tj;
   cplx acc[4][4];
   if (active) {
-    const int4* __restrict__ g4 = reinterpret_cast<const int4*>(bg1 + ((int64_t)bid * 16 + w) * 16);
+    const int4* __restrict__ g4 = reinterpret_cast<const int4*>(bg1 + ((int64_t)bid * NW + w) * 16);
     int src[16];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -875,15 +878,19 @@ __global__ __launch_bounds__(1024) void k_schur_sym_blk(DevPattern P, const int4
   // stage copy: row slot rho of pivot u: rho < 16 -> L21 row i0 + rho, rho < 32 -> L21 row
   // j0 + rho - 16, rho = 32 -> U(k, k); wave w copies slots w and w + 16 of every pivot, wave u
   // the pivot of step u.  Rows past the block and pivots past ns read clamped (valid) addresses.
-  const cplx* ra = base + ((int64_t)(ns + min(bk.y + w, r - 1)) * f) * Fc;
+  // wave w copies row operands w + NW h (h < BR / NW), column operand w and, if w == u, U(k, k)
+  const cplx* ra[BR / NW];
+#pragma unroll
+  for (int h = 0; h < BR / NW; ++h) ra[h] = base + ((int64_t)(ns + min(bk.y + w + NW * h, r - 1)) * f) * Fc;
   const cplx* rb = base + ((int64_t)(ns + min(bk.z + w, r - 1)) * f) * Fc;
   auto stage = [&](int buf, int k0) {
 #pragma unroll
     for (int u = 0; u < KC; ++u) {
       const int k = max(min(k0 + u, ns - 1), 0);
-      if (w == u) glds16(base + (int64_t)k * (f + 1) * Fc, &sop[buf][u][2 * SCHUR_BLK][0]);
-      glds16(ra + (int64_t)k * Fc, &sop[buf][u][w][0]);
-      glds16(rb + (int64_t)k * Fc, &sop[buf][u][SCHUR_BLK + w][0]);
+      if (w == u) glds16(base + (int64_t)k * (f + 1) * Fc, &sop[buf][u][BR + BC][0]);
+#pragma unroll
+      for (int h = 0; h < BR / NW; ++h) glds16(ra[h] + (int64_t)k * Fc, &sop[buf][u][w + NW * h][0]);
+      glds16(rb + (int64_t)k * Fc, &sop[buf][u][BR + w][0]);
     }
   };
   auto compute = [&](int buf, int k0) {
@@ -891,12 +898,12 @@ __global__ __launch_bounds__(1024) void k_schur_sym_blk(DevPattern P, const int4
 #pragma unroll
     for (int u = 0; u < KC; ++u) {
       if (k0 + u < ns) {
-        const cplx d = sop[buf][u][2 * SCHUR_BLK][lane];
+        const cplx d = sop[buf][u][BR + BC][lane];
         cplx a[4], b[4];
 #pragma unroll
         for (int m = 0; m < 4; ++m) a[m] = cmul(sop[buf][u][ti + m][lane], d);
 #pragma unroll
-        for (int n = 0; n < 4; ++n) b[n] = sop[buf][u][SCHUR_BLK + tj + n][lane];
+        for (int n = 0; n < 4; ++n) b[n] = sop[buf][u][BR + tj + n][lane];
 #pragma unroll
         for (int m = 0; m < 4; ++m)
 #pragma unroll
@@ -920,7 +927,7 @@ __global__ __launch_bounds__(1024) void k_schur_sym_blk(DevPattern P, const int4
     // retire stage st: NB - 2 later stages may stay in flight (2 KC copies per wave and stage;
     // waves 0 .. KC-1 issue their pivot copy first and one more per stage, so they wait for a
     // copy or two more than needed)
-    PFR_WAIT_VM((NB - 2) * 2 * KC);
+    PFR_WAIT_VM((NB - 2) * (BR / NW + 1) * KC);
     PFR_BARRIER();   // stage st visible to all; everyone done with stage st - 1
     stage((st + NB - 1) % NB, (st + NB - 1) * KC);
     compute(st % NB, st * KC);
@@ -1887,18 +1894,23 @@ void launch_schur(bool sym, const DevPattern& P, const int4* tiles, int ntiles, 
   else LAUNCH(k_schur_level, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
 }
 
-void launch_schur_blk(const DevPattern& P, const int4* blocks, int nblocks, const int* bg1, const int* bgxp,
+void launch_schur_blk(int bc, const DevPattern& P, const int4* blocks, int nblocks, const int* bg1, const int* bgxp,
                       const int2* bgx, int ngroups, double2* F, int64_t Fc, hipStream_t st) {
   if (nblocks <= 0) return;
   static const int cfg = [] {
     const char* e = getenv("PFR_SCHUR_BLK_CFG");   // tuning knob: buffers x 10 + pivots per stage
     return e ? atoi(e) : 41;
   }();
-  const dim3 g(nblocks, ngroups), b(1024);
-  if (cfg == 31) LAUNCH((k_schur_sym_blk<3, 1>), g, b, st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
-  else if (cfg == 41) LAUNCH((k_schur_sym_blk<4, 1>), g, b, st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
-  else if (cfg == 21) LAUNCH((k_schur_sym_blk<2, 1>), g, b, st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
-  else LAUNCH((k_schur_sym_blk<2, 2>), g, b, st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
+  const dim3 g(nblocks, ngroups), b(64 * bc);
+  if (bc == 8) {
+    if (cfg == 31) LAUNCH((k_schur_sym_blk<3, 1, 8>), g, b, st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
+    else LAUNCH((k_schur_sym_blk<4, 1, 8>), g, b, st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
+  } else {
+    if (cfg == 31) LAUNCH((k_schur_sym_blk<3, 1, 16>), g, b, st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
+    else if (cfg == 21) LAUNCH((k_schur_sym_blk<2, 1, 16>), g, b, st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
+    else if (cfg == 22) LAUNCH((k_schur_sym_blk<2, 2, 16>), g, b, st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
+    else LAUNCH((k_schur_sym_blk<4, 1, 16>), g, b, st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
+  }
 }
 
 void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, const int2* xl, int ngroups, double2* F,

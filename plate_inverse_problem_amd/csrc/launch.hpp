@@ -43,7 +43,7 @@ void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems
 void launch_schur(bool sym, const DevPattern& P, const int4* tiles, int ntiles, const int* g1, const int* gxp,
                   const int2* gx, int ngroups, double2* F, int64_t Fc, hipStream_t st);
 // symmetric mode, large update blocks: 16 x 16 blocks, operands staged in LDS per workgroup
-void launch_schur_blk(const DevPattern& P, const int4* blocks, int nblocks, const int* bg1, const int* bgxp,
+void launch_schur_blk(int bc, const DevPattern& P, const int4* blocks, int nblocks, const int* bg1, const int* bgxp,
                       const int2* bgx, int ngroups, double2* F, int64_t Fc, hipStream_t st);
 // which: 0 = L (bottom-up), 1 = U (top-down), 2 = U^T (bottom-up), 3 = L^T (top-down)
 void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups,

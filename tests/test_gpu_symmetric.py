@@ -84,11 +84,13 @@ def test_explicit_solve_refused_on_symmetric_solver():
         eng.solver.solve(torch.view_as_real(data), nnz, torch.view_as_real(b), n, torch.view_as_real(x), False, 1)
 
 
-@pytest.mark.parametrize("blk_min", ["0", "4", "24"])
-def test_schur_kernel_split_matches_oracle(blk_min, monkeypatch):
+@pytest.mark.parametrize("blk_min,bc", [("0", "16"), ("4", "16"), ("24", "16"), ("4", "8")])
+def test_schur_kernel_split_matches_oracle(blk_min, bc, monkeypatch):
     """Symmetric Schur complement through the 4 x 4 tile kernel alone (PFR_SCHUR_BLK_MIN=0),
-    the 16 x 16 LDS block kernel for almost every front (4) and the default split (24)."""
+    the LDS block kernel for almost every front (4) and the default split (24); 16 x 16 blocks
+    (default) and 16 x 8 blocks (PFR_SCHUR_BC=8)."""
     monkeypatch.setenv("PFR_SCHUR_BLK_MIN", blk_min)
+    monkeypatch.setenv("PFR_SCHUR_BC", bc)
     p = make_problem("orthotropic", ny=6, device="cuda:0")
     freqs = np.linspace(40.0, 600.0, 130)
     fr = p.solveForward(freqs)
