@@ -217,6 +217,19 @@ int finish_timing(pfr_solver* s, const bool* used) {
 
 void reset_timing(pfr_solver* s) { s->n_tev = 0; }
 
+// Waves per workgroup of a solve launch over nf fronts of level l: the level's size-based count,
+// raised (up to 8) when the launch has too few workgroups to fill the chip -- the sparse passes
+// and the top levels, which are latency-bound: every wave more takes rows off each wave's chain.
+int solve_W(const pfr_solver* s, int l, int nf) {
+  static const int wmax = [] {
+    const char* e = getenv("PFR_SOLVE_WMAX");   // tuning knob
+    return e ? atoi(e) : 8;
+  }();
+  const int64_t wgs = std::max<int64_t>(1, (int64_t)nf * (s->Fc / 64));
+  const int64_t fill = (4096 + wgs - 1) / wgs;
+  return (int)std::max<int64_t>(s->level_W[l], std::min<int64_t>(wmax, fill));
+}
+
 // after_panel(l): called once level l's L21 panel is launched (its L factor complete in stream order)
 int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nvalid, hipStream_t st,
                const std::function<void(int)>& after_panel = nullptr) {
@@ -285,7 +298,7 @@ int solve_all(pfr_solver* s, int which, int rhs_mode, const pfr::RhsDesc& rd, co
       lvl = s->d_reach_fronts[subset] + s->reach_ptr[subset][l];
       nf = s->reach_ptr[subset][l + 1] - s->reach_ptr[subset][l];
     }
-    pfr::launch_solve(which, rhs_mode, s->sym, s->P, lvl, nf, s->level_W[l], ngroups, s->F, s->Fc, s->WV, rd, Yin, Out,
+    pfr::launch_solve(which, rhs_mode, s->sym, s->P, lvl, nf, solve_W(s, l, nf), ngroups, s->F, s->Fc, s->WV, rd, Yin, Out,
                       reach, st);
   }
   HIP_TRY(hipGetLastError());
@@ -349,7 +362,7 @@ int sym_top_down_support(pfr_solver* s, const pfr::RhsDesc& rd, hipStream_t st) 
   const int ngroups = (int)(s->Fc / 64);
   for (int l = L - 1; l >= 0; --l) {
     const int nf = s->reach_ptr[1][l + 1] - s->reach_ptr[1][l];
-    pfr::launch_solve(1, 0, true, s->P, s->d_reach_fronts[1] + s->reach_ptr[1][l], nf, s->level_W[l], ngroups, s->F,
+    pfr::launch_solve(1, 0, true, s->P, s->d_reach_fronts[1] + s->reach_ptr[1][l], nf, solve_W(s, l, nf), ngroups, s->F,
                       s->Fc, s->WV, rd, s->Y, s->X, s->d_reach[0], st);
   }
   HIP_TRY(hipGetLastError());
@@ -361,7 +374,7 @@ int sym_top_down_pair(pfr_solver* s, hipStream_t st) {
   const int ngroups = (int)(s->Fc / 64);
   for (int l = L - 1; l >= 0; --l) {
     const int nf = s->level_ptr[l + 1] - s->level_ptr[l];
-    pfr::launch_usolve2(true, s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_W[l], s->level_maxf[l], ngroups,
+    pfr::launch_usolve2(true, s->P, s->d_level_fronts + s->level_ptr[l], nf, solve_W(s, l, nf), s->level_maxf[l], ngroups,
                         s->F, s->Fc, s->Y,
                         s->X, s->d_reach[0], s->d_reach[1], s->Y2, s->XA, s->d_reach[1], st);
   }
@@ -1119,7 +1132,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
         (void)hipEventRecord(s->lev_ev[l], st);
         (void)hipStreamWaitEvent(s->aux, s->lev_ev[l], 0);
         const int nf = s->reach_ptr[0][l + 1] - s->reach_ptr[0][l];
-        pfr::launch_solve(0, rmode, true, s->P, s->d_reach_fronts[0] + s->reach_ptr[0][l], nf, s->level_W[l], ngroups_,
+        pfr::launch_solve(0, rmode, true, s->P, s->d_reach_fronts[0] + s->reach_ptr[0][l], nf, solve_W(s, l, nf), ngroups_,
                           s->F, s->Fc, s->WV, rf, nullptr, s->Y, s->d_reach[0], s->aux);
       };
       rc = factor_all(s, 0, nullptr, 0, nv, st, hook);

@@ -1109,7 +1109,10 @@ __global__ __launch_bounds__(512) void k_lsolve_level(DevPattern P, const int* _
     if (k1 < ns) {
       cplx z[KBS];
 #pragma unroll
-      for (int t = 0; t < KBS; ++t) z[t] = cscale(V(k0 + min(t, kb - 1)), t < kb ? 1.0 : 0.0);
+      for (int t = 0; t < KBS; ++t) z[t] = V(k0 + min(t, kb - 1));
+      __builtin_amdgcn_sched_group_barrier(0x020, KBS, 0);   // the KBS loads in flight together
+#pragma unroll
+      for (int t = 0; t < KBS; ++t) z[t] = cscale(z[t], t < kb ? 1.0 : 0.0);
       for (int i = k1 + c.w; i < ns; i += c.W) {
         cplx v = V(i);
 #pragma unroll
@@ -1259,7 +1262,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
     if (k0 > 0) {
       cplx x[KBS];
 #pragma unroll
-      for (int t = 0; t < KBS; ++t) x[t] = cscale(V(k0 + min(t, kb - 1)), t < kb ? 1.0 : 0.0);
+      for (int t = 0; t < KBS; ++t) x[t] = V(k0 + min(t, kb - 1));
+      __builtin_amdgcn_sched_group_barrier(0x020, KBS, 0);   // the KBS loads in flight together
+#pragma unroll
+      for (int t = 0; t < KBS; ++t) x[t] = cscale(x[t], t < kb ? 1.0 : 0.0);
       for (int i = c.w; i < k0; i += c.W) {
         cplx v = V(i);
 #pragma unroll
@@ -1386,7 +1392,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
         if (act[v]) {
           cplx x[KBS];
 #pragma unroll
-          for (int t = 0; t < KBS; ++t) x[t] = cscale(XV(v, k0 + min(t, kb - 1)), t < kb ? 1.0 : 0.0);
+          for (int t = 0; t < KBS; ++t) x[t] = XV(v, k0 + min(t, kb - 1));
+          __builtin_amdgcn_sched_group_barrier(0x020, KBS, 0);   // the KBS loads in flight together
+#pragma unroll
+          for (int t = 0; t < KBS; ++t) x[t] = cscale(x[t], t < kb ? 1.0 : 0.0);
           for (int i = c.w; i < k0; i += c.W) {
             cplx y = XV(v, i);
 #pragma unroll
