@@ -491,7 +491,10 @@ __global__ __launch_bounds__(PFR_FAC_LB) void k_factor_sym(DevPattern P, const i
 // entries each step reads are the same for the four lane groups of a wave.
 // Item = (front, first row / column, kind): one wave = 16 frequencies x 4
 // consecutive rows (columns).
-constexpr int OB = 8;
+#ifndef PFR_OB
+#define PFR_OB 8
+#endif
+constexpr int OB = PFR_OB;   // columns per left-looking chunk of k_offdiag_level
 
 // Where the off-diagonal entries come from (the panel entries of L21 / U12 are
 // assembled here, at their first load, instead of being stored by the assembly
