@@ -121,6 +121,10 @@ class _Engine:
             max_batch = (-(-per_lane // n_chunks) + 63) // 64 * 64
         self.solvers = [_native.Solver(self.sym, device.index, max_batch) for _ in range(self.n_lanes)]
         self.streams = [torch.cuda.Stream(device) for _ in range(self.n_lanes)]
+        self._pool = None
+        if self.n_lanes > 1 and os.environ.get("PFR_PAR_LAUNCH", "1") != "0":
+            from concurrent.futures import ThreadPoolExecutor
+            self._pool = ThreadPoolExecutor(max_workers=self.n_lanes, thread_name_prefix="pfr-lane")
         self.solver = self.solvers[0]
         self.stiff = torch.as_tensor(np.ascontiguousarray(vals[:18].T), device=device)       # (nnz, 18)
         I0, I0c, I2, I2c = prob.I0, prob.I0Corr, prob.I2, prob.I2Corr
@@ -162,17 +166,30 @@ class _Engine:
 
     def _run(self, call, n, accum):
         """``call(solver, lo, hi, bufs)`` on every lane's stream; per-lane ``accum``
-        buffers (zeros like each given tensor) are summed into the given tensors."""
+        buffers (zeros like each given tensor) are summed into the given tensors.  With several
+        lanes each lane's launches are issued from its own host thread (the C calls release the
+        GIL): issued one after the other, the second lane started a whole sweep's enqueue time
+        (~9 ms) after the first and finished that much later."""
         cur = torch.cuda.current_stream(self.device)
-        parts = []
+        jobs = []
         for sv, st, (lo, hi) in zip(self.solvers, self.streams, self._split(n)):
             if hi <= lo:
                 continue
             st.wait_stream(cur)
-            with torch.cuda.stream(st):
-                bufs = [None if a is None else torch.zeros_like(a) for a in accum]
+            jobs.append((sv, st, lo, hi, [None if a is None else torch.zeros_like(a) for a in accum]))
+
+        def lane(job):
+            sv, st, lo, hi, bufs = job
+            with torch.cuda.device(self.device), torch.cuda.stream(st):
                 call(sv, lo, hi, bufs)
-            parts.append((st, bufs))
+
+        if len(jobs) > 1 and self._pool is not None:
+            for f in [self._pool.submit(lane, j) for j in jobs]:
+                f.result()
+        else:
+            for j in jobs:
+                lane(j)
+        parts = [(st, bufs) for _, st, _, _, bufs in jobs]
         for st, bufs in parts:
             cur.wait_stream(st)
             for a, b in zip(accum, bufs):
