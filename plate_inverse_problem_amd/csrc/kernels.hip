@@ -340,24 +340,24 @@ __device__ __forceinline__ void glds16(const cplx* g, cplx* lds_row) {
 // diagonal block and L rows, then ONE rank-8 update of the trailing lower triangle -- which is
 // read and written once per 8 pivots instead of once per 4 (the dominant traffic of this kernel).
 // Lane map as k_factor_level; up to 16 waves per front.
-template <int JBU>
-__device__ __forceinline__ void row_update8(const cplx* __restrict__ rd, cplx* __restrict__ wr, int64_t row_i,
-                                            int64_t row_k0, int f, int64_t Fc, int j0, int jend, int kb8,
-                                            const cplx (&l)[2 * KB]) {
+template <int R, int JBU>
+__device__ __forceinline__ void row_updateR(const cplx* __restrict__ rd, cplx* __restrict__ wr, int64_t row_i,
+                                            int64_t row_k0, int f, int64_t Fc, int j0, int jend, int kr,
+                                            const cplx (&l)[R]) {
 #pragma unroll 2
   for (int jb = j0; jb < jend; jb += JBU) {
-    cplx u[2 * KB][JBU], v[JBU];
+    cplx u[R][JBU], v[JBU];
 #pragma unroll
     for (int jj = 0; jj < JBU; ++jj) {
       const int j = min(jb + jj, jend - 1);
       v[jj] = rd[(row_i + j) * Fc];
 #pragma unroll
-      for (int t = 0; t < 2 * KB; ++t) u[t][jj] = rd[(row_k0 + (int64_t)min(t, kb8 - 1) * f + j) * Fc];
+      for (int t = 0; t < R; ++t) u[t][jj] = rd[(row_k0 + (int64_t)min(t, kr - 1) * f + j) * Fc];
     }
 #pragma unroll
     for (int jj = 0; jj < JBU; ++jj)
 #pragma unroll
-      for (int t = 0; t < 2 * KB; ++t) v[jj] = cfms(v[jj], l[t], u[t][jj]);   // l[t] = 0 for t >= kb8
+      for (int t = 0; t < R; ++t) v[jj] = cfms(v[jj], l[t], u[t][jj]);   // l[t] = 0 for t >= kr
 #pragma unroll
     for (int jj = 0; jj < JBU; ++jj)
       if (jb + jj < jend) wr[(row_i + jb + jj) * Fc] = v[jj];
@@ -369,6 +369,9 @@ __device__ __forceinline__ void row_update8(const cplx* __restrict__ rd, cplx* _
 #endif
 #ifndef PFR_FAC_LB
 #define PFR_FAC_LB 1024
+#endif
+#ifndef PFR_FAC_SB
+#define PFR_FAC_SB 2          // 4-pivot blocks per super-block (rank of the trailing update / 4)
 #endif
 
 __global__ __launch_bounds__(PFR_FAC_LB) void k_factor_sym(DevPattern P, const int* __restrict__ lvl, cplx* __restrict__ F,
@@ -448,34 +451,37 @@ __global__ __launch_bounds__(PFR_FAC_LB) void k_factor_sym(DevPattern P, const i
         }
     }
   };
-  for (int k0 = 0; k0 < ns; k0 += 2 * KB) {
-    const int kb8 = min(2 * KB, ns - k0), kbA = min(KB, kb8), kbB = kb8 - kbA;
-    diag(k0, kbA);
-    __syncthreads();
-    rows(k0, kbA, k0 + kbA);
-    __syncthreads();
-    if (kbB > 0) {
-      // block B's columns (lower part) updated by block A: rank kbA
-      for (int i = k0 + KB + r0; i < ns; i += rs) {
-        cplx l[KB];
+  constexpr int SB = PFR_FAC_SB, R = SB * KB;
+  for (int k0 = 0; k0 < ns; k0 += R) {
+    const int kr = min(R, ns - k0);
+#pragma unroll 1
+    for (int b = 0; b < SB; ++b) {
+      const int kb0 = k0 + KB * b, kbs = min(KB, kr - KB * b);
+      if (kbs <= 0) break;
+      if (b > 0) {
+        // this block's columns (lower part) updated by the super-block's earlier blocks: rank 4b
+        for (int i = kb0 + r0; i < ns; i += rs) {
+          cplx l[R];
 #pragma unroll
-        for (int t = 0; t < KB; ++t) l[t] = cscale(E(i, k0 + min(t, kbA - 1)), t < kbA ? 1.0 : 0.0);
-        row_update(base, base, (int64_t)i * f, (int64_t)k0 * f, f, Fc, k0 + KB, min(k0 + KB + kbB, i + 1), kbA, l);
+          for (int t = 0; t < R; ++t) l[t] = cscale(E(i, k0 + min(t, KB * b - 1)), t < KB * b ? 1.0 : 0.0);
+          row_updateR<R, 1>(base, base, (int64_t)i * f, (int64_t)k0 * f, f, Fc, kb0, min(kb0 + kbs, i + 1),
+                            KB * b, l);
+        }
+        __syncthreads();
       }
+      diag(kb0, kbs);
       __syncthreads();
-      diag(k0 + KB, kbB);
-      __syncthreads();
-      rows(k0 + KB, kbB, k0 + kb8);
+      rows(kb0, kbs, kb0 + kbs);
       __syncthreads();
     }
-    const int k1 = k0 + kb8;
+    const int k1 = k0 + kr;
     if (k1 < ns) {
-      // trailing lower triangle: A(i, j) -= L(i, k0:k1) U(k0:k1, j), k1 <= j <= i, rank kb8
+      // trailing lower triangle: A(i, j) -= L(i, k0:k1) U(k0:k1, j), k1 <= j <= i, rank kr
       for (int i = k1 + r0; i < ns; i += rs) {
-        cplx l[2 * KB];
+        cplx l[R];
 #pragma unroll
-        for (int t = 0; t < 2 * KB; ++t) l[t] = cscale(E(i, k0 + min(t, kb8 - 1)), t < kb8 ? 1.0 : 0.0);
-        row_update8<PFR_FAC_JBU>(base, base, (int64_t)i * f, (int64_t)k0 * f, f, Fc, k1, i + 1, kb8, l);
+        for (int t = 0; t < R; ++t) l[t] = cscale(E(i, k0 + min(t, kr - 1)), t < kr ? 1.0 : 0.0);
+        row_updateR<R, PFR_FAC_JBU>(base, base, (int64_t)i * f, (int64_t)k0 * f, f, Fc, k1, i + 1, kr, l);
       }
       __syncthreads();
     }
