@@ -1756,17 +1756,21 @@ __global__ __launch_bounds__(64) void k_contract(DevPattern P, const double* __r
 #pragma unroll
   for (int k = 0; k < NSTIFF_MAX; ++k) acc[k] = make_double2(0, 0);
   int64_t nz = nz0;
-  // 4 nonzeros per step: their 8 vector loads are in flight together
-  for (; nz + 4 <= nz1; nz += 4) {
-    cplx pv[4];
+  // CNZ nonzeros per step: their 2 CNZ vector loads are in flight together
+#ifndef PFR_CNZ
+#define PFR_CNZ 4
+#endif
+  constexpr int CNZ = PFR_CNZ;
+  for (; nz + CNZ <= nz1; nz += CNZ) {
+    cplx pv[CNZ];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < CNZ; ++u) {
       const cplx l = Lam[(int64_t)P.prow[nz + u] * Fc + q];
       const cplx x = X[(int64_t)P.pcol[nz + u] * Fc + q];
       pv[u] = cmul(l, x);
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < CNZ; ++u) {
       const double* s = stiff + (nz + u) * n_stiff;
 #pragma unroll
       for (int k = 0; k < NSTIFF_MAX; ++k)
