@@ -95,3 +95,21 @@ def test_schur_kernel_split_matches_oracle(blk_min, bc, monkeypatch):
     freqs = np.linspace(40.0, 600.0, 130)
     fr = p.solveForward(freqs)
     assert _rel(fr, oracle_for(p).fr(freqs, p.parameters)) < FR_RTOL
+
+
+def test_side_stream_forward_solve_matches_oracle(monkeypatch):
+    """PFR_AUX=1: the forward sparse L-solve runs on a side stream level by level behind the
+    factorisation (event-ordered); loss and gradient must equal the in-stream path's."""
+    from oracle.plate_oracle import loss_and_grad
+    monkeypatch.setenv("PFR_AUX", "1")
+    monkeypatch.setenv("PFR_LANES", "1")
+    p = make_problem("orthotropic", ny=5, device="cuda:0")
+    freqs = np.linspace(40.0, 600.0, 96)
+    ref = p.solveForward(freqs) * np.exp(0.1j) * 1.02
+    theta = p.parameters * 1.04
+    x = torch.tensor(theta, requires_grad=True)
+    val = p.getLossFunction(freqs, ref, "MSE_LOG_AFC")(x)
+    val.backward()
+    lo, go = loss_and_grad(oracle_for(p), freqs, ref, "MSE_LOG_AFC", theta)
+    assert abs(val.item() - lo) / abs(lo) < FR_RTOL
+    assert _rel(x.grad.numpy(), go) < GRAD_RTOL
