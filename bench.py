@@ -164,6 +164,14 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # backward errors of the last timed step's solves (checked on the device in every sweep)
+    berr = eng.last_berr.cpu().numpy()
+    check = {"measure": "componentwise backward error max_i |b - A x|_i / (|A||x| + |b|)_i per frequency "
+                        "(UMFPACK's omega1), on the device in every sweep",
+             "mode": eng.check_mode, "tol": eng.check_tol,
+             "max_forward": float(np.nanmax(berr[:, 0])), "max_adjoint": float(np.nanmax(berr[:, 1])),
+             "median_forward": float(np.nanmedian(berr[:, 0])),
+             "flagged": int(np.count_nonzero(eng.last_flags)) if eng.last_flags is not None else None}
     eng.set_timing(True, kernels=True)
     step()
     torch.cuda.synchronize()
@@ -256,6 +264,7 @@ def main():
         "phase_ms": {"factor": phase[0], "fwd_solves": phase[1], "functional": phase[2],
                      "adj_solves": phase[3], "contract": phase[4], "note": "device ms per step summed over lanes"},
         "loss": val,
+        "backward_error": check,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(prob, freqs, ref, theta)

@@ -34,6 +34,15 @@ extern "C" {
 
 /* per-frequency status flags (bitwise OR into an int32 array) */
 #define PFR_FLAG_BAD_PIVOT 1 /* zero / non-finite static pivot */
+#define PFR_FLAG_BACKWARD_ERROR 2     /* forward solution: normwise backward error above the tolerance */
+#define PFR_FLAG_BACKWARD_ERROR_ADJ 4 /* adjoint solution: normwise backward error above the tolerance */
+
+/* pfr_set_check modes (bitwise OR) */
+#define PFR_CHECK_FORWARD 1   /* backward error of the forward solution (A x = b) */
+#define PFR_CHECK_ADJOINT 2   /* backward error of the adjoint solution (A^T l = g; loss sweeps, transposed solves) */
+#define PFR_CHECK_REFINE 4    /* one step of iterative refinement of the forward (and, in loss sweeps, the
+                               * adjoint) solution on the same factors, x += A^{-1} (b - A x), before the
+                               * checks (UMFPACK refines by default, up to 2 steps) */
 
 /* loss types (Problem.py:948-975) */
 #define PFR_LOSS_NONE -1
@@ -187,6 +196,21 @@ PFR_API int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int
 PFR_API int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t loss_type,
                               const double* ref_dev, double scale, int32_t n_dir, const double* dcoef,
                               double* loss_dev, double* w_dev, double* h_dev, int32_t* flags_dev, void* stream);
+
+/* Backward-error checks of the solves (the failure detection a static pivot order needs; the
+ * reference turns UMFPACK's status into an exception, umfpack_interface.h:10-18, and its solves
+ * refine by default).  After each solve the componentwise (Oettli-Prager) backward error
+ *   berr = max_i |b - A x|_i / (|A| |x| + |b|)_i        (|z| = |re| + |im|)
+ * of the ORIGINAL system is computed on the device per frequency / batch item -- UMFPACK's sparse
+ * backward error, invariant under row / column scaling -- and the item's flag
+ * PFR_FLAG_BACKWARD_ERROR (forward) / PFR_FLAG_BACKWARD_ERROR_ADJ (adjoint) is set when berr > tol
+ * (or not finite).  mode: PFR_CHECK_* bits (0 = off, the default).  berr_dev (device, may be NULL):
+ * every later pfr_sweep / pfr_solve call writes berr_dev[2 q] (forward) and berr_dev[2 q + 1]
+ * (adjoint) for its items q = 0 .. nfreq - 1 (slots of a solve that is not checked are left
+ * alone), so it must hold 2 nfreq doubles of every such call.  With PFR_CHECK_REFINE a loss sweep
+ * runs its forward solve, refinement and adjoint in sequence (not the paired top-down pass).  Not
+ * applied by pfr_hessian_sweep. */
+PFR_API int pfr_set_check(pfr_solver* s, int32_t mode, double tol, double* berr_dev);
 
 /* Per-phase device times [ms] of the last pfr_sweep/pfr_solve call on this solver, measured with HIP
  * events on the call's stream (0 = factor, 1 = forward solves, 2 = functional, 3 = adjoint solves,

@@ -18,6 +18,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import numpy as np
+
 from .Accelerometer import Accelerometer
 
 TEMPLATES = ['sh_r', 'sh_i', 'symm']
@@ -79,17 +81,46 @@ class Geometry:
         self.accel_r = accelerometer.radius
         self.ny = int(ny)
         self.nx = max(1, int(round(self.ny * self.length / self.width)))
+        self._ff = None
+
+    @classmethod
+    def from_freefem_output(cls, source, height: float, accelerometer: Accelerometer = None) -> "Geometry":
+        """A geometry discretised by FreeFem++: ``source`` is the standard output (a path or the text)
+        of the reference's matrix-export script -- the geometry's ``.edp`` followed by the varf block
+        of ``pyFFInterface.py:175-275`` -- as pyFreeFem reads it (``fem.freefem``).  The 26-matrix
+        layout, union pattern and solver then proceed exactly as for a template geometry."""
+        from .fem.freefem import load_freefem_output
+        ff = load_freefem_output(source)
+        g = cls.__new__(cls)
+        g.template = 'freefem'
+        xy = ff["Th"].vertices
+        g.length = float(xy[:, 0].max() - xy[:, 0].min())
+        g.width = float(xy[:, 1].max() - xy[:, 1].min())
+        g.height = float(height)
+        g.accel_x, g.accel_y = float(ff["xtest"]), float(ff["ytest"])
+        g.accel_r = accelerometer.radius if accelerometer is not None else None
+        g.nx = g.ny = None
+        g._ff = ff
+        return g
 
     @property
     def n_dofs(self) -> int:
+        if self._ff is not None:
+            return 2 * np.asarray(self._ff["vBCLh"]).size + np.asarray(self._ff["vBCMh"]).size
         return dofs_for_density(self.ny, self.length, self.width)
 
     def build_varfs(self) -> dict:
-        """Mesh the strip and assemble every varf of ``pyFFInterface.py:175-275``."""
+        """Mesh the strip and assemble every varf of ``pyFFInterface.py:175-275`` (or return the
+        FreeFEM-exported ones)."""
+        if self._ff is not None:
+            return dict(self._ff)
         from .fem import strip_mesh, plate_varfs
         mesh = strip_mesh(self.length, self.width, self.nx, self.ny)
         return plate_varfs(mesh, (self.accel_x, self.accel_y), self.accel_r)
 
     def __str__(self):
+        if self._ff is not None:
+            return (f'Geometry from FreeFEM output: {self.length} x {self.width} x {self.height} m, accelerometer '
+                    f'at ({self.accel_x}, {self.accel_y}), {self.n_dofs} DOF.')
         return (f'Geometry {self.template}: {self.length} x {self.width} x {self.height} m, '
                 f'accelerometer at ({self.accel_x}, {self.accel_y}), mesh {self.nx} x {self.ny} cells.')

@@ -17,10 +17,10 @@ differences), with the reference's non-conjugate transpose (``Sparse.py:211-219`
 """
 from __future__ import annotations
 
-import functools
 import json
 import os
 import warnings
+import weakref
 from typing import Callable
 
 import numpy as np
@@ -107,25 +107,11 @@ class _Engine:
                                     relax=tuple(int(v) for v in relax.split(",")) if relax else None,
                                     max_ns=int(max_ns) if max_ns else None)
         self.stats = self.sym.stats()
-        if lanes is None:
-            lanes = int(os.environ.get("PFR_LANES", "2"))
-        n_freqs = max(1, n_freqs)
-        self.n_lanes = max(1, min(lanes, -(-n_freqs // 64)))
-        per_lane = -(-n_freqs // self.n_lanes)
-        if not max_batch:
-            # per lane as many frequencies per chunk as fit in its share of ~85% of free
-            # HBM (multiple of 64, <= 4096), even chunks
-            free, _ = torch.cuda.mem_get_info(device)
-            cap = max(64, min(4096, int(0.85 * free / self.n_lanes / self.sym.workspace_bytes(64)) * 64))
-            n_chunks = -(-per_lane // cap)
-            max_batch = (-(-per_lane // n_chunks) + 63) // 64 * 64
-        self.solvers = [_native.Solver(self.sym, device.index, max_batch) for _ in range(self.n_lanes)]
-        self.streams = [torch.cuda.Stream(device) for _ in range(self.n_lanes)]
-        self._pool = None
-        if self.n_lanes > 1 and os.environ.get("PFR_PAR_LAUNCH", "1") != "0":
-            from concurrent.futures import ThreadPoolExecutor
-            self._pool = ThreadPoolExecutor(max_workers=self.n_lanes, thread_name_prefix="pfr-lane")
-        self.solver = self.solvers[0]
+        self._lanes_req = int(os.environ.get("PFR_LANES", "2")) if lanes is None else int(lanes)
+        self._fixed_batch = max_batch
+        self.solvers, self.streams, self._pool = [], [], None
+        self.n_lanes = 0
+        self._sized_for = set()
         self.stiff = torch.as_tensor(np.ascontiguousarray(vals[:18].T), device=device)       # (nnz, 18)
         I0, I0c, I2, I2c = prob.I0, prob.I0Corr, prob.I2, prob.I2Corr
         mass = I0 * (vals[18] + vals[20] + vals[22]) + I0c * (vals[19] + vals[21] + vals[23]) \
@@ -135,14 +121,81 @@ class _Engine:
         self.K = torch.empty(self.keep.size, dtype=torch.complex128, device=device)
         self.e = np.concatenate([np.zeros(12), RHS_WEIGHTS_D])
         aU, aV, aW = prob.averaging_vectors()
-        sup = np.nonzero((aU != 0) | (aV != 0) | (aW != 0))[0]
+        self._sup = np.nonzero((aU != 0) | (aV != 0) | (aW != 0))[0]
+        self._a3 = np.stack([aU[self._sup], aV[self._sup], aW[self._sup]])
+        self._ts = prob.accelerometer.transverse_sensitivity
+        self.rhs = prob.vec
+        self._coef_key = None
+        self.last_berr = None          # (F, 2) componentwise backward errors of the last sweep (device)
+        self.last_flags = None         # its status flags (host)
+        # backward-error checks of every solve (pfr_set_check): forward + adjoint by default,
+        # PFR_CHECK=<PFR_CHECK_* bits> / PFR_CHECK_TOL override; refinement (bit 4) off by default
+        self.check_mode = int(os.environ.get("PFR_CHECK", str(_native.PFR_CHECK_FORWARD | _native.PFR_CHECK_ADJOINT)))
+        self.check_tol = float(os.environ.get("PFR_CHECK_TOL", "1e-10"))
+        self.ensure(n_freqs)
+
+    def _shape_for(self, n_freqs: int):
+        """(lanes, frequencies per chunk) for a sweep of ``n_freqs``: up to ``lanes`` lanes of at
+        least 64 frequencies; per lane as many frequencies per chunk as fit in its share of ~85 %
+        of the free HBM (multiple of 64, <= 4096), in even chunks."""
+        n_freqs = max(1, n_freqs)
+        n_lanes = max(1, min(self._lanes_req, -(-n_freqs // 64)))
+        if self._fixed_batch:
+            return n_lanes, int(self._fixed_batch)
+        per_lane = -(-n_freqs // n_lanes)
+        free, _ = torch.cuda.mem_get_info(self.device)
+        free += sum(self.sym.workspace_bytes(sv.max_batch) for sv in self.solvers)   # ours, if rebuilt
+        cap = max(64, min(4096, int(0.85 * free / n_lanes / self.sym.workspace_bytes(64)) * 64))
+        n_chunks = -(-per_lane // cap)
+        return n_lanes, (-(-per_lane // n_chunks) + 63) // 64 * 64
+
+    def ensure(self, n_freqs: int):
+        """Size the lanes for a sweep of ``n_freqs`` frequencies.  The solvers are rebuilt only when
+        the sweep needs more lanes or larger chunks than the current ones have (a small first call
+        must not pin 1 lane and 64-frequency chunks on every later large sweep); smaller sweeps run
+        on the existing solvers."""
+        if self.solvers:
+            per_lane = -(-max(1, n_freqs) // self.n_lanes)
+            if n_freqs in self._sized_for or (min(self._lanes_req, -(-max(1, n_freqs) // 64)) <= self.n_lanes
+                                              and per_lane <= self.max_batch):
+                return
+        self._sized_for.add(n_freqs)
+        lanes, batch = self._shape_for(n_freqs)
+        if self.solvers and lanes <= self.n_lanes and batch <= self.max_batch:
+            return
+        lanes = max(lanes, self.n_lanes)
+        batch = max(batch, self.max_batch if self.solvers else 0)
+        if self.solvers:
+            torch.cuda.synchronize(self.device)
+        self.solvers, self.streams = [], []       # free the old workspaces before allocating
+        if self._pool is not None:
+            self._pool.shutdown(wait=True)
+            self._pool = None
+        self.n_lanes = lanes
+        self.solvers = [_native.Solver(self.sym, self.device.index, batch) for _ in range(lanes)]
+        self.streams = [torch.cuda.Stream(self.device) for _ in range(lanes)]
+        if lanes > 1 and os.environ.get("PFR_PAR_LAUNCH", "1") != "0":
+            from concurrent.futures import ThreadPoolExecutor
+            self._pool = ThreadPoolExecutor(max_workers=lanes, thread_name_prefix="pfr-lane")
         for sv in self.solvers:
             sv.set_stiffness(self.stiff, self.e)
             sv.set_operator(torch.view_as_real(self.K), self.mass)      # K(theta) shared by the lanes
-            sv.set_functional(sup, np.stack([aU[sup], aV[sup], aW[sup]]),
-                              prob.accelerometer.transverse_sensitivity)
-        self.rhs = prob.vec
-        self._coef_key = None
+            sv.set_functional(self._sup, self._a3, self._ts)
+            sv.set_check(self.check_mode, self.check_tol)
+        self._coef_key = None          # new solvers: rhs scale not set yet
+
+    def set_check(self, mode: int | None = None, tol: float | None = None):
+        """Backward-error check mode (PFR_CHECK_* bits) and flag tolerance of every lane."""
+        if mode is not None:
+            self.check_mode = int(mode)
+        if tol is not None:
+            self.check_tol = float(tol)
+        for sv in self.solvers:
+            sv.set_check(self.check_mode, self.check_tol)
+
+    @property
+    def solver(self):
+        return self.solvers[0]
 
     @property
     def max_batch(self) -> int:
@@ -175,35 +228,57 @@ class _Engine:
         for sv, st, (lo, hi) in zip(self.solvers, self.streams, self._split(n)):
             if hi <= lo:
                 continue
+            # the lane's accumulation buffers are zero-filled on the current stream BEFORE the lane
+            # stream is ordered after it (k_reduce accumulates into them with +=)
+            bufs = [None if a is None else torch.zeros_like(a) for a in accum]
             st.wait_stream(cur)
-            jobs.append((sv, st, lo, hi, [None if a is None else torch.zeros_like(a) for a in accum]))
+            jobs.append((sv, st, lo, hi, bufs))
 
         def lane(job):
             sv, st, lo, hi, bufs = job
             with torch.cuda.device(self.device), torch.cuda.stream(st):
                 call(sv, lo, hi, bufs)
 
+        err = None
         if len(jobs) > 1 and self._pool is not None:
-            for f in [self._pool.submit(lane, j) for j in jobs]:
-                f.result()
+            from concurrent.futures import wait
+            futs = [self._pool.submit(lane, j) for j in jobs]
+            wait(futs)                       # every lane has issued its work (or failed) ...
+            errs = [f.exception() for f in futs if f.exception() is not None]
+            err = errs[0] if errs else None
         else:
             for j in jobs:
-                lane(j)
-        parts = [(st, bufs) for _, st, _, _, bufs in jobs]
-        for st, bufs in parts:
+                try:
+                    lane(j)
+                except Exception as e:       # noqa: BLE001 -- re-raised once every lane is joined
+                    err = e
+                    break
+        for _, st, _, _, bufs in jobs:       # ... and the current stream is ordered after all of them
             cur.wait_stream(st)
+            for b in bufs:
+                if b is not None:
+                    b.record_stream(cur)
+        if err is not None:
+            raise err
+        for _, st, _, _, bufs in jobs:
             for a, b in zip(accum, bufs):
                 if a is not None:
-                    b.record_stream(cur)
                     a.add_(b)
 
     def sweep(self, freqs, loss_type=_native.LOSS_NONE, ref=None, scale=1.0, fr=None, loss=None, w=None,
-              flags=None):
-        """``Solver.sweep`` over all lanes (fr / flags written in place, loss / w accumulated)."""
+              flags=None, berr=None):
+        """``Solver.sweep`` over all lanes (fr / flags / berr (F, 2) written in place, loss / w
+        accumulated)."""
         def call(sv, lo, hi, bufs):
-            sv.sweep(freqs[lo:hi], loss_type, ref=None if ref is None else ref[lo:hi], scale=scale,
-                     fr=None if fr is None else fr[lo:hi], loss=bufs[0], w=bufs[1],
-                     flags=None if flags is None else flags[lo:hi])
+            if berr is not None:
+                sv.set_check(self.check_mode, self.check_tol, berr[lo:hi])
+            try:
+                sv.sweep(freqs[lo:hi], loss_type, ref=None if ref is None else ref[lo:hi], scale=scale,
+                         fr=None if fr is None else fr[lo:hi], loss=bufs[0], w=bufs[1],
+                         flags=None if flags is None else flags[lo:hi])
+            finally:
+                if berr is not None:
+                    sv.set_check(self.check_mode, self.check_tol)
         self._run(call, freqs.numel(), [loss, w])
 
     def hessian_sweep(self, freqs, loss_type, ref, scale, dcoef, loss=None, w=None, h=None, flags=None):
@@ -240,8 +315,10 @@ class _SweepFR(torch.autograd.Function):
         engine.set_coefficients(cn)
         fr = torch.empty(freqs.numel(), dtype=torch.float64, device=engine.device)
         flags = torch.zeros(freqs.numel(), dtype=torch.int32, device=engine.device)
-        engine.sweep(freqs, _native.LOSS_NONE, fr=fr, flags=flags)
-        _check_flags(flags)
+        berr = torch.full((freqs.numel(), 2), float('nan'), dtype=torch.float64, device=engine.device)
+        engine.sweep(freqs, _native.LOSS_NONE, fr=fr, flags=flags, berr=berr)
+        engine.last_berr = berr
+        engine.last_flags = _check_flags(flags)
         ctx.engine, ctx.freqs, ctx.cn = engine, freqs, cn
         return fr
 
@@ -268,9 +345,11 @@ class _SweepLoss(torch.autograd.Function):
         w = torch.zeros(18, dtype=torch.complex128, device=engine.device)
         loss = torch.zeros(1, dtype=torch.float64, device=engine.device)
         flags = torch.zeros(freqs.numel(), dtype=torch.int32, device=engine.device)
+        berr = torch.full((freqs.numel(), 2), float('nan'), dtype=torch.float64, device=engine.device)
         engine.sweep(freqs, loss_id, ref=torch.view_as_real(ref), scale=1.0 / n_total,
-                     loss=loss, w=torch.view_as_real(w), flags=flags)
-        _check_flags(flags)
+                     loss=loss, w=torch.view_as_real(w), flags=flags, berr=berr)
+        engine.last_berr = berr
+        engine.last_flags = _check_flags(flags)
         packed = torch.cat([loss.to(torch.complex128), w])
         if reduce_fn is not None:
             packed = reduce_fn(packed)
@@ -284,10 +363,22 @@ class _SweepLoss(torch.autograd.Function):
 
 
 def _check_flags(flags):
-    bad = int((flags != 0).sum().item())
-    if bad:
-        warnings.warn(f"{bad} frequencies hit a zero/non-finite static pivot (PFR_FLAG_BAD_PIVOT); "
-                      "their results are not reliable", RuntimeWarning)
+    """Warn about frequencies whose solves were flagged (one device->host copy of F int32)."""
+    f = flags.cpu().numpy()
+    if not f.any():
+        return f
+    msgs = []
+    for bit, what in ((_native.PFR_FLAG_BAD_PIVOT, "hit a zero/non-finite static pivot"),
+                      (_native.PFR_FLAG_BACKWARD_ERROR, "have a forward solution whose backward error exceeds "
+                                                        "the check tolerance"),
+                      (_native.PFR_FLAG_BACKWARD_ERROR_ADJ, "have an adjoint solution whose backward error exceeds "
+                                                            "the check tolerance")):
+        n = int(np.count_nonzero(f & bit))
+        if n:
+            msgs.append(f"{n} frequencies {what}")
+    warnings.warn("; ".join(msgs) + " -- their results are not reliable (Problem.solveForwardChecked reports "
+                  "the backward errors; PFR_CHECK=7 adds a refinement step)", RuntimeWarning)
+    return f
 
 
 class Problem:
@@ -318,6 +409,7 @@ class Problem:
         self._device = device
         self._max_batch = max_batch
         self._engine = None
+        self._fr_function = None
         self._build_system()
 
     # ------------------------------------------------------------------ setup
@@ -421,12 +513,16 @@ class Problem:
             self._device = _default_device()
         return torch.device(self._device)
 
-    def engine(self, n_freqs: int = 1024) -> _Engine:
+    def engine(self, n_freqs: int | None = None) -> _Engine:
+        """The device engine, sized -- and re-sized when a sweep needs more -- for ``n_freqs``
+        (``None``: as it is, or for 1024 frequencies when it is first built)."""
         if self._engine is None:
             dev = self.device
             if dev.type != 'cuda':
                 raise _native.NativeError('the plate solver needs a ROCm device (no CPU fallback)')
-            self._engine = _Engine(self, dev, n_freqs, self._max_batch)
+            self._engine = _Engine(self, dev, 1024 if n_freqs is None else n_freqs, self._max_batch)
+        elif n_freqs is not None:
+            self._engine.ensure(n_freqs)
         return self._engine
 
     def _transform(self):
@@ -437,10 +533,13 @@ class Problem:
                                else freqs, dtype=torch.float64, device=self.device).contiguous()
 
     # ------------------------------------------------------------------ API
-    @functools.cache
     def getFRFunction(self) -> Callable:
         """``fr(freqs, params) -> (F,) float64 tensor`` on the device, differentiable in params
-        (``Problem.py:377-518``)."""
+        (``Problem.py:377-518``).  Cached per instance while the caller holds it (the reference's ``functools.cache`` on the
+        method would keep every Problem -- and its device workspaces -- alive for the process)."""
+        fn = self._fr_function() if self._fr_function is not None else None
+        if fn is not None:
+            return fn
         transform = self._transform()
 
         def fr_function(freqs, params):
@@ -449,6 +548,7 @@ class Problem:
             c = _coeffs18(transform, p.to(torch.float64).cpu())
             return _SweepFR.apply(c, self.engine(f.numel()), f)
 
+        self._fr_function = weakref.ref(fr_function)    # no Problem <-> closure reference cycle
         return fr_function
 
     getAFCFunction = getFRFunction
@@ -461,6 +561,30 @@ class Problem:
             return self.getFRFunction()(freqs, params).cpu().numpy()
 
     solve_forward = solveForward
+
+    def solveForwardChecked(self, freqs, params=None, *, refine: bool = False):
+        """``(fr, berr, flags)``: the forward sweep with the componentwise backward error of every
+        frequency's solve (``max_i |b - A x|_i / (|A||x| + |b|)_i``, the measure UMFPACK's
+        refinement monitors) and its status flags (PFR_FLAG_*); ``refine=True`` adds one step of
+        iterative refinement on the same factors first (as the reference's UMFPACK solves do by
+        default, ``InnerState.h:246-247`` with a NULL Control)."""
+        if params is None:
+            params = self.parameters
+        f = self._freqs(freqs)
+        p = torch.as_tensor(np.asarray(params, dtype=np.float64))
+        c = _coeffs18(self._transform(), p).detach().numpy()
+        eng = self.engine(f.numel())
+        eng.set_coefficients(c)
+        fr = torch.empty(f.numel(), dtype=torch.float64, device=eng.device)
+        flags = torch.zeros(f.numel(), dtype=torch.int32, device=eng.device)
+        berr = torch.full((f.numel(), 2), float('nan'), dtype=torch.float64, device=eng.device)
+        mode = eng.check_mode
+        eng.set_check(mode | _native.PFR_CHECK_FORWARD | (_native.PFR_CHECK_REFINE if refine else 0))
+        try:
+            eng.sweep(f, _native.LOSS_NONE, fr=fr, flags=flags, berr=berr)
+        finally:
+            eng.set_check(mode)
+        return fr.cpu().numpy(), berr[:, 0].cpu().numpy(), flags.cpu().numpy()
 
     def getLossFunction(self, frequencies, reference_fr, func_type: str, scaling_params=None,
                         *, distributed: bool = False) -> Callable:

@@ -19,6 +19,7 @@ Gradients follow torch's conjugate-Wirtinger convention (``torch.linalg.solve``)
 """
 from __future__ import annotations
 
+import warnings
 from multiprocessing import cpu_count
 
 import numpy as np
@@ -57,6 +58,9 @@ class SolverState:
         if e["solver"] is None:
             mb = e["max_batch"] or max(64, min(1024, (batch + 63) // 64 * 64))
             e["solver"] = _native.Solver(e["sym"], device.index, mb)
+            # UMFPACK's default solve (the reference passes a NULL Control) refines up to 2 steps; the
+            # static pivot order here gets one refinement step and a backward-error check of every solve
+            e["solver"].set_check(CHECK_MODE, CHECK_TOL)
         return e["solver"]
 
     def entry(self, num: int) -> dict:
@@ -64,6 +68,20 @@ class SolverState:
 
 
 _SOLVER_STATE = SolverState()
+CHECK_MODE = _native.PFR_CHECK_FORWARD | _native.PFR_CHECK_ADJOINT | _native.PFR_CHECK_REFINE
+CHECK_TOL = 1e-10
+
+
+def _flags(flags):
+    """Bad static pivot -> error (UMFPACK reports a singular matrix as an error status,
+    umfpack_interface.h:10-18); backward error above the tolerance after refinement -> warning."""
+    f = flags.cpu().numpy()
+    if (f & _native.PFR_FLAG_BAD_PIVOT).any():
+        raise _native.NativeError("zero/non-finite static pivot in spsolve (matrix singular in the fixed order)")
+    bad = int(np.count_nonzero(f & (_native.PFR_FLAG_BACKWARD_ERROR | _native.PFR_FLAG_BACKWARD_ERROR_ADJ)))
+    if bad:
+        warnings.warn(f"spsolve: {bad} of {f.size} solves keep a componentwise backward error above {CHECK_TOL:g} "
+                      "after refinement (static pivot order unstable for these matrices)", RuntimeWarning)
 
 
 def create_symbolic(N: int, indices: np.ndarray, mat_dtype=np.complex128, *, device=None, max_batch=None):
@@ -103,8 +121,7 @@ def _raw_solve(num, data, b, transpose):
     x = torch.empty_like(b)
     flags = torch.zeros(B, dtype=torch.int32, device=b.device)
     s.solve(torch.view_as_real(data), ds, torch.view_as_real(b), e["N"], torch.view_as_real(x), transpose, B, flags)
-    if int((flags != 0).sum()):
-        raise _native.NativeError("zero/non-finite static pivot in spsolve (matrix singular in the fixed order)")
+    _flags(flags)
     return x
 
 
@@ -119,8 +136,7 @@ def _raw_solve_multi(num, data, b, transpose):
     flags = torch.zeros(B, dtype=torch.int32, device=b.device)
     s.solve_multi(torch.view_as_real(data), ds, torch.view_as_real(b), e["N"], B * e["N"], torch.view_as_real(x),
                   B * e["N"], transpose, B, J, flags)
-    if int((flags != 0).sum()):
-        raise _native.NativeError("zero/non-finite static pivot in spsolve (matrix singular in the fixed order)")
+    _flags(flags)
     return x
 
 

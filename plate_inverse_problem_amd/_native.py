@@ -21,6 +21,9 @@ HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__fil
 
 PFR_OK = 0
 PFR_FLAG_BAD_PIVOT = 1
+PFR_FLAG_BACKWARD_ERROR = 2
+PFR_FLAG_BACKWARD_ERROR_ADJ = 4
+PFR_CHECK_FORWARD, PFR_CHECK_ADJOINT, PFR_CHECK_REFINE = 1, 2, 4
 LOSS_NONE, LOSS_MSE, LOSS_RMSE, LOSS_MSE_AFC, LOSS_MSE_LOG_AFC, LOSS_COTANGENT = -1, 0, 1, 2, 3, 4
 LOSS_IDS = {"MSE": LOSS_MSE, "RMSE": LOSS_RMSE, "MSE_AFC": LOSS_MSE_AFC, "MSE_LOG_AFC": LOSS_MSE_LOG_AFC}
 
@@ -74,6 +77,7 @@ _PROTOS = {
                                   C.c_int32, _P, _P]),
     "pfr_hessian_sweep": (C.c_int, [_P, C.c_int32, _P, C.c_int32, _P, C.c_double, C.c_int32, _P, _P, _P, _P, _P,
                                     _P]),
+    "pfr_set_check": (C.c_int, [_P, C.c_int32, C.c_double, _P]),
     "pfr_set_timing": (C.c_int, [_P, C.c_int32]),
     "pfr_last_timings": (C.c_int, [_P, _DP]),
     "pfr_last_kernel_timings": (C.c_int, [_P, _DP, _P]),
@@ -288,6 +292,12 @@ class Solver:
     def matvec(self, data, data_stride, x, x_stride, y, transpose, batch):
         check(lib().pfr_matvec(self._h, int(batch), _ptr(data), int(data_stride), _ptr(x), int(x_stride), _ptr(y),
                                int(bool(transpose)), self._stream(y)), "pfr_matvec")
+
+    # ---- backward-error checks
+    def set_check(self, mode: int, tol: float, berr=None):
+        """PFR_CHECK_* bits, flag tolerance; ``berr`` (device float64, 2 per frequency of each later
+        call, or None) receives the componentwise backward errors (forward, adjoint)."""
+        check(lib().pfr_set_check(self._h, int(mode), float(tol), _ptr(berr)), "pfr_set_check")
 
     # ---- timing
     def set_timing(self, on, kernels: bool = False):

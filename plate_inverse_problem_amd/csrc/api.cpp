@@ -106,6 +106,7 @@ struct pfr_solver {
   int32_t* d_reach_fronts[2] = {nullptr, nullptr};
   std::vector<int32_t> reach_ptr[2];
   double2 *F = nullptr, *WV = nullptr, *X = nullptr, *Y = nullptr, *XA = nullptr, *G = nullptr, *Y2 = nullptr;
+  double2* XR = nullptr;                // refinement correction of the adjoint (PFR_CHECK_REFINE)
   // Hessian sweep: permuted matrix by rows and by columns ((ptr, index, nz) each),
   // tangent solution / adjoint vectors, combined tangent operators (lazily allocated)
   int32_t *d_rptr = nullptr, *d_ridx = nullptr, *d_rnz = nullptr;
@@ -143,6 +144,18 @@ struct pfr_solver {
   std::vector<ChunkEvents> tev;
   int n_tev = 0;                        // chunks recorded by the last call
   int64_t alg_bytes[5]{};               // algorithmic HBM bytes per frequency of each class (one sweep)
+  // launch-shape tuning knobs, read from the environment when the solver is created (so that a
+  // process can build solvers with different settings, e.g. tests forcing each kernel variant):
+  // PFR_SOLVE_WMAX (waves per solve workgroup, at most), PFR_FAC_WMAX (waves per A11 LU
+  // workgroup, at most), PFR_US2_SMALL (largest front of a level the paired top-down solve treats
+  // with its low-register small-front variant)
+  int solve_wmax = 8, fac_wmax = 16, us2_small = 110;
+  // backward-error checks (pfr_set_check): PFR_CHECK_* bits, tolerance, optional per-item output;
+  // per-frequency maximum scratch (kept zero between checks)
+  int check_mode = 0;
+  double check_tol = 1e-10;
+  double* berr_out = nullptr;
+  double* d_berr_acc = nullptr;
 
   ~pfr_solver() {
     for (auto e : lev_ev) (void)hipEventDestroy(e);
@@ -179,7 +192,7 @@ int64_t workspace_bytes(const Symbolic& S, int64_t Fc) {
   int64_t b = 0;
   b += S.factor_entries * Fc * 16;   // F
   b += S.total_rows * Fc * 16;       // WV
-  b += 5 * (int64_t)S.n * Fc * 16;   // X, Y, XA, G, Y2
+  b += 6 * (int64_t)S.n * Fc * 16;   // X, Y, XA, G, Y2, XR
   b += Fc * (8 + 8 + 4 + 16);        // freqs, loss terms, flags, tq
   return b;
 }
@@ -221,10 +234,7 @@ void reset_timing(pfr_solver* s) { s->n_tev = 0; }
 // raised (up to 8) when the launch has too few workgroups to fill the chip -- the sparse passes
 // and the top levels, which are latency-bound: every wave more takes rows off each wave's chain.
 int solve_W(const pfr_solver* s, int l, int nf) {
-  static const int wmax = [] {
-    const char* e = getenv("PFR_SOLVE_WMAX");   // tuning knob
-    return e ? atoi(e) : 8;
-  }();
+  const int wmax = s->solve_wmax;
   const int64_t wgs = std::max<int64_t>(1, (int64_t)nf * (s->Fc / 64));
   const int64_t fill = (4096 + wgs - 1) / wgs;
   return (int)std::max<int64_t>(s->level_W[l], std::min<int64_t>(wmax, fill));
@@ -251,10 +261,7 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     // each (no idle waves at the block barriers); few large fronts -> more waves
     // (symmetric kernel: up to 16 waves -- the top levels' few fronts are latency-bound, every
     // wave more takes rows off each wave's serial chain)
-    static const int fac_wmax = [] {
-      const char* e = getenv("PFR_FAC_WMAX");   // tuning knob
-      return e ? atoi(e) : 16;
-    }();
+    const int fac_wmax = s->fac_wmax;
     const int64_t wgs = (int64_t)nf * ngroups * pfr::FAC_G;
     const int64_t wfill = (4096 + wgs - 1) / wgs;
     const int Wp = (int)std::max<int64_t>(
@@ -374,7 +381,8 @@ int sym_top_down_pair(pfr_solver* s, hipStream_t st) {
   const int ngroups = (int)(s->Fc / 64);
   for (int l = L - 1; l >= 0; --l) {
     const int nf = s->level_ptr[l + 1] - s->level_ptr[l];
-    pfr::launch_usolve2(true, s->P, s->d_level_fronts + s->level_ptr[l], nf, solve_W(s, l, nf), s->level_maxf[l], ngroups,
+    pfr::launch_usolve2(s->P, s->d_level_fronts + s->level_ptr[l], nf, solve_W(s, l, nf),
+                        s->level_maxf[l] <= s->us2_small, ngroups,
                         s->F, s->Fc, s->Y,
                         s->X, s->d_reach[0], s->d_reach[1], s->Y2, s->XA, s->d_reach[1], st);
   }
@@ -402,6 +410,42 @@ int set_reach(pfr_solver* s, int which, const std::vector<int32_t>& prows) {
   HIP_TRY(hipMemcpy(s->d_reach[which], mark.data(), nf * 4, hipMemcpyHostToDevice));
   if (!list.empty()) HIP_TRY(hipMemcpy(s->d_reach_fronts[which], list.data(), list.size() * 4, hipMemcpyHostToDevice));
   return PFR_OK;
+}
+
+// Backward error of the solution X (permuted, frequency-minor) of the original system (which = 0:
+// A x = b over the rows, 1: A^T l = g over the columns); mode 0 operator form, 1 explicit batch
+// (data, ds, nvalid); rhs as pfr::ResidDesc (0 operator, 1 explicit B, 2 vector G).  Sets the
+// chunk's flags and the caller's berr slots (q0 < 0: no berr output).  R != NULL: only the residual
+// b - A x is written there (the refinement step), nothing is checked.
+void check_solution(pfr_solver* s, int which, int mode, int rhs, const pfr::RhsDesc& rd, const double2* data,
+                    int64_t ds, int nvalid, const double2* X, double2* R, int64_t q0, hipStream_t st) {
+  pfr::ResidDesc d;
+  d.ptr = which == 0 ? s->d_rptr : s->d_cptr;
+  d.idx = which == 0 ? s->d_ridx : s->d_cidx;
+  d.nzs = which == 0 ? s->d_rnz : s->d_cnz;
+  d.n = s->n;
+  d.K = s->K;
+  d.M = s->M;
+  d.freqs = s->freqs;
+  d.data = data;
+  d.data_stride = ds;
+  d.nvalid = nvalid;
+  d.rhsP = rd.rhsP;
+  d.beta_re = rd.beta_re;
+  d.beta_im = rd.beta_im;
+  d.mass_sum = rd.mass_sum;
+  d.B = rd.B;
+  d.b_stride = rd.b_stride;
+  d.perm = s->P.perm;
+  d.G = rd.G;
+  if (R) {   // refinement residual only: no maxima, no flags
+    pfr::launch_residual(mode, rhs, d, X, s->Fc, R, nullptr, st);
+    return;
+  }
+  pfr::launch_residual(mode, rhs, d, X, s->Fc, nullptr, s->d_berr_acc, st);
+  pfr::launch_berr_finish(s->d_berr_acc, s->Fc, nvalid, s->check_tol,
+                          which == 0 ? PFR_FLAG_BACKWARD_ERROR : PFR_FLAG_BACKWARD_ERROR_ADJ, s->flags,
+                          q0 >= 0 ? s->berr_out : nullptr, q0, which, st);
 }
 
 }  // namespace
@@ -547,6 +591,13 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     return fail(PFR_ERR_ARG, "front larger than MAX_FRONT (device_types.hpp)");
   }
   s->device = device;
+  auto knob = [](const char* name, int def, int lo, int hi) {
+    const char* e = getenv(name);
+    return e ? std::max(lo, std::min(hi, atoi(e))) : def;
+  };
+  s->solve_wmax = knob("PFR_SOLVE_WMAX", 8, 1, 8);
+  s->fac_wmax = knob("PFR_FAC_WMAX", 16, 1, 16);
+  s->us2_small = knob("PFR_US2_SMALL", 110, 0, pfr::MAX_FRONT);
   s->n = S.n;
   s->nnz = S.nnz;
   s->Fc = round64(max_batch);
@@ -885,10 +936,11 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   if ((rc = s->alloc(&s->F, S.factor_entries * Fc)) || (rc = s->alloc(&s->WV, S.total_rows * Fc)) ||
       (rc = s->alloc(&s->X, (int64_t)S.n * Fc)) || (rc = s->alloc(&s->Y, (int64_t)S.n * Fc)) ||
       (rc = s->alloc(&s->XA, (int64_t)S.n * Fc)) || (rc = s->alloc(&s->G, (int64_t)S.n * Fc)) ||
-      (rc = s->alloc(&s->Y2, (int64_t)S.n * Fc)) ||
+      (rc = s->alloc(&s->Y2, (int64_t)S.n * Fc)) || (rc = s->alloc(&s->XR, (int64_t)S.n * Fc)) ||
       (rc = s->alloc(&s->freqs, Fc)) || (rc = s->alloc(&s->loss_terms, Fc)) || (rc = s->alloc(&s->flags, Fc)) ||
-      (rc = s->alloc(&s->tq, Fc)))
+      (rc = s->alloc(&s->tq, Fc)) || (rc = s->alloc(&s->d_berr_acc, Fc)))
     return bail(rc);
+  HIP_TRY(hipMemset(s->d_berr_acc, 0, Fc * sizeof(double)));
   // PFR_AUX=1: run the forward sparse L-solve on a side stream, level by level behind the
   // factorisation (+2% with one solver lane; with two lanes the extra queues cost more than it saves)
   const char* aux_env = getenv("PFR_AUX");
@@ -915,6 +967,14 @@ int32_t pfr_solver_max_batch(const pfr_solver* s) { return s ? (int32_t)s->Fc : 
 int pfr_set_timing(pfr_solver* s, int32_t enable) {
   if (!s) return fail(PFR_ERR_ARG, "null solver");
   s->timing = enable == 0 ? 0 : (enable | 1);
+  return PFR_OK;
+}
+
+int pfr_set_check(pfr_solver* s, int32_t mode, double tol, double* berr_dev) {
+  if (!s || mode < 0 || mode > 7 || !(tol >= 0.0)) return fail(PFR_ERR_ARG, "bad check arguments");
+  s->check_mode = mode;
+  s->check_tol = tol;
+  s->berr_out = berr_dev;
   return PFR_OK;
 }
 
@@ -1109,7 +1169,8 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
     rd.beta_im = s->beta_im;
     rd.mass_sum = s->mass_sum;
     rd.freqs = s->freqs;
-    const bool paired = s->sym && reverse;
+    const bool refine = (s->check_mode & PFR_CHECK_REFINE) != 0;
+    const bool paired = s->sym && reverse && !refine;
     pfr::RhsDesc rf = rd;
     int rc;
     if (paired && !s->aux) {
@@ -1148,8 +1209,17 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
     // combined top-down pass (sym_top_down_pair); otherwise the full forward solve first
     if (paired) {
       if ((rc = sym_top_down_support(s, rf, st))) return rc;
-    } else if ((rc = forward_solve(s, 0, rd, s->X, st, 0))) {
-      return rc;
+    } else {
+      if ((rc = forward_solve(s, 0, rd, s->X, st, 0))) return rc;
+      if (refine) {
+        // one refinement step on the same factors: r = b - A x (into G), A d = r (into XA), x += d
+        check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, s->G, q0, st);
+        pfr::RhsDesc rr;
+        rr.G = s->G;
+        if ((rc = forward_solve(s, 2, rr, s->XA, st))) return rc;
+        pfr::launch_axpy_vec(s->X, s->XA, (int64_t)s->n * Fc, st);
+      }
+      if (s->check_mode & PFR_CHECK_FORWARD) check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st);
     }
     record(s, 2, st);
     pfr::FunctionalArgs fa = s->fn;
@@ -1165,9 +1235,21 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
       if (paired) {
         if ((rc = solve_all(s, 0, 2, rg, nullptr, s->Y2, st, 1)) || (rc = sym_top_down_pair(s, st))) return rc;
         pfr::launch_dirichlet_post(dir_desc(s), s->n_dir, s->XA, s->Fc, st);
-      } else if ((rc = adjoint_solve(s, rg, s->XA, st, 1))) {
-        return rc;
+      } else {
+        if ((rc = adjoint_solve(s, rg, s->XA, st, 1))) return rc;
+        if (refine) {
+          // l += A^{-T} (g - A^T l): residual into Y2, correction into XR
+          check_solution(s, 1, 0, 2, rg, nullptr, 0, nv, s->XA, s->Y2, q0, st);
+          pfr::RhsDesc rr;
+          rr.G = s->Y2;
+          if ((rc = adjoint_solve(s, rr, s->XR, st))) return rc;
+          pfr::launch_axpy_vec(s->XA, s->XR, (int64_t)s->n * Fc, st);
+        }
       }
+      // backward errors: the paired pass completes the forward solution only now
+      if (paired && (s->check_mode & PFR_CHECK_FORWARD))
+        check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st);
+      if (s->check_mode & PFR_CHECK_ADJOINT) check_solution(s, 1, 0, 2, rg, nullptr, 0, nv, s->XA, nullptr, q0, st);
       record(s, 4, st);
       pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->XA, s->X, Fc, nv, s->partial,
                            st);
@@ -1327,6 +1409,19 @@ int pfr_solve_multi(pfr_solver* s, int32_t batch, int32_t nrhs, const double* da
         if ((rc = solve_all(s, 2, 1, rd, nullptr, s->Y, st))) return rc;
         if ((rc = solve_all(s, 3, 1, rd, s->Y, s->X, st))) return rc;
       }
+      const int which = transpose ? 1 : 0;
+      const double2* dq = data + q0 * data_stride;
+      if (s->check_mode & PFR_CHECK_REFINE) {
+        // x += A^{-1} (b - A x) (or the transposed system) on the same factors
+        check_solution(s, which, 1, 1, rd, dq, data_stride, nv, s->X, s->G, r == 0 ? q0 : -1, st);
+        pfr::RhsDesc rr;
+        rr.G = s->G;
+        if ((rc = solve_all(s, transpose ? 2 : 0, 2, rr, nullptr, s->Y, st))) return rc;
+        if ((rc = solve_all(s, transpose ? 3 : 1, 0, rr, s->Y, s->XA, st))) return rc;
+        pfr::launch_axpy_vec(s->X, s->XA, (int64_t)s->n * Fc, st);
+      }
+      if (s->check_mode & (transpose ? PFR_CHECK_ADJOINT : PFR_CHECK_FORWARD))
+        check_solution(s, which, 1, 1, rd, dq, data_stride, nv, s->X, nullptr, r == 0 ? q0 : -1, st);
       pfr::launch_unpermute(s->P.perm, s->n, s->X, Fc, nv, Xo + r * x_rhs_stride + q0 * s->n, st);
     }
     record(s, 4, st);

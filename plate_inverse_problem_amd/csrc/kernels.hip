@@ -19,6 +19,8 @@
 #include <cstdint>
 #include <cstdlib>
 
+#include <algorithm>
+
 #include "launch.hpp"
 
 namespace pfr {
@@ -1614,6 +1616,125 @@ __global__ __launch_bounds__(256) void k_tangent_spmv(const int* __restrict__ pt
   Y[(int64_t)p * Fc + q] = acc;
 }
 
+// ------------------------------------------------------------------ backward error (per frequency)
+// Componentwise (Oettli-Prager) backward error of a computed solution,
+//   berr = max_p |b - A x|_p / (|A| |x| + |b|)_p      (|z| = |re z| + |im z|, LAPACK's CABS1),
+// per frequency -- the sparse backward error UMFPACK's refinement monitors (its omega1; the
+// reference's solves run it by default, Control = NULL at InnerState.h:246-247), invariant under
+// row and column scaling, so it stays meaningful for these badly scaled systems (membrane, bending
+// and unit Dirichlet rows; a normwise measure is dominated by the membrane rows).  A is the
+// ORIGINAL system on the permuted pattern: its rows (forward, A x = b) or its columns (adjoint,
+// A^T l = g), A = K - omega^2 M (MODE 0) or the explicit batch (MODE 1).  A wave takes rows
+// p = wave id, wave id + waves, ... for 64 frequencies and keeps a per-lane maximum, merged once
+// per wave into acc[q] by atomicMax on its bit pattern (non-negative doubles order like their
+// 64-bit patterns).  RHS: 0 = operator rhs (rhsP (beta - omega^2 mass_sum)), 1 = explicit batch B
+// (caller numbering, through perm), 2 = vector G (permuted).  R (may be NULL) receives r.
+struct ResidArgs {
+  const int* ptr;
+  const int* idx;
+  const int* nzs;
+  int n;
+  const cplx* K;
+  const double* M;
+  const double* freqs;
+  const cplx* data;
+  int64_t data_stride;
+  int nvalid;
+  const double* rhsP;
+  double beta_re, beta_im, mass_sum;
+  const cplx* B;
+  int64_t b_stride;
+  const int* perm;
+  const cplx* G;
+};
+
+__device__ __forceinline__ double cabs1(cplx z) { return fabs(z.x) + fabs(z.y); }
+
+template <int MODE>
+__device__ __forceinline__ cplx resid_entry(const ResidArgs& A, const cplx* __restrict__ dq, int nz, double om2) {
+  if (MODE == 0) {
+    const cplx k = A.K[nz];
+    return make_double2(fma(-om2, A.M[nz], k.x), k.y);
+  }
+  return dq[nz];
+}
+
+template <int MODE, int RHS>
+__global__ __launch_bounds__(256) void k_residual(ResidArgs A, const cplx* __restrict__ X, int64_t Fc,
+                                                  cplx* __restrict__ R, double* __restrict__ acc) {
+  const int64_t q = (int64_t)blockIdx.y * 64 + (threadIdx.x & 63);
+  const int wave0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const int nwaves = gridDim.x * (blockDim.x >> 6);
+  double om2 = 0.0;
+  if (MODE == 0 || RHS == 0) {
+    const double om = 6.283185307179586 * A.freqs[q];
+    om2 = om * om;
+  }
+  const int64_t item = min(q, (int64_t)A.nvalid - 1);
+  const cplx* __restrict__ dq = A.data + item * A.data_stride;
+  double berr = 0.0;
+  bool bad = false;         // NaN / Inf residual or a non-zero residual over a zero denominator
+  for (int p = wave0; p < A.n; p += nwaves) {
+    cplx b;
+    if (RHS == 0) {
+      const double v = A.rhsP[p];
+      b = make_double2(v * fma(-om2, A.mass_sum, A.beta_re), v * A.beta_im);
+    } else if (RHS == 1) {
+      b = A.B[item * A.b_stride + A.perm[p]];
+    } else {
+      b = A.G[(int64_t)p * Fc + q];
+    }
+    cplx r = b;
+    double den = cabs1(b);
+    const int e1 = A.ptr[p + 1];
+    int e = A.ptr[p];
+    for (; e + 4 <= e1; e += 4) {
+      cplx a[4], x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] = resid_entry<MODE>(A, dq, A.nzs[e + u], om2);
+        x[u] = X[(int64_t)A.idx[e + u] * Fc + q];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        r = cfms(r, a[u], x[u]);
+        den = fma(cabs1(a[u]), cabs1(x[u]), den);
+      }
+    }
+    for (; e < e1; ++e) {
+      const cplx a = resid_entry<MODE>(A, dq, A.nzs[e], om2);
+      const cplx x = X[(int64_t)A.idx[e] * Fc + q];
+      r = cfms(r, a, x);
+      den = fma(cabs1(a), cabs1(x), den);
+    }
+    if (R) R[(int64_t)p * Fc + q] = r;
+    const double cr = cabs1(r);
+    bad = bad || !isfinite(cr) || !isfinite(den) || (den == 0.0 && cr > 0.0);
+    if (den > 0.0) berr = fmax(berr, cr / den);
+  }
+  if (!acc) return;          // residual only (refinement step)
+  if (bad) berr = __longlong_as_double(0x7ff0000000000000LL);     // +inf
+  atomicMax(reinterpret_cast<unsigned long long*>(acc + q), (unsigned long long)__double_as_longlong(berr));
+}
+
+// flag the frequencies whose backward error exceeds tol; optional per-frequency output (global
+// index q0 + q, slot `which` of 2); the maxima are cleared for the next check.
+__global__ void k_berr_finish(double* __restrict__ acc, int64_t Fc, int nvalid, double tol, int flag,
+                              int* __restrict__ flags, double* __restrict__ berr_out, int64_t q0, int which) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Fc) return;
+  const double berr = acc[q];
+  if (q < nvalid && !(berr <= tol)) atomicOr(flags + q, flag);
+  if (berr_out && q < nvalid) berr_out[2 * (q0 + q) + which] = berr;
+  acc[q] = 0.0;
+}
+
+// X += D over a permuted frequency-minor vector (iterative refinement)
+__global__ void k_axpy_vec(cplx* __restrict__ X, const cplx* __restrict__ D, int64_t count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) X[i] = cadd(X[i], D[i]);
+}
+
 // Directional derivative of the loss cotangent G (k_functional) along dx:
 //   G = s h,  s = scale l'(fr) / fr,  h = ts^2 conj(U) aU + ts^2 conj(V) aV + conj(W) aW
 //   dG = ds h + s dh,  ds = scale (l''(fr) / fr - l'(fr) / fr^2) dfr,
@@ -1997,21 +2118,15 @@ void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const 
   }
 }
 
-void launch_usolve2(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int maxf, int ngroups,
+void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, bool small, int ngroups,
                     const double2* F, int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0,
                     const double2* Y1, double2* X1, const int* reach1, hipStream_t st) {
   if (nfronts <= 0) return;
   UPair a{Y0, X0, reach0, skip0}, b{Y1, X1, reach1, nullptr};
   dim3 g(nfronts, ngroups), bl(64 * W);
-  static const int small_max = [] {
-    const char* e = getenv("PFR_US2_SMALL");   // tuning knob: largest front of a "small-front" level
-    return e ? atoi(e) : 110;
-  }();
-  const bool small = maxf <= small_max;
-  if (sym && small) LAUNCH((k_usolve2_level<true, 2, 4, 4>), g, bl, st, P, lvl, F, Fc, a, b);
-  else if (sym) LAUNCH((k_usolve2_level<true, 4, 8, 2>), g, bl, st, P, lvl, F, Fc, a, b);
-  else if (small) LAUNCH((k_usolve2_level<false, 2, 4, 4>), g, bl, st, P, lvl, F, Fc, a, b);
-  else LAUNCH((k_usolve2_level<false, 4, 8, 2>), g, bl, st, P, lvl, F, Fc, a, b);
+  // symmetric mode only (the paired top-down pass serves the symmetric loss + gradient sweep)
+  if (small) LAUNCH((k_usolve2_level<true, 2, 4, 4>), g, bl, st, P, lvl, F, Fc, a, b);
+  else LAUNCH((k_usolve2_level<true, 4, 8, 2>), g, bl, st, P, lvl, F, Fc, a, b);
 }
 
 void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nrows, const double2* Kd,
@@ -2019,6 +2134,30 @@ void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nro
                          hipStream_t st) {
   LAUNCH(k_tangent_spmv, dim3((nrows + 3) / 4, (unsigned)(Fc / 64)), dim3(256), st, ptr, idx, nzs, nrows, Kd, X, Fc,
          rhsP, beta, Y, accumulate);
+}
+
+void launch_residual(int mode, int rhs, const ResidDesc& d, const double2* X, int64_t Fc, double2* R, double* acc,
+                     hipStream_t st) {
+  ResidArgs a;
+  a.ptr = d.ptr; a.idx = d.idx; a.nzs = d.nzs; a.n = d.n;
+  a.K = d.K; a.M = d.M; a.freqs = d.freqs; a.data = d.data; a.data_stride = d.data_stride; a.nvalid = d.nvalid;
+  a.rhsP = d.rhsP; a.beta_re = d.beta_re; a.beta_im = d.beta_im; a.mass_sum = d.mass_sum;
+  a.B = d.B; a.b_stride = d.b_stride; a.perm = d.perm; a.G = d.G;
+  const dim3 g((unsigned)std::min<int64_t>((d.n + 3) / 4, 256), (unsigned)(Fc / 64)), b(256);
+  if (mode == 0 && rhs == 0) LAUNCH((k_residual<0, 0>), g, b, st, a, X, Fc, R, acc);
+  else if (mode == 0) LAUNCH((k_residual<0, 2>), g, b, st, a, X, Fc, R, acc);
+  else if (rhs == 1) LAUNCH((k_residual<1, 1>), g, b, st, a, X, Fc, R, acc);
+  else LAUNCH((k_residual<1, 2>), g, b, st, a, X, Fc, R, acc);
+}
+
+void launch_berr_finish(double* acc, int64_t Fc, int nvalid, double tol, int flag, int* flags, double* berr_out,
+                        int64_t q0, int which, hipStream_t st) {
+  LAUNCH(k_berr_finish, dim3((unsigned)((Fc + 63) / 64)), dim3(64), st, acc, Fc, nvalid, tol, flag, flags, berr_out,
+         q0, which);
+}
+
+void launch_axpy_vec(double2* X, const double2* D, int64_t count, hipStream_t st) {
+  LAUNCH(k_axpy_vec, dim3((unsigned)((count + 255) / 256)), dim3(256), st, X, D, count);
 }
 
 void launch_functional_tangent(const FunctionalArgs& A, const double2* X, const double2* DX, int64_t Fc, int nvalid,

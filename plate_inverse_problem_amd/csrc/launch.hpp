@@ -49,8 +49,9 @@ void launch_schur_blk(int bc, const DevPattern& P, const int4* blocks, int nbloc
 void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups,
                   const double2* F, int64_t Fc, double2* WV, const RhsDesc& rd, const double2* Yin, double2* Out,
                   const int* reach, hipStream_t st);
-// two top-down U solves in one pass (vector 0 skipped on the fronts flagged in skip0)
-void launch_usolve2(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int maxf, int ngroups,
+// two top-down U solves in one pass (vector 0 skipped on the fronts flagged in skip0), symmetric
+// mode; small: the low-register variant for levels of small fronts
+void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, bool small, int ngroups,
                     const double2* F, int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0,
                     const double2* Y1, double2* X1, const int* reach1, hipStream_t st);
 // Hessian sweep: tangent right-hand sides (rows of the permuted matrix, or of its
@@ -75,6 +76,34 @@ void launch_reduce(const double2* partial, int nparts, int n_stiff, const double
 void launch_dirichlet_rhs(int src, const DirDesc& d, int n_crow, const RhsDesc& rd, double2* G, double2* Bc,
                           int64_t Fc, hipStream_t st);
 void launch_dirichlet_post(const DirDesc& d, int n_dir, double2* X, int64_t Fc, hipStream_t st);
+// Backward-error check: the original system's rows (forward) or columns (adjoint) in the permuted
+// numbering, A = K - omega^2 M (mode 0) or the explicit batch (mode 1); rhs 0 operator, 1 explicit
+// B, 2 vector G.  The per-frequency componentwise backward error accumulates in acc (max, zero on
+// entry); acc == NULL: only the residual is written to R.
+struct ResidDesc {
+  const int* ptr = nullptr;
+  const int* idx = nullptr;
+  const int* nzs = nullptr;
+  int n = 0;
+  const double2* K = nullptr;
+  const double* M = nullptr;
+  const double* freqs = nullptr;
+  const double2* data = nullptr;
+  int64_t data_stride = 0;
+  int nvalid = 1;
+  const double* rhsP = nullptr;
+  double beta_re = 0, beta_im = 0, mass_sum = 0;
+  const double2* B = nullptr;
+  int64_t b_stride = 0;
+  const int* perm = nullptr;
+  const double2* G = nullptr;
+};
+void launch_residual(int mode, int rhs, const ResidDesc& d, const double2* X, int64_t Fc, double2* R, double* acc,
+                     hipStream_t st);
+// flags |= flag where acc[q] > tol (or not finite); acc cleared
+void launch_berr_finish(double* acc, int64_t Fc, int nvalid, double tol, int flag, int* flags, double* berr_out,
+                        int64_t q0, int which, hipStream_t st);
+void launch_axpy_vec(double2* X, const double2* D, int64_t count, hipStream_t st);
 void launch_unpermute(const int* perm, int n, const double2* X, int64_t Fc, int nvalid, double2* out, hipStream_t st);
 void launch_matvec(const int* colptr, const int* rowind, int n, const double2* data, int64_t ds, const double2* x,
                    int64_t xs, double2* y, int transpose, int batch, hipStream_t st);

@@ -1,0 +1,177 @@
+"""GPU parity at the benchmark sizes and for every kernel variant those sizes select.
+
+* C3 (BASELINE.json configs[2]): orthotropic plate, ny = 25 -> 19,353 DOF.  One 4,096-frequency
+  forward sweep in 40-600 Hz (the bench's engine shape: 2 lanes x 2,048-frequency chunks, the
+  top levels' 16-wave A11 LU, k_usolve2_level<true, 4, 8, 2> on the levels of fronts > 110 rows),
+  32 of its frequencies -- three of them on the resonance peak (the peak sample and its two
+  neighbours) -- compared with the oracle; then the
+  MSE_LOG_AFC loss + gradient on those 32 frequencies against the oracle adjoint.
+* C2 (configs[1]): isotropic plate, ny = 12, 1,024-frequency forward sweep, 32 sampled.
+* kernel variants forced on small meshes through the per-solver launch knobs (read when a solver
+  is created): PFR_US2_SMALL=0 (every level through the large-front paired top-down solve),
+  PFR_US2_SMALL=1024 (every level through the small-front variant), PFR_FAC_WMAX=1 / 16 and
+  PFR_SOLVE_WMAX=1 (one-wave and widest LU / solve workgroups).
+
+Tolerances.  These systems are badly scaled (membrane, bending and unit Dirichlet rows) and their
+conditioning grows like (mesh size)^-4.  At C3 the fr of the fp64 problem data is numerically
+determined only to ~1e-7 .. 1e-6 near the resonance: fp64 solves with componentwise backward errors
+at machine precision (SuperLU + the reference's default UMFPACK refinement, a static-pivot
+factorisation + refinement) scatter by that much around the extended-precision solution
+(tests/golden/make_c3_truth.py), while unrefined threshold-pivoted SuperLU is
+off by up to 4e-5.  Hence per size: fr and loss relative error <= 2e-9 (ny <= 6), <= 5e-7 (C2, at
+its resonance peaks), <= 2e-6 (C3 against the extended-precision fixture; median <= 5e-8);
+gradient (inf-norm relative) <= 1e-7 (ny <= 6), <= 5e-6 (C3).  The componentwise backward error of
+every GPU solve (the measure UMFPACK's refinement monitors) must be <= 1e-12.
+"""
+import gc
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import make_problem, oracle_for
+
+pytestmark = pytest.mark.gpu
+
+FR_RTOL = 2e-9          # ny <= 6
+GRAD_RTOL = 1e-7
+FR_RTOL_C2 = 5e-7
+FR_RTOL_C3 = 2e-6
+FR_MEDIAN_C3 = 5e-8
+GRAD_RTOL_C3 = 5e-6
+BERR_MAX = 1e-12
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _rel(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-300))
+
+
+def _report(name, **vals):
+    """Measured errors, appended to $PFR_TEST_REPORT (JSON lines) when set."""
+    path = os.environ.get("PFR_TEST_REPORT")
+    if path:
+        import json
+        with open(path, "a") as f:
+            f.write(json.dumps({"test": name, **{k: float(v) for k, v in vals.items()}}) + "\n")
+
+
+def _peaks(fr, n):
+    """Indices of the n highest interior local maxima of fr."""
+    i = np.nonzero((fr[1:-1] > fr[:-2]) & (fr[1:-1] > fr[2:]))[0] + 1
+    return i[np.argsort(fr[i])[::-1][:n]]
+
+
+@pytest.fixture(scope="module")
+def c3():
+    p = make_problem("orthotropic", ny=25, device="cuda:0")
+    yield p
+    del p
+    gc.collect()
+    torch.cuda.empty_cache()
+
+
+def test_c3_forward_sweep_matches_truth(c3):
+    """4,096-frequency sweep at C3; 32 frequencies (3 on the resonance peak) against the
+    extended-precision fixture, and their componentwise backward errors."""
+    T = np.load(os.path.join(GOLDEN, "c3_truth.npz"))
+    assert c3.mat_size == 19353 and int(T["ny"]) == 25
+    freqs = np.linspace(40.0, 600.0, 4096)
+    fr = c3.solveForward(freqs)
+    eng = c3.engine()
+    assert eng.n_lanes == 2 and eng.max_batch == 2048
+    assert np.all(np.isfinite(fr))
+    assert np.argmax(fr) == 1179                      # the resonance the fixture samples
+    idx = T["index"]
+    assert np.array_equal(freqs[idx], T["freqs"])
+    err = np.abs(fr[idx] / T["fr_true"] - 1)
+    err_orc = np.abs(T["fr_oracle"] / T["fr_true"] - 1)
+    _report("c3_fr_vs_truth", gpu_max=err.max(), gpu_median=np.median(err), oracle_max=err_orc.max(),
+            worst_hz=freqs[idx][np.argmax(err)])
+    # the same frequencies with their backward errors, without and with one refinement step
+    checked = {}
+    for refine in (False, True):
+        fr2, berr, flags = c3.solveForwardChecked(T["freqs"], refine=refine)
+        e2 = np.abs(fr2 / T["fr_true"] - 1)
+        checked[refine] = (berr, flags, e2)
+        _report(f"c3_checked_refine{int(refine)}", berr_max=berr.max(), berr_median=np.median(berr),
+                err_max=e2.max(), err_median=np.median(e2), flagged=np.count_nonzero(flags))
+    assert err.max() < FR_RTOL_C3, f"max rel err {err.max():.3e} at {freqs[idx][np.argmax(err)]:.2f} Hz"
+    assert np.median(err) < FR_MEDIAN_C3
+    for refine, (berr, flags, e2) in checked.items():
+        assert np.all(flags == 0) and np.all(berr <= BERR_MAX), (refine, berr.max())
+        assert e2.max() < FR_RTOL_C3
+
+
+def test_c3_loss_and_grad_matches_oracle(c3):
+    from oracle.plate_oracle import loss_and_grad
+    T = np.load(os.path.join(GOLDEN, "c3_truth.npz"))
+    f = T["freqs"]
+    ref = T["fr_true"].astype(np.complex128)                  # synthetic measurement, phase 0
+    theta = c3.parameters * (1 + np.array([0.1, 0.1, 0.2, 0.1, 0.1]))
+    x = torch.tensor(theta, requires_grad=True)
+    val = c3.getLossFunction(f, ref, "MSE_LOG_AFC")(x)
+    val.backward()
+    lo, go = loss_and_grad(oracle_for(c3), f, ref, "MSE_LOG_AFC", theta)
+    _report("c3_loss_grad", loss_rel=abs(val.item() - lo) / abs(lo), grad_rel=_rel(x.grad.numpy(), go))
+    assert abs(val.item() - lo) / abs(lo) < FR_RTOL_C3
+    assert _rel(x.grad.numpy(), go) < GRAD_RTOL_C3
+
+
+def test_c2_forward_sweep_matches_truth():
+    T = np.load(os.path.join(GOLDEN, "c2_truth.npz"))
+    p = make_problem("isotropic", ny=12, device="cuda:0")
+    freqs = np.linspace(40.0, 600.0, 1024)
+    fr = p.solveForward(freqs)
+    idx = T["index"]
+    assert np.array_equal(freqs[idx], T["freqs"])
+    pk = _peaks(fr, 2)                                # resonance peaks against the live oracle
+    ref = oracle_for(p).fr(freqs[pk], p.parameters)
+    _report("c2_fr_vs_truth", gpu_max=_rel(fr[idx] / T["fr_true"], np.ones(idx.size)),
+            peak_vs_oracle=_rel(fr[pk] / ref, np.ones(pk.size)))
+    assert _rel(fr[idx] / T["fr_true"], np.ones(idx.size)) < FR_RTOL_C2
+    assert _rel(fr[pk] / ref, np.ones(pk.size)) < FR_RTOL_C2
+
+
+@pytest.mark.parametrize("env", [
+    {"PFR_US2_SMALL": "0"},
+    {"PFR_US2_SMALL": "1024"},
+    {"PFR_FAC_WMAX": "1", "PFR_SOLVE_WMAX": "1"},
+    {"PFR_FAC_WMAX": "16", "PFR_SOLVE_WMAX": "8"},
+])
+def test_kernel_variants_match_oracle(env, monkeypatch):
+    from oracle.plate_oracle import loss_and_grad
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    p = make_problem("orthotropic", ny=6, device="cuda:0")
+    freqs = np.linspace(40.0, 600.0, 100)
+    orc = oracle_for(p)
+    fr = p.solveForward(freqs)
+    assert _rel(fr / orc.fr(freqs, p.parameters), np.ones(freqs.size)) < FR_RTOL
+    ref = fr * np.exp(0.1j) * 1.02
+    theta = p.parameters * 1.04
+    x = torch.tensor(theta, requires_grad=True)
+    val = p.getLossFunction(freqs, ref, "MSE_LOG_AFC")(x)
+    val.backward()
+    lo, go = loss_and_grad(orc, freqs, ref, "MSE_LOG_AFC", theta)
+    _report("variant " + ",".join(f"{k}={v}" for k, v in env.items()), loss_rel=abs(val.item() - lo) / abs(lo),
+            grad_rel=_rel(x.grad.numpy(), go))
+    assert abs(val.item() - lo) / abs(lo) < FR_RTOL
+    assert _rel(x.grad.numpy(), go) < GRAD_RTOL
+
+
+def test_engine_grows_after_small_first_call():
+    """A small first sweep must not pin 1 lane and 64-frequency chunks on later large sweeps."""
+    p = make_problem("isotropic", ny=4, device="cuda:0")
+    freqs = np.linspace(40.0, 600.0, 4096)
+    small = p.solveForward(freqs[:32])
+    eng = p.engine()
+    assert eng.n_lanes == 1 and eng.max_batch == 64
+    fr = p.solveForward(freqs)
+    eng = p.engine()
+    assert eng.n_lanes == 2 and eng.max_batch >= 2048
+    assert np.array_equal(fr[:32], small) or _rel(fr[:32], small) < 1e-13
+    p.solveForward(freqs[:100])                     # smaller again: no rebuild
+    assert p.engine() is eng and eng.max_batch >= 2048
