@@ -166,7 +166,9 @@ PFR_API int pfr_matvec(pfr_solver* s, int32_t batch, const double* data_dev, int
  *   w_k = sum_q ( -lam_q^T S_k x_q + e_k lam_q^T rhs ),   A^T lam_q = d loss / d x_q.
  * The (F, nnz) matrix batch is never materialised. */
 
-/* K_out_dev = sum_k coef_k * S_k  (S registered by pfr_set_stiffness), complex nnz */
+/* K_out_dev = sum_k coef_k * S_k  (S registered by pfr_set_stiffness), complex nnz.  n_stiff is 18
+ * (A, B, D coefficient matrices of Problem.py:440-445) or 12 (A and D only: the B coefficients vanish
+ * for mid-plane symmetric laminates, so their matrices and gradient partials are left out). */
 PFR_API int pfr_set_stiffness(pfr_solver* s, int32_t n_stiff, const double* stiff_dev /* (nnz, n_stiff) */,
                               const double* rhs_weights /* host, n_stiff: e_k */);
 PFR_API int pfr_combine(pfr_solver* s, const double* coef /* host complex n_stiff */, double* K_out_dev,

@@ -127,7 +127,7 @@ def sparse_lu(A):
     """SuperLU with a diagonal-preferring threshold (0.001), like UMFPACK's
     symmetric strategy; partial pivoting (threshold 1.0) on these FE matrices
     picks off-diagonal pivots and fills in 10x more (measured)."""
-    A = A.tocsc()
+    A = A.tocsc(copy=True)             # eliminate_zeros works in place: never on the caller's arrays
     A.eliminate_zeros()
     return spla.splu(A, permc_spec="COLAMD", diag_pivot_thresh=0.001, options=dict(SymmetricMode=True))
 

@@ -112,7 +112,12 @@ class _Engine:
         self.solvers, self.streams, self._pool = [], [], None
         self.n_lanes = 0
         self._sized_for = set()
-        self.stiff = torch.as_tensor(np.ascontiguousarray(vals[:18].T), device=device)       # (nnz, 18)
+        # the coefficient matrices contracted for the gradient: all 18, or the 12 of A and D when the
+        # coupling coefficients B vanish identically (mid-plane symmetric materials: dB/dtheta = 0, so
+        # their gradient partials are exactly zero and need not be formed)
+        self.kidx = np.r_[0:6, 12:18] if prob.material.is_mps else np.arange(18)
+        self.n_stiff = int(self.kidx.size)
+        self.stiff = torch.as_tensor(np.ascontiguousarray(vals[self.kidx].T), device=device)  # (nnz, n_stiff)
         I0, I0c, I2, I2c = prob.I0, prob.I0Corr, prob.I2, prob.I2Corr
         mass = I0 * (vals[18] + vals[20] + vals[22]) + I0c * (vals[19] + vals[21] + vals[23]) \
             + I2 * vals[24] + I2c * vals[25]                                                  # Problem.py:441-443
@@ -178,7 +183,7 @@ class _Engine:
             from concurrent.futures import ThreadPoolExecutor
             self._pool = ThreadPoolExecutor(max_workers=lanes, thread_name_prefix="pfr-lane")
         for sv in self.solvers:
-            sv.set_stiffness(self.stiff, self.e)
+            sv.set_stiffness(self.stiff, self.e[self.kidx])
             sv.set_operator(torch.view_as_real(self.K), self.mass)      # K(theta) shared by the lanes
             sv.set_functional(self._sup, self._a3, self._ts)
             sv.set_check(self.check_mode, self.check_tol)
@@ -201,12 +206,20 @@ class _Engine:
     def max_batch(self) -> int:
         return self.solver.max_batch
 
+    def expand(self, v: torch.Tensor) -> torch.Tensor:
+        """Partials over the contracted matrices (last axis n_stiff) -> over all 18 (zeros elsewhere)."""
+        if self.n_stiff == 18:
+            return v
+        out = torch.zeros(v.shape[:-1] + (18,), dtype=v.dtype, device=v.device)
+        out[..., torch.as_tensor(self.kidx, device=v.device)] = v
+        return out
+
     def set_coefficients(self, c: np.ndarray):
         """Precombine K(theta) = sum_k c_k S_k on the device and the rhs scale."""
         key = c.tobytes()
         if key == self._coef_key:
             return
-        self.solver.combine(c, torch.view_as_real(self.K))
+        self.solver.combine(np.asarray(c)[self.kidx], torch.view_as_real(self.K))
         beta = complex(self.e @ c)
         for sv in self.solvers:
             sv.set_rhs(self.rhs, beta, self.mass_sum)
@@ -328,11 +341,11 @@ class _SweepFR(torch.autograd.Function):
         engine.set_coefficients(ctx.cn)
         ref = torch.zeros(ctx.freqs.numel(), dtype=torch.complex128, device=engine.device)
         ref.real.copy_(grad_fr.to(torch.float64))
-        w = torch.zeros(18, dtype=torch.complex128, device=engine.device)
+        w = torch.zeros(engine.n_stiff, dtype=torch.complex128, device=engine.device)
         loss = torch.zeros(1, dtype=torch.float64, device=engine.device)
         engine.sweep(ctx.freqs, _native.LOSS_COTANGENT, ref=torch.view_as_real(ref), scale=1.0,
                      loss=loss, w=torch.view_as_real(w))
-        return torch.conj(w).to(torch.complex128).cpu(), None, None
+        return torch.conj(engine.expand(w)).to(torch.complex128).cpu(), None, None
 
 
 class _SweepLoss(torch.autograd.Function):
@@ -342,7 +355,7 @@ class _SweepLoss(torch.autograd.Function):
     def forward(ctx, c, engine, freqs, ref, loss_id, n_total, reduce_fn):
         cn = c.detach().cpu().numpy()
         engine.set_coefficients(cn)
-        w = torch.zeros(18, dtype=torch.complex128, device=engine.device)
+        w = torch.zeros(engine.n_stiff, dtype=torch.complex128, device=engine.device)
         loss = torch.zeros(1, dtype=torch.float64, device=engine.device)
         flags = torch.zeros(freqs.numel(), dtype=torch.int32, device=engine.device)
         berr = torch.full((freqs.numel(), 2), float('nan'), dtype=torch.float64, device=engine.device)
@@ -350,7 +363,7 @@ class _SweepLoss(torch.autograd.Function):
                      loss=loss, w=torch.view_as_real(w), flags=flags, berr=berr)
         engine.last_berr = berr
         engine.last_flags = _check_flags(flags)
-        packed = torch.cat([loss.to(torch.complex128), w])
+        packed = torch.cat([loss.to(torch.complex128), engine.expand(w)])
         if reduce_fn is not None:
             packed = reduce_fn(packed)
         ctx.save_for_backward(packed[1:].cpu())
@@ -662,14 +675,14 @@ class Problem:
             eng = self.engine(max(1, hi - lo))
             eng.set_coefficients(c)
             dev = eng.device
-            w = torch.zeros(18, dtype=torch.complex128, device=dev)
-            h = torch.zeros(n, 18, dtype=torch.complex128, device=dev)
+            w = torch.zeros(eng.n_stiff, dtype=torch.complex128, device=dev)
+            h = torch.zeros(n, eng.n_stiff, dtype=torch.complex128, device=dev)
             loss = torch.zeros(1, dtype=torch.float64, device=dev)
             flags = torch.zeros(f_local.numel(), dtype=torch.int32, device=dev)
-            eng.hessian_sweep(f_local, loss_id, torch.view_as_real(ref_local), 1.0 / n_total, dc.T,
+            eng.hessian_sweep(f_local, loss_id, torch.view_as_real(ref_local), 1.0 / n_total, dc[eng.kidx].T,
                               loss=loss, w=torch.view_as_real(w), h=torch.view_as_real(h), flags=flags)
             _check_flags(flags)
-            packed = torch.cat([loss.to(torch.complex128), w, h.reshape(-1)])
+            packed = torch.cat([loss.to(torch.complex128), eng.expand(w), eng.expand(h).reshape(-1)])
             if reduce_fn is not None:
                 packed = reduce_fn(packed)
             packed = packed.cpu().numpy()

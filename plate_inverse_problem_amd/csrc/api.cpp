@@ -112,6 +112,11 @@ struct pfr_solver {
   int32_t *d_rptr = nullptr, *d_ridx = nullptr, *d_rnz = nullptr;
   int32_t *d_cptr = nullptr, *d_cidx = nullptr, *d_cnz = nullptr;
   double2 *DX = nullptr, *DL = nullptr, *Kdir = nullptr;
+  // fused contraction + checks (k_contract_rows): per permuted row a pseudo-entry (-1, -1, -1, i),
+  // then (column, nz of (i, j) or -1, nz of (j, i) or -1, i) over the union of the row's and the
+  // column's patterns; entry ranges of whole rows, about equal size (kContractBlocks of them)
+  int32_t* d_ublk = nullptr;
+  int4* d_uent = nullptr;
   int n_kdir = 0;
   double2 *partial = nullptr, *tq = nullptr;
   double *freqs = nullptr, *loss_terms = nullptr;
@@ -151,7 +156,7 @@ struct pfr_solver {
   // with its low-register small-front variant)
   int solve_wmax = 8, fac_wmax = 16, us2_small = 110;
   // backward-error checks (pfr_set_check): PFR_CHECK_* bits, tolerance, optional per-item output;
-  // per-frequency maximum scratch (kept zero between checks)
+  // per-frequency maxima scratch, forward and adjoint (kept zero between checks)
   int check_mode = 0;
   double check_tol = 1e-10;
   double* berr_out = nullptr;
@@ -446,6 +451,13 @@ void check_solution(pfr_solver* s, int which, int mode, int rhs, const pfr::RhsD
   pfr::launch_berr_finish(s->d_berr_acc, s->Fc, nvalid, s->check_tol,
                           which == 0 ? PFR_FLAG_BACKWARD_ERROR : PFR_FLAG_BACKWARD_ERROR_ADJ, s->flags,
                           q0 >= 0 ? s->berr_out : nullptr, q0, which, st);
+}
+
+// s_{q,k} partials of sum_nz S_k(nz) lam[row] x[col] (no checks), row-ordered like the loss sweep's
+void contract_rows(pfr_solver* s, const double2* lam, const double2* x, int nv, hipStream_t st) {
+  pfr::RowCheckDesc cd;
+  pfr::launch_contract_rows(false, s->d_ublk, s->d_uent, kContractBlocks, (int)(s->Fc / 64), s->stiff, s->n_stiff, cd,
+                            lam, x, s->Fc, nv, s->partial, nullptr, nullptr, st);
 }
 
 }  // namespace
@@ -913,6 +925,43 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     if ((rc = compress(S.prow, S.pcol, &s->d_rptr, &s->d_ridx, &s->d_rnz)) ||
         (rc = compress(S.pcol, S.prow, &s->d_cptr, &s->d_cidx, &s->d_cnz)))
       return bail(rc);
+    // union row structure of the fused contraction + checks
+    std::vector<int64_t> key(S.nnz);
+    std::vector<int32_t> ord(S.nnz);
+    for (int64_t e = 0; e < S.nnz; ++e) {
+      key[e] = (int64_t)S.prow[e] * S.n + S.pcol[e];
+      ord[e] = (int32_t)e;
+    }
+    std::sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return key[a] < key[b]; });
+    auto find = [&](int64_t k) -> int32_t {
+      auto it = std::lower_bound(ord.begin(), ord.end(), k, [&](int32_t a, int64_t v) { return key[a] < v; });
+      return (it != ord.end() && key[*it] == k) ? *it : -1;
+    };
+    std::vector<std::vector<int4>> rows(S.n);
+    for (int32_t e : ord) {   // row-major, columns ascending
+      const int32_t i = S.prow[e], j = S.pcol[e];
+      rows[i].push_back(make_int4(j, e, find((int64_t)j * S.n + i), 0));
+    }
+    for (int32_t e : ord) {   // (i, j) whose mirror (j, i) is not in the pattern: column-only entry of row j
+      const int32_t i = S.prow[e], j = S.pcol[e];
+      if (find((int64_t)j * S.n + i) < 0) rows[j].push_back(make_int4(i, -1, e, 0));
+    }
+    std::vector<int32_t> uptr(S.n + 1, 0);
+    std::vector<int4> uent;
+    for (int i = 0; i < S.n; ++i) {
+      std::sort(rows[i].begin(), rows[i].end(), [](const int4& a, const int4& b) { return a.x < b.x; });
+      uent.push_back(make_int4(-1, -1, -1, i));
+      for (const int4& v : rows[i]) uent.push_back(make_int4(v.x, v.y, v.z, i));
+      uptr[i + 1] = (int32_t)uent.size();
+    }
+    std::vector<int32_t> ublk(1, 0);   // entry offsets at row starts
+    for (int b = 1; b < kContractBlocks; ++b) {
+      const int64_t target = (int64_t)uent.size() * b / kContractBlocks;
+      const int32_t at = *std::lower_bound(uptr.begin(), uptr.end(), (int32_t)target);
+      ublk.push_back(std::max(ublk.back(), at));
+    }
+    ublk.push_back((int32_t)uent.size());
+    if ((rc = s->up(&s->d_uent, uent)) || (rc = s->up(&s->d_ublk, ublk))) return bail(rc);
   }
   s->P = DevPattern{d_fronts, idx, relpos, rowf, ap, ac, an, ep, es, pm, pr, pc, S.n};
   {
@@ -938,9 +987,9 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       (rc = s->alloc(&s->XA, (int64_t)S.n * Fc)) || (rc = s->alloc(&s->G, (int64_t)S.n * Fc)) ||
       (rc = s->alloc(&s->Y2, (int64_t)S.n * Fc)) || (rc = s->alloc(&s->XR, (int64_t)S.n * Fc)) ||
       (rc = s->alloc(&s->freqs, Fc)) || (rc = s->alloc(&s->loss_terms, Fc)) || (rc = s->alloc(&s->flags, Fc)) ||
-      (rc = s->alloc(&s->tq, Fc)) || (rc = s->alloc(&s->d_berr_acc, Fc)))
+      (rc = s->alloc(&s->tq, Fc)) || (rc = s->alloc(&s->d_berr_acc, 2 * Fc)))
     return bail(rc);
-  HIP_TRY(hipMemset(s->d_berr_acc, 0, Fc * sizeof(double)));
+  HIP_TRY(hipMemset(s->d_berr_acc, 0, 2 * Fc * sizeof(double)));
   // PFR_AUX=1: run the forward sparse L-solve on a side stream, level by level behind the
   // factorisation (+2% with one solver lane; with two lanes the extra queues cost more than it saves)
   const char* aux_env = getenv("PFR_AUX");
@@ -1039,7 +1088,8 @@ int pfr_solver_solve_bytes(const pfr_solver* s, int64_t* bytes) {
 }
 
 int pfr_set_stiffness(pfr_solver* s, int32_t n_stiff, const double* stiff_dev, const double* w) {
-  if (!s || n_stiff <= 0 || n_stiff > 18 || !stiff_dev || !w) return fail(PFR_ERR_ARG, "bad stiffness arguments");
+  if (!s || (n_stiff != 12 && n_stiff != 18) || !stiff_dev || !w)
+    return fail(PFR_ERR_ARG, "bad stiffness arguments (n_stiff must be 12 or 18)");
   s->stiff = stiff_dev;
   s->n_stiff = n_stiff;
   std::memset(&s->e, 0, sizeof(s->e));
@@ -1246,13 +1296,30 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
           pfr::launch_axpy_vec(s->XA, s->XR, (int64_t)s->n * Fc, st);
         }
       }
-      // backward errors: the paired pass completes the forward solution only now
-      if (paired && (s->check_mode & PFR_CHECK_FORWARD))
-        check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st);
-      if (s->check_mode & PFR_CHECK_ADJOINT) check_solution(s, 1, 0, 2, rg, nullptr, 0, nv, s->XA, nullptr, q0, st);
       record(s, 4, st);
-      pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->XA, s->X, Fc, nv, s->partial,
-                           st);
+      // gradient contraction fused with the backward-error checks of both solutions (the forward
+      // check of a refined / unpaired sweep is already done above)
+      const bool fwd_done = !paired;
+      const int want = s->check_mode & ((fwd_done ? 0 : PFR_CHECK_FORWARD) | PFR_CHECK_ADJOINT);
+      pfr::RowCheckDesc cd;
+      cd.K = s->K;
+      cd.M = s->M;
+      cd.freqs = s->freqs;
+      cd.rhsP = s->rhsP;
+      cd.beta_re = s->beta_re;
+      cd.beta_im = s->beta_im;
+      cd.mass_sum = s->mass_sum;
+      cd.G = s->G;
+      pfr::launch_contract_rows(want != 0, s->d_ublk, s->d_uent, kContractBlocks, ngroups, s->stiff, s->n_stiff, cd,
+                                s->XA, s->X, Fc, nv, s->partial, s->d_berr_acc, s->d_berr_acc + Fc, st);
+      for (int w = 0; w < 2; ++w) {
+        double* acc = s->d_berr_acc + w * Fc;
+        if (want & (w == 0 ? PFR_CHECK_FORWARD : PFR_CHECK_ADJOINT))
+          pfr::launch_berr_finish(acc, Fc, nv, s->check_tol, w == 0 ? PFR_FLAG_BACKWARD_ERROR : PFR_FLAG_BACKWARD_ERROR_ADJ,
+                                  s->flags, s->berr_out, q0, w, st);
+        else if (want)
+          HIP_TRY(hipMemsetAsync(acc, 0, Fc * sizeof(double), st));   // computed, not requested: keep zero
+      }
       pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st);
       pfr::launch_reduce(s->partial, kContractBlocks * ngroups, s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
                          reinterpret_cast<double2*>(w_dev), loss_dev, st);
@@ -1330,7 +1397,7 @@ int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int
     rg.rhsP = s->rhsP;
     rg.freqs = s->freqs;
     if ((rc = adjoint_solve(s, rg, s->XA, st, 1))) return rc;
-    pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->XA, s->X, Fc, nv, s->partial, st);
+    contract_rows(s, s->XA, s->X, nv, st);
     pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st);
     pfr::launch_reduce(s->partial, kContractBlocks * ngroups, s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
                        reinterpret_cast<double2*>(w_dev), loss_dev, st);
@@ -1346,13 +1413,11 @@ int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int
       pfr::launch_tangent_spmv(s->d_cptr, s->d_cidx, s->d_cnz, (int)n, Kd, s->XA, Fc, nullptr, make_double2(0, 0),
                                s->G, 1, st);
       if ((rc = adjoint_solve(s, rg, s->DL, st))) return rc;
-      pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->DL, s->X, Fc, nv, s->partial,
-                           st);
+      contract_rows(s, s->DL, s->X, nv, st);
       pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->DL, Fc, s->tq, st);
       pfr::launch_reduce(s->partial, kContractBlocks * ngroups, s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
                          H + (int64_t)i * s->n_stiff, nullptr, st);
-      pfr::launch_contract(s->P, s->stiff, s->n_stiff, s->nnz, kContractBlocks, ngroups, s->XA, s->DX, Fc, nv,
-                           s->partial, st);
+      contract_rows(s, s->XA, s->DX, nv, st);
       pfr::launch_reduce(s->partial, kContractBlocks * ngroups, s->n_stiff, s->tq, zero, s->loss_terms, nv, Fc,
                          H + (int64_t)i * s->n_stiff, nullptr, st);
     }

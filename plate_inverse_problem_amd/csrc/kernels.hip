@@ -1861,69 +1861,135 @@ __global__ void k_functional(FunctionalArgs A, const cplx* __restrict__ X, int64
   }
 }
 
-// ------------------------------------------------------------------ K5: gradient contraction
+// ------------------------------------------------------------------ K5: gradient contraction + checks
 // s_{q,k} = sum_nz stiff[nz][k] * Lam[prow] * X[pcol]   (Sparse.py:173-176 matrix cotangent,
-// contracted with the stiffness matrices as JAX's einsum transpose does)
-constexpr int NSTIFF_MAX = 18;
-__global__ __launch_bounds__(64) void k_contract(DevPattern P, const double* __restrict__ stiff, int n_stiff,
-                                                 int64_t nnz, int64_t nz_per_blk, const cplx* __restrict__ Lam,
-                                                 const cplx* __restrict__ X, int64_t Fc, int nvalid,
-                                                 cplx* __restrict__ partial) {
+// contracted with the stiffness matrices as JAX's einsum transpose does), fused with the checks.
+// Row-ordered gradient contraction with the backward-error checks of both solutions in the same pass.
+// Entries, rows ascending: each permuted row i starts with a pseudo-entry (-1, -1, -1, i), followed
+// by (column j, nz of A(i, j) or -1, nz of A(j, i) or -1, i) over the union of row i's and column
+// i's patterns.  One walk gathers x_j and lambda_j once per entry for
+//   s_{q,k} += S_k(i, j) lambda_i x_j                        (contraction, as k_contract)
+//   r_i = b_i - sum_j A(i, j) x_j,   s_i = g_i - sum_j A(j, i) lambda_j   (forward / adjoint residuals)
+// and the componentwise backward errors max_i |r_i| / (|A||x| + |b|)_i (resp. |A^T||lambda| + |g|);
+// the pseudo-entry gathers lambda_i and g_i instead (kept in registers for the row), so every entry
+// costs two vector loads whatever its kind (the base pointers are selected per entry, wave-uniform).
+// The walk is flat over the block's entries, 4 per step with all loads of a step independent (a
+// row-by-row loop chains several memory round trips per short row).  Block = a range of whole rows of
+// about equal entry count, one wave of 64 frequencies; partials as k_contract (k_reduce sums them).
+struct RowCheckArgs {
+  const cplx* K;
+  const double* M;
+  const double* freqs;
+  const double* rhsP;
+  double beta_re, beta_im, mass_sum;
+  const cplx* G;
+};
+
+// NS: stiffness matrices contracted (12 when the coupling block B is absent, 18 otherwise).
+// Branch-free per entry (pseudo-entry and tail handling by selects), so that the loads of a step stay
+// counted waits instead of the vmcnt(0) a branch between them would force.
+template <bool CHECK, int NS>
+__global__ __launch_bounds__(64) void k_contract_rows(const int* __restrict__ eblk, const int4* __restrict__ ent,
+                                                      const double* __restrict__ stiff, RowCheckArgs A,
+                                                      const cplx* __restrict__ Lam, const cplx* __restrict__ X,
+                                                      int64_t Fc, int nvalid, cplx* __restrict__ partial,
+                                                      double* __restrict__ acc_f, double* __restrict__ acc_a) {
+  constexpr int U = CHECK ? 2 : 4;          // entries per step
   const int lane = threadIdx.x & 63;
   const int64_t q = (int64_t)blockIdx.y * 64 + lane;
-  const int64_t nz0 = (int64_t)blockIdx.x * nz_per_blk;
-  const int64_t nz1 = min(nnz, nz0 + nz_per_blk);
-  cplx acc[NSTIFF_MAX];
+  const int e0 = eblk[blockIdx.x], e1 = eblk[blockIdx.x + 1];
+  cplx acc[NS];
 #pragma unroll
-  for (int k = 0; k < NSTIFF_MAX; ++k) acc[k] = make_double2(0, 0);
-  int64_t nz = nz0;
-  // CNZ nonzeros per step: their 2 CNZ vector loads are in flight together
-#ifndef PFR_CNZ
-#define PFR_CNZ 4
-#endif
-  constexpr int CNZ = PFR_CNZ;
-  for (; nz + CNZ <= nz1; nz += CNZ) {
-    cplx pv[CNZ];
-#pragma unroll
-    for (int u = 0; u < CNZ; ++u) {
-      const cplx l = Lam[(int64_t)P.prow[nz + u] * Fc + q];
-      const cplx x = X[(int64_t)P.pcol[nz + u] * Fc + q];
-      pv[u] = cmul(l, x);
-    }
-#pragma unroll
-    for (int u = 0; u < CNZ; ++u) {
-      const double* s = stiff + (nz + u) * n_stiff;
-#pragma unroll
-      for (int k = 0; k < NSTIFF_MAX; ++k)
-        if (k < n_stiff) {
-          acc[k].x = fma(s[k], pv[u].x, acc[k].x);
-          acc[k].y = fma(s[k], pv[u].y, acc[k].y);
-        }
-    }
+  for (int k = 0; k < NS; ++k) acc[k] = make_double2(0, 0);
+  double om2 = 0.0, bsr = 0.0, bsi = 0.0;
+  if (CHECK) {
+    const double om = 6.283185307179586 * A.freqs[q];
+    om2 = om * om;
+    bsr = fma(-om2, A.mass_sum, A.beta_re);
+    bsi = A.beta_im;
   }
-  for (; nz < nz1; ++nz) {
-    const cplx p = cmul(Lam[(int64_t)P.prow[nz] * Fc + q], X[(int64_t)P.pcol[nz] * Fc + q]);
-    const double* s = stiff + nz * n_stiff;
+  double bf = 0.0, ba = 0.0, open = 0.0;
+  bool bad = false;
+  cplx lam = make_double2(0, 0), r = lam, s = lam;
+  double dr = 0.0, ds = 0.0;
+  const cplx* __restrict__ Xq = X + q;
+  const cplx* __restrict__ Lq = Lam + q;
+  const cplx* __restrict__ Gq = A.G + q;
+  for (int e = e0; e < e1; e += U) {
+    int4 en[U];
 #pragma unroll
-    for (int k = 0; k < NSTIFF_MAX; ++k)
-      if (k < n_stiff) {
-        acc[k].x = fma(s[k], p.x, acc[k].x);
-        acc[k].y = fma(s[k], p.y, acc[k].y);
+    for (int u = 0; u < U; ++u) en[u] = ent[min(e + u, e1 - 1)];
+    cplx v1[U], v2[U];
+    double rv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool pseudo = en[u].x < 0;                           // wave-uniform
+      const int64_t o = (int64_t)(pseudo ? en[u].w : en[u].x) * Fc;
+      v1[u] = (pseudo ? Lq : Xq)[o];                             // lambda_i | x_j
+      if (CHECK) {
+        v2[u] = (pseudo ? Gq : Lq)[o];                           // g_i | lambda_j
+        rv[u] = A.rhsP[en[u].w];
       }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool in = e + u < e1;                                // wave-uniform
+      const bool start = in && en[u].x < 0;                      // a row starts here
+      const double mij = in && en[u].y >= 0 ? 1.0 : 0.0;
+      const int nz = max(en[u].y, 0);
+      lam = start ? v1[u] : lam;
+      const cplx p = cscale(cmul(lam, v1[u]), mij);
+      const double* sk = stiff + (int64_t)nz * NS;
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        acc[k].x = fma(sk[k], p.x, acc[k].x);
+        acc[k].y = fma(sk[k], p.y, acc[k].y);
+      }
+      if (CHECK) {
+        // close the previous row where a new one starts
+        const double cr = cabs1(r), cs = cabs1(s);
+        const bool closing = start && open != 0.0;
+        bad = bad || (closing && (!isfinite(cr) || !isfinite(cs) || !isfinite(dr) || !isfinite(ds) ||
+                                  (dr == 0.0 && cr > 0.0) || (ds == 0.0 && cs > 0.0)));
+        bf = closing && dr > 0.0 ? fmax(bf, cr / dr) : bf;
+        ba = closing && ds > 0.0 ? fmax(ba, cs / ds) : ba;
+        open = start ? 1.0 : open;
+        const double mji = in && en[u].z >= 0 ? 1.0 : 0.0;
+        const int nzt = max(en[u].z, 0);
+        const cplx kij = A.K[nz], kji = A.K[nzt];
+        const cplx aij = cscale(make_double2(fma(-om2, A.M[nz], kij.x), kij.y), mij);
+        const cplx aji = cscale(make_double2(fma(-om2, A.M[nzt], kji.x), kji.y), mji);
+        const cplx b = make_double2(rv[u] * bsr, rv[u] * bsi);
+        r = start ? b : cfms(r, aij, v1[u]);
+        s = start ? v2[u] : cfms(s, aji, v2[u]);
+        dr = start ? cabs1(b) : fma(cabs1(aij), cabs1(v1[u]), dr);
+        ds = start ? cabs1(v2[u]) : fma(cabs1(aji), cabs1(v2[u]), ds);
+      }
+    }
   }
-  // sum over the wave's frequencies (padded lanes excluded): one partial per block
   const bool valid = q < nvalid;
 #pragma unroll
-  for (int k = 0; k < NSTIFF_MAX; ++k)
-    if (k < n_stiff) {
-      double re = valid ? acc[k].x : 0.0, im = valid ? acc[k].y : 0.0;
+  for (int k = 0; k < NS; ++k) {
+    double re = valid ? acc[k].x : 0.0, im = valid ? acc[k].y : 0.0;
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        re += __shfl_xor(re, o);
-        im += __shfl_xor(im, o);
-      }
-      if (lane == 0) partial[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * n_stiff + k] = make_double2(re, im);
+    for (int o = 32; o > 0; o >>= 1) {
+      re += __shfl_xor(re, o);
+      im += __shfl_xor(im, o);
     }
+    if (lane == 0) partial[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * NS + k] = make_double2(re, im);
+  }
+  if (CHECK) {
+    if (open != 0.0) {
+      const double cr = cabs1(r), cs = cabs1(s);
+      bad = bad || !isfinite(cr) || !isfinite(cs) || !isfinite(dr) || !isfinite(ds) || (dr == 0.0 && cr > 0.0) ||
+            (ds == 0.0 && cs > 0.0);
+      if (dr > 0.0) bf = fmax(bf, cr / dr);
+      if (ds > 0.0) ba = fmax(ba, cs / ds);
+    }
+    if (bad) bf = ba = __longlong_as_double(0x7ff0000000000000LL);
+    atomicMax(reinterpret_cast<unsigned long long*>(acc_f + q), (unsigned long long)__double_as_longlong(bf));
+    atomicMax(reinterpret_cast<unsigned long long*>(acc_a + q), (unsigned long long)__double_as_longlong(ba));
+  }
 }
 
 // t_q = sum_p Lam[p] * rhsP[p] over the Dirichlet support (d b / d beta)
@@ -2170,10 +2236,22 @@ void launch_functional(const FunctionalArgs& A, const double2* X, int64_t Fc, in
   LAUNCH(k_functional, dim3((unsigned)((Fc + 63) / 64)), dim3(64), st, A, X, Fc, nvalid, q0, fr_out, loss_terms, G);
 }
 
-void launch_contract(const DevPattern& P, const double* stiff, int n_stiff, int64_t nnz, int nblk, int ngroups,
-                     const double2* Lam, const double2* X, int64_t Fc, int nvalid, double2* partial, hipStream_t st) {
-  int64_t per = (nnz + nblk - 1) / nblk;
-  LAUNCH(k_contract, dim3(nblk, ngroups), dim3(64), st, P, stiff, n_stiff, nnz, per, Lam, X, Fc, nvalid, partial);
+void launch_contract_rows(bool check, const int* eblk, const int4* ent, int nblk, int ngroups, const double* stiff,
+                          int n_stiff, const RowCheckDesc& d, const double2* Lam, const double2* X, int64_t Fc,
+                          int nvalid, double2* partial, double* acc_f, double* acc_a, hipStream_t st) {
+  RowCheckArgs a;
+  a.K = d.K; a.M = d.M; a.freqs = d.freqs; a.rhsP = d.rhsP; a.beta_re = d.beta_re; a.beta_im = d.beta_im;
+  a.mass_sum = d.mass_sum; a.G = d.G;
+  const dim3 g(nblk, ngroups), b(64);
+#define CR(C, N) LAUNCH((k_contract_rows<C, N>), g, b, st, eblk, ent, stiff, a, Lam, X, Fc, nvalid, partial, acc_f, acc_a)
+  if (n_stiff == 12) {
+    if (check) CR(true, 12);
+    else CR(false, 12);
+  } else if (n_stiff == 18) {
+    if (check) CR(true, 18);
+    else CR(false, 18);
+  }
+#undef CR
 }
 
 void launch_rhs_dot(const int* sup, const double* val, int n_sup, const double2* Lam, int64_t Fc, double2* t_out,

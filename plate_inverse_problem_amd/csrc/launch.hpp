@@ -63,8 +63,20 @@ void launch_functional_tangent(const FunctionalArgs& A, const double2* X, const 
                                int64_t q0, double2* G, hipStream_t st);
 void launch_functional(const FunctionalArgs& A, const double2* X, int64_t Fc, int nvalid, int64_t q0, double* fr_out,
                        double* loss_terms, double2* G, hipStream_t st);
-void launch_contract(const DevPattern& P, const double* stiff, int n_stiff, int64_t nnz, int nblk, int ngroups,
-                     const double2* Lam, const double2* X, int64_t Fc, int nvalid, double2* partial, hipStream_t st);
+// Row-ordered gradient contraction fused with the forward / adjoint backward-error checks
+// (check = false: contraction only); partials as launch_contract; acc_f / acc_a: per-frequency
+// maxima (zero on entry), finished by launch_berr_finish
+struct RowCheckDesc {
+  const double2* K = nullptr;
+  const double* M = nullptr;
+  const double* freqs = nullptr;
+  const double* rhsP = nullptr;
+  double beta_re = 0, beta_im = 0, mass_sum = 0;
+  const double2* G = nullptr;
+};
+void launch_contract_rows(bool check, const int* eblk, const int4* ent, int nblk, int ngroups, const double* stiff,
+                          int n_stiff, const RowCheckDesc& d, const double2* Lam, const double2* X, int64_t Fc,
+                          int nvalid, double2* partial, double* acc_f, double* acc_a, hipStream_t st);
 void launch_rhs_dot(const int* sup, const double* val, int n_sup, const double2* Lam, int64_t Fc, double2* t_out,
                     hipStream_t st);
 // w_out[k] += -sum(partial[., k]) + e_k sum_q t_q ;  loss_out += sum_q loss_terms (q < nvalid)

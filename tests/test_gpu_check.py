@@ -92,8 +92,10 @@ def test_plate_checks_are_clean_and_match_host():
 
 
 def test_lightly_damped_resonance():
-    """beta = 1e-6 (nearly singular at the resonance): the sweep through the first resonance peak
-    either matches the oracle or flags the frequency -- never an unflagged wrong answer."""
+    """beta = 1e-6 (nearly singular at the resonance, condition ~1/beta times the undamped one):
+    through the first resonance peak the static-pivot solves stay componentwise backward stable
+    (berr at machine precision, nothing flagged), so they agree with the oracle to the conditioning
+    (measured 1.4e-6 at the peak, against 1e-9 at beta = 3e-3)."""
     from helpers import make_geometry
     from plate_inverse_problem_amd.Material import get_material
     from plate_inverse_problem_amd.Problem import Problem
@@ -109,7 +111,6 @@ def test_lightly_damped_resonance():
     sel = fine[max(0, j - 2):j + 3]
     fr, berr, flags = p.solveForwardChecked(sel)
     ref = oracle_for(p).fr(sel, p.parameters)
-    ok = flags != 0
-    ok |= (berr < 1e-12) & (np.abs(fr / ref - 1) < 1e-6)
-    assert ok.all(), (fr / ref - 1, berr, flags)
+    assert np.all(flags == 0) and berr.max() < 1e-14, (berr, flags)
+    assert np.abs(fr / ref - 1).max() < 2e-5, fr / ref - 1
     assert fr.max() > 50 * np.median(fc)                 # the peak is resolved
