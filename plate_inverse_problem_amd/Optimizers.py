@@ -2,10 +2,13 @@
 
 Same names, arguments and ``optResult`` as the reference; ``jax.value_and_grad``
 becomes one fused forward + adjoint GPU sweep (``Problem.getLossFunction``).
-Additions: ``optimize_lbfgs`` (torch L-BFGS with strong-Wolfe line search, the
-BASELINE.json C5 driver).  The trust-region Newton model uses a Hessian from
-central differences of the adjoint gradient (2 n_theta extra fused sweeps) in
-place of JAX's forward-over-reverse (``Optimizers.py:125-136``).
+Additions: ``optimize_lbfgs`` (two-loop L-BFGS with a capped step and Armijo
+backtracking, the BASELINE.json C5 driver).  The trust-region Newton model
+(``Optimizers.py:125-136``, JAX forward-over-reverse there) takes the EXACT Hessian
+from ``Problem.getLossHessianFunction`` when ``solveInverse`` passes it as ``model``
+(one factorisation + forward/adjoint/second-order solves per evaluation, factors
+reused on the device); called without ``model`` it falls back to central
+differences of the adjoint gradient (2 n_theta extra fused sweeps).
 """
 from __future__ import annotations
 
@@ -211,10 +214,12 @@ def optimize_lbfgs(f, x_0, N_steps=50, history_size=10, max_step=0.05, c1=1e-4, 
                    tolerance_grad=1e-12, f_min=1e-16):
     """L-BFGS (two-loop recursion) with Armijo backtracking.
 
-    One fused forward + adjoint sweep per function evaluation.  The first step is
+    One fused forward + adjoint sweep per function evaluation.  Every trial step is
     capped at ``max_step`` (infinity norm, in the optimiser's coordinates): the FR
     misfit's basin in the stiffness moduli is only a few percent wide (resonances
-    move past each other), so an unscaled gradient step would leave it.
+    move past each other), so an unscaled gradient step -- or a quasi-Newton step
+    whose curvature pair s.y is barely positive -- would leave it (and the loss far
+    outside, with every resonance pushed past the band, can be LOWER than inside).
     """
     vg = value_and_grad(f)
     x = np.asarray(x_0, dtype=np.float64).copy()
@@ -249,9 +254,7 @@ def optimize_lbfgs(f, x_0, N_steps=50, history_size=10, max_step=0.05, c1=1e-4, 
             Y.clear()
             d = -g
             gtd = g @ d
-        t = 1.0
-        if not S:
-            t = min(1.0, max_step / max(np.max(np.abs(d)), 1e-300))
+        t = min(1.0, max_step / max(np.max(np.abs(d)), 1e-300))
         for _ in range(max_backtrack):
             x_new = x + t * d
             f_new, g_new = vg(x_new)

@@ -45,7 +45,7 @@ int upload(T** dst, const std::vector<T>& src) {
 
 int64_t round64(int64_t x) { return (x + 63) / 64 * 64; }
 
-constexpr int kContractBlocks = 256;    // nonzero ranges per frequency group
+constexpr int kContractBlocks = 2048;   // row ranges per frequency group of the row kernels (at most)
 }  // namespace
 
 struct pfr_solver {
@@ -117,6 +117,9 @@ struct pfr_solver {
   // column's patterns; entry ranges of whole rows, about equal size (kContractBlocks of them)
   int32_t* d_ublk = nullptr;
   int4* d_uent = nullptr;
+  int n_uent = 0, n_ublk = 0;           // entries; row ranges (one single-wave workgroup each per 64 frequencies)
+  double2* d_kme = nullptr;             // entry-ordered K(i, j), K(j, i), (M(i, j), M(j, i)) (refreshed per sweep)
+  double* d_se = nullptr;               // entry-ordered S_k(i, j) (pfr_set_stiffness)
   int n_kdir = 0;
   double2 *partial = nullptr, *tq = nullptr;
   double *freqs = nullptr, *loss_terms = nullptr;
@@ -155,6 +158,7 @@ struct pfr_solver {
   // workgroup, at most), PFR_US2_SMALL (largest front of a level the paired top-down solve treats
   // with its low-register small-front variant)
   int solve_wmax = 8, fac_wmax = 16, us2_small = 110;
+  int check_fused = 0;                  // PFR_CHECK_FUSED=1: loss sweeps check both solutions in one entry walk
   // backward-error checks (pfr_set_check): PFR_CHECK_* bits, tolerance, optional per-item output;
   // per-frequency maxima scratch, forward and adjoint (kept zero between checks)
   int check_mode = 0;
@@ -455,9 +459,7 @@ void check_solution(pfr_solver* s, int which, int mode, int rhs, const pfr::RhsD
 
 // s_{q,k} partials of sum_nz S_k(nz) lam[row] x[col] (no checks), row-ordered like the loss sweep's
 void contract_rows(pfr_solver* s, const double2* lam, const double2* x, int nv, hipStream_t st) {
-  pfr::RowCheckDesc cd;
-  pfr::launch_contract_rows(false, s->d_ublk, s->d_uent, kContractBlocks, (int)(s->Fc / 64), s->stiff, s->n_stiff, cd,
-                            lam, x, s->Fc, nv, s->partial, nullptr, nullptr, st);
+  pfr::launch_contract_eg(s->d_uent, s->n_uent, s->d_se, s->n_stiff, lam, x, s->Fc, nv, s->partial, st);
 }
 
 }  // namespace
@@ -610,6 +612,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->solve_wmax = knob("PFR_SOLVE_WMAX", 8, 1, 8);
   s->fac_wmax = knob("PFR_FAC_WMAX", 16, 1, 16);
   s->us2_small = knob("PFR_US2_SMALL", 110, 0, pfr::MAX_FRONT);
+  s->check_fused = knob("PFR_CHECK_FUSED", 0, 0, 1);   // measured 2.3 ms against 2 x 0.87 ms per 2,048-frequency chunk
   s->n = S.n;
   s->nnz = S.nnz;
   s->Fc = round64(max_batch);
@@ -955,13 +958,18 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       uptr[i + 1] = (int32_t)uent.size();
     }
     std::vector<int32_t> ublk(1, 0);   // entry offsets at row starts
-    for (int b = 1; b < kContractBlocks; ++b) {
-      const int64_t target = (int64_t)uent.size() * b / kContractBlocks;
+    // enough single-wave workgroups to fill the chip (many short walks: the walk is latency-bound)
+    s->n_ublk = std::max(1, std::min(kContractBlocks, S.n));
+    for (int b = 1; b < s->n_ublk; ++b) {
+      const int64_t target = (int64_t)uent.size() * b / s->n_ublk;
       const int32_t at = *std::lower_bound(uptr.begin(), uptr.end(), (int32_t)target);
       ublk.push_back(std::max(ublk.back(), at));
     }
     ublk.push_back((int32_t)uent.size());
-    if ((rc = s->up(&s->d_uent, uent)) || (rc = s->up(&s->d_ublk, ublk))) return bail(rc);
+    s->n_uent = (int)uent.size();
+    for (int pad = 0; pad < 4; ++pad) uent.push_back(make_int4(-1, -1, -1, -1));   // a step reads 4 entries at once
+    if ((rc = s->up(&s->d_uent, uent)) || (rc = s->up(&s->d_ublk, ublk)) || (rc = s->alloc(&s->d_kme, 3 * ((int64_t)s->n_uent + 4))))
+      return bail(rc);
   }
   s->P = DevPattern{d_fronts, idx, relpos, rowf, ap, ac, an, ep, es, pm, pr, pc, S.n};
   {
@@ -1094,11 +1102,17 @@ int pfr_set_stiffness(pfr_solver* s, int32_t n_stiff, const double* stiff_dev, c
   s->n_stiff = n_stiff;
   std::memset(&s->e, 0, sizeof(s->e));
   for (int k = 0; k < n_stiff; ++k) s->e.re[k] = w[k];
+  HIP_TRY(hipSetDevice(s->device));
   if (!s->partial) {
-    HIP_TRY(hipSetDevice(s->device));
-    int rc = s->alloc(&s->partial, (int64_t)kContractBlocks * 18 * (s->Fc / 64));
+    int rc = s->alloc(&s->partial, (int64_t)pfr::contract_eg_parts(s->n_uent) * 18);
     if (rc) return rc;
   }
+  if (!s->d_se) {
+    int rc = s->alloc(&s->d_se, (int64_t)18 * (s->n_uent + 4));
+    if (rc) return rc;
+  }
+  pfr::launch_gather_entries(s->d_uent, s->n_uent + 4, nullptr, nullptr, stiff_dev, n_stiff, nullptr, s->d_se, nullptr);
+  HIP_TRY(hipDeviceSynchronize());
   return PFR_OK;
 }
 
@@ -1206,6 +1220,9 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
   const int64_t Fc = s->Fc;
   const int ngroups = (int)(Fc / 64);
   bool used[5] = {true, true, true, reverse, reverse};
+  // K may have been recombined since the last sweep (pfr_combine, any solver): refresh the entry-ordered
+  // copy the fused contraction + checks read (2.6 % of one chunk's traffic at C3, once per call)
+  if (reverse) pfr::launch_gather_entries(s->d_uent, s->n_uent + 4, s->K, s->M, nullptr, 0, s->d_kme, nullptr, st);
   for (int64_t q0 = 0; q0 < nfreq; q0 += Fc) {
     const int nv = (int)std::min<int64_t>(Fc, nfreq - q0);
     HIP_TRY(hipMemcpyAsync(s->freqs, freqs_dev + q0, nv * sizeof(double), hipMemcpyDeviceToDevice, st));
@@ -1300,7 +1317,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
       // gradient contraction fused with the backward-error checks of both solutions (the forward
       // check of a refined / unpaired sweep is already done above)
       const bool fwd_done = !paired;
-      const int want = s->check_mode & ((fwd_done ? 0 : PFR_CHECK_FORWARD) | PFR_CHECK_ADJOINT);
+      int want = s->check_mode & ((fwd_done ? 0 : PFR_CHECK_FORWARD) | PFR_CHECK_ADJOINT);
       pfr::RowCheckDesc cd;
       cd.K = s->K;
       cd.M = s->M;
@@ -1310,8 +1327,16 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
       cd.beta_im = s->beta_im;
       cd.mass_sum = s->mass_sum;
       cd.G = s->G;
-      pfr::launch_contract_rows(want != 0, s->d_ublk, s->d_uent, kContractBlocks, ngroups, s->stiff, s->n_stiff, cd,
-                                s->XA, s->X, Fc, nv, s->partial, s->d_berr_acc, s->d_berr_acc + Fc, st);
+      pfr::launch_contract_eg(s->d_uent, s->n_uent, s->d_se, s->n_stiff, s->XA, s->X, Fc, nv, s->partial, st);
+      if (want && s->check_fused)
+        pfr::launch_contract_rows(true, s->d_ublk, s->d_uent, s->n_ublk, ngroups, s->d_se, s->n_stiff, s->d_kme, cd,
+                                  s->XA, s->X, Fc, nv, nullptr, s->d_berr_acc, s->d_berr_acc + Fc, st);
+      else if (want) {
+        // the two checks as row / column walks of the original pattern (k_residual)
+        if (want & PFR_CHECK_FORWARD) check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st);
+        if (want & PFR_CHECK_ADJOINT) check_solution(s, 1, 0, 2, rg, nullptr, 0, nv, s->XA, nullptr, q0, st);
+        want = 0;
+      }
       for (int w = 0; w < 2; ++w) {
         double* acc = s->d_berr_acc + w * Fc;
         if (want & (w == 0 ? PFR_CHECK_FORWARD : PFR_CHECK_ADJOINT))
@@ -1321,7 +1346,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
           HIP_TRY(hipMemsetAsync(acc, 0, Fc * sizeof(double), st));   // computed, not requested: keep zero
       }
       pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st);
-      pfr::launch_reduce(s->partial, kContractBlocks * ngroups, s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
+      pfr::launch_reduce(s->partial, pfr::contract_eg_parts(s->n_uent), s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
                          reinterpret_cast<double2*>(w_dev), loss_dev, st);
     } else {
       record(s, 4, st);
@@ -1349,7 +1374,6 @@ int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int
   hipStream_t st = (hipStream_t)stream;
   reset_timing(s);
   const int64_t Fc = s->Fc, n = s->n;
-  const int ngroups = (int)(Fc / 64);
   int rc;
   if (!s->DX && ((rc = s->alloc(&s->DX, n * Fc)) || (rc = s->alloc(&s->DL, n * Fc)))) return rc;
   if (s->n_kdir < n_dir) {
@@ -1399,7 +1423,7 @@ int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int
     if ((rc = adjoint_solve(s, rg, s->XA, st, 1))) return rc;
     contract_rows(s, s->XA, s->X, nv, st);
     pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st);
-    pfr::launch_reduce(s->partial, kContractBlocks * ngroups, s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
+    pfr::launch_reduce(s->partial, pfr::contract_eg_parts(s->n_uent), s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
                        reinterpret_cast<double2*>(w_dev), loss_dev, st);
     // second order, per direction i (same factors):
     //   A dx_i = db_i - dA_i x ;  A^T dl_i = dG_i(dx_i) - dA_i^T l
@@ -1415,10 +1439,10 @@ int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int
       if ((rc = adjoint_solve(s, rg, s->DL, st))) return rc;
       contract_rows(s, s->DL, s->X, nv, st);
       pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->DL, Fc, s->tq, st);
-      pfr::launch_reduce(s->partial, kContractBlocks * ngroups, s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
+      pfr::launch_reduce(s->partial, pfr::contract_eg_parts(s->n_uent), s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
                          H + (int64_t)i * s->n_stiff, nullptr, st);
       contract_rows(s, s->XA, s->DX, nv, st);
-      pfr::launch_reduce(s->partial, kContractBlocks * ngroups, s->n_stiff, s->tq, zero, s->loss_terms, nv, Fc,
+      pfr::launch_reduce(s->partial, pfr::contract_eg_parts(s->n_uent), s->n_stiff, s->tq, zero, s->loss_terms, nv, Fc,
                          H + (int64_t)i * s->n_stiff, nullptr, st);
     }
     if (flags_dev) pfr::launch_flags_merge(s->flags, nv, flags_dev + q0, st);

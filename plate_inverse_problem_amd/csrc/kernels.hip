@@ -1885,20 +1885,48 @@ struct RowCheckArgs {
   const cplx* G;
 };
 
-// NS: stiffness matrices contracted (12 when the coupling block B is absent, 18 otherwise).
+// Per-entry coefficients in entry order (so that a step's scalar loads are addressed by the entry
+// counter alone, not by a loaded index): kme[3 e] = K(i, j), kme[3 e + 1] = K(j, i),
+// kme[3 e + 2] = (M(i, j), M(j, i)) (zeros where the entry is absent), se[NS e + k] = S_k(i, j).
+// Refreshed on the device whenever K may have changed (every sweep) / once for S.
+__global__ void k_gather_entries(const int4* __restrict__ ent, int nent, const cplx* __restrict__ K,
+                                 const double* __restrict__ M, const double* __restrict__ stiff, int ns,
+                                 cplx* __restrict__ kme, double* __restrict__ se) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nent) return;
+  const int4 en = ent[e];
+  const bool ij = en.x >= 0 && en.y >= 0, ji = en.x >= 0 && en.z >= 0;
+  if (kme) {
+    kme[3 * (int64_t)e] = ij ? K[en.y] : make_double2(0, 0);
+    kme[3 * (int64_t)e + 1] = ji ? K[en.z] : make_double2(0, 0);
+    kme[3 * (int64_t)e + 2] = make_double2(ij ? M[en.y] : 0.0, ji ? M[en.z] : 0.0);
+  }
+  if (se)
+    for (int k = 0; k < ns; ++k) se[(int64_t)e * ns + k] = ij ? stiff[(int64_t)en.y * ns + k] : 0.0;
+}
+
+// NS: stiffness matrices contracted (12 when the coupling block B is absent, 18 otherwise; 0 = no
+// contraction, checks only).  The contraction and the checks run as two launches over the same
+// entries (CHECK = false, NS > 0 / CHECK = true, NS = 0): fused, the pair of varying gathers per entry
+// (x_j and lambda_j; the contraction alone gathers only x_j, lambda_i once per row) at the register
+// footprint of the 12-18 accumulators halves the loads in flight per SIMD -- measured 5.1 ms per
+// 2,048-frequency chunk against 0.9 + 1.2 ms for the two launches.
 // Branch-free per entry (pseudo-entry and tail handling by selects), so that the loads of a step stay
 // counted waits instead of the vmcnt(0) a branch between them would force.
 template <bool CHECK, int NS>
 __global__ __launch_bounds__(64) void k_contract_rows(const int* __restrict__ eblk, const int4* __restrict__ ent,
-                                                      const double* __restrict__ stiff, RowCheckArgs A,
-                                                      const cplx* __restrict__ Lam, const cplx* __restrict__ X,
-                                                      int64_t Fc, int nvalid, cplx* __restrict__ partial,
-                                                      double* __restrict__ acc_f, double* __restrict__ acc_a) {
-  constexpr int U = CHECK ? 2 : 4;          // entries per step
+                                                      const double* __restrict__ se, const cplx* __restrict__ kme,
+                                                      RowCheckArgs A, const cplx* __restrict__ Lam,
+                                                      const cplx* __restrict__ X, int64_t Fc, int nvalid,
+                                                      cplx* __restrict__ partial, double* __restrict__ acc_f,
+                                                      double* __restrict__ acc_a) {
+  // entries per step: every scalar operand of a step (entries, S rows / K, M values) is loaded up front
+  // in SGPRs, then every vector load, then one wait -- S needs 2 NS dwords per entry
+  constexpr int U = NS > 0 ? 2 : 4;
   const int lane = threadIdx.x & 63;
   const int64_t q = (int64_t)blockIdx.y * 64 + lane;
   const int e0 = eblk[blockIdx.x], e1 = eblk[blockIdx.x + 1];
-  cplx acc[NS];
+  cplx acc[NS > 0 ? NS : 1];
 #pragma unroll
   for (int k = 0; k < NS; ++k) acc[k] = make_double2(0, 0);
   double om2 = 0.0, bsr = 0.0, bsi = 0.0;
@@ -1916,34 +1944,45 @@ __global__ __launch_bounds__(64) void k_contract_rows(const int* __restrict__ eb
   const cplx* __restrict__ Lq = Lam + q;
   const cplx* __restrict__ Gq = A.G + q;
   for (int e = e0; e < e1; e += U) {
+    // the entry array is padded by 4 entries: the step's entries load as one block
     int4 en[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) en[u] = ent[min(e + u, e1 - 1)];
-    cplx v1[U], v2[U];
+    for (int u = 0; u < U; ++u) en[u] = ent[e + u];
+    double sv[U][NS > 0 ? NS : 1];
+    cplx kij[U], kji[U], mm[U];
     double rv[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const bool pseudo = en[u].x < 0;                           // wave-uniform
-      const int64_t o = (int64_t)(pseudo ? en[u].w : en[u].x) * Fc;
-      v1[u] = (pseudo ? Lq : Xq)[o];                             // lambda_i | x_j
+#pragma unroll
+      for (int k = 0; k < NS; ++k) sv[u][k] = se[(int64_t)(e + u) * NS + k];
       if (CHECK) {
-        v2[u] = (pseudo ? Gq : Lq)[o];                           // g_i | lambda_j
-        rv[u] = A.rhsP[en[u].w];
+        kij[u] = kme[3 * (int64_t)(e + u)];
+        kji[u] = kme[3 * (int64_t)(e + u) + 1];
+        mm[u] = kme[3 * (int64_t)(e + u) + 2];
+        rv[u] = A.rhsP[max(en[u].w, 0)];
       }
     }
+    cplx v1[U], v2[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool pseudo = en[u].x < 0;                           // wave-uniform
+      const int64_t o = (int64_t)(pseudo ? max(en[u].w, 0) : en[u].x) * Fc;
+      v1[u] = (pseudo ? Lq : Xq)[o];                             // lambda_i | x_j
+      if (CHECK) v2[u] = (pseudo ? Gq : Lq)[o];                  // g_i | lambda_j
+    }
+    __builtin_amdgcn_sched_group_barrier(0x020, CHECK ? 2 * U : U, 0);   // the step's vector loads first
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const bool in = e + u < e1;                                // wave-uniform
       const bool start = in && en[u].x < 0;                      // a row starts here
-      const double mij = in && en[u].y >= 0 ? 1.0 : 0.0;
-      const int nz = max(en[u].y, 0);
-      lam = start ? v1[u] : lam;
-      const cplx p = cscale(cmul(lam, v1[u]), mij);
-      const double* sk = stiff + (int64_t)nz * NS;
+      if (NS > 0) {
+        lam = start ? v1[u] : lam;
+        const cplx p = cscale(cmul(lam, v1[u]), in ? 1.0 : 0.0);   // S is zero on pseudo / absent entries
 #pragma unroll
-      for (int k = 0; k < NS; ++k) {
-        acc[k].x = fma(sk[k], p.x, acc[k].x);
-        acc[k].y = fma(sk[k], p.y, acc[k].y);
+        for (int k = 0; k < NS; ++k) {
+          acc[k].x = fma(sv[u][k], p.x, acc[k].x);
+          acc[k].y = fma(sv[u][k], p.y, acc[k].y);
+        }
       }
       if (CHECK) {
         // close the previous row where a new one starts
@@ -1954,11 +1993,9 @@ __global__ __launch_bounds__(64) void k_contract_rows(const int* __restrict__ eb
         bf = closing && dr > 0.0 ? fmax(bf, cr / dr) : bf;
         ba = closing && ds > 0.0 ? fmax(ba, cs / ds) : ba;
         open = start ? 1.0 : open;
-        const double mji = in && en[u].z >= 0 ? 1.0 : 0.0;
-        const int nzt = max(en[u].z, 0);
-        const cplx kij = A.K[nz], kji = A.K[nzt];
-        const cplx aij = cscale(make_double2(fma(-om2, A.M[nz], kij.x), kij.y), mij);
-        const cplx aji = cscale(make_double2(fma(-om2, A.M[nzt], kji.x), kji.y), mji);
+        const double m = in ? 1.0 : 0.0;                          // kme is zero on pseudo / absent entries
+        const cplx aij = cscale(make_double2(fma(-om2, mm[u].x, kij[u].x), kij[u].y), m);
+        const cplx aji = cscale(make_double2(fma(-om2, mm[u].y, kji[u].x), kji[u].y), m);
         const cplx b = make_double2(rv[u] * bsr, rv[u] * bsi);
         r = start ? b : cfms(r, aij, v1[u]);
         s = start ? v2[u] : cfms(s, aji, v2[u]);
@@ -1989,6 +2026,74 @@ __global__ __launch_bounds__(64) void k_contract_rows(const int* __restrict__ eb
     if (bad) bf = ba = __longlong_as_double(0x7ff0000000000000LL);
     atomicMax(reinterpret_cast<unsigned long long*>(acc_f + q), (unsigned long long)__double_as_longlong(bf));
     atomicMax(reinterpret_cast<unsigned long long*>(acc_a + q), (unsigned long long)__double_as_longlong(ba));
+  }
+}
+
+// Gradient contraction, entry-major: w_k = sum_e S_k(e) P_e with P_e = sum_q lambda_i(q) x_j(q) -- the
+// frequency sum is taken first.  A wave owns EW consecutive entries and walks every 64-frequency group
+// of the chunk, accumulating P_e per lane (contiguous 1 KiB runs of x_j and lambda_i per group); then one
+// cross-lane sum per entry and S_k(e) P_e with the S row read once per entry (not once per entry and
+// frequency group: with the sum over frequencies inside, the 12-18 scalar stiffness loads per entry and
+// the per-lane accumulators of all stiffness matrices drop out of the frequency loop).
+// Pseudo entries (row starts) and absent entries carry S = 0.  One partial per wave (k_reduce).
+#ifndef PFR_CEG_EW
+#define PFR_CEG_EW 8
+#endif
+constexpr int CEG_EW = PFR_CEG_EW;   // entries per wave of k_contract_eg
+template <int NS, int EW>
+__global__ __launch_bounds__(256) void k_contract_eg(const int4* __restrict__ ent, int nent,
+                                                     const double* __restrict__ se, const cplx* __restrict__ Lam,
+                                                     const cplx* __restrict__ X, int64_t Fc, int nvalid,
+                                                     cplx* __restrict__ partial) {
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const int e0 = wv * EW;
+  if (e0 >= nent) return;
+  int64_t oi[EW], oj[EW];
+#pragma unroll
+  for (int u = 0; u < EW; ++u) {
+    const int4 en = ent[min(e0 + u, nent - 1)];
+    oi[u] = (int64_t)max(en.w, 0) * Fc + lane;
+    oj[u] = (int64_t)max(en.x, 0) * Fc + lane;
+  }
+  cplx P[EW];
+#pragma unroll
+  for (int u = 0; u < EW; ++u) P[u] = make_double2(0, 0);
+  for (int64_t g = 0; g < Fc; g += 64) {
+    cplx li[EW], xj[EW];
+#pragma unroll
+    for (int u = 0; u < EW; ++u) {
+      li[u] = Lam[oi[u] + g];
+      xj[u] = X[oj[u] + g];
+    }
+    const double m = g + lane < nvalid ? 1.0 : 0.0;
+#pragma unroll
+    for (int u = 0; u < EW; ++u) P[u] = cadd(P[u], cscale(cmul(li[u], xj[u]), m));
+  }
+  cplx part[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) part[k] = make_double2(0, 0);
+#pragma unroll
+  for (int u = 0; u < EW; ++u) {
+    double re = P[u].x, im = P[u].y;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      re += __shfl_xor(re, o);
+      im += __shfl_xor(im, o);
+    }
+    const double in = e0 + u < nent ? 1.0 : 0.0;
+    const double* sk = se + (int64_t)min(e0 + u, nent - 1) * NS;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      part[k].x = fma(sk[k] * in, re, part[k].x);
+      part[k].y = fma(sk[k] * in, im, part[k].y);
+    }
+  }
+  if (lane < NS) {
+    cplx v = part[0];
+#pragma unroll
+    for (int k = 1; k < NS; ++k) v = lane == k ? part[k] : v;
+    partial[(int64_t)wv * NS + lane] = v;
   }
 }
 
@@ -2236,22 +2341,32 @@ void launch_functional(const FunctionalArgs& A, const double2* X, int64_t Fc, in
   LAUNCH(k_functional, dim3((unsigned)((Fc + 63) / 64)), dim3(64), st, A, X, Fc, nvalid, q0, fr_out, loss_terms, G);
 }
 
-void launch_contract_rows(bool check, const int* eblk, const int4* ent, int nblk, int ngroups, const double* stiff,
-                          int n_stiff, const RowCheckDesc& d, const double2* Lam, const double2* X, int64_t Fc,
-                          int nvalid, double2* partial, double* acc_f, double* acc_a, hipStream_t st) {
+void launch_gather_entries(const int4* ent, int nent, const double2* K, const double* M, const double* stiff, int ns,
+                           double2* kme, double* se, hipStream_t st) {
+  if (nent <= 0) return;
+  LAUNCH(k_gather_entries, dim3((nent + 255) / 256), dim3(256), st, ent, nent, K, M, stiff, ns, kme, se);
+}
+
+void launch_contract_rows(bool check, const int* eblk, const int4* ent, int nblk, int ngroups, const double* se,
+                          int n_stiff, const double2* kme, const RowCheckDesc& d, const double2* Lam, const double2* X,
+                          int64_t Fc, int nvalid, double2* partial, double* acc_f, double* acc_a, hipStream_t st) {
   RowCheckArgs a;
   a.K = d.K; a.M = d.M; a.freqs = d.freqs; a.rhsP = d.rhsP; a.beta_re = d.beta_re; a.beta_im = d.beta_im;
   a.mass_sum = d.mass_sum; a.G = d.G;
   const dim3 g(nblk, ngroups), b(64);
-#define CR(C, N) LAUNCH((k_contract_rows<C, N>), g, b, st, eblk, ent, stiff, a, Lam, X, Fc, nvalid, partial, acc_f, acc_a)
-  if (n_stiff == 12) {
-    if (check) CR(true, 12);
-    else CR(false, 12);
-  } else if (n_stiff == 18) {
-    if (check) CR(true, 18);
-    else CR(false, 18);
-  }
+#define CR(C, N) LAUNCH((k_contract_rows<C, N>), g, b, st, eblk, ent, se, kme, a, Lam, X, Fc, nvalid, partial, acc_f, acc_a)
+  if (check) CR(true, 0);
 #undef CR
+}
+
+int contract_eg_parts(int nent) { return (nent + CEG_EW - 1) / CEG_EW; }
+
+void launch_contract_eg(const int4* ent, int nent, const double* se, int n_stiff, const double2* Lam, const double2* X,
+                        int64_t Fc, int nvalid, double2* partial, hipStream_t st) {
+  const int waves = contract_eg_parts(nent);
+  const dim3 g((waves + 3) / 4), b(256);
+  if (n_stiff == 12) LAUNCH((k_contract_eg<12, CEG_EW>), g, b, st, ent, nent, se, Lam, X, Fc, nvalid, partial);
+  else LAUNCH((k_contract_eg<18, CEG_EW>), g, b, st, ent, nent, se, Lam, X, Fc, nvalid, partial);
 }
 
 void launch_rhs_dot(const int* sup, const double* val, int n_sup, const double2* Lam, int64_t Fc, double2* t_out,

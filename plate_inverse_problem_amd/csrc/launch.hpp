@@ -74,9 +74,16 @@ struct RowCheckDesc {
   double beta_re = 0, beta_im = 0, mass_sum = 0;
   const double2* G = nullptr;
 };
-void launch_contract_rows(bool check, const int* eblk, const int4* ent, int nblk, int ngroups, const double* stiff,
-                          int n_stiff, const RowCheckDesc& d, const double2* Lam, const double2* X, int64_t Fc,
-                          int nvalid, double2* partial, double* acc_f, double* acc_a, hipStream_t st);
+void launch_contract_rows(bool check, const int* eblk, const int4* ent, int nblk, int ngroups, const double* se,
+                          int n_stiff, const double2* kme, const RowCheckDesc& d, const double2* Lam, const double2* X,
+                          int64_t Fc, int nvalid, double2* partial, double* acc_f, double* acc_a, hipStream_t st);
+// gradient contraction with the frequency sum first (one partial per wave: contract_eg_parts of them)
+int contract_eg_parts(int nent);
+void launch_contract_eg(const int4* ent, int nent, const double* se, int n_stiff, const double2* Lam, const double2* X,
+                        int64_t Fc, int nvalid, double2* partial, hipStream_t st);
+// entry-ordered copies of K / M (kme, may be NULL) and of the stiffness matrices (se, may be NULL)
+void launch_gather_entries(const int4* ent, int nent, const double2* K, const double* M, const double* stiff, int ns,
+                           double2* kme, double* se, hipStream_t st);
 void launch_rhs_dot(const int* sup, const double* val, int n_sup, const double2* Lam, int64_t Fc, double2* t_out,
                     hipStream_t st);
 // w_out[k] += -sum(partial[., k]) + e_k sum_q t_q ;  loss_out += sum_q loss_terms (q < nvalid)

@@ -140,6 +140,7 @@ def test_c2_forward_sweep_matches_truth():
     {"PFR_US2_SMALL": "1024"},
     {"PFR_FAC_WMAX": "1", "PFR_SOLVE_WMAX": "1"},
     {"PFR_FAC_WMAX": "16", "PFR_SOLVE_WMAX": "8"},
+    {"PFR_CHECK_FUSED": "1"},
 ])
 def test_kernel_variants_match_oracle(env, monkeypatch):
     from oracle.plate_oracle import loss_and_grad

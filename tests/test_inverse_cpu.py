@@ -65,7 +65,7 @@ def test_trust_region_with_exact_model():
 
 def test_lbfgs_converges():
     f, xs = _quad()
-    r = O.optimize_lbfgs(f, np.zeros(3), N_steps=20)
+    r = O.optimize_lbfgs(f, np.zeros(3), N_steps=20, max_step=10.0)
     assert np.allclose(r.x, xs, atol=1e-7) and r.f < 1e-12
 
 
