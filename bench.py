@@ -24,7 +24,7 @@ forward + adjoint (loss + gradient), fp64.
   lanes overlap, so a launch's duration there also contains the other lane's
   work: reported as ``concurrent_*``); ``traffic`` = measured HBM bytes per
   launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes
-  (profiles/r01/pmc_traffic.json, gfx950-corrected); the whole factorisation
+  (the newest profiles/rNN/pmc_traffic.json, gfx950-corrected); the whole factorisation
   (``factor_roofline``) and the triangular solves (``sptrsv_roofline``) beside it;
 * ``cpu_baseline``: the oracle (scipy SuperLU, one process per core) on a
   bounded sample of the same workload, rank 0, N = 1 only.
@@ -34,6 +34,7 @@ Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--freqs F] [--ny NY]
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -48,10 +49,12 @@ sys.path.insert(0, REPO)
 
 FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 vector/matrix (spec; MI355X_MICROARCH.md lists no fp64 row)
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
-PMC_FILE = os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")
+# the newest round's committed PMC traffic summary (profiles/rNN/pmc_traffic.json)
+PMC_FILE = (sorted(glob.glob(os.path.join(REPO, "profiles", "r[0-9][0-9]", "pmc_traffic.json")))
+            or [os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")])[-1]
 # kernel classes of the factorisation (libpfr per-class HIP-event timings, pfr_last_kernel_timings
 # order); the rocprof names of a class's kernels start with one of its prefixes
-KERNELS = (("k_assemble_level",), ("k_factor_level",), ("k_offdiag_level",), ("k_schur_sym_blk",),
+KERNELS = (("k_assemble_level",), ("k_factor_level", "k_factor_sym"), ("k_offdiag_level",), ("k_schur_sym_blk",),
            ("k_schur_level", "k_schur_sym_level"))
 KERNEL_NAMES = ("k_assemble_level", "k_factor_level", "k_offdiag_level", "k_schur_sym_blk",
                 "k_schur_sym_level / k_schur_level")

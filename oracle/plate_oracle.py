@@ -18,9 +18,10 @@ A numpy/scipy restatement of the reference's per-frequency computation:
   not available; this oracle uses scipy SuperLU (complex128, threshold partial
   pivoting) followed by UMFPACK's default iterative refinement (the reference
   passes a NULL Control, so ``umfpack_zi_solve`` refines up to UMFPACK_IRSTEP = 2
-  steps, ``refined_solve``).  **Parity at the UMFPACK boundary is unpinned** (no
-  reference test pins solver outputs): parity is defined against
-  this fp64 restatement and checked by a dense ``numpy.linalg.solve`` cross-check;
+  steps, ``refined_solve``).  UMFPACK itself cannot be built here and no reference
+  test pins solver outputs; the restatement is pinned against the
+  reference's own Problem / Optimizers code run with this solve in UMFPACK's place
+  (``reference_run.npz``, below) and by a dense ``numpy.linalg.solve`` cross-check;
 * ``functional``     -- ``Problem.py:454-477`` (dense interpolation, means,
   ``fr = sqrt((ts|U|)^2 + (ts|V|)^2 + |W|^2)``);
 * ``loss``           -- ``Problem.py:948-975`` (MSE, RMSE, MSE_AFC, MSE_LOG_AFC);
@@ -30,9 +31,16 @@ A numpy/scipy restatement of the reference's per-frequency computation:
   ``InnerState.h:183-185``); the matrix cotangent is ``ct[row] * x[col]``
   (``Sparse.py:173-176``).
 
-Pins of the restatement itself: ``tests/golden/material_abd.json`` (reference
-``Material.py`` outputs), ``tests/golden/layout_*.npz`` (reference block
-layout), finite differences and a dense-solve cross-check (tests/).
+Pins of the restatement itself: ``tests/golden/reference_run.npz`` -- outputs of
+the reference's own ``Problem.solveForward`` / ``getLossFunction`` (4 losses) /
+``Optimizers.optimize_gd`` / ``optimize_cd`` run here on CPU under numpy stand-ins
+for JAX (``tests/golden/make_reference_run.py``; the only non-reference arithmetic
+in that chain is this module's ``refined_solve`` standing in for UMFPACK),
+``tests/golden/material_abd.json`` (reference ``Material.py`` outputs),
+``tests/golden/layout_*.npz`` / ``freefem_stream.npz`` (reference block layout and
+FreeFEM stream parsers), extended-precision truth fixtures at C2 / C3 size
+(``tests/golden/make_c3_truth.py``), finite differences and a dense-solve
+cross-check (tests/).
 """
 from __future__ import annotations
 
