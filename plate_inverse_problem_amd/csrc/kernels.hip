@@ -502,6 +502,7 @@ __global__ __launch_bounds__(PFR_FAC_LB) void k_factor_sym(DevPattern P, const i
 #ifndef PFR_OB
 #define PFR_OB 8
 #endif
+static_assert(PFR_OB >= 1 && PFR_OB <= 16, "k_offdiag_level tail cases cover chunks of at most 16 columns");
 constexpr int OB = PFR_OB;   // columns per left-looking chunk of k_offdiag_level
 
 // Where the off-diagonal entries come from (the panel entries of L21 / U12 are
@@ -656,6 +657,9 @@ __global__ __launch_bounds__(256) void k_offdiag_level(DevPattern P, const int4*
 #define TAIL(n) \
   case n: offdiag_chunk<MODE, n>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q); break;
     TAIL(1) TAIL(2) TAIL(3) TAIL(4) TAIL(5) TAIL(6) TAIL(7)
+#if PFR_OB > 8
+    TAIL(8) TAIL(9) TAIL(10) TAIL(11) TAIL(12) TAIL(13) TAIL(14) TAIL(15)
+#endif
 #undef TAIL
     default: break;
   }
@@ -887,21 +891,54 @@ __global__ __launch_bounds__(64 * BC) void k_schur_sym_blk(DevPattern P, const i
     }
   }
   // stage copy: row slot rho of pivot u: rho < 16 -> L21 row i0 + rho, rho < 32 -> L21 row
-  // j0 + rho - 16, rho = 32 -> U(k, k); wave w copies slots w and w + 16 of every pivot, wave u
-  // the pivot of step u.  Rows past the block and pivots past ns read clamped (valid) addresses.
-  // wave w copies row operands w + NW h (h < BR / NW), column operand w and, if w == u, U(k, k)
-  const cplx* ra[BR / NW];
+  // j0 + rho - 16, rho = 32 -> U(k, k); wave w copies row operands w + NW h (h < BR / NW), column
+  // operand w and, if w == u, U(k, k).  Rows past the block and pivots past ns read clamped (valid)
+  // addresses.  Every address is scalar (saddr form: wave-uniform row pointer + lane * 16) and the
+  // pivot offsets advance by one scalar add per stage: the scalar unit issues for all 16 waves of the
+  // CU, and the per-copy 64-bit index products, generic->LDS casts and M0 saves it had to issue
+  // before set the pivot rate (measured: as many scalar as vector instructions per pivot).
+  const uint32_t voff = (uint32_t)lane * 16u;
+  const int64_t rowb = Fc * 16;                                  // bytes between consecutive entries
+  const char* sb = reinterpret_cast<const char*>(F + fr.off * Fc + (int64_t)by * 64);   // uniform
+  const char* ra[BR / NW];
 #pragma unroll
-  for (int h = 0; h < BR / NW; ++h) ra[h] = base + ((int64_t)(ns + min(bk.y + w + NW * h, r - 1)) * f) * Fc;
-  const cplx* rb = base + ((int64_t)(ns + min(bk.z + w, r - 1)) * f) * Fc;
-  auto stage = [&](int buf, int k0) {
+  for (int h = 0; h < BR / NW; ++h) ra[h] = sb + (int64_t)(ns + min(bk.y + w + NW * h, r - 1)) * f * rowb;
+  const char* rb = sb + (int64_t)(ns + min(bk.z + w, r - 1)) * f * rowb;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&sop[0][0][0][0]);
+  constexpr uint32_t kRowB = 64 * sizeof(cplx), kPivB = BROWS * kRowB, kBufB = KC * kPivB;
+  // pivot of the next stage to issue, and its byte offsets (row entry k, diagonal entry (k, k))
+  int kn = 0;
+  int64_t offk = 0, offd = 0;
+  const int64_t diagb = (int64_t)(f + 1) * rowb;
+  auto stage = [&](int buf) {
 #pragma unroll
     for (int u = 0; u < KC; ++u) {
-      const int k = max(min(k0 + u, ns - 1), 0);
-      if (w == u) glds16(base + (int64_t)k * (f + 1) * Fc, &sop[buf][u][BR + BC][0]);
+      const uint32_t d = lds0 + (uint32_t)buf * kBufB + (uint32_t)u * kPivB;
+      uint32_t keep;
+      if (w == u)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(voff), "s"(sb + offd), "s"(d + (uint32_t)(BR + BC) * kRowB)
+                     : "memory");
+      asm volatile(
+          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
+          "s_mov_b32 m0, %5\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %3\n\ts_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "v"(voff), "s"(ra[0] + offk), "s"(rb + offk), "s"(d + (uint32_t)w * kRowB),
+            "s"(d + (uint32_t)(BR + w) * kRowB)
+          : "memory");
 #pragma unroll
-      for (int h = 0; h < BR / NW; ++h) glds16(ra[h] + (int64_t)k * Fc, &sop[buf][u][w + NW * h][0]);
-      glds16(rb + (int64_t)k * Fc, &sop[buf][u][BR + w][0]);
+      for (int h = 1; h < BR / NW; ++h)   // BC = 8: a second row operand per wave
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep)
+                     : "v"(voff), "s"(ra[h] + offk), "s"(d + (uint32_t)(w + NW * h) * kRowB)
+                     : "memory");
+      if (kn < ns - 1) {        // advance; past the last pivot the copies repeat it (never read)
+        ++kn;
+        offk += rowb;
+        offd += diagb;
+      }
     }
   };
   auto compute = [&](int buf, int k0) {
@@ -927,7 +964,7 @@ __global__ __launch_bounds__(64 * BC) void k_schur_sym_blk(DevPattern P, const i
   // children's entries gathered above are older than these copies, so the first counted wait
   // retires them together with stage 0: one memory round trip for both.
 #pragma unroll
-  for (int p = 0; p < NB - 1; ++p) stage(p, p * KC);
+  for (int p = 0; p < NB - 1; ++p) stage(p);
   // the gathered values are needed from here on: tie them down once (otherwise the compiler waits
   // for them -- vmcnt(0), copies in flight included -- inside the loop, every step)
 #pragma unroll
@@ -940,7 +977,7 @@ __global__ __launch_bounds__(64 * BC) void k_schur_sym_blk(DevPattern P, const i
     // copy or two more than needed)
     PFR_WAIT_VM((NB - 2) * (BR / NW + 1) * KC);
     PFR_BARRIER();   // stage st visible to all; everyone done with stage st - 1
-    stage((st + NB - 1) % NB, (st + NB - 1) * KC);
+    stage((st + NB - 1) % NB);
     compute(st % NB, st * KC);
   }
   PFR_WAIT_VM(0);
