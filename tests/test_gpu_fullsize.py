@@ -18,7 +18,10 @@ determined only to ~1e-7 .. 1e-6 near the resonance: fp64 solves with componentw
 at machine precision (SuperLU + the reference's default UMFPACK refinement, a static-pivot
 factorisation + refinement) scatter by that much around the extended-precision solution
 (tests/golden/make_c3_truth.py), while unrefined threshold-pivoted SuperLU is
-off by up to 4e-5.  Hence per size: fr and loss relative error <= 2e-9 (ny <= 6), <= 5e-7 (C2, at
+off by up to 4e-5.  At ny = 6 the band is ~1e-9 near the first resonance (the oracle itself is
+1.15e-9 from the extended-precision solution there, both GPU A11 LU kernels 1.6e-9 / 2.2e-9, all
+with componentwise backward error 1.7e-15: tools/acc_check.py), so two such solvers differ by up to
+the sum.  Hence per size: fr and loss relative error <= 5e-9 (ny <= 6), <= 5e-7 (C2, at
 its resonance peaks), <= 2e-6 (C3 against the extended-precision fixture; median <= 5e-8);
 gradient (inf-norm relative) <= 1e-7 (ny <= 6), <= 5e-6 (C3).  The componentwise backward error of
 every GPU solve (the measure UMFPACK's refinement monitors) must be <= 1e-12.
@@ -34,7 +37,7 @@ from helpers import make_problem, oracle_for
 
 pytestmark = pytest.mark.gpu
 
-FR_RTOL = 2e-9          # ny <= 6
+FR_RTOL = 5e-9          # ny <= 6
 GRAD_RTOL = 1e-7
 FR_RTOL_C2 = 5e-7
 FR_RTOL_C3 = 2e-6
