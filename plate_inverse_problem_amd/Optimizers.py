@@ -7,8 +7,9 @@ backtracking, the BASELINE.json C5 driver).  The trust-region Newton model
 (``Optimizers.py:125-136``, JAX forward-over-reverse there) takes the EXACT Hessian
 from ``Problem.getLossHessianFunction`` when ``solveInverse`` passes it as ``model``
 (one factorisation + forward/adjoint/second-order solves per evaluation, factors
-reused on the device); called without ``model`` it falls back to central
-differences of the adjoint gradient (2 n_theta extra fused sweeps).
+reused on the device; ``solveInverse(..., exact_hessian=False)`` opts out); called
+without ``model`` it falls back to central differences of the adjoint gradient
+(2 n_theta extra fused sweeps).
 """
 from __future__ import annotations
 
