@@ -53,3 +53,12 @@ def oracle_for(p):
                          p.Lh_size, (p.I0, p.I0Corr, p.I2, p.I2Corr), p.accelerometer.height,
                          p.accelerometer.effective_height, p.accelerometer.transverse_sensitivity,
                          m.atype, p.geometry.height, angles)
+
+
+def report(name, **vals):
+    """Measured errors of a GPU test, appended to $PFR_TEST_REPORT (JSON lines) when set."""
+    path = os.environ.get("PFR_TEST_REPORT")
+    if path:
+        import json
+        with open(path, "a") as f:
+            f.write(json.dumps({"test": name, **{k: float(v) for k, v in vals.items()}}) + "\n")

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import make_problem, oracle_for
+from helpers import make_problem, oracle_for, report
 
 pytestmark = pytest.mark.gpu
 
@@ -35,6 +35,7 @@ def test_forward_parity(material):
     fr = p.solveForward(freqs)
     ref = oracle_for(p).fr(freqs, p.parameters)
     assert np.all(np.isfinite(fr))
+    report("forward " + material, fr_rel=np.max(np.abs(fr - ref) / np.abs(ref)))
     assert np.max(np.abs(fr - ref) / np.abs(ref)) < FR_RTOL
 
 
@@ -44,6 +45,7 @@ def test_forward_chunking_and_padding():
     freqs = np.linspace(40.0, 600.0, 151)
     fr = p.solveForward(freqs)
     ref = oracle_for(p).fr(freqs, p.parameters)
+    report("chunking", fr_rel=np.max(np.abs(fr - ref) / np.abs(ref)))
     assert np.max(np.abs(fr - ref) / np.abs(ref)) < FR_RTOL
 
 
@@ -66,6 +68,7 @@ def test_loss_and_grad_parity(loss_type):
     val = loss_fn(x)
     val.backward()
     lo, go = loss_and_grad(oracle_for(p), freqs, ref, loss_type, theta)
+    report("loss+grad " + loss_type, loss_rel=abs(val.item() - lo) / abs(lo), grad_rel=_rel(x.grad.numpy(), go))
     assert abs(val.item() - lo) / abs(lo) < FR_RTOL
     assert _rel(x.grad.numpy(), go) < GRAD_RTOL
 
@@ -92,6 +95,7 @@ def test_scaling_params():
     x = torch.tensor(np.array([1.05, 0.97, 1.1]), requires_grad=True)
     p.getLossFunction(freqs, ref, "MSE", scaling_params=s)(x).backward()
     lo, go = loss_and_grad(oracle_for(p), freqs, ref, "MSE", x.detach().numpy(), scaling=s)
+    report("scaling params", grad_rel=_rel(x.grad.numpy(), go))
     assert _rel(x.grad.numpy(), go) < GRAD_RTOL
 
 
@@ -130,6 +134,7 @@ def test_coupled_laminate_gradient():
     val = p.getLossFunction(freqs, ref, "MSE_AFC")(x)
     val.backward()
     lo, go = loss_and_grad(oracle_for(p), freqs, ref, "MSE_AFC", theta)
+    report("coupled laminate", loss_rel=abs(val.item() - lo) / abs(lo), grad_rel=_rel(x.grad.numpy(), go))
     assert abs(val.item() - lo) / abs(lo) < FR_RTOL
     assert _rel(x.grad.numpy(), go) < GRAD_RTOL
 
