@@ -18,7 +18,8 @@ __global__ __launch_bounds__(256) void k_mfma(double* out, int iters, double a0)
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
-__global__ __launch_bounds__(256) void k_valu(double* out, int iters, double a0) {
+__global__ __launch_bounds__(256) void k_valu(double* out, int iters, double a0, long long* clk) {
+  const long long c0 = clock64(), w0 = wall_clock64();
   double acc[16];
   for (int i = 0; i < 16; ++i) acc[i] = i;
   double a = a0 + threadIdx.x * 1e-9, b = a0 - threadIdx.x * 1e-9;
@@ -29,11 +30,19 @@ __global__ __launch_bounds__(256) void k_valu(double* out, int iters, double a0)
   double s = 0;
   for (int i = 0; i < 16; ++i) s += acc[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    clk[0] = clock64() - c0;
+    clk[1] = wall_clock64() - w0;
+  }
 }
 
 int main() {
   double* out;
+  long long* clk;
   hipMalloc(&out, 256 * 4096 * sizeof(double));
+  hipMalloc(&clk, 2 * sizeof(long long));
+  int wall_khz = 0;
+  hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, 0);
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
@@ -48,12 +57,15 @@ int main() {
     double flops = 2.0 * 16 * 16 * 4 * 4 * (double)iters * (blocks * 4);
     printf("mfma f64 16x16x4: %.3f ms  %.1f TFLOP/s\n", ms, flops / ms / 1e9);
     hipEventRecord(e0);
-    k_valu<<<blocks, 256>>>(out, iters, 1.0);
+    k_valu<<<blocks, 256>>>(out, iters, 1.0, clk);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
     hipEventElapsedTime(&ms, e0, e1);
     flops = 2.0 * 16 * (double)iters * blocks * 256;
-    printf("valu f64 fma:     %.3f ms  %.1f TFLOP/s\n", ms, flops / ms / 1e9);
+    long long c[2];
+    hipMemcpy(c, clk, sizeof(c), hipMemcpyDeviceToHost);
+    printf("valu f64 fma:     %.3f ms  %.1f TFLOP/s  (block 0: %lld shader cycles in %lld wall ticks at %d kHz -> %.2f GHz)\n",
+           ms, flops / ms / 1e9, c[0], c[1], wall_khz, wall_khz > 0 ? (double)c[0] / ((double)c[1] / (wall_khz * 1e3)) / 1e9 : 0.0);
   }
   return 0;
 }
