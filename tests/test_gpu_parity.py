@@ -1,10 +1,13 @@
 """GPU parity: the HIP path (through the C ABI) against the CPU oracle.
 
-Tolerances (fp64 throughout, stated per SURVEY.md §8c and DESIGN.md):
-* fr: relative error <= 1e-8 (static-pivot multifrontal vs SuperLU threshold
-  pivoting on the same matrices; both fp64, orderings differ);
-* loss: relative <= 1e-8; gradient: relative (inf-norm) <= 1e-6 against the
-  oracle adjoint, <= 1e-4 against central finite differences.
+Tolerances (fp64 throughout; SURVEY.md §8c proposes fr <= 1e-9, gradient <= 1e-7):
+* fr and loss: relative error <= 5e-9.  On these meshes (ny 4-6) fr near the first resonance is
+  determined by the fp64 problem data only to ~1e-9: the oracle (SuperLU + UMFPACK's refinement)
+  is itself 1.15e-9 from the extended-precision solution at ny = 6, both backward stable
+  (tools/acc_check.py), so two such solvers differ by up to the sum.  Measured (round 2, written
+  to $PFR_TEST_REPORT): fr 7e-11 .. 1.33e-9, loss 2e-11 .. 4e-10;
+* gradient: relative (inf-norm) <= 1e-7 against the oracle adjoint (measured 3e-11 .. 1.7e-9),
+  <= 1e-4 against central finite differences.
 """
 import numpy as np
 import pytest
@@ -14,8 +17,8 @@ from helpers import make_problem, oracle_for, report
 
 pytestmark = pytest.mark.gpu
 
-FR_RTOL = 1e-8
-GRAD_RTOL = 1e-6
+FR_RTOL = 5e-9
+GRAD_RTOL = 1e-7
 
 
 def _rel(a, b):
