@@ -123,10 +123,18 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    # rehearsal of the N > 1 path on one GPU (tests/test_gpu_bench_ranks.py): every rank on cuda:0,
+    # gloo collectives; the driver's multi-GPU runs use the defaults (cuda:LOCAL_RANK, RCCL)
+    if os.environ.get("PFR_BENCH_ONE_DEVICE") == "1":
+        local = 0
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        backend = os.environ.get("PFR_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
 
     prob = build_problem(args.ny, device, args.chunk)
     n_total = args.freqs * world
@@ -180,7 +188,7 @@ def main():
     torch.cuda.synchronize()
     kms, klaunch = eng.last_kernel_timings()
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = 1e3 * elapsed / args.steps

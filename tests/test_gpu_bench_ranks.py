@@ -1,0 +1,51 @@
+"""GPU: bench.py's N > 1 path (the driver's multi-GPU contract) rehearsed on one GPU.
+
+Two ranks under ``torch.distributed.run`` (127.0.0.1), both on cuda:0 (``PFR_BENCH_ONE_DEVICE=1``)
+with gloo collectives (``PFR_DIST_BACKEND=gloo``; RCCL needs one GPU per rank), a small mesh so
+that two engines share the device.  Checks the contract of the JSON line (rank 0 prints exactly
+one; ``n_gpus`` = 2; ``value`` = all frequencies of both ranks / max-over-ranks time; weak
+scaling) and that the distributed loss equals the single-process loss over the same frequencies
+(each rank sweeps its shard, one all-reduce of the partials).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--ny", "6", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--chunk", "256"]
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(cmd, env):
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_bench_on_one_gpu():
+    env = dict(os.environ, PFR_BENCH_ONE_DEVICE="1", PFR_DIST_BACKEND="gloo", PFR_LANES="1")
+    two = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+                "--freqs", "256"] + ARGS, env)
+    one = _run([sys.executable, "bench.py", "--freqs", "512"] + ARGS, env)
+    assert two["n_gpus"] == 2 and one["n_gpus"] == 1 and two["scaling"] == "weak"
+    assert two["steps"] == 2 and two["value"] > 0 and two["ms_per_step"] > 0
+    # value = 2 ranks x 256 frequencies per step / max-over-ranks time per step
+    assert abs(two["value"] - 512 / (two["ms_per_step"] / 1e3)) <= 1e-6 * two["value"]
+    assert abs(two["loss"] / one["loss"] - 1) < 1e-12
