@@ -457,7 +457,8 @@ void check_solution(pfr_solver* s, int which, int mode, int rhs, const pfr::RhsD
                           q0 >= 0 ? s->berr_out : nullptr, q0, which, st);
 }
 
-// s_{q,k} partials of sum_nz S_k(nz) lam[row] x[col] (no checks), row-ordered like the loss sweep's
+// s_{q,k} partials of sum_nz S_k(nz) lam[row] x[col] over the union pattern's distinct entries
+// (k_contract_eg, the loss sweep's contraction; no checks)
 void contract_rows(pfr_solver* s, const double2* lam, const double2* x, int nv, hipStream_t st) {
   pfr::launch_contract_eg(s->d_uent, s->n_uent, s->d_se, s->n_stiff, lam, x, s->Fc, nv, s->partial, st);
 }
