@@ -8,6 +8,15 @@ Prints one JSON line: iterations, loss history, relative parameter errors, wall 
 iteration and per loss + gradient evaluation.
 
     python tools/c5_lbfgs.py [--ny 25] [--freqs 4096] [--steps 30]
+
+C5 proper (BASELINE.json configs[4]) is the same fit over N GPUs, --freqs per GPU, one process per GPU:
+
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/c5_lbfgs.py
+
+Each rank sweeps its contiguous block of the frequencies; one all-reduce of the loss and gradient
+partials per evaluation (Problem.getLossFunction(..., distributed=True)); every rank runs the same
+L-BFGS iterates, rank 0 prints.  PFR_BENCH_ONE_DEVICE=1 / PFR_DIST_BACKEND=gloo rehearse it on one
+GPU (as bench.py).
 """
 from __future__ import annotations
 
@@ -30,6 +39,18 @@ def main():
     ap.add_argument("--freqs", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=30)
     a = ap.parse_args()
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = 0 if os.environ.get("PFR_BENCH_ONE_DEVICE") == "1" else int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        backend = os.environ.get("PFR_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
     from plate_inverse_problem_amd.Accelerometer import Accelerometer
     from plate_inverse_problem_amd.Geometry import Geometry, GeometryParams
     from plate_inverse_problem_amd.Material import get_material
@@ -40,15 +61,19 @@ def main():
     geom = Geometry("sh_i", acc, GeometryParams(100e-3, 20e-3, 2e-3, None, None), ny=a.ny)
     mat = get_material(1500.0, "orthotropic_d4", E1=120e9, E2=8e9, G12=5e9, nu12=0.3, b1=0.01, b2=0.02, b3=0.015,
                        b4=0.005)
+    from plate_inverse_problem_amd.distributed import shard_range
     t0 = time.perf_counter()
-    p = Problem(geom, mat, acc, device=torch.device("cuda", 0))
-    freqs = np.linspace(40.0, 600.0, a.freqs)
-    fr = p.solveForward(freqs)
+    p = Problem(geom, mat, acc, device=device)
+    n_total = a.freqs * world
+    freqs = np.linspace(40.0, 600.0, n_total)
+    lo, hi = shard_range(n_total, rank, world)
+    fr = np.zeros(n_total, dtype=np.complex128)
+    fr[lo:hi] = p.solveForward(freqs[lo:hi])          # each rank measures its own block
     torch.cuda.synchronize()
     t_setup = time.perf_counter() - t0
     rel0 = np.array([0.02, -0.02, 0.03, 0.01, 0.05, -0.05, 0.04, 0.03])
     theta0 = np.asarray(p.parameters, dtype=np.float64)
-    loss = p.getLossFunction(freqs, fr, "MSE_LOG_AFC", theta0 * (1 + rel0))
+    loss = p.getLossFunction(freqs, fr, "MSE_LOG_AFC", theta0 * (1 + rel0), distributed=world > 1)
     n_eval = [0]
 
     def counted(x):
@@ -60,13 +85,21 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     x = np.asarray(res.x) * theta0 * (1 + rel0)
-    out = {"workload": f"C5 on 1 GPU: orthotropic_d4 L-BFGS, {p.mat_size} DOF x {a.freqs} freqs, MSE_LOG_AFC",
-           "n_dofs": p.mat_size, "freqs": a.freqs, "iterations": int(res.niter) + 1, "evaluations": n_eval[0],
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device=device if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    out = {"workload": f"C5 on {world} GPU(s): orthotropic_d4 L-BFGS, {p.mat_size} DOF x {n_total} freqs, MSE_LOG_AFC",
+           "n_gpus": world, "n_dofs": p.mat_size, "freqs": n_total, "iterations": int(res.niter) + 1,
+           "evaluations": n_eval[0],
            "status": res.status, "f_history": [float(v) for v in res.f_history] + [float(res.f)],
            "rel_error_start": rel0.tolist(), "rel_error_end": ((x - theta0) / theta0).tolist(),
            "wall_s": wall, "s_per_iteration": wall / (int(res.niter) + 1), "s_per_evaluation": wall / n_eval[0],
-           "freq_solves_per_s": n_eval[0] * a.freqs / wall, "setup_s": t_setup}
-    print(json.dumps(out), flush=True)
+           "freq_solves_per_s": n_eval[0] * n_total / wall, "setup_s": t_setup}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":
