@@ -63,6 +63,19 @@ struct Ctx {
   int lane, w, W;
   int64_t q;
 };
+// ctx() for the level-solve kernels with the XCD-aware workgroup order: the workgroups of one
+// 64-frequency group run on one XCD, so the solution rows that many fronts of a level gather
+// (their common ancestors' pivots) are fetched into one L2, not eight.  bx: the front slot.
+__device__ __forceinline__ Ctx ctx_xcd(int& bx) {
+  const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
+  bx = (int)(lid % gridDim.x);
+  Ctx c;
+  c.lane = threadIdx.x & 63;
+  c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  c.W = blockDim.x >> 6;
+  c.q = (lid / gridDim.x) * 64 + c.lane;
+  return c;
+}
 __device__ __forceinline__ Ctx ctx() {
   Ctx c;
   c.lane = threadIdx.x & 63;
@@ -1126,8 +1139,9 @@ constexpr int SRB = 4, SKC = 8;
 template <int RHS>
 __global__ __launch_bounds__(512) void k_lsolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
                                cplx* __restrict__ WV, RhsArgs R, cplx* __restrict__ Y, const int* __restrict__ reach) {
-  const Ctx c = ctx();
-  const Front fr = P.fronts[lvl[blockIdx.x]];
+  int bx;
+  const Ctx c = ctx_xcd(bx);
+  const Front fr = P.fronts[lvl[bx]];
   const int f = fr.f, ns = fr.ns;
   const cplx* __restrict__ base = F + fr.off * Fc + c.q;
   cplx* __restrict__ wv = WV + (int64_t)fr.row0 * Fc + c.q;
@@ -1227,9 +1241,10 @@ template <bool SYM>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_usolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
                                cplx* __restrict__ WV, const cplx* __restrict__ Y, cplx* __restrict__ X,
                                const int* __restrict__ reach) {
-  const bool live = !reach || reach[lvl[blockIdx.x]];   // unreached front: y = 0
-  const Ctx c = ctx();
-  const Front fr = P.fronts[lvl[blockIdx.x]];
+  int bx;
+  const Ctx c = ctx_xcd(bx);
+  const bool live = !reach || reach[lvl[bx]];   // unreached front: y = 0
+  const Front fr = P.fronts[lvl[bx]];
   const int f = fr.f, ns = fr.ns;
   const cplx* __restrict__ base = F + fr.off * Fc + c.q;
   cplx* __restrict__ wv = WV + (int64_t)fr.row0 * Fc + c.q;
@@ -1346,12 +1361,13 @@ struct UPair {
 template <bool SYM, int SR, int SK, int WPE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void k_usolve2_level(
     DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc, UPair A, UPair B) {
-  const int ft = lvl[blockIdx.x];
+  int bx;
+  const Ctx c = ctx_xcd(bx);
+  const int ft = lvl[bx];
   const bool act[2] = {!A.skip || !A.skip[ft], !B.skip || !B.skip[ft]};
   const bool live[2] = {!A.reach || A.reach[ft], !B.reach || B.reach[ft]};
   const cplx* Ys[2] = {A.Y, B.Y};
   cplx* Xs[2] = {A.X, B.X};
-  const Ctx c = ctx();
   const Front fr = P.fronts[ft];
   const int f = fr.f, ns = fr.ns;
   const cplx* __restrict__ base = F + fr.off * Fc + c.q;
@@ -1462,8 +1478,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
 template <int RHS>
 __global__ __launch_bounds__(512) void k_utsolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
                                 cplx* __restrict__ WV, RhsArgs R, cplx* __restrict__ Y, const int* __restrict__ reach) {
-  const Ctx c = ctx();
-  const Front fr = P.fronts[lvl[blockIdx.x]];
+  int bx;
+  const Ctx c = ctx_xcd(bx);
+  const Front fr = P.fronts[lvl[bx]];
   const int f = fr.f, ns = fr.ns;
   const cplx* __restrict__ base = F + fr.off * Fc + c.q;
   cplx* __restrict__ wv = WV + (int64_t)fr.row0 * Fc + c.q;
@@ -1502,9 +1519,10 @@ __global__ __launch_bounds__(512) void k_utsolve_level(DevPattern P, const int* 
 __global__ __launch_bounds__(512) void k_ltsolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
                                 cplx* __restrict__ WV, const cplx* __restrict__ Y, cplx* __restrict__ X,
                                const int* __restrict__ reach) {
-  const bool live = !reach || reach[lvl[blockIdx.x]];   // unreached front: y = 0
-  const Ctx c = ctx();
-  const Front fr = P.fronts[lvl[blockIdx.x]];
+  int bx;
+  const Ctx c = ctx_xcd(bx);
+  const bool live = !reach || reach[lvl[bx]];   // unreached front: y = 0
+  const Front fr = P.fronts[lvl[bx]];
   const int f = fr.f, ns = fr.ns;
   const cplx* __restrict__ base = F + fr.off * Fc + c.q;
   cplx* __restrict__ wv = WV + (int64_t)fr.row0 * Fc + c.q;
@@ -1699,8 +1717,13 @@ __device__ __forceinline__ cplx resid_entry(const ResidArgs& A, const cplx* __re
 template <int MODE, int RHS>
 __global__ __launch_bounds__(256) void k_residual(ResidArgs A, const cplx* __restrict__ X, int64_t Fc,
                                                   cplx* __restrict__ R, double* __restrict__ acc) {
-  const int64_t q = (int64_t)blockIdx.y * 64 + (threadIdx.x & 63);
-  const int wave0 = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  // XCD-aware order: the workgroups of one 64-frequency group run together on one XCD, so the
+  // solution rows their window of rows gathers (~2 MB) stay in that XCD's L2 instead of every
+  // XCD's L2 holding windows of eight groups
+  const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
+  const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
+  const int64_t q = (int64_t)by * 64 + (threadIdx.x & 63);
+  const int wave0 = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
   const int nwaves = gridDim.x * (blockDim.x >> 6);
   double om2 = 0.0;
   if (MODE == 0 || RHS == 0) {
