@@ -53,7 +53,7 @@ struct pfr_solver {
   int n = 0;
   int64_t nnz = 0;
   int64_t Fc = 0;  // frequencies per chunk (multiple of 64)
-  std::vector<int32_t> level_ptr, level_maxf, level_W, perm, iperm;
+  std::vector<int32_t> level_ptr, level_maxf, level_maxns, level_W, perm, iperm;
   DevPattern P{};
   // owned device arrays
   std::vector<void*> owned;
@@ -279,7 +279,7 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     mark(l, 2);
     pfr::launch_offdiag(mode, s->P, s->d_items + s->item_ptr[l], s->item_ptr[l + 1] - s->item_ptr[l], s->d_orec,
                         s->d_oxp + s->item_ptr[l], s->d_ox, ngroups, s->F, s->Fc, s->freqs, s->K, s->M, data, ds,
-                        nvalid, st);
+                        nvalid, s->level_maxns[l], st);
     if (after_panel) after_panel(l);
     mark(l, 3);
     pfr::launch_schur_blk(s->schur_bc, s->P, s->d_blocks + s->blk_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
@@ -622,6 +622,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->perm = S.perm;
   s->iperm = S.iperm;
   for (int m : S.level_maxf) s->level_W.push_back(waves_for(m));
+  s->level_maxns.assign(S.level_maxf.size(), 0);   // largest pivot block of each level
+  for (const Front& F : S.fronts) s->level_maxns[F.level] = std::max(s->level_maxns[F.level], F.ns);
   Front* d_fronts = nullptr;
   int rc = PFR_OK;
   std::vector<Front> fv(S.fronts);

@@ -551,7 +551,7 @@ __device__ __forceinline__ cplx off_source(const OffSrc& S, const cplx* __restri
 // One chunk of NB consecutive columns (kind 0) / rows (kind 1) c0 .. c0+NB-1 of
 // this lane's OFF_RPL rows (columns); the shared L11 / U11 values each step loads
 // serve all of them.
-template <int MODE, int NB>
+template <int MODE, int NB, bool PRE = true>
 __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int64_t (&so)[OFF_RPL], int64_t sc,
                                               int64_t sa, int64_t sb, bool unit, const bool (&valid)[OFF_RPL],
                                               int c0, const OffSrc& S, const cplx* __restrict__ F, int64_t Fc,
@@ -575,9 +575,9 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
         }
     }
   }
-  // x -= own(0:c0) * shared(0:c0, c0:c0+NB)
+  // x -= own(0:c0) * shared(0:c0, c0:c0+NB)   (PRE = false: c0 = 0, no prefix)
 #pragma unroll 2
-  for (int t = 0; t < c0; ++t) {
+  for (int t = 0; t < (PRE ? c0 : 0); ++t) {
     cplx l[OFF_RPL], u[NB];
 #pragma unroll
     for (int h = 0; h < OFF_RPL; ++h) l[h] = base[(so[h] + (int64_t)t * sc) * Fc];
@@ -617,8 +617,12 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
 // consecutive rows (columns); row i0 + OFF_G h + lane group.  Default: lane = frequency
 // (OFF_G = 1), 2 rows per lane: every load a 1 KiB run, each U11 value serving two rows
 // (measured 26 % faster than 16 frequencies x 4 rows).
-template <int MODE>
-__global__ __launch_bounds__(256) void k_offdiag_level(DevPattern P, const int4* __restrict__ items, int nitems,
+// SMALL: every front of the launch has ns <= OB (one chunk, no prefix loop): the register budget of
+// the prefix loop is not needed (96 VGPRs: 5 waves/SIMD against 4) -- the bottom levels'
+// rows are short and their waves bound by the latency of their item -> front -> record -> source
+// load chain, which more resident waves overlap.
+template <int MODE, bool SMALL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMALL ? 5 : 1))) void k_offdiag_level(DevPattern P, const int4* __restrict__ items, int nitems,
                                                         const int2* __restrict__ orec, const int* __restrict__ oxp,
                                                         const int2* __restrict__ ox, cplx* __restrict__ F, int64_t Fc,
                                                         const double* __restrict__ freqs, const cplx* __restrict__ K,
@@ -664,6 +668,16 @@ __global__ __launch_bounds__(256) void k_offdiag_level(DevPattern P, const int4*
   S.K = K;
   S.M = M;
   S.dq = data + min(q, (int64_t)nvalid - 1) * data_stride;
+  if (SMALL) {
+    switch (ns) {
+#define SMALLC(n) \
+  case n: offdiag_chunk<MODE, n, false>(base, so, sc, sa, sb, unit, valid, 0, S, F, Fc, q); break;
+      SMALLC(1) SMALLC(2) SMALLC(3) SMALLC(4) SMALLC(5) SMALLC(6) SMALLC(7) SMALLC(8)
+#undef SMALLC
+      default: break;
+    }
+    return;
+  }
   int c0 = 0;
   for (; c0 + OB <= ns; c0 += OB) offdiag_chunk<MODE, OB>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q);
   switch (ns - c0) {     // wave-uniform tail width
@@ -2304,13 +2318,18 @@ void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, i
 
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
                     const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,
-                    const double* M, const double2* data, int64_t ds, int nvalid, hipStream_t st) {
+                    const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st) {
   if (nitems <= 0) return;
   dim3 g((nitems + 3) / 4, ngroups * OFF_G), b(256);
-  if (mode == 0)
-    LAUNCH(k_offdiag_level<0>, g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid);
-  else
-    LAUNCH(k_offdiag_level<1>, g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid);
+  static const bool small_ok = !getenv("PFR_OFF_SMALL") || atoi(getenv("PFR_OFF_SMALL")) != 0;
+  const bool small = small_ok && maxns <= 8;
+  static_assert(OB >= 8, "the SMALL variant covers pivot blocks of up to 8");
+#define OL(MD, SM) LAUNCH((k_offdiag_level<MD, SM>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid)
+  if (mode == 0 && small) OL(0, true);
+  else if (mode == 0) OL(0, false);
+  else if (small) OL(1, true);
+  else OL(1, false);
+#undef OL
 }
 
 static RhsArgs make_rhs(const RhsDesc& d) {
