@@ -158,6 +158,7 @@ struct pfr_solver {
   // workgroup, at most), PFR_US2_SMALL (largest front of a level the paired top-down solve treats
   // with its low-register small-front variant)
   int solve_wmax = 8, fac_wmax = 16, us2_small = 110;
+  int off_small = 1;                    // PFR_OFF_SMALL: no-prefix off-diagonal variant on levels of ns <= 8
   int check_fused = 0;                  // PFR_CHECK_FUSED=1: loss sweeps check both solutions in one entry walk
   // backward-error checks (pfr_set_check): PFR_CHECK_* bits, tolerance, optional per-item output;
   // per-frequency maxima scratch, forward and adjoint (kept zero between checks)
@@ -279,7 +280,7 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     mark(l, 2);
     pfr::launch_offdiag(mode, s->P, s->d_items + s->item_ptr[l], s->item_ptr[l + 1] - s->item_ptr[l], s->d_orec,
                         s->d_oxp + s->item_ptr[l], s->d_ox, ngroups, s->F, s->Fc, s->freqs, s->K, s->M, data, ds,
-                        nvalid, s->level_maxns[l], st);
+                        nvalid, s->off_small ? s->level_maxns[l] : pfr::MAX_FRONT, st);
     if (after_panel) after_panel(l);
     mark(l, 3);
     pfr::launch_schur_blk(s->schur_bc, s->P, s->d_blocks + s->blk_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
@@ -613,6 +614,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->solve_wmax = knob("PFR_SOLVE_WMAX", 8, 1, 8);
   s->fac_wmax = knob("PFR_FAC_WMAX", 16, 1, 16);
   s->us2_small = knob("PFR_US2_SMALL", 110, 0, pfr::MAX_FRONT);
+  s->off_small = knob("PFR_OFF_SMALL", 1, 0, 1);
   s->check_fused = knob("PFR_CHECK_FUSED", 0, 0, 1);   // measured 2.3 ms against 2 x 0.87 ms per 2,048-frequency chunk
   s->n = S.n;
   s->nnz = S.nnz;

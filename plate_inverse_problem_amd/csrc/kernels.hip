@@ -2321,8 +2321,7 @@ void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems
                     const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st) {
   if (nitems <= 0) return;
   dim3 g((nitems + 3) / 4, ngroups * OFF_G), b(256);
-  static const bool small_ok = !getenv("PFR_OFF_SMALL") || atoi(getenv("PFR_OFF_SMALL")) != 0;
-  const bool small = small_ok && maxns <= 8;
+  const bool small = maxns <= 8;
   static_assert(OB >= 8, "the SMALL variant covers pivot blocks of up to 8");
 #define OL(MD, SM) LAUNCH((k_offdiag_level<MD, SM>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid)
   if (mode == 0 && small) OL(0, true);

@@ -10,7 +10,8 @@
 * kernel variants forced on small meshes through the per-solver launch knobs (read when a solver
   is created): PFR_US2_SMALL=0 (every level through the large-front paired top-down solve),
   PFR_US2_SMALL=1024 (every level through the small-front variant), PFR_FAC_WMAX=1 / 16 and
-  PFR_SOLVE_WMAX=1 (one-wave and widest LU / solve workgroups).
+  PFR_SOLVE_WMAX=1 (one-wave and widest LU / solve workgroups), PFR_OFF_SMALL=0 (the bottom
+  levels' off-diagonal rows through the general kernel instead of the no-prefix variant).
 
 Tolerances.  These systems are badly scaled (membrane, bending and unit Dirichlet rows) and their
 conditioning grows like (mesh size)^-4.  At C3 the fr of the fp64 problem data is numerically
@@ -144,6 +145,7 @@ def test_c2_forward_sweep_matches_truth():
     {"PFR_FAC_WMAX": "1", "PFR_SOLVE_WMAX": "1"},
     {"PFR_FAC_WMAX": "16", "PFR_SOLVE_WMAX": "8"},
     {"PFR_CHECK_FUSED": "1"},
+    {"PFR_OFF_SMALL": "0"},
 ])
 def test_kernel_variants_match_oracle(env, monkeypatch):
     from oracle.plate_oracle import loss_and_grad
