@@ -1,35 +1,43 @@
 """Benchmark: freq-solves/s (forward + adjoint) of the C3 workload on N GPUs.
 
 BASELINE.json metric "freq-solves/sec (forward+adjoint) @20k DOF; achieved HBM
-GB/s vs peak", config C3: orthotropic plate, ~20k DOF, 4096 frequencies,
-forward + adjoint (loss + gradient), fp64.
+GB/s vs peak", config C3 (N = 1): orthotropic plate, ~20k DOF, 4096 frequencies,
+forward + adjoint (loss + gradient), fp64; C4 (N > 1): the same 4096 frequencies
+sharded across the N GPUs.
 
 * one STEP = one loss + gradient evaluation (``getLossFunction`` +
   ``backward``) over the frequency sweep: per frequency assemble -> LU ->
   forward solves -> FR -> loss cotangent -> adjoint solves -> contraction;
-* weak scaling: every rank sweeps 4096 frequencies (its contiguous block of
-  ``linspace(40, 600, 4096 * N)``); one all-reduce (RCCL) of the loss/gradient
-  partials per step;
-* ``value`` = 4096 * N / (max-over-ranks seconds per step);
+* strong scaling (default, C4 as BASELINE.json defines it): ``--freqs`` (4096)
+  frequencies in total, rank r sweeps its contiguous block
+  ``shard_range(4096, r, N)`` (512 per rank at N = 8); one all-reduce (RCCL) of
+  the loss/gradient partials per step.  ``--weak``: ``--freqs`` per rank.  With
+  N > 1 a strong run also times the weak workload (4096 per rank) and reports it
+  in the ``weak`` field;
+* ``value`` = all frequencies of all ranks / (max-over-ranks seconds per step);
 * each GPU runs ``lanes`` (default 2) solvers on their own HIP streams over
-  contiguous halves of its frequencies, concurrently (one lane's latency-bound
-  top levels overlap the other's bandwidth-bound ones);
+  contiguous halves of its frequencies, concurrently;
 * ``roofline``: the dominant kernel class by device time -- at C3 ``k_schur_sym_blk``
   (Schur complement of the large update blocks of the multifrontal factorisation;
   HBM-bound): algorithmic bytes per launch (the solver's count: A22 stores +
   gathered children's entries + L21 read once, 16 B per complex entry) / average
-  launch time, from HIP events that libpfr
-  records around every launch on the lane's stream during one isolated lane-0
-  sweep of a full chunk right after the timed region (inside the timed region the
-  lanes overlap, so a launch's duration there also contains the other lane's
-  work: reported as ``concurrent_*``); ``traffic`` = measured HBM bytes per
-  launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes
-  (the newest profiles/rNN/pmc_traffic.json, gfx950-corrected); the whole factorisation
-  (``factor_roofline``) and the triangular solves (``sptrsv_roofline``) beside it;
-* ``cpu_baseline``: the oracle (scipy SuperLU, one process per core) on a
-  bounded sample of the same workload, rank 0, N = 1 only.
+  launch time, from HIP events that libpfr records around every launch on the
+  lane's stream during one isolated lane-0 sweep of a full chunk right after the
+  timed region (inside the timed region the lanes overlap, so a launch's duration
+  there also contains the other lane's work: reported as ``concurrent_*``);
+  ``traffic`` = measured HBM bytes per launch from the committed rocprofv3
+  FETCH_SIZE/WRITE_SIZE passes (the newest profiles/rNN/pmc_traffic.json,
+  gfx950-corrected); the whole factorisation (``factor_roofline``) and the
+  triangular solves (``sptrsv_roofline``) beside it;
+* ``cpu_baseline`` (rank 0, N = 1 only): the oracle (scipy SuperLU, one process
+  per core) on a bounded sample of the same workload -- best-CPU (one
+  factorisation per frequency, reused for the transpose solve) as ``value``, the
+  reference-faithful count (a factorisation per primal / transpose bind, as the
+  reference's JAX rules do) beside it;
+* ``parity``: the oracle partials of the CPU leg against a GPU sweep of the same
+  frequencies (full-size C3 parity, paid for by the CPU leg).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--freqs F] [--ny NY]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--freqs F] [--weak] [--ny NY]
 """
 from __future__ import annotations
 
@@ -58,17 +66,22 @@ KERNELS = (("k_assemble_level",), ("k_factor_level", "k_factor_sym"), ("k_offdia
            ("k_schur_level", "k_schur_sym_level"))
 KERNEL_NAMES = ("k_assemble_level", "k_factor_level", "k_offdiag_level", "k_schur_sym_blk",
                 "k_schur_sym_level / k_schur_level")
+SOLVE_KERNELS = ("k_lsolve_level", "k_usolve_level", "k_usolve2_level")
+
+
+def _pmc():
+    try:
+        return json.load(open(PMC_FILE))
+    except (OSError, ValueError):
+        return None
 
 
 def pmc_traffic(chunk, symmetric):
     """Measured HBM bytes per launch of each factorisation kernel class, scaled to ``chunk``."""
-    try:
-        d = json.load(open(PMC_FILE))
-    except (OSError, ValueError):
+    d = _pmc()
+    if d is None or d.get("factorisation") != ("symmetric" if symmetric else "general"):
         return [None] * len(KERNELS)
     out = []
-    if d.get("factorisation") != ("symmetric" if symmetric else "general"):
-        return [None] * len(KERNELS)
     for k in KERNELS:
         es = [e for name, e in d["kernels"].items() if name.startswith(k)]
         if not es:
@@ -77,6 +90,20 @@ def pmc_traffic(chunk, symmetric):
         byts = sum(e["read_bytes"] + e["write_bytes"] for e in es)
         out.append(byts / sum(e["dispatches"] for e in es) * chunk / d["freqs_per_sweep"])
     return out
+
+
+def pmc_solve_traffic(symmetric):
+    """Measured HBM bytes per frequency of one sweep's triangular solves (every launch of the solve
+    kernels; sweeps counted by their k_functional launches)."""
+    d = _pmc()
+    if d is None or d.get("factorisation") != ("symmetric" if symmetric else "general"):
+        return None
+    k = d["kernels"]
+    sweeps = sum(e["dispatches"] for n, e in k.items() if n.startswith("k_functional") and "tangent" not in n)
+    if not sweeps:
+        return None
+    byts = sum(e["read_bytes"] + e["write_bytes"] for n, e in k.items() if n.startswith(SOLVE_KERNELS))
+    return byts / sweeps / d["freqs_per_sweep"]
 
 
 def build_problem(ny, device, max_batch=None):
@@ -90,9 +117,9 @@ def build_problem(ny, device, max_batch=None):
     return Problem(geom, mat, acc, device=device, max_batch=max_batch)
 
 
-def cpu_baseline(prob, freqs, ref, theta, sample_per_core=128):
-    """Oracle CPU sweep on a bounded sample (rank 0, N = 1)."""
-    sys.path.insert(0, REPO)
+def cpu_baseline(prob, freqs, ref, theta, sample_per_core=128, faithful_per_core=24):
+    """Oracle CPU sweeps on bounded samples (rank 0, N = 1): best-CPU and reference-faithful.
+    Returns (baseline dict, (sample frequencies, loss_sum, w) of the best-CPU sample)."""
     from tests.helpers import oracle_for
     from oracle.plate_oracle import parallel_partials
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
@@ -101,12 +128,71 @@ def cpu_baseline(prob, freqs, ref, theta, sample_per_core=128):
     n = min(freqs.size, sample_per_core * cores)
     idx = np.linspace(0, freqs.size - 1, n).round().astype(int)
     t0 = time.perf_counter()
-    parallel_partials(orc, freqs[idx], ref[idx], "MSE_LOG_AFC", theta, n_workers=cores)
+    loss_sum, w, _ = parallel_partials(orc, freqs[idx], ref[idx], "MSE_LOG_AFC", theta, n_workers=cores)
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "freq-solves/s", "cores": cores, "kind": "port",
-            "sample": f"{n} of the {freqs.size} frequencies (evenly spaced), forward+adjoint, one SuperLU "
-                      f"factorisation per frequency reused for the transpose solve (best-CPU), {cores} processes, "
-                      f"{dt:.1f} s"}
+    # the reference's count: its JAX rules bind spsolve twice in the primal / linearisation and twice
+    # transposed, each bind a fresh UMFPACK factorisation (Sparse.py:200-222, InnerState.h:276-288);
+    # >= 3 survive XLA's CSE of the identical primal callbacks
+    nf = min(freqs.size, faithful_per_core * cores)
+    idf = np.linspace(0, freqs.size - 1, nf).round().astype(int)
+    t0 = time.perf_counter()
+    parallel_partials(orc, freqs[idf], ref[idf], "MSE_LOG_AFC", theta, n_workers=cores, factorisations=3)
+    dtf = time.perf_counter() - t0
+    out = {"value": n / dt, "unit": "freq-solves/s", "cores": cores, "kind": "port",
+           "sample": f"{n} of the {freqs.size} frequencies (evenly spaced), forward+adjoint, one SuperLU "
+                     f"factorisation per frequency reused for the transpose solve (best-CPU), every solve with "
+                     f"UMFPACK's default refinement, {cores} processes, {dt:.1f} s",
+           "reference_faithful": {"value": nf / dtf, "unit": "freq-solves/s", "cores": cores,
+                                  "factorisations_per_frequency": 3,
+                                  "sample": f"{nf} of the {freqs.size} frequencies, a fresh factorisation for the "
+                                            f"primal solve and for each of the two transposed binds (the reference's "
+                                            f"spsolve rules after CSE), {cores} processes, {dtf:.1f} s"}}
+    return out, (freqs[idx], ref[idx], loss_sum, w)
+
+
+def gpu_parity(prob, sample, theta):
+    """The CPU leg's oracle partials (loss sum, 18 gradient partials w_k) against one GPU sweep of
+    the same frequencies: full-size C3 parity."""
+    from plate_inverse_problem_amd import _native
+    from plate_inverse_problem_amd.Problem import _coeffs18
+    f, ref, loss_o, w_o = sample
+    eng = prob.engine(f.size)
+    c = _coeffs18(prob._transform(), torch.as_tensor(theta)).detach().numpy()
+    eng.set_coefficients(c)
+    dev = eng.device
+    w = torch.zeros(eng.n_stiff, dtype=torch.complex128, device=dev)
+    loss = torch.zeros(1, dtype=torch.float64, device=dev)
+    eng.sweep(torch.as_tensor(f, device=dev), _native.LOSS_MSE_LOG_AFC,
+              ref=torch.view_as_real(torch.as_tensor(ref.astype(np.complex128), device=dev)), scale=1.0 / f.size,
+              loss=loss, w=torch.view_as_real(w))
+    wg = eng.expand(w).cpu().numpy()
+    lg = float(loss.item())
+    return {"frequencies": int(f.size), "loss_rel": abs(lg - loss_o) / abs(loss_o),
+            "grad_partials_rel": float(np.max(np.abs(wg - w_o)) / np.max(np.abs(w_o))),
+            "measure": "oracle (SuperLU + UMFPACK-default refinement) loss sum and the 18 complex gradient "
+                       "partials w_k = sum_f(-lam^T S_k x + e_k lam^T b0) against one GPU sweep of the same "
+                       "frequencies; relative, max-norm over k"}
+
+
+def timed(step, steps, warmup, world, device):
+    """W untimed steps, then K steps bracketed by barrier + synchronize; max over ranks."""
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
 
 
 def main():
@@ -114,14 +200,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--freqs", type=int, default=4096, help="frequencies per GPU")
+    ap.add_argument("--freqs", type=int, default=4096, help="frequencies in total (strong) / per GPU (--weak)")
+    ap.add_argument("--weak", action="store_true", help="--freqs per GPU instead of in total")
     ap.add_argument("--ny", type=int, default=25, help="mesh cells across the width (25 -> 19,353 DOF)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--chunk", type=int, default=None, help="frequencies per chunk (default: from free HBM)")
     args = ap.parse_args()
 
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
     # rehearsal of the N > 1 path on one GPU (tests/test_gpu_bench_ranks.py): every rank on cuda:0,
     # gloo collectives; the driver's multi-GPU runs use the defaults (cuda:LOCAL_RANK, RCCL)
@@ -129,52 +214,47 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    if world > 1:
-        backend = os.environ.get("PFR_DIST_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
-        else:
-            dist.init_process_group(backend)
+    from plate_inverse_problem_amd.distributed import init_from_env, shard_range
+    import plate_inverse_problem_amd.distributed as pdist
+    rank, world, backend = init_from_env(device)       # under torch.distributed.run: always (RCCL)
 
     prob = build_problem(args.ny, device, args.chunk)
-    n_total = args.freqs * world
-    freqs = np.linspace(40.0, 600.0, n_total)
     theta_true = prob.parameters.copy()
     theta = theta_true * (1 + np.array([0.1, 0.1, 0.2, 0.1, 0.1]))
 
-    from plate_inverse_problem_amd.distributed import shard_range
-    lo, hi = shard_range(n_total, rank, world)
-    ref = np.zeros(n_total, dtype=np.complex128)
-    ref[lo:hi] = prob.solveForward(freqs[lo:hi], theta_true)          # synthetic measurement, phase 0
-    loss_fn = prob.getLossFunction(freqs, ref, "MSE_LOG_AFC", distributed=world > 1)
+    def workload(n_total):
+        freqs = np.linspace(40.0, 600.0, n_total)
+        lo, hi = shard_range(n_total, rank, world)
+        ref = np.zeros(n_total, dtype=np.complex128)
+        ref[lo:hi] = prob.solveForward(freqs[lo:hi], theta_true)          # synthetic measurement, phase 0
+        loss_fn = prob.getLossFunction(freqs, ref, "MSE_LOG_AFC", distributed=backend is not None)
+
+        def step():
+            x = torch.tensor(theta, requires_grad=True)
+            val = loss_fn(x)
+            val.backward()
+            return val.item(), x.grad
+        return freqs, ref, lo, hi, step
+
+    n_total = args.freqs * world if args.weak else args.freqs
+    freqs, ref, lo, hi, step = workload(n_total)
     eng = prob.engine()
     solver = eng.solver
     # timed region: per-phase HIP events only (bracketing every launch costs host time that delays
     # the second lane's launches); per-launch events in one extra untimed step afterwards
     eng.set_timing(True, kernels=False)
-
-    def step():
-        x = torch.tensor(theta, requires_grad=True)
-        val = loss_fn(x)
-        val.backward()
-        return val.item(), x.grad
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
     phase = np.zeros(5)
-    kms = np.zeros(len(KERNELS))
-    klaunch = np.zeros(len(KERNELS))
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        val, grad = step()
-        phase += eng.last_timings()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    n_coll0 = pdist.N_COLLECTIVES
+    last = {}
+
+    def step_acc():
+        last["val"], last["grad"] = step()
+        phase[:] += eng.last_timings()
+
+    elapsed = timed(step_acc, args.steps, args.warmup, world, device)
+    phase *= 1.0 / (args.steps + args.warmup)
+    collectives = (pdist.N_COLLECTIVES - n_coll0) / (args.steps + args.warmup)
+    val = last["val"]
     # backward errors of the last timed step's solves (checked on the device in every sweep)
     berr = eng.last_berr.cpu().numpy()
     check = {"measure": "componentwise backward error max_i |b - A x|_i / (|A||x| + |b|)_i per frequency "
@@ -187,17 +267,12 @@ def main():
     step()
     torch.cuda.synchronize()
     kms, klaunch = eng.last_kernel_timings()
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
     ms_per_step = 1e3 * elapsed / args.steps
     value = n_total / (elapsed / args.steps)
 
     from plate_inverse_problem_amd import _native
     st = eng.stats
     nv = hi - lo
-    phase /= args.steps                      # device ms per step, per phase, summed over lanes
 
     # Kernel rooflines: one isolated sweep (lane 0 alone, its full chunk, same workload and
     # theta) right after the timed region, HIP events on lane 0's stream around every launch.
@@ -206,7 +281,7 @@ def main():
     chunk = solver.max_batch
     f_iso = torch.as_tensor(freqs[lo:lo + min(chunk, nv)], device=device)
     r_iso = torch.as_tensor(ref[lo:lo + f_iso.numel()], device=device)
-    w_iso = torch.zeros(18, dtype=torch.complex128, device=device)
+    w_iso = torch.zeros(eng.n_stiff, dtype=torch.complex128, device=device)
     l_iso = torch.zeros(1, dtype=torch.float64, device=device)
     with torch.cuda.stream(eng.streams[0]):
         solver.sweep(f_iso, _native.LOSS_MSE_LOG_AFC, ref=torch.view_as_real(r_iso), scale=1.0 / n_total, loss=l_iso,
@@ -227,10 +302,14 @@ def main():
     fact_tfs = st["factor_flops"] * n_iso / (iso_phase[0] * 1e-3) / 1e12
     fact_traffic = None if any(t is None and n > 0 for t, n in zip(traffic, iso_n)) else \
         float(sum(t * n for t, n in zip(traffic, iso_n) if n > 0))
-    # solve pairs: bottom-up pass over the fronts the rhs support reaches + full top-down pass
-    # (libpfr's count of factor entries read once, 16 B each, plus rhs in / solution out)
-    trsv_bytes = n_iso * float(solver.solve_bytes().sum())
-    trsv_gbs = trsv_bytes / ((iso_phase[1] + iso_phase[3]) * 1e-3) / 1e9
+    # triangular solves of the sweep: libpfr's count of the factor entries each pass must read (the
+    # paired top-down pass reads U once for the adjoint and the rest of the forward solution), 16 B
+    # each, plus rhs in / solution out; PMC traffic of the same kernels beside it
+    sb = solver.solve_bytes().astype(float)
+    trsv_bytes = n_iso * float(sb.sum())
+    trsv_ms = iso_phase[1] + iso_phase[3]
+    trsv_gbs = trsv_bytes / (trsv_ms * 1e-3) / 1e9
+    trsv_traffic = pmc_solve_traffic(eng.symmetric)
     conc_launch = kms / np.maximum(klaunch, 1)
     out = {
         "metric": "freq-solves/sec (forward+adjoint) @20k DOF",
@@ -241,20 +320,22 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if args.weak else "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (FE plate model built in-repo; reference FR = forward sweep at theta_true)",
-        "config": {"workload": "C3: orthotropic CFRP-like plate, sh_i strip 100x20x2 mm + AP1030, "
-                               f"{st['n']} DOF, {args.freqs} freqs/GPU in 40-600 Hz, forward+adjoint, "
+        "config": {"workload": ("C3" if world == 1 else "C4") + ": orthotropic CFRP-like plate, sh_i strip "
+                               f"100x20x2 mm + AP1030, {st['n']} DOF, {n_total} freqs in 40-600 Hz "
+                               f"({'per GPU' if args.weak else 'in total'}, {nv} on rank 0), forward+adjoint, "
                                "loss MSE_LOG_AFC + gradient",
-                   "n_dofs": st["n"], "freqs_per_gpu": args.freqs, "chunk": chunk,
+                   "n_dofs": st["n"], "freqs_total": n_total, "freqs_rank0": nv, "chunk": chunk,
                    "lanes": eng.n_lanes,
                    "factorisation": "symmetric: A = L U, U = diag(U) L^T implicit, Dirichlet nodes decoupled"
                                     if eng.symmetric else "general: A = L U",
                    "nnz_lu": st["nnz_lu"], "factor_gflop_per_freq": st["factor_flops"] / 1e9,
                    "parallelism": f"frequency shards x{world} + 1 all-reduce/step; {eng.n_lanes} concurrent "
-                                  "solver lanes (HIP streams) per GPU"},
+                                  "solver lanes (HIP streams) per GPU",
+                   "backend": backend, "collectives_per_step": collectives},
         "roofline": {"bound": "hbm", "kernel": kernels[dom], "achieved": gbs[dom], "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": gbs[dom] / HBM_PEAK_GBS, "traffic": traffic[dom],
                      "alg_bytes_per_launch": alg_launch[dom], "avg_launch_ms": ms_launch[dom],
@@ -268,20 +349,32 @@ def main():
                             "alg_bytes": fact_alg, "traffic": fact_traffic, "frequencies": n_iso,
                             "fp64_TFLOPs": fact_tfs, "fp64_frac": fact_tfs / FP64_PEAK_TFLOPS,
                             "concurrent_ms_per_step": kms.tolist()},
-        "sptrsv_roofline": {"bound": "hbm", "kernel": "k_lsolve_level + k_usolve_level (forward and adjoint pairs)",
-                            "achieved": trsv_gbs, "alg_bytes": trsv_bytes,
-                            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": trsv_gbs / HBM_PEAK_GBS,
-                            "traffic": None},
+        "sptrsv_roofline": {"bound": "hbm",
+                            "kernel": "k_lsolve_level + k_usolve_level + k_usolve2_level (forward and adjoint)",
+                            "achieved": trsv_gbs, "alg_bytes": trsv_bytes, "alg_bytes_per_freq": sb.tolist(),
+                            "ms": trsv_ms, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": trsv_gbs / HBM_PEAK_GBS,
+                            "traffic": None if trsv_traffic is None else trsv_traffic * n_iso,
+                            "frequencies": n_iso},
         "phase_ms": {"factor": phase[0], "fwd_solves": phase[1], "functional": phase[2],
-                     "adj_solves": phase[3], "contract": phase[4], "note": "device ms per step summed over lanes"},
+                     "adj_solves": phase[3], "contract": phase[4],
+                     "note": "device ms per step summed over lanes (phases: forward solves include the functional "
+                             "correction's residual walk when on)"},
         "loss": val,
         "backward_error": check,
     }
+    if world > 1 and not args.weak:
+        # the weak-scaling figure beside the strong one: 4096 frequencies per rank
+        n_w = args.freqs * world
+        _, _, lo_w, hi_w, step_w = workload(n_w)
+        el_w = timed(step_w, args.steps, args.warmup, world, device)
+        out["weak"] = {"value": n_w / (el_w / args.steps), "ms_per_step": 1e3 * el_w / args.steps,
+                       "freqs_per_gpu": args.freqs, "freqs_total": n_w}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(prob, freqs, ref, theta)
+        out["cpu_baseline"], sample = cpu_baseline(prob, freqs, ref, theta)
+        out["parity"] = gpu_parity(prob, sample, theta)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if backend is not None:
         dist.destroy_process_group()
 
 

@@ -34,8 +34,8 @@ extern "C" {
 
 /* per-frequency status flags (bitwise OR into an int32 array) */
 #define PFR_FLAG_BAD_PIVOT 1 /* zero / non-finite static pivot */
-#define PFR_FLAG_BACKWARD_ERROR 2     /* forward solution: normwise backward error above the tolerance */
-#define PFR_FLAG_BACKWARD_ERROR_ADJ 4 /* adjoint solution: normwise backward error above the tolerance */
+#define PFR_FLAG_BACKWARD_ERROR 2     /* forward solution: componentwise backward error above the tolerance */
+#define PFR_FLAG_BACKWARD_ERROR_ADJ 4 /* adjoint solution: componentwise backward error above the tolerance */
 
 /* pfr_set_check modes (bitwise OR) */
 #define PFR_CHECK_FORWARD 1   /* backward error of the forward solution (A x = b) */
@@ -168,7 +168,10 @@ PFR_API int pfr_matvec(pfr_solver* s, int32_t batch, const double* data_dev, int
 
 /* K_out_dev = sum_k coef_k * S_k  (S registered by pfr_set_stiffness), complex nnz.  n_stiff is 18
  * (A, B, D coefficient matrices of Problem.py:440-445) or 12 (A and D only: the B coefficients vanish
- * for mid-plane symmetric laminates, so their matrices and gradient partials are left out). */
+ * for mid-plane symmetric laminates, so their matrices and gradient partials are left out).
+ * pfr_set_stiffness registers stiff_dev for pfr_combine (read at every call) AND takes a copy of its
+ * values for the gradient contraction: after the caller changes the buffer's values it must call
+ * pfr_set_stiffness again (the call returns once the copy is made). */
 PFR_API int pfr_set_stiffness(pfr_solver* s, int32_t n_stiff, const double* stiff_dev /* (nnz, n_stiff) */,
                               const double* rhs_weights /* host, n_stiff: e_k */);
 PFR_API int pfr_combine(pfr_solver* s, const double* coef /* host complex n_stiff */, double* K_out_dev,
@@ -232,9 +235,13 @@ PFR_API int pfr_last_kernel_timings(const pfr_solver* s, double* ms_out /* 5 */,
  * entries it gathers, factor blocks it consumes); index data, shared by all frequencies, excluded. */
 PFR_API int pfr_solver_alg_bytes(const pfr_solver* s, int64_t* bytes_out /* 5 */);
 
-/* Algorithmic HBM bytes per frequency of the triangular solves of one pfr_sweep: [0] forward pair
- * (bottom-up pass over the fronts the rhs reaches + full top-down pass), [1] adjoint pair (reach of the
- * functional support + full pass): factor entries read once (16 B each) plus rhs in / solution out. */
+/* Algorithmic HBM bytes per frequency of the triangular solves of one loss pfr_sweep under the
+ * solver's current check mode: factor entries each pass must read (16 B each) plus rhs in / solution
+ * out.  Symmetric mode without refinement (the paired passes): [0] forward bottom-up over the fronts
+ * the rhs reaches + forward top-down over the fronts the loss support reaches, [1] adjoint bottom-up
+ * over that reach + the single top-down pass that reads every U value once for the adjoint and the
+ * rest of the forward solution.  Otherwise [0] / [1] forward / adjoint pair (reached bottom-up + full
+ * top-down; with PFR_CHECK_REFINE plus the full correction solve). */
 PFR_API int pfr_solver_solve_bytes(const pfr_solver* s, int64_t* bytes_out /* 2 */);
 
 #ifdef __cplusplus

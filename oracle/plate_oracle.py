@@ -335,11 +335,16 @@ def loss(prob: OracleProblem, freqs, ref, loss_type, theta):
 
 
 def frequency_partials(prob: OracleProblem, freqs, ref, loss_type, theta, n_total=None,
-                       refactor_adjoint=False):
+                       refactor_adjoint=False, factorisations=None):
     """Per-chunk partial sums (loss_sum, w (18,) complex) -- the quantity the
     GPU sweep reduces and ranks all-reduce.  ``w_k = sum_f (-lam^T m_k x + e_k lam^T b0)``.
     ``refactor_adjoint=True`` refactorises for the adjoint solve like the
-    reference's transpose bind (InnerState.h:276-288)."""
+    reference's transpose bind (InnerState.h:276-288); ``factorisations=n`` (n >= 2)
+    runs the reference's full count per frequency: the primal factorisation, then
+    n - 1 transposed binds, each with a fresh factorisation (Sparse.py:211-222 binds
+    ``spsolve(..., transpose=True)`` once per cotangent branch, and every bind
+    factorises, InnerState.h:276-288) -- the repeated
+    adjoints are identical, only the count of work differs."""
     freqs = np.asarray(freqs, dtype=np.float64)
     ref = np.asarray(ref)
     n_total = freqs.size if n_total is None else n_total
@@ -350,6 +355,7 @@ def frequency_partials(prob: OracleProblem, freqs, ref, loss_type, theta, n_tota
     w = np.zeros(18, dtype=complex)
     loss_sum = 0.0
     rows, cols, m18 = prob.rows, prob.cols, prob.mats[:18]
+    n_fact = factorisations or (2 if refactor_adjoint else 1)
     for i, f in enumerate(freqs):
         A = prob.matrix(f, c)
         lu = sparse_lu(A)
@@ -359,9 +365,10 @@ def frequency_partials(prob: OracleProblem, freqs, ref, loss_type, theta, n_tota
         loss_sum += float(loss_terms(fr, ref[i], loss_type))
         dl = float(loss_term_derivative(fr, ref[i], loss_type)) / n_total
         g = (dl / fr) * (ts2 * np.conj(U) * aU + ts2 * np.conj(V) * aV + np.conj(W) * aW)
-        if refactor_adjoint:
-            lu = sparse_lu(A)
-        lam = refined_solve(lu, A, g, trans=True)
+        if n_fact == 1:
+            lam = refined_solve(lu, A, g, trans=True)
+        for _ in range(n_fact - 1):
+            lam = refined_solve(sparse_lu(A), A, g, trans=True)
         p = lam[rows] * x[cols]
         w += -_mr(m18, p) + e * (lam @ prob.rhs_vec)
     return loss_sum, w
@@ -403,13 +410,13 @@ def _pool_worker(args):
     # one process per core: keep BLAS single-threaded (oversubscription otherwise
     # multiplies the run time many-fold on a cgroup-limited host)
     from threadpoolctl import threadpool_limits
-    freqs, ref, loss_type, theta, n_total, refactor = args
+    freqs, ref, loss_type, theta, n_total, refactor, nfact = args
     with threadpool_limits(1):
-        return frequency_partials(_POOL_PROB, freqs, ref, loss_type, theta, n_total, refactor)
+        return frequency_partials(_POOL_PROB, freqs, ref, loss_type, theta, n_total, refactor, nfact)
 
 
 def parallel_partials(prob: OracleProblem, freqs, ref, loss_type, theta, n_workers=None,
-                      refactor_adjoint=False):
+                      refactor_adjoint=False, factorisations=None):
     """Process-pool CPU sweep (SuperLU holds the GIL, so processes, not threads).
     Returns (loss_sum, w, n_workers)."""
     import multiprocessing as mp
@@ -421,7 +428,7 @@ def parallel_partials(prob: OracleProblem, freqs, ref, loss_type, theta, n_worke
     _POOL_PROB = prob
     ctx = mp.get_context("fork")
     with ctx.Pool(len(chunks)) as pool:
-        parts = pool.map(_pool_worker, [(freqs[c], ref[c], loss_type, theta, freqs.size, refactor_adjoint)
-                                        for c in chunks])
+        parts = pool.map(_pool_worker, [(freqs[c], ref[c], loss_type, theta, freqs.size, refactor_adjoint,
+                                         factorisations) for c in chunks])
     _POOL_PROB = None
     return sum(p[0] for p in parts), sum(p[1] for p in parts), len(chunks)

@@ -343,8 +343,14 @@ class _SweepFR(torch.autograd.Function):
         ref.real.copy_(grad_fr.to(torch.float64))
         w = torch.zeros(engine.n_stiff, dtype=torch.complex128, device=engine.device)
         loss = torch.zeros(1, dtype=torch.float64, device=engine.device)
+        # the cotangent sweep's solves are checked like the forward ones: flags and backward errors
+        # reported, not dropped
+        flags = torch.zeros(ctx.freqs.numel(), dtype=torch.int32, device=engine.device)
+        berr = torch.full((ctx.freqs.numel(), 2), float('nan'), dtype=torch.float64, device=engine.device)
         engine.sweep(ctx.freqs, _native.LOSS_COTANGENT, ref=torch.view_as_real(ref), scale=1.0,
-                     loss=loss, w=torch.view_as_real(w))
+                     loss=loss, w=torch.view_as_real(w), flags=flags, berr=berr)
+        engine.last_berr = berr
+        engine.last_flags = _check_flags(flags)
         return torch.conj(engine.expand(w)).to(torch.complex128).cpu(), None, None
 
 
@@ -566,10 +572,22 @@ class Problem:
 
     getAFCFunction = getFRFunction
 
-    def solveForward(self, freqs, params=None) -> np.ndarray:
-        """Frequency response at ``freqs`` [Hz] (``Problem.py:611-639``)."""
+    def solveForward(self, freqs, params=None, *, distributed: bool = False) -> np.ndarray:
+        """Frequency response at ``freqs`` [Hz] (``Problem.py:611-639``).
+
+        With ``distributed=True`` and an initialised ``torch.distributed`` group every rank sweeps
+        its contiguous block of ``freqs`` and one all-gather assembles the whole response on every
+        rank."""
         if params is None:
             params = self.parameters
+        if distributed:
+            from .distributed import all_gather_cat, shard_range
+            f = np.asarray(freqs, dtype=np.float64)
+            lo, hi = shard_range(f.size)
+            with torch.no_grad():
+                part = self.getFRFunction()(f[lo:hi], params) if hi > lo else \
+                    torch.zeros(0, dtype=torch.float64, device=self.device)
+                return all_gather_cat(part, f.size).cpu().numpy()
         with torch.no_grad():
             return self.getFRFunction()(freqs, params).cpu().numpy()
 

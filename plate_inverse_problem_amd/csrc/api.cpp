@@ -1088,14 +1088,34 @@ int pfr_solver_alg_bytes(const pfr_solver* s, int64_t* bytes) {
 
 int pfr_solver_solve_bytes(const pfr_solver* s, int64_t* bytes) {
   if (!s || !bytes) return fail(PFR_ERR_ARG, "null argument");
-  for (int w = 0; w < 2; ++w) {
-    int64_t lower = 0, upper = 0;
-    for (size_t t = 0; t < s->front_ns.size(); ++t) {
-      const int64_t ns = s->front_ns[t], r = s->front_f[t] - ns;
-      upper += ns * (ns + 1) / 2 + r * ns;                      // U11 + U12 (symmetric: L21)
-      if (s->reach_host[w][t]) lower += ns * (ns - 1) / 2 + r * ns;   // L11 + L21, reached fronts
-    }
-    bytes[w] = 16 * (lower + upper) + 2 * 16 * (int64_t)s->n;
+  // factor entries each pass reads once: lower[w] = L11 + L21 of the fronts reach w holds (the
+  // bottom-up pass of rhs w), upper_r[w] = U11 + U12 of those fronts, upper / lower_all = every front
+  int64_t lower[2] = {0, 0}, upper_r[2] = {0, 0}, upper = 0, lower_all = 0;
+  for (size_t t = 0; t < s->front_ns.size(); ++t) {
+    const int64_t ns = s->front_ns[t], r = s->front_f[t] - ns;
+    const int64_t u = ns * (ns + 1) / 2 + r * ns;             // U11 + U12 (symmetric: diag(U) L^T)
+    const int64_t l = ns * (ns - 1) / 2 + r * ns;             // L11 (unit diagonal) + L21
+    upper += u;
+    lower_all += l;
+    for (int w = 0; w < 2; ++w)
+      if (s->reach_host[w][t]) {
+        lower[w] += l;
+        upper_r[w] += u;
+      }
+  }
+  const int64_t vec = 2 * 16 * (int64_t)s->n;                 // rhs in, solution out
+  const bool refine = (s->check_mode & PFR_CHECK_REFINE) != 0;
+  if (s->sym && !refine) {
+    // loss sweep, paired: forward bottom-up over its reach + forward top-down over the fronts the loss
+    // support reaches; adjoint bottom-up over that reach + ONE top-down pass over every front that
+    // forms the adjoint and the rest of the forward solution together (each U value loaded once)
+    bytes[0] = 16 * (lower[0] + upper_r[1]) + vec;
+    bytes[1] = 16 * (lower[1] + upper) + 2 * vec;
+  } else {
+    // forward and adjoint solved one after the other; a refinement step adds a full pair each
+    const int64_t ref = refine ? 16 * (lower_all + upper) + vec : 0;
+    bytes[0] = 16 * (lower[0] + upper) + vec + ref;
+    bytes[1] = 16 * (lower[1] + upper) + vec + ref;
   }
   return PFR_OK;
 }
@@ -1116,8 +1136,10 @@ int pfr_set_stiffness(pfr_solver* s, int32_t n_stiff, const double* stiff_dev, c
     int rc = s->alloc(&s->d_se, (int64_t)18 * (s->n_uent + 4));
     if (rc) return rc;
   }
+  // the entry-ordered copy of S the gradient contraction reads (taken now: a later change of the
+  // registered buffer needs another pfr_set_stiffness, include/pfr.h)
   pfr::launch_gather_entries(s->d_uent, s->n_uent + 4, nullptr, nullptr, stiff_dev, n_stiff, nullptr, s->d_se, nullptr);
-  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipStreamSynchronize(nullptr));
   return PFR_OK;
 }
 
@@ -1226,8 +1248,10 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
   const int ngroups = (int)(Fc / 64);
   bool used[5] = {true, true, true, reverse, reverse};
   // K may have been recombined since the last sweep (pfr_combine, any solver): refresh the entry-ordered
-  // copy the fused contraction + checks read (2.6 % of one chunk's traffic at C3, once per call)
-  if (reverse) pfr::launch_gather_entries(s->d_uent, s->n_uent + 4, s->K, s->M, nullptr, 0, s->d_kme, nullptr, st);
+  // copy the fused contraction + checks read (2.6 % of one chunk's traffic at C3, once per call) -- only
+  // when that fused check path will run
+  if (reverse && s->check_fused && (s->check_mode & (PFR_CHECK_FORWARD | PFR_CHECK_ADJOINT)))
+    pfr::launch_gather_entries(s->d_uent, s->n_uent + 4, s->K, s->M, nullptr, 0, s->d_kme, nullptr, st);
   for (int64_t q0 = 0; q0 < nfreq; q0 += Fc) {
     const int nv = (int)std::min<int64_t>(Fc, nfreq - q0);
     HIP_TRY(hipMemcpyAsync(s->freqs, freqs_dev + q0, nv * sizeof(double), hipMemcpyDeviceToDevice, st));

@@ -14,7 +14,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from plate_inverse_problem_amd.distributed import all_reduce_sum, shard_range
+from plate_inverse_problem_amd.distributed import all_gather_cat, all_reduce_sum, shard_range
 
 
 def test_shard_range_partitions():
@@ -52,7 +52,9 @@ def _worker(rank, world, port, out_q):
         tot = all_reduce_sum(packed)
         x = torch.tensor([float(rank + 1)], dtype=torch.float64)
         all_reduce_sum(x)
-        out_q.put((rank, tot.numpy(), float(x.item()), (lo, hi)))
+        # solveForward(..., distributed=True)'s all-gather of the fr shards (complex: the measured FR)
+        full = all_gather_cat(torch.as_tensor(ref[lo:hi]), freqs.size)
+        out_q.put((rank, tot.numpy(), float(x.item()), (lo, hi), full.numpy(), ref))
     finally:
         dist.destroy_process_group()
 
@@ -72,8 +74,9 @@ def test_two_rank_gloo_reduction_matches_single_process():
         pr.join(timeout=60)
         assert pr.exitcode == 0
     res.sort()
-    (_, t0, x0, s0), (_, t1, x1, s1) = res
+    (_, t0, x0, s0, g0, r0), (_, t1, x1, s1, g1, _) = res
     assert s0 == (0, 6) and s1 == (6, 11)
+    assert np.array_equal(g0, r0) and np.array_equal(g1, r0)
     assert x0 == x1 == 3.0
     assert np.array_equal(t0, t1)                       # every rank holds the same totals
     p = make_problem("orthotropic", ny=3)
@@ -83,3 +86,39 @@ def test_two_rank_gloo_reduction_matches_single_process():
     ls, w = frequency_partials(o, freqs, ref, "MSE_LOG_AFC", p.parameters * 1.05)
     assert np.isclose(t0[0].real, ls, rtol=1e-12)
     assert np.allclose(t0[1:], w, rtol=1e-10, atol=1e-12 * np.abs(w).max())
+
+
+def _world_one(out_q, port):
+    # the launcher's environment for one rank: init_from_env joins (gloo here, RCCL on the GPU box)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
+                      PFR_DIST_BACKEND="gloo")
+    import plate_inverse_problem_amd.distributed as pdist
+    rank, world, backend = pdist.init_from_env()
+    try:
+        t = pdist.all_reduce_sum(torch.tensor([1.5 + 2j], dtype=torch.complex128))
+        g = pdist.all_gather_cat(torch.arange(5, dtype=torch.float64), 5)
+        out_q.put((rank, world, backend, pdist.N_COLLECTIVES, complex(t[0]), g.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_world_size_one_group_runs_the_collectives():
+    """Under a launcher with one rank the group is joined and the collectives really run (the RCCL
+    path at world size 1 is exercised the same way on the GPU box, tests/test_gpu_nccl.py)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    pr = ctx.Process(target=_world_one, args=(q, _free_port()))
+    pr.start()
+    rank, world, backend, ncoll, t, g = q.get(timeout=100)
+    pr.join(timeout=30)
+    assert pr.exitcode == 0
+    assert (rank, world, backend) == (0, 1, "gloo") and ncoll == 2
+    assert t == 1.5 + 2j and g == [0.0, 1.0, 2.0, 3.0, 4.0]
+
+
+def test_no_group_is_a_no_op():
+    import plate_inverse_problem_amd.distributed as pdist
+    assert not dist.is_initialized()
+    t = torch.tensor([2.0])
+    assert pdist.all_reduce_sum(t) is t and pdist.all_gather_cat(t, 1) is t

@@ -4,9 +4,10 @@ rehearsed on one GPU.
 Two ranks under ``torch.distributed.run`` (127.0.0.1), both on cuda:0 (``PFR_BENCH_ONE_DEVICE=1``)
 with gloo collectives (``PFR_DIST_BACKEND=gloo``; RCCL needs one GPU per rank), a small mesh so
 that two engines share the device.  Checks the contract of the JSON line (rank 0 prints exactly
-one; ``n_gpus`` = 2; ``value`` = all frequencies of both ranks / max-over-ranks time; weak
-scaling) and that the distributed loss equals the single-process loss over the same frequencies
-(each rank sweeps its shard, one all-reduce of the partials).
+one; ``n_gpus`` = 2; ``value`` = all frequencies of both ranks / max-over-ranks time; strong
+scaling -- C4: the total fixed, each rank its shard -- with the weak figure beside it) and that the
+distributed loss equals the single-process loss over the same frequencies (each rank sweeps its
+shard, one all-reduce of the partials).
 """
 import json
 import os
@@ -43,13 +44,18 @@ def test_two_rank_bench_on_one_gpu():
     env = dict(os.environ, PFR_BENCH_ONE_DEVICE="1", PFR_DIST_BACKEND="gloo", PFR_LANES="1")
     two = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                 "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
-                "--freqs", "256"] + ARGS, env)
+                "--freqs", "512"] + ARGS, env)
     one = _run([sys.executable, "bench.py", "--freqs", "512"] + ARGS, env)
-    assert two["n_gpus"] == 2 and one["n_gpus"] == 1 and two["scaling"] == "weak"
+    assert two["n_gpus"] == 2 and one["n_gpus"] == 1 and two["scaling"] == one["scaling"] == "strong"
     assert two["steps"] == 2 and two["value"] > 0 and two["ms_per_step"] > 0
-    # value = 2 ranks x 256 frequencies per step / max-over-ranks time per step
+    assert two["config"]["freqs_total"] == 512 and two["config"]["freqs_rank0"] == 256
+    assert two["config"]["backend"] == "gloo" and two["config"]["collectives_per_step"] == 1
+    # value = 512 frequencies in total per step / max-over-ranks time per step
     assert abs(two["value"] - 512 / (two["ms_per_step"] / 1e3)) <= 1e-6 * two["value"]
     assert abs(two["loss"] / one["loss"] - 1) < 1e-12
+    # the weak figure: 512 frequencies per rank
+    w = two["weak"]
+    assert w["freqs_total"] == 1024 and abs(w["value"] - 1024 / (w["ms_per_step"] / 1e3)) <= 1e-6 * w["value"]
 
 
 @pytest.mark.timeout(300)
@@ -63,7 +69,7 @@ def test_two_rank_c5_lbfgs_matches_single_process():
     env = dict(os.environ, PFR_BENCH_ONE_DEVICE="1", PFR_DIST_BACKEND="gloo", PFR_LANES="1")
     small = ["--ny", "6", "--steps", "4"]
     two = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "tools/c5_lbfgs.py", "--freqs", "256"]
+                "--master-addr", "127.0.0.1", "--master-port", str(_port()), "tools/c5_lbfgs.py", "--freqs", "512"]
                + small, env)
     one = _run([sys.executable, "tools/c5_lbfgs.py", "--freqs", "512"] + small, env)
     assert two["n_gpus"] == 2 and one["n_gpus"] == 1 and two["freqs"] == one["freqs"] == 512

@@ -166,6 +166,24 @@ def test_kernel_variants_match_oracle(env, monkeypatch):
             grad_rel=_rel(x.grad.numpy(), go))
     assert abs(val.item() - lo) / abs(lo) < FR_RTOL
     assert _rel(x.grad.numpy(), go) < GRAD_RTOL
+    if env.get("PFR_CHECK_FUSED") == "1":
+        # the fused contraction + checks walk (k_contract_rows) must report the backward errors the
+        # separate k_residual walks report: same solutions, same per-frequency maxima (to rounding)
+        eng = p.engine()
+        fused_berr, fused_flags = eng.last_berr.cpu().numpy(), eng.last_flags
+        monkeypatch.setenv("PFR_CHECK_FUSED", "0")
+        q = make_problem("orthotropic", ny=6, device="cuda:0")
+        y = torch.tensor(theta, requires_grad=True)
+        q.getLossFunction(freqs, ref, "MSE_LOG_AFC")(y).backward()
+        plain_berr = q.engine().last_berr.cpu().numpy()
+        assert not fused_flags.any() and not q.engine().last_flags.any()
+        assert np.all(np.isfinite(fused_berr)) and np.all(fused_berr <= BERR_MAX)
+        # the residuals are rounding-level (~1e-16 .. 1e-15) and the two walks sum them in different
+        # orders: per frequency within a factor 4, the sweep's maximum of each column within 2
+        ratio = (fused_berr + 1e-18) / (plain_berr + 1e-18)
+        assert np.all(ratio < 4.0) and np.all(ratio > 0.25), (ratio.min(), ratio.max())
+        mr = fused_berr.max(axis=0) / plain_berr.max(axis=0)
+        assert np.all(mr < 2.0) and np.all(mr > 0.5), mr
 
 
 def test_engine_grows_after_small_first_call():

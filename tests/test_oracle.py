@@ -62,7 +62,9 @@ def test_refactor_adjoint_mode_same_result(small):
     th = p.parameters * 1.1
     a = orc.frequency_partials(o, freqs, ref, "MSE", th)
     b = orc.frequency_partials(o, freqs, ref, "MSE", th, refactor_adjoint=True)
+    c = orc.frequency_partials(o, freqs, ref, "MSE", th, factorisations=3)    # the reference-faithful count
     assert np.isclose(a[0], b[0], rtol=1e-13) and np.allclose(a[1], b[1], rtol=1e-10)
+    assert np.isclose(a[0], c[0], rtol=1e-13) and np.allclose(a[1], c[1], rtol=1e-10)
 
 
 def test_first_resonance_near_euler_bernoulli():

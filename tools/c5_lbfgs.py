@@ -9,7 +9,8 @@ iteration and per loss + gradient evaluation.
 
     python tools/c5_lbfgs.py [--ny 25] [--freqs 4096] [--steps 30]
 
-C5 proper (BASELINE.json configs[4]) is the same fit over N GPUs, --freqs per GPU, one process per GPU:
+C5 proper (BASELINE.json configs[4]) is the same fit over N GPUs (C4's sharding: --freqs in total,
+--weak for --freqs per GPU), one process per GPU:
 
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/c5_lbfgs.py
 
@@ -38,19 +39,14 @@ def main():
     ap.add_argument("--ny", type=int, default=25)
     ap.add_argument("--freqs", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--weak", action="store_true", help="--freqs per GPU instead of in total")
     a = ap.parse_args()
     import torch.distributed as dist
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
     local = 0 if os.environ.get("PFR_BENCH_ONE_DEVICE") == "1" else int(os.environ.get("LOCAL_RANK", 0))
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    if world > 1:
-        backend = os.environ.get("PFR_DIST_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
-        else:
-            dist.init_process_group(backend)
+    from plate_inverse_problem_amd.distributed import init_from_env
+    rank, world, backend = init_from_env(device)
     from plate_inverse_problem_amd.Accelerometer import Accelerometer
     from plate_inverse_problem_amd.Geometry import Geometry, GeometryParams
     from plate_inverse_problem_amd.Material import get_material
@@ -64,7 +60,7 @@ def main():
     from plate_inverse_problem_amd.distributed import shard_range
     t0 = time.perf_counter()
     p = Problem(geom, mat, acc, device=device)
-    n_total = a.freqs * world
+    n_total = a.freqs * world if a.weak else a.freqs
     freqs = np.linspace(40.0, 600.0, n_total)
     lo, hi = shard_range(n_total, rank, world)
     fr = np.zeros(n_total, dtype=np.complex128)
@@ -73,7 +69,7 @@ def main():
     t_setup = time.perf_counter() - t0
     rel0 = np.array([0.02, -0.02, 0.03, 0.01, 0.05, -0.05, 0.04, 0.03])
     theta0 = np.asarray(p.parameters, dtype=np.float64)
-    loss = p.getLossFunction(freqs, fr, "MSE_LOG_AFC", theta0 * (1 + rel0), distributed=world > 1)
+    loss = p.getLossFunction(freqs, fr, "MSE_LOG_AFC", theta0 * (1 + rel0), distributed=backend is not None)
     n_eval = [0]
 
     def counted(x):
@@ -98,7 +94,7 @@ def main():
            "freq_solves_per_s": n_eval[0] * n_total / wall, "setup_s": t_setup}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if backend is not None:
         dist.destroy_process_group()
 
 
