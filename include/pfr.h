@@ -43,6 +43,10 @@ extern "C" {
 #define PFR_CHECK_REFINE 4    /* one step of iterative refinement of the forward (and, in loss sweeps, the
                                * adjoint) solution on the same factors, x += A^{-1} (b - A x), before the
                                * checks (UMFPACK refines by default, up to 2 steps) */
+#define PFR_CHECK_CORRECT 8   /* functional correction (pfr_sweep): fr += Re(mu^T (b - A x)) with mu the adjoint
+                               * of fr (A^T mu = d fr / d x) -- fr to second order in the solve's error, the
+                               * accuracy the reference's refined UMFPACK solves give; the loss, its
+                               * cotangent and the gradient are formed from the corrected fr */
 
 /* loss types (Problem.py:948-975) */
 #define PFR_LOSS_NONE -1
@@ -202,9 +206,9 @@ PFR_API int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_
                               const double* ref_dev, double scale, int32_t n_dir, const double* dcoef,
                               double* loss_dev, double* w_dev, double* h_dev, int32_t* flags_dev, void* stream);
 
-/* Backward-error checks of the solves (the failure detection a static pivot order needs; the
- * reference turns UMFPACK's status into an exception, umfpack_interface.h:10-18, and its solves
- * refine by default).  After each solve the componentwise (Oettli-Prager) backward error
+/* Backward-error checks of the solves and the accuracy options (the failure detection a static pivot
+ * order needs; the reference turns UMFPACK's status into an exception, umfpack_interface.h:10-18, and
+ * its solves refine by default).  After each solve the componentwise (Oettli-Prager) backward error
  *   berr = max_i |b - A x|_i / (|A| |x| + |b|)_i        (|z| = |re| + |im|)
  * of the ORIGINAL system is computed on the device per frequency / batch item -- UMFPACK's sparse
  * backward error, invariant under row / column scaling -- and the item's flag
@@ -213,8 +217,12 @@ PFR_API int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_
  * every later pfr_sweep / pfr_solve call writes berr_dev[2 q] (forward) and berr_dev[2 q + 1]
  * (adjoint) for its items q = 0 .. nfreq - 1 (slots of a solve that is not checked are left
  * alone), so it must hold 2 nfreq doubles of every such call.  With PFR_CHECK_REFINE a loss sweep
- * runs its forward solve, refinement and adjoint in sequence (not the paired top-down pass).  Not
- * applied by pfr_hessian_sweep. */
+ * runs its forward solve, refinement and adjoint in sequence (not the paired top-down pass).
+ * PFR_CHECK_CORRECT: every pfr_sweep (forward-only sweeps too) also solves for the adjoint of fr --
+ * in symmetric mode inside the paired top-down pass -- and the forward residual walk (the forward
+ * check) accumulates the correction; in a loss sweep that adjoint is the loss adjoint up to one
+ * scalar per frequency, so the correction costs only the residual walk.  Not applied by
+ * pfr_hessian_sweep. */
 PFR_API int pfr_set_check(pfr_solver* s, int32_t mode, double tol, double* berr_dev);
 
 /* Per-phase device times [ms] of the last pfr_sweep/pfr_solve call on this solver, measured with HIP

@@ -133,9 +133,11 @@ class _Engine:
         self._coef_key = None
         self.last_berr = None          # (F, 2) componentwise backward errors of the last sweep (device)
         self.last_flags = None         # its status flags (host)
-        # backward-error checks of every solve (pfr_set_check): forward + adjoint by default,
-        # PFR_CHECK=<PFR_CHECK_* bits> / PFR_CHECK_TOL override; refinement (bit 4) off by default
-        self.check_mode = int(os.environ.get("PFR_CHECK", str(_native.PFR_CHECK_FORWARD | _native.PFR_CHECK_ADJOINT)))
+        # backward-error checks of every solve (pfr_set_check) and the functional correction (fr to
+        # second order in the solve's error, the accuracy of the reference's refined UMFPACK solves) by
+        # default; PFR_CHECK=<PFR_CHECK_* bits> / PFR_CHECK_TOL override; refinement (bit 4) off by default
+        self.check_mode = int(os.environ.get("PFR_CHECK", str(_native.PFR_CHECK_FORWARD | _native.PFR_CHECK_ADJOINT
+                                                              | _native.PFR_CHECK_CORRECT)))
         self.check_tol = float(os.environ.get("PFR_CHECK_TOL", "1e-10"))
         self.ensure(n_freqs)
 
@@ -396,7 +398,7 @@ def _check_flags(flags):
         if n:
             msgs.append(f"{n} frequencies {what}")
     warnings.warn("; ".join(msgs) + " -- their results are not reliable (Problem.solveForwardChecked reports "
-                  "the backward errors; PFR_CHECK=7 adds a refinement step)", RuntimeWarning)
+                  "the backward errors; PFR_CHECK=15 adds a refinement step)", RuntimeWarning)
     return f
 
 
@@ -593,12 +595,13 @@ class Problem:
 
     solve_forward = solveForward
 
-    def solveForwardChecked(self, freqs, params=None, *, refine: bool = False):
+    def solveForwardChecked(self, freqs, params=None, *, refine: bool = False, correct: bool | None = None):
         """``(fr, berr, flags)``: the forward sweep with the componentwise backward error of every
         frequency's solve (``max_i |b - A x|_i / (|A||x| + |b|)_i``, the measure UMFPACK's
         refinement monitors) and its status flags (PFR_FLAG_*); ``refine=True`` adds one step of
         iterative refinement on the same factors first (as the reference's UMFPACK solves do by
-        default, ``InnerState.h:246-247`` with a NULL Control)."""
+        default, ``InnerState.h:246-247`` with a NULL Control); ``correct`` turns the functional
+        correction on / off (None: the engine's setting, on by default)."""
         if params is None:
             params = self.parameters
         f = self._freqs(freqs)
@@ -610,7 +613,10 @@ class Problem:
         flags = torch.zeros(f.numel(), dtype=torch.int32, device=eng.device)
         berr = torch.full((f.numel(), 2), float('nan'), dtype=torch.float64, device=eng.device)
         mode = eng.check_mode
-        eng.set_check(mode | _native.PFR_CHECK_FORWARD | (_native.PFR_CHECK_REFINE if refine else 0))
+        m = mode | _native.PFR_CHECK_FORWARD | (_native.PFR_CHECK_REFINE if refine else 0)
+        if correct is not None:
+            m = (m | _native.PFR_CHECK_CORRECT) if correct else (m & ~_native.PFR_CHECK_CORRECT)
+        eng.set_check(m)
         try:
             eng.sweep(f, _native.LOSS_NONE, fr=fr, flags=flags, berr=berr)
         finally:

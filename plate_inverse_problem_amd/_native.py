@@ -23,7 +23,7 @@ PFR_OK = 0
 PFR_FLAG_BAD_PIVOT = 1
 PFR_FLAG_BACKWARD_ERROR = 2
 PFR_FLAG_BACKWARD_ERROR_ADJ = 4
-PFR_CHECK_FORWARD, PFR_CHECK_ADJOINT, PFR_CHECK_REFINE = 1, 2, 4
+PFR_CHECK_FORWARD, PFR_CHECK_ADJOINT, PFR_CHECK_REFINE, PFR_CHECK_CORRECT = 1, 2, 4, 8
 LOSS_NONE, LOSS_MSE, LOSS_RMSE, LOSS_MSE_AFC, LOSS_MSE_LOG_AFC, LOSS_COTANGENT = -1, 0, 1, 2, 3, 4
 LOSS_IDS = {"MSE": LOSS_MSE, "RMSE": LOSS_RMSE, "MSE_AFC": LOSS_MSE_AFC, "MSE_LOG_AFC": LOSS_MSE_LOG_AFC}
 

@@ -123,6 +123,10 @@ struct pfr_solver {
   int n_kdir = 0;
   double2 *partial = nullptr, *tq = nullptr;
   double *freqs = nullptr, *loss_terms = nullptr;
+  // functional correction (PFR_CHECK_CORRECT): fr of the solve, per-frequency cotangent scale, and
+  // the residual walk's per-workgroup dot-product partials (residual_parts(n) x Fc)
+  double *fr0 = nullptr, *mscale = nullptr;
+  double2* cpart = nullptr;
   int32_t* flags = nullptr;
   // operator / rhs / functional / stiffness state
   const double2* K = nullptr;
@@ -204,6 +208,7 @@ int64_t workspace_bytes(const Symbolic& S, int64_t Fc) {
   b += S.total_rows * Fc * 16;       // WV
   b += 6 * (int64_t)S.n * Fc * 16;   // X, Y, XA, G, Y2, XR
   b += Fc * (8 + 8 + 4 + 16);        // freqs, loss terms, flags, tq
+  b += Fc * (8 + 8) + (int64_t)pfr::residual_parts(S.n) * Fc * 16;   // fr0, mscale, cpart
   return b;
 }
 
@@ -428,7 +433,8 @@ int set_reach(pfr_solver* s, int which, const std::vector<int32_t>& prows) {
 // chunk's flags and the caller's berr slots (q0 < 0: no berr output).  R != NULL: only the residual
 // b - A x is written there (the refinement step), nothing is checked.
 void check_solution(pfr_solver* s, int which, int mode, int rhs, const pfr::RhsDesc& rd, const double2* data,
-                    int64_t ds, int nvalid, const double2* X, double2* R, int64_t q0, hipStream_t st) {
+                    int64_t ds, int nvalid, const double2* X, double2* R, int64_t q0, hipStream_t st,
+                    const double2* Mu = nullptr, bool check = true) {
   pfr::ResidDesc d;
   d.ptr = which == 0 ? s->d_rptr : s->d_cptr;
   d.idx = which == 0 ? s->d_ridx : s->d_cidx;
@@ -452,7 +458,10 @@ void check_solution(pfr_solver* s, int which, int mode, int rhs, const pfr::RhsD
     pfr::launch_residual(mode, rhs, d, X, s->Fc, R, nullptr, st);
     return;
   }
-  pfr::launch_residual(mode, rhs, d, X, s->Fc, nullptr, s->d_berr_acc, st);
+  // Mu: the forward walk also accumulates the functional correction's dot products (s->cpart);
+  // check = false: only those (no backward error)
+  pfr::launch_residual(mode, rhs, d, X, s->Fc, nullptr, check ? s->d_berr_acc : nullptr, st, Mu, Mu ? s->cpart : nullptr);
+  if (!check) return;
   pfr::launch_berr_finish(s->d_berr_acc, s->Fc, nvalid, s->check_tol,
                           which == 0 ? PFR_FLAG_BACKWARD_ERROR : PFR_FLAG_BACKWARD_ERROR_ADJ, s->flags,
                           q0 >= 0 ? s->berr_out : nullptr, q0, which, st);
@@ -1000,7 +1009,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       (rc = s->alloc(&s->XA, (int64_t)S.n * Fc)) || (rc = s->alloc(&s->G, (int64_t)S.n * Fc)) ||
       (rc = s->alloc(&s->Y2, (int64_t)S.n * Fc)) || (rc = s->alloc(&s->XR, (int64_t)S.n * Fc)) ||
       (rc = s->alloc(&s->freqs, Fc)) || (rc = s->alloc(&s->loss_terms, Fc)) || (rc = s->alloc(&s->flags, Fc)) ||
-      (rc = s->alloc(&s->tq, Fc)) || (rc = s->alloc(&s->d_berr_acc, 2 * Fc)))
+      (rc = s->alloc(&s->tq, Fc)) || (rc = s->alloc(&s->d_berr_acc, 2 * Fc)) || (rc = s->alloc(&s->fr0, Fc)) ||
+      (rc = s->alloc(&s->mscale, Fc)) || (rc = s->alloc(&s->cpart, (int64_t)pfr::residual_parts(S.n) * Fc)))
     return bail(rc);
   HIP_TRY(hipMemset(s->d_berr_acc, 0, 2 * Fc * sizeof(double)));
   // PFR_AUX=1: run the forward sparse L-solve on a side stream, level by level behind the
@@ -1033,7 +1043,7 @@ int pfr_set_timing(pfr_solver* s, int32_t enable) {
 }
 
 int pfr_set_check(pfr_solver* s, int32_t mode, double tol, double* berr_dev) {
-  if (!s || mode < 0 || mode > 7 || !(tol >= 0.0)) return fail(PFR_ERR_ARG, "bad check arguments");
+  if (!s || mode < 0 || mode > 15 || !(tol >= 0.0)) return fail(PFR_ERR_ARG, "bad check arguments");
   s->check_mode = mode;
   s->check_tol = tol;
   s->berr_out = berr_dev;
@@ -1246,11 +1256,19 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
   reset_timing(s);
   const int64_t Fc = s->Fc;
   const int ngroups = (int)(Fc / 64);
-  bool used[5] = {true, true, true, reverse, reverse};
+  const bool refine = (s->check_mode & PFR_CHECK_REFINE) != 0;
+  // functional correction: the adjoint of fr is solved in every sweep (in a loss sweep it IS the loss
+  // adjoint up to one scalar per frequency) and the forward residual walk adds Re(mu^T r) to fr
+  const bool correct = (s->check_mode & PFR_CHECK_CORRECT) != 0;
+  const bool adj = reverse || correct;                 // an adjoint solve runs
+  const bool paired = s->sym && adj && !refine;        // one top-down pass for both solutions
+  const bool fwd_late = paired || correct;             // forward residual walk after the adjoint
+  bool used[5] = {true, true, true, adj, adj};
   // K may have been recombined since the last sweep (pfr_combine, any solver): refresh the entry-ordered
   // copy the fused contraction + checks read (2.6 % of one chunk's traffic at C3, once per call) -- only
   // when that fused check path will run
-  if (reverse && s->check_fused && (s->check_mode & (PFR_CHECK_FORWARD | PFR_CHECK_ADJOINT)))
+  const bool fused_checks = reverse && !correct && s->check_fused && (s->check_mode & (PFR_CHECK_FORWARD | PFR_CHECK_ADJOINT));
+  if (fused_checks)
     pfr::launch_gather_entries(s->d_uent, s->n_uent + 4, s->K, s->M, nullptr, 0, s->d_kme, nullptr, st);
   for (int64_t q0 = 0; q0 < nfreq; q0 += Fc) {
     const int nv = (int)std::min<int64_t>(Fc, nfreq - q0);
@@ -1265,8 +1283,6 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
     rd.beta_im = s->beta_im;
     rd.mass_sum = s->mass_sum;
     rd.freqs = s->freqs;
-    const bool refine = (s->check_mode & PFR_CHECK_REFINE) != 0;
-    const bool paired = s->sym && reverse && !refine;
     pfr::RhsDesc rf = rd;
     int rc;
     if (paired && !s->aux) {
@@ -1301,7 +1317,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
       if (rc) return rc;
     }
     record(s, 1, st);
-    // symmetric loss + gradient: forward top-down only over the loss support's fronts, then one
+    // symmetric mode with an adjoint: forward top-down only over the loss support's fronts, then one
     // combined top-down pass (sym_top_down_pair); otherwise the full forward solve first
     if (paired) {
       if ((rc = sym_top_down_support(s, rf, st))) return rc;
@@ -1315,17 +1331,24 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
         if ((rc = forward_solve(s, 2, rr, s->XA, st))) return rc;
         pfr::launch_axpy_vec(s->X, s->XA, (int64_t)s->n * Fc, st);
       }
-      if (s->check_mode & PFR_CHECK_FORWARD) check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st);
+      if (!fwd_late && (s->check_mode & PFR_CHECK_FORWARD))
+        check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st);
     }
     record(s, 2, st);
     pfr::FunctionalArgs fa = s->fn;
     fa.loss_type = reverse ? loss_type : -1;
     fa.ref = reinterpret_cast<const double2*>(ref_dev);
     fa.scale = scale;
-    if (reverse) HIP_TRY(hipMemsetAsync(s->G, 0, (size_t)s->n * Fc * 16, st));
-    pfr::launch_functional(fa, s->X, Fc, nv, q0, fr_dev, s->loss_terms, s->G, st);
+    if (adj) HIP_TRY(hipMemsetAsync(s->G, 0, (size_t)s->n * Fc * 16, st));
+    if (correct) {
+      pfr::FunctionalArgs fs = fa;
+      fs.fr0 = s->fr0;          // seed: fr of this solve kept, G = d fr / d x
+      pfr::launch_functional(fs, s->X, Fc, nv, q0, nullptr, nullptr, s->G, st);
+    } else {
+      pfr::launch_functional(fa, s->X, Fc, nv, q0, fr_dev, s->loss_terms, s->G, st);
+    }
     record(s, 3, st);
-    if (reverse) {
+    if (adj) {
       pfr::RhsDesc rg;
       rg.G = s->G;
       if (paired) {
@@ -1343,40 +1366,49 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
         }
       }
       record(s, 4, st);
-      // gradient contraction fused with the backward-error checks of both solutions (the forward
-      // check of a refined / unpaired sweep is already done above)
-      const bool fwd_done = !paired;
-      int want = s->check_mode & ((fwd_done ? 0 : PFR_CHECK_FORWARD) | PFR_CHECK_ADJOINT);
-      pfr::RowCheckDesc cd;
-      cd.K = s->K;
-      cd.M = s->M;
-      cd.freqs = s->freqs;
-      cd.rhsP = s->rhsP;
-      cd.beta_re = s->beta_re;
-      cd.beta_im = s->beta_im;
-      cd.mass_sum = s->mass_sum;
-      cd.G = s->G;
-      pfr::launch_contract_eg(s->d_uent, s->n_uent, s->d_se, s->n_stiff, s->XA, s->X, Fc, nv, s->partial, st);
-      if (want && s->check_fused)
+      bool want_f = fwd_late && (s->check_mode & PFR_CHECK_FORWARD);
+      bool want_a = (s->check_mode & PFR_CHECK_ADJOINT) != 0;
+      if (correct) {
+        // the forward residual walk: backward error (when checked) + the correction's dot products,
+        // then the corrected fr, its loss terms and the per-frequency cotangent scales
+        check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st, s->XA, want_f);
+        want_f = false;
+        pfr::launch_correct_finish(fa, s->fr0, s->cpart, pfr::residual_parts(s->n), Fc, nv, q0, fr_dev, s->loss_terms,
+                                   s->mscale, st);
+      }
+      const double* msc = correct ? s->mscale : nullptr;
+      if (reverse) pfr::launch_contract_eg(s->d_uent, s->n_uent, s->d_se, s->n_stiff, s->XA, s->X, Fc, nv, s->partial, st, msc);
+      if (fused_checks && (want_f || want_a)) {
+        // gradient contraction's row walk fused with both checks (PFR_CHECK_FUSED=1)
+        pfr::RowCheckDesc cd;
+        cd.K = s->K;
+        cd.M = s->M;
+        cd.freqs = s->freqs;
+        cd.rhsP = s->rhsP;
+        cd.beta_re = s->beta_re;
+        cd.beta_im = s->beta_im;
+        cd.mass_sum = s->mass_sum;
+        cd.G = s->G;
         pfr::launch_contract_rows(true, s->d_ublk, s->d_uent, s->n_ublk, ngroups, s->d_se, s->n_stiff, s->d_kme, cd,
                                   s->XA, s->X, Fc, nv, nullptr, s->d_berr_acc, s->d_berr_acc + Fc, st);
-      else if (want) {
-        // the two checks as row / column walks of the original pattern (k_residual)
-        if (want & PFR_CHECK_FORWARD) check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st);
-        if (want & PFR_CHECK_ADJOINT) check_solution(s, 1, 0, 2, rg, nullptr, 0, nv, s->XA, nullptr, q0, st);
-        want = 0;
+        for (int w = 0; w < 2; ++w) {
+          double* acc = s->d_berr_acc + w * Fc;
+          if (w == 0 ? want_f : want_a)
+            pfr::launch_berr_finish(acc, Fc, nv, s->check_tol, w == 0 ? PFR_FLAG_BACKWARD_ERROR : PFR_FLAG_BACKWARD_ERROR_ADJ,
+                                    s->flags, s->berr_out, q0, w, st);
+          else
+            HIP_TRY(hipMemsetAsync(acc, 0, Fc * sizeof(double), st));   // computed, not requested: keep zero
+        }
+      } else {
+        // the checks as row / column walks of the original pattern (k_residual)
+        if (want_f) check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st);
+        if (want_a) check_solution(s, 1, 0, 2, rg, nullptr, 0, nv, s->XA, nullptr, q0, st);
       }
-      for (int w = 0; w < 2; ++w) {
-        double* acc = s->d_berr_acc + w * Fc;
-        if (want & (w == 0 ? PFR_CHECK_FORWARD : PFR_CHECK_ADJOINT))
-          pfr::launch_berr_finish(acc, Fc, nv, s->check_tol, w == 0 ? PFR_FLAG_BACKWARD_ERROR : PFR_FLAG_BACKWARD_ERROR_ADJ,
-                                  s->flags, s->berr_out, q0, w, st);
-        else if (want)
-          HIP_TRY(hipMemsetAsync(acc, 0, Fc * sizeof(double), st));   // computed, not requested: keep zero
+      if (reverse) {
+        pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st, msc);
+        pfr::launch_reduce(s->partial, pfr::contract_eg_parts(s->n_uent), s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
+                           reinterpret_cast<double2*>(w_dev), loss_dev, st);
       }
-      pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st);
-      pfr::launch_reduce(s->partial, pfr::contract_eg_parts(s->n_uent), s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
-                         reinterpret_cast<double2*>(w_dev), loss_dev, st);
     } else {
       record(s, 4, st);
     }

@@ -77,6 +77,8 @@ struct FunctionalArgs {
   int32_t loss_type;      // PFR_LOSS_* or -1 (forward only)
   const double2* ref;     // reference FR (complex) or cotangent (re), indexed by global frequency
   double scale;           // 1 / F_total (mean over the whole sweep)
+  double* fr0;            // != NULL: seed mode of k_functional (functional correction): fr of the solve -> fr0,
+                          // G = d fr / d x (no loss terms); k_correct_finish forms the corrected fr and the loss
 };
 
 }  // namespace pfr

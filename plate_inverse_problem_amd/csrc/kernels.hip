@@ -1728,9 +1728,10 @@ __device__ __forceinline__ cplx resid_entry(const ResidArgs& A, const cplx* __re
   return dq[nz];
 }
 
-template <int MODE, int RHS>
+template <int MODE, int RHS, bool DOT = false>
 __global__ __launch_bounds__(256) void k_residual(ResidArgs A, const cplx* __restrict__ X, int64_t Fc,
-                                                  cplx* __restrict__ R, double* __restrict__ acc) {
+                                                  cplx* __restrict__ R, double* __restrict__ acc,
+                                                  const cplx* __restrict__ Mu, cplx* __restrict__ cpart) {
   // XCD-aware order: the workgroups of one 64-frequency group run together on one XCD, so the
   // solution rows their window of rows gathers (~2 MB) stay in that XCD's L2 instead of every
   // XCD's L2 holding windows of eight groups
@@ -1748,6 +1749,7 @@ __global__ __launch_bounds__(256) void k_residual(ResidArgs A, const cplx* __res
   const cplx* __restrict__ dq = A.data + item * A.data_stride;
   double berr = 0.0;
   bool bad = false;         // NaN / Inf residual or a non-zero residual over a zero denominator
+  cplx dot = make_double2(0, 0);   // sum_p Mu_p r_p (functional correction, Mu != NULL)
   for (int p = wave0; p < A.n; p += nwaves) {
     cplx b;
     if (RHS == 0) {
@@ -1782,13 +1784,88 @@ __global__ __launch_bounds__(256) void k_residual(ResidArgs A, const cplx* __res
       den = fma(cabs1(a), cabs1(x), den);
     }
     if (R) R[(int64_t)p * Fc + q] = r;
+    if (DOT) {
+      const cplx m = Mu[(int64_t)p * Fc + q];
+      dot = cadd(dot, cmul(m, r));
+    }
     const double cr = cabs1(r);
     bad = bad || !isfinite(cr) || !isfinite(den) || (den == 0.0 && cr > 0.0);
     if (den > 0.0) berr = fmax(berr, cr / den);
   }
-  if (!acc) return;          // residual only (refinement step)
+  if (DOT) {
+    // deterministic per-workgroup partial of the correction dot product: the waves' sums in LDS,
+    // added in wave order, one partial per (workgroup, frequency) (k_correct_finish sums them in order)
+    __shared__ cplx sdot[4][64];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    sdot[w][lane] = dot;
+    __syncthreads();
+    if (w == 0) {
+      cplx t = sdot[0][lane];
+      for (int k = 1; k < (int)(blockDim.x >> 6); ++k) t = cadd(t, sdot[k][lane]);
+      cpart[(int64_t)bx * Fc + q] = t;
+    }
+  }
+  if (!acc) return;          // residual only (refinement step / correction without a check)
   if (bad) berr = __longlong_as_double(0x7ff0000000000000LL);     // +inf
   atomicMax(reinterpret_cast<unsigned long long*>(acc + q), (unsigned long long)__double_as_longlong(berr));
+}
+
+// Per-frequency loss term and its derivative d term / d fr (Problem.py:948-975); PFR_LOSS_COTANGENT:
+// no term, derivative = ref.re (dL/dfr supplied by the caller).
+__device__ __forceinline__ void loss_term(int loss_type, double fr, cplx r, double& term, double& dl) {
+  const double rabs = sqrt(r.x * r.x + r.y * r.y);
+  term = 0.0;
+  dl = 0.0;
+  switch (loss_type) {
+    case PFR_LOSS_MSE: {
+      const double dre = fr - r.x;
+      term = dre * dre + r.y * r.y;
+      dl = 2.0 * dre;
+    } break;
+    case PFR_LOSS_RMSE: {
+      const double dre = fr - r.x, r2 = rabs * rabs;
+      term = (dre * dre + r.y * r.y) / r2;
+      dl = 2.0 * dre / r2;
+    } break;
+    case PFR_LOSS_MSE_AFC: {
+      const double d = fr - rabs;
+      term = d * d;
+      dl = 2.0 * d;
+    } break;
+    case PFR_LOSS_MSE_LOG_AFC: {
+      const double d = log(fr) - log(rabs);
+      term = d * d;
+      dl = 2.0 * d / fr;
+    } break;
+    case PFR_LOSS_COTANGENT:
+      dl = r.x;
+      break;
+    default:
+      break;
+  }
+}
+
+// Functional correction (adjoint-weighted residual): with mu the adjoint of fr (A^T mu = d fr / d x,
+// k_functional's seed mode) and r = b - A x the forward residual, fr(x*) = fr(x) + Re(mu^T r) up to
+// second order in the solve's error -- the accuracy UMFPACK's default refinement (IRSTEP = 2) buys the
+// reference's fr, for one dot product per row folded into the residual walk.  Per frequency: the
+// corrected fr (fr_out, global index), the loss term of it and the cotangent scale
+// m_q = scale * d term / d fr (lambda = m_q mu: the gradient contraction and k_rhs_dot take it).
+__global__ void k_correct_finish(FunctionalArgs A, const double* __restrict__ fr0, const cplx* __restrict__ cpart,
+                                 int nparts, int64_t Fc, int nvalid, int64_t q_global0, double* __restrict__ fr_out,
+                                 double* __restrict__ loss_terms, double* __restrict__ mscale) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Fc) return;
+  cplx d = make_double2(0, 0);
+  for (int b = 0; b < nparts; ++b) d = cadd(d, cpart[(int64_t)b * Fc + q]);
+  const bool valid = q < nvalid;
+  const double fr = fr0[q] + d.x;
+  if (valid && fr_out) fr_out[q_global0 + q] = fr;
+  if (A.loss_type < 0) return;
+  double term = 0.0, dl = 0.0;
+  if (valid) loss_term(A.loss_type, fr, A.ref[q_global0 + q], term, dl);
+  loss_terms[q] = term;
+  mscale[q] = valid ? dl * A.scale : 0.0;
 }
 
 // flag the frequencies whose backward error exceeds tol; optional per-frequency output (global
@@ -1887,42 +1964,19 @@ __global__ void k_functional(FunctionalArgs A, const cplx* __restrict__ X, int64
   const double u2 = U.x * U.x + U.y * U.y, v2 = Vv.x * Vv.x + Vv.y * Vv.y, w2 = W.x * W.x + W.y * W.y;
   const double fr = sqrt(ts2 * u2 + ts2 * v2 + w2);
   const bool valid = q < nvalid;
-  if (valid && fr_out) fr_out[q_global0 + q] = fr;
-  if (A.loss_type < 0) return;
-  double term = 0.0, dl = 0.0;
-  if (valid) {
-    const cplx r = A.ref[q_global0 + q];
-    const double rabs = sqrt(r.x * r.x + r.y * r.y);
-    switch (A.loss_type) {
-      case PFR_LOSS_MSE: {
-        const double dre = fr - r.x;
-        term = dre * dre + r.y * r.y;
-        dl = 2.0 * dre;
-      } break;
-      case PFR_LOSS_RMSE: {
-        const double dre = fr - r.x, r2 = rabs * rabs;
-        term = (dre * dre + r.y * r.y) / r2;
-        dl = 2.0 * dre / r2;
-      } break;
-      case PFR_LOSS_MSE_AFC: {
-        const double d = fr - rabs;
-        term = d * d;
-        dl = 2.0 * d;
-      } break;
-      case PFR_LOSS_MSE_LOG_AFC: {
-        const double d = log(fr) - log(rabs);
-        term = d * d;
-        dl = 2.0 * d / fr;
-      } break;
-      case PFR_LOSS_COTANGENT:
-        dl = r.x;   // dL/dfr supplied by the caller (ref.re), no loss value
-        break;
-      default:
-        break;
-    }
+  double s = 0.0;
+  if (A.fr0) {
+    // seed mode (functional correction): fr of this solve kept for k_correct_finish, G = d fr / d x
+    A.fr0[q] = valid ? fr : 0.0;
+    s = valid && fr > 0.0 ? 1.0 / fr : 0.0;
+  } else {
+    if (valid && fr_out) fr_out[q_global0 + q] = fr;
+    if (A.loss_type < 0) return;
+    double term = 0.0, dl = 0.0;
+    if (valid) loss_term(A.loss_type, fr, A.ref[q_global0 + q], term, dl);
+    loss_terms[q] = term;
+    s = valid && fr > 0.0 ? dl * A.scale / fr : 0.0;
   }
-  loss_terms[q] = term;
-  const double s = valid && fr > 0.0 ? dl * A.scale / fr : 0.0;
   const cplx cU = make_double2(s * ts2 * U.x, -s * ts2 * U.y);
   const cplx cV = make_double2(s * ts2 * Vv.x, -s * ts2 * Vv.y);
   const cplx cW = make_double2(s * W.x, -s * W.y);
@@ -2114,11 +2168,13 @@ __global__ __launch_bounds__(64) void k_contract_rows(const int* __restrict__ eb
 #define PFR_CEG_EW 8
 #endif
 constexpr int CEG_EW = PFR_CEG_EW;   // entries per wave of k_contract_eg
-template <int NS, int EW>
+// MS: lambda = m_q Lam per frequency (functional correction: Lam is the adjoint of fr, m_q the loss
+// cotangent scale k_correct_finish formed); m_q = 0 on the padded frequencies.
+template <int NS, int EW, bool MS>
 __global__ __launch_bounds__(256) void k_contract_eg(const int4* __restrict__ ent, int nent,
                                                      const double* __restrict__ se, const cplx* __restrict__ Lam,
                                                      const cplx* __restrict__ X, int64_t Fc, int nvalid,
-                                                     cplx* __restrict__ partial) {
+                                                     const double* __restrict__ msc, cplx* __restrict__ partial) {
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   const int e0 = wv * EW;
@@ -2140,7 +2196,7 @@ __global__ __launch_bounds__(256) void k_contract_eg(const int4* __restrict__ en
       li[u] = Lam[oi[u] + g];
       xj[u] = X[oj[u] + g];
     }
-    const double m = g + lane < nvalid ? 1.0 : 0.0;
+    const double m = MS ? msc[g + lane] : (g + lane < nvalid ? 1.0 : 0.0);
 #pragma unroll
     for (int u = 0; u < EW; ++u) P[u] = cadd(P[u], cscale(cmul(li[u], xj[u]), m));
   }
@@ -2173,7 +2229,8 @@ __global__ __launch_bounds__(256) void k_contract_eg(const int4* __restrict__ en
 
 // t_q = sum_p Lam[p] * rhsP[p] over the Dirichlet support (d b / d beta)
 __global__ void k_rhs_dot(const int* __restrict__ sup, const double* __restrict__ val, int n_sup,
-                          const cplx* __restrict__ Lam, int64_t Fc, cplx* __restrict__ t_out) {
+                          const cplx* __restrict__ Lam, int64_t Fc, const double* __restrict__ msc,
+                          cplx* __restrict__ t_out) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= Fc) return;
   cplx t = make_double2(0, 0);
@@ -2182,7 +2239,7 @@ __global__ void k_rhs_dot(const int* __restrict__ sup, const double* __restrict_
     t.x = fma(val[s], l.x, t.x);
     t.y = fma(val[s], l.y, t.y);
   }
-  t_out[q] = t;
+  t_out[q] = msc ? cscale(t, msc[q]) : t;
 }
 
 // Deterministic reduction over (blocks, valid frequencies):
@@ -2385,18 +2442,28 @@ void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nro
          rhsP, beta, Y, accumulate);
 }
 
+int residual_parts(int n) { return (int)std::min<int64_t>((n + 3) / 4, 256); }
+
 void launch_residual(int mode, int rhs, const ResidDesc& d, const double2* X, int64_t Fc, double2* R, double* acc,
-                     hipStream_t st) {
+                     hipStream_t st, const double2* Mu, double2* cpart) {
   ResidArgs a;
   a.ptr = d.ptr; a.idx = d.idx; a.nzs = d.nzs; a.n = d.n;
   a.K = d.K; a.M = d.M; a.freqs = d.freqs; a.data = d.data; a.data_stride = d.data_stride; a.nvalid = d.nvalid;
   a.rhsP = d.rhsP; a.beta_re = d.beta_re; a.beta_im = d.beta_im; a.mass_sum = d.mass_sum;
   a.B = d.B; a.b_stride = d.b_stride; a.perm = d.perm; a.G = d.G;
-  const dim3 g((unsigned)std::min<int64_t>((d.n + 3) / 4, 256), (unsigned)(Fc / 64)), b(256);
-  if (mode == 0 && rhs == 0) LAUNCH((k_residual<0, 0>), g, b, st, a, X, Fc, R, acc);
-  else if (mode == 0) LAUNCH((k_residual<0, 2>), g, b, st, a, X, Fc, R, acc);
-  else if (rhs == 1) LAUNCH((k_residual<1, 1>), g, b, st, a, X, Fc, R, acc);
-  else LAUNCH((k_residual<1, 2>), g, b, st, a, X, Fc, R, acc);
+  const dim3 g((unsigned)residual_parts(d.n), (unsigned)(Fc / 64)), b(256);
+  if (mode == 0 && rhs == 0 && Mu) LAUNCH((k_residual<0, 0, true>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
+  else if (mode == 0 && rhs == 0) LAUNCH((k_residual<0, 0>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
+  else if (mode == 0) LAUNCH((k_residual<0, 2>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
+  else if (rhs == 1) LAUNCH((k_residual<1, 1>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
+  else LAUNCH((k_residual<1, 2>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
+}
+
+void launch_correct_finish(const FunctionalArgs& A, const double* fr0, const double2* cpart, int nparts, int64_t Fc,
+                           int nvalid, int64_t q0, double* fr_out, double* loss_terms, double* mscale,
+                           hipStream_t st) {
+  LAUNCH(k_correct_finish, dim3((unsigned)((Fc + 63) / 64)), dim3(64), st, A, fr0, cpart, nparts, Fc, nvalid, q0,
+         fr_out, loss_terms, mscale);
 }
 
 void launch_berr_finish(double* acc, int64_t Fc, int nvalid, double tol, int flag, int* flags, double* berr_out,
@@ -2440,16 +2507,18 @@ void launch_contract_rows(bool check, const int* eblk, const int4* ent, int nblk
 int contract_eg_parts(int nent) { return (nent + CEG_EW - 1) / CEG_EW; }
 
 void launch_contract_eg(const int4* ent, int nent, const double* se, int n_stiff, const double2* Lam, const double2* X,
-                        int64_t Fc, int nvalid, double2* partial, hipStream_t st) {
+                        int64_t Fc, int nvalid, double2* partial, hipStream_t st, const double* msc) {
   const int waves = contract_eg_parts(nent);
   const dim3 g((waves + 3) / 4), b(256);
-  if (n_stiff == 12) LAUNCH((k_contract_eg<12, CEG_EW>), g, b, st, ent, nent, se, Lam, X, Fc, nvalid, partial);
-  else LAUNCH((k_contract_eg<18, CEG_EW>), g, b, st, ent, nent, se, Lam, X, Fc, nvalid, partial);
+  if (n_stiff == 12 && msc) LAUNCH((k_contract_eg<12, CEG_EW, true>), g, b, st, ent, nent, se, Lam, X, Fc, nvalid, msc, partial);
+  else if (n_stiff == 12) LAUNCH((k_contract_eg<12, CEG_EW, false>), g, b, st, ent, nent, se, Lam, X, Fc, nvalid, msc, partial);
+  else if (msc) LAUNCH((k_contract_eg<18, CEG_EW, true>), g, b, st, ent, nent, se, Lam, X, Fc, nvalid, msc, partial);
+  else LAUNCH((k_contract_eg<18, CEG_EW, false>), g, b, st, ent, nent, se, Lam, X, Fc, nvalid, msc, partial);
 }
 
 void launch_rhs_dot(const int* sup, const double* val, int n_sup, const double2* Lam, int64_t Fc, double2* t_out,
-                    hipStream_t st) {
-  LAUNCH(k_rhs_dot, dim3((unsigned)((Fc + 63) / 64)), dim3(64), st, sup, val, n_sup, Lam, Fc, t_out);
+                    hipStream_t st, const double* msc) {
+  LAUNCH(k_rhs_dot, dim3((unsigned)((Fc + 63) / 64)), dim3(64), st, sup, val, n_sup, Lam, Fc, msc, t_out);
 }
 
 void launch_reduce(const double2* partial, int nparts, int n_stiff, const double2* t_q, const CoefPack& e,

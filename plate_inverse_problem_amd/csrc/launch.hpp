@@ -79,13 +79,14 @@ void launch_contract_rows(bool check, const int* eblk, const int4* ent, int nblk
                           int64_t Fc, int nvalid, double2* partial, double* acc_f, double* acc_a, hipStream_t st);
 // gradient contraction with the frequency sum first (one partial per wave: contract_eg_parts of them)
 int contract_eg_parts(int nent);
+// msc (may be NULL): per-frequency factor of Lam (functional correction: the loss cotangent scale)
 void launch_contract_eg(const int4* ent, int nent, const double* se, int n_stiff, const double2* Lam, const double2* X,
-                        int64_t Fc, int nvalid, double2* partial, hipStream_t st);
+                        int64_t Fc, int nvalid, double2* partial, hipStream_t st, const double* msc = nullptr);
 // entry-ordered copies of K / M (kme, may be NULL) and of the stiffness matrices (se, may be NULL)
 void launch_gather_entries(const int4* ent, int nent, const double2* K, const double* M, const double* stiff, int ns,
                            double2* kme, double* se, hipStream_t st);
 void launch_rhs_dot(const int* sup, const double* val, int n_sup, const double2* Lam, int64_t Fc, double2* t_out,
-                    hipStream_t st);
+                    hipStream_t st, const double* msc = nullptr);
 // w_out[k] += -sum(partial[., k]) + e_k sum_q t_q ;  loss_out += sum_q loss_terms (q < nvalid)
 void launch_reduce(const double2* partial, int nparts, int n_stiff, const double2* t_q, const CoefPack& e,
                    const double* loss_terms, int nvalid, int64_t Fc, double2* w_out, double* loss_out,
@@ -117,8 +118,15 @@ struct ResidDesc {
   const int* perm = nullptr;
   const double2* G = nullptr;
 };
+// Mu != NULL (mode 0, rhs 0): also the functional-correction dot products sum_p Mu_p r_p, one partial
+// per workgroup and frequency in cpart (residual_parts(n) x Fc), summed by launch_correct_finish
+int residual_parts(int n);
 void launch_residual(int mode, int rhs, const ResidDesc& d, const double2* X, int64_t Fc, double2* R, double* acc,
-                     hipStream_t st);
+                     hipStream_t st, const double2* Mu = nullptr, double2* cpart = nullptr);
+// corrected fr (fr_out, global index; may be NULL), loss terms and cotangent scales of a chunk
+void launch_correct_finish(const FunctionalArgs& A, const double* fr0, const double2* cpart, int nparts, int64_t Fc,
+                           int nvalid, int64_t q0, double* fr_out, double* loss_terms, double* mscale,
+                           hipStream_t st);
 // flags |= flag where acc[q] > tol (or not finite); acc cleared
 void launch_berr_finish(double* acc, int64_t Fc, int nvalid, double tol, int flag, int* flags, double* berr_out,
                         int64_t q0, int which, hipStream_t st);

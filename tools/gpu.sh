@@ -56,7 +56,7 @@ pmc() {
 trace() {
   local F=${1:-2048}; shift
   env PFR_LANES=1 "$@" timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d "$O" -o run -- \
-    python3 bench.py --steps 1 --warmup 0 --freqs "$F" --chunk "$F" --no-cpu-baseline > "$O/b.json" 2> "$O/err" || return $?
+    python3 bench.py --steps "${STEPS:-1}" --warmup 0 --freqs "$F" --chunk "$F" --no-cpu-baseline > "$O/b.json" 2> "$O/err" || return $?
   python3 tools/level_times.py "$O/run_kernel_trace.csv"
 }
 envs() {

@@ -29,6 +29,19 @@ def main(path, L=17):
             continue
         per = " ".join("%5.2f" % t.get(l, 0.0) for l in range(L)) if "x" not in t else ""
         print("%-20s %7.2f %s" % (n[:20], tot, per))
+    # whole-sweep view: device span of every sweep (first k_pad_freqs .. last kernel before the next
+    # one), the kernels' busy time inside it, and the idle time between consecutive sweeps (host side)
+    pads = [i for i, n in enumerate(names) if n == "k_pad_freqs"]
+    spans = []
+    for a, b in zip(pads, pads[1:] + [len(rows)]):
+        t0 = int(rows[a]["Start_Timestamp"])
+        t1 = max(int(r["End_Timestamp"]) for r in rows[a:b])
+        busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows[a:b])
+        spans.append((t0, t1, busy, b - a))
+    for k, (t0, t1, busy, nk) in enumerate(spans):
+        gap = (t0 - spans[k - 1][1]) / 1e6 if k else float("nan")
+        print("sweep %2d: span %7.3f ms  busy %7.3f ms  kernels %4d  idle before %7.3f ms"
+              % (k, (t1 - t0) / 1e6, busy / 1e6, nk, gap))
 
 
 if __name__ == "__main__":
