@@ -221,8 +221,8 @@ PFR_API int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_
  * PFR_CHECK_CORRECT: every pfr_sweep (forward-only sweeps too) also solves for the adjoint of fr --
  * in symmetric mode inside the paired top-down pass -- and the forward residual walk (the forward
  * check) accumulates the correction; in a loss sweep that adjoint is the loss adjoint up to one
- * scalar per frequency, so the correction costs only the residual walk.  Not applied by
- * pfr_hessian_sweep. */
+ * scalar per frequency, so the correction costs only the residual walk.  pfr_hessian_sweep applies
+ * the correction (its loss and gradient equal pfr_sweep's), not the checks. */
 PFR_API int pfr_set_check(pfr_solver* s, int32_t mode, double tol, double* berr_dev);
 
 /* Per-phase device times [ms] of the last pfr_sweep/pfr_solve call on this solver, measured with HIP

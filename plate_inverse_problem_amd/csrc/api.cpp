@@ -1476,12 +1476,26 @@ int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int
     fa.ref = reinterpret_cast<const double2*>(ref_dev);
     fa.scale = scale;
     HIP_TRY(hipMemsetAsync(s->G, 0, (size_t)n * Fc * 16, st));
-    pfr::launch_functional(fa, s->X, Fc, nv, q0, nullptr, s->loss_terms, s->G, st);
     pfr::RhsDesc rg;
     rg.G = s->G;
     rg.rhsP = s->rhsP;
     rg.freqs = s->freqs;
-    if ((rc = adjoint_solve(s, rg, s->XA, st, 1))) return rc;
+    if (s->check_mode & PFR_CHECK_CORRECT) {
+      // as pfr_sweep: the adjoint of fr, the corrected fr's loss terms and cotangent scales, then
+      // lambda = m_q mu in place -- loss and gradient equal the corrected loss sweep's
+      pfr::FunctionalArgs fs = fa;
+      fs.fr0 = s->fr0;
+      pfr::launch_functional(fs, s->X, Fc, nv, q0, nullptr, nullptr, s->G, st);
+      if ((rc = adjoint_solve(s, rg, s->XA, st, 1))) return rc;
+      check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st, s->XA, false);
+      pfr::launch_correct_finish(fa, s->fr0, s->cpart, pfr::residual_parts(s->n), Fc, nv, q0, nullptr, s->loss_terms,
+                                 s->mscale, st);
+      pfr::launch_scale_vec(s->XA, s->mscale, s->n, Fc, st);
+      // the second-order seeds G (k_functional_tangent) are formed from fa, not the seed mode
+    } else {
+      pfr::launch_functional(fa, s->X, Fc, nv, q0, nullptr, s->loss_terms, s->G, st);
+      if ((rc = adjoint_solve(s, rg, s->XA, st, 1))) return rc;
+    }
     contract_rows(s, s->XA, s->X, nv, st);
     pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st);
     pfr::launch_reduce(s->partial, pfr::contract_eg_parts(s->n_uent), s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,

@@ -1880,6 +1880,12 @@ __global__ void k_berr_finish(double* __restrict__ acc, int64_t Fc, int nvalid, 
   acc[q] = 0.0;
 }
 
+// X[p, q] *= m[q] over a permuted frequency-minor vector (lambda = m_q mu, functional correction)
+__global__ void k_scale_vec(cplx* __restrict__ X, const double* __restrict__ m, int n, int64_t Fc) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < (int64_t)n * Fc) X[i] = cscale(X[i], m[i % Fc]);
+}
+
 // X += D over a permuted frequency-minor vector (iterative refinement)
 __global__ void k_axpy_vec(cplx* __restrict__ X, const cplx* __restrict__ D, int64_t count) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2470,6 +2476,11 @@ void launch_berr_finish(double* acc, int64_t Fc, int nvalid, double tol, int fla
                         int64_t q0, int which, hipStream_t st) {
   LAUNCH(k_berr_finish, dim3((unsigned)((Fc + 63) / 64)), dim3(64), st, acc, Fc, nvalid, tol, flag, flags, berr_out,
          q0, which);
+}
+
+void launch_scale_vec(double2* X, const double* m, int n, int64_t Fc, hipStream_t st) {
+  const int64_t count = (int64_t)n * Fc;
+  LAUNCH(k_scale_vec, dim3((unsigned)((count + 255) / 256)), dim3(256), st, X, m, n, Fc);
 }
 
 void launch_axpy_vec(double2* X, const double2* D, int64_t count, hipStream_t st) {

@@ -131,6 +131,7 @@ void launch_correct_finish(const FunctionalArgs& A, const double* fr0, const dou
 void launch_berr_finish(double* acc, int64_t Fc, int nvalid, double tol, int flag, int* flags, double* berr_out,
                         int64_t q0, int which, hipStream_t st);
 void launch_axpy_vec(double2* X, const double2* D, int64_t count, hipStream_t st);
+void launch_scale_vec(double2* X, const double* m, int n, int64_t Fc, hipStream_t st);
 void launch_unpermute(const int* perm, int n, const double2* X, int64_t Fc, int nvalid, double2* out, hipStream_t st);
 void launch_matvec(const int* colptr, const int* rowind, int n, const double2* data, int64_t ds, const double2* x,
                    int64_t xs, double2* y, int transpose, int batch, hipStream_t st);

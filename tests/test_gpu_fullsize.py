@@ -76,6 +76,7 @@ def _peaks(fr, n):
 def c3():
     p = make_problem("orthotropic", ny=25, device="cuda:0")
     yield p
+    p._engine = None           # free the device workspaces even if a failed test's traceback keeps p
     del p
     gc.collect()
     torch.cuda.empty_cache()

@@ -1,7 +1,7 @@
 """Per-level factorisation kernel table from rocprofv3 FETCH_SIZE / WRITE_SIZE passes.
 
 Usage: python tools/level_table.py PROFDIR   (PROFDIR holds fetch/ and write/ as written by
-tools/gpu_prof.sh).  Prints, for the last sweep (after the last k_combine), every
+tools/gpu.sh traffic / stats).  Prints, for the last sweep (after the last k_combine), every
 factorisation launch with its level, duration, HBM read/write (FETCH_SIZE x2, gfx950) and
 rate.
 """

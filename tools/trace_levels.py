@@ -1,4 +1,4 @@
-"""Per-level durations of chosen kernels from tools/gpu_trace_env.sh traces (last sweep).
+"""Per-level durations of chosen kernels from tools/gpu.sh trace runs (last sweep).
 
 Usage: python tools/trace_levels.py gpurun_out/trace/t1 [t2 ...] [--kernels schur,offdiag]
 """
