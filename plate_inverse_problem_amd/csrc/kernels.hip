@@ -1851,13 +1851,22 @@ __device__ __forceinline__ void loss_term(int loss_type, double fr, cplx r, doub
 // reference's fr, for one dot product per row folded into the residual walk.  Per frequency: the
 // corrected fr (fr_out, global index), the loss term of it and the cotangent scale
 // m_q = scale * d term / d fr (lambda = m_q mu: the gradient contraction and k_rhs_dot take it).
-__global__ void k_correct_finish(FunctionalArgs A, const double* __restrict__ fr0, const cplx* __restrict__ cpart,
-                                 int nparts, int64_t Fc, int nvalid, int64_t q_global0, double* __restrict__ fr_out,
-                                 double* __restrict__ loss_terms, double* __restrict__ mscale) {
-  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= Fc) return;
+__global__ __launch_bounds__(256) void k_correct_finish(FunctionalArgs A, const double* __restrict__ fr0,
+                                                        const cplx* __restrict__ cpart, int nparts, int64_t Fc,
+                                                        int nvalid, int64_t q_global0, double* __restrict__ fr_out,
+                                                        double* __restrict__ loss_terms, double* __restrict__ mscale) {
+  // 4 waves per 64 frequencies: wave w sums the partials b = w, w + 4, ... (8 loads in flight), then
+  // wave 0 adds the four in order -- a fixed summation order (deterministic)
+  __shared__ cplx sd[4][64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 64 + lane;
   cplx d = make_double2(0, 0);
-  for (int b = 0; b < nparts; ++b) d = cadd(d, cpart[(int64_t)b * Fc + q]);
+#pragma unroll 8
+  for (int b = w; b < nparts; b += 4) d = cadd(d, cpart[(int64_t)b * Fc + q]);
+  sd[w][lane] = d;
+  __syncthreads();
+  if (w != 0) return;
+  d = cadd(cadd(sd[0][lane], sd[1][lane]), cadd(sd[2][lane], sd[3][lane]));
   const bool valid = q < nvalid;
   const double fr = fr0[q] + d.x;
   if (valid && fr_out) fr_out[q_global0 + q] = fr;
@@ -1959,6 +1968,7 @@ __global__ void k_functional(FunctionalArgs A, const cplx* __restrict__ X, int64
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= Fc) return;
   cplx U = make_double2(0, 0), Vv = make_double2(0, 0), W = make_double2(0, 0);
+#pragma unroll 8
   for (int s = 0; s < A.n_support; ++s) {
     const cplx x = X[(int64_t)A.pidx[s] * Fc + q];
     const double au = A.a[s], av = A.a[A.n_support + s], aw = A.a[2 * A.n_support + s];
@@ -2183,8 +2193,7 @@ __global__ __launch_bounds__(256) void k_contract_eg(const int4* __restrict__ en
                                                      const double* __restrict__ msc, cplx* __restrict__ partial) {
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-  const int e0 = wv * EW;
-  if (e0 >= nent) return;
+  const int e0 = min(wv * EW, nent - 1);     // waves past the end: clamped entries, masked below
   int64_t oi[EW], oj[EW];
 #pragma unroll
   for (int u = 0; u < EW; ++u) {
@@ -2217,7 +2226,7 @@ __global__ __launch_bounds__(256) void k_contract_eg(const int4* __restrict__ en
       re += __shfl_xor(re, o);
       im += __shfl_xor(im, o);
     }
-    const double in = e0 + u < nent ? 1.0 : 0.0;
+    const double in = wv * EW + u < nent ? 1.0 : 0.0;
     const double* sk = se + (int64_t)min(e0 + u, nent - 1) * NS;
 #pragma unroll
     for (int k = 0; k < NS; ++k) {
@@ -2225,12 +2234,19 @@ __global__ __launch_bounds__(256) void k_contract_eg(const int4* __restrict__ en
       part[k].y = fma(sk[k] * in, im, part[k].y);
     }
   }
+  // the workgroup's 4 wave partials summed in wave order (one partial per workgroup: k_reduce's loop
+  // is 4x shorter; deterministic)
+  __shared__ cplx sp[4][NS];
+  const int w = threadIdx.x >> 6;
   if (lane < NS) {
     cplx v = part[0];
 #pragma unroll
     for (int k = 1; k < NS; ++k) v = lane == k ? part[k] : v;
-    partial[(int64_t)wv * NS + lane] = v;
+    sp[w][lane] = v;
   }
+  __syncthreads();
+  if (w == 0 && lane < NS)
+    partial[(int64_t)blockIdx.x * NS + lane] = cadd(cadd(sp[0][lane], sp[1][lane]), cadd(sp[2][lane], sp[3][lane]));
 }
 
 // t_q = sum_p Lam[p] * rhsP[p] over the Dirichlet support (d b / d beta)
@@ -2253,10 +2269,11 @@ __global__ void k_rhs_dot(const int* __restrict__ sup, const double* __restrict_
 __global__ void k_reduce(const cplx* __restrict__ partial, int nparts, int n_stiff, const cplx* __restrict__ t_q,
                          CoefPack e, const double* __restrict__ loss_terms, int nvalid, int64_t Fc,
                          cplx* __restrict__ w_out, double* __restrict__ loss_out) {
-  __shared__ double sre[256], sim[256];
+  __shared__ double sre[1024], sim[1024];
   const int k = blockIdx.x;   // 0..n_stiff-1: stiffness; n_stiff: loss
   double re = 0, im = 0;
   if (k < n_stiff) {
+#pragma unroll 4
     for (int b = threadIdx.x; b < nparts; b += blockDim.x) {
       const cplx v = partial[(int64_t)b * n_stiff + k];
       re -= v.x;
@@ -2468,7 +2485,7 @@ void launch_residual(int mode, int rhs, const ResidDesc& d, const double2* X, in
 void launch_correct_finish(const FunctionalArgs& A, const double* fr0, const double2* cpart, int nparts, int64_t Fc,
                            int nvalid, int64_t q0, double* fr_out, double* loss_terms, double* mscale,
                            hipStream_t st) {
-  LAUNCH(k_correct_finish, dim3((unsigned)((Fc + 63) / 64)), dim3(64), st, A, fr0, cpart, nparts, Fc, nvalid, q0,
+  LAUNCH(k_correct_finish, dim3((unsigned)(Fc / 64)), dim3(256), st, A, fr0, cpart, nparts, Fc, nvalid, q0,
          fr_out, loss_terms, mscale);
 }
 
@@ -2515,12 +2532,11 @@ void launch_contract_rows(bool check, const int* eblk, const int4* ent, int nblk
 #undef CR
 }
 
-int contract_eg_parts(int nent) { return (nent + CEG_EW - 1) / CEG_EW; }
+int contract_eg_parts(int nent) { return ((nent + CEG_EW - 1) / CEG_EW + 3) / 4; }   // workgroups of 4 waves
 
 void launch_contract_eg(const int4* ent, int nent, const double* se, int n_stiff, const double2* Lam, const double2* X,
                         int64_t Fc, int nvalid, double2* partial, hipStream_t st, const double* msc) {
-  const int waves = contract_eg_parts(nent);
-  const dim3 g((waves + 3) / 4), b(256);
+  const dim3 g(contract_eg_parts(nent)), b(256);
   if (n_stiff == 12 && msc) LAUNCH((k_contract_eg<12, CEG_EW, true>), g, b, st, ent, nent, se, Lam, X, Fc, nvalid, msc, partial);
   else if (n_stiff == 12) LAUNCH((k_contract_eg<12, CEG_EW, false>), g, b, st, ent, nent, se, Lam, X, Fc, nvalid, msc, partial);
   else if (msc) LAUNCH((k_contract_eg<18, CEG_EW, true>), g, b, st, ent, nent, se, Lam, X, Fc, nvalid, msc, partial);
@@ -2535,7 +2551,7 @@ void launch_rhs_dot(const int* sup, const double* val, int n_sup, const double2*
 void launch_reduce(const double2* partial, int nparts, int n_stiff, const double2* t_q, const CoefPack& e,
                    const double* loss_terms, int nvalid, int64_t Fc, double2* w_out, double* loss_out,
                    hipStream_t st) {
-  LAUNCH(k_reduce, dim3(n_stiff + 1), dim3(256), st, partial, nparts, n_stiff, t_q, e, loss_terms, nvalid, Fc, w_out,
+  LAUNCH(k_reduce, dim3(n_stiff + 1), dim3(1024), st, partial, nparts, n_stiff, t_q, e, loss_terms, nvalid, Fc, w_out,
          loss_out);
 }
 
