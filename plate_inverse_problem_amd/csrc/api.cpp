@@ -163,6 +163,8 @@ struct pfr_solver {
   // with its low-register small-front variant)
   int solve_wmax = 8, fac_wmax = 16, us2_small = 110;
   int off_small = 1;                    // PFR_OFF_SMALL: no-prefix off-diagonal variant on levels of ns <= 8
+  int split_target = 512;               // PFR_SOLVE_SPLIT: solve launches with fewer (front, group) workgroups
+                                        // split their update parts up to about this many workgroups (0: off)
   int check_fused = 0;                  // PFR_CHECK_FUSED=1: loss sweeps check both solutions in one entry walk
   // backward-error checks (pfr_set_check): PFR_CHECK_* bits, tolerance, optional per-item output;
   // per-frequency maxima scratch, forward and adjoint (kept zero between checks)
@@ -255,6 +257,14 @@ int solve_W(const pfr_solver* s, int l, int nf) {
   return (int)std::max<int64_t>(s->level_W[l], std::min<int64_t>(wmax, fill));
 }
 
+// Workgroups per (front, frequency group) for the update part of a solve launch over nf fronts: 1 when the
+// launch already has split_target workgroups, else enough to reach it (at most 16).
+int solve_split(const pfr_solver* s, int nf) {
+  const int64_t wgs = (int64_t)nf * (s->Fc / 64);
+  if (s->split_target <= 0 || wgs >= s->split_target) return 1;
+  return (int)std::min<int64_t>(16, (s->split_target + wgs - 1) / wgs);
+}
+
 // after_panel(l): called once level l's L21 panel is launched (its L factor complete in stream order)
 int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nvalid, hipStream_t st,
                const std::function<void(int)>& after_panel = nullptr) {
@@ -320,8 +330,10 @@ int solve_all(pfr_solver* s, int which, int rhs_mode, const pfr::RhsDesc& rd, co
       lvl = s->d_reach_fronts[subset] + s->reach_ptr[subset][l];
       nf = s->reach_ptr[subset][l + 1] - s->reach_ptr[subset][l];
     }
+    // the update parts split over several workgroups: L solves, and U solves in symmetric mode
+    const int split = (which == 0 || (which == 1 && s->sym)) ? solve_split(s, nf) : 1;
     pfr::launch_solve(which, rhs_mode, s->sym, s->P, lvl, nf, solve_W(s, l, nf), ngroups, s->F, s->Fc, s->WV, rd, Yin, Out,
-                      reach, st);
+                      reach, st, split);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -385,7 +397,7 @@ int sym_top_down_support(pfr_solver* s, const pfr::RhsDesc& rd, hipStream_t st) 
   for (int l = L - 1; l >= 0; --l) {
     const int nf = s->reach_ptr[1][l + 1] - s->reach_ptr[1][l];
     pfr::launch_solve(1, 0, true, s->P, s->d_reach_fronts[1] + s->reach_ptr[1][l], nf, solve_W(s, l, nf), ngroups, s->F,
-                      s->Fc, s->WV, rd, s->Y, s->X, s->d_reach[0], st);
+                      s->Fc, s->WV, rd, s->Y, s->X, s->d_reach[0], st, solve_split(s, nf));
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -399,7 +411,7 @@ int sym_top_down_pair(pfr_solver* s, hipStream_t st) {
     pfr::launch_usolve2(s->P, s->d_level_fronts + s->level_ptr[l], nf, solve_W(s, l, nf),
                         s->level_maxf[l] <= s->us2_small, ngroups,
                         s->F, s->Fc, s->Y,
-                        s->X, s->d_reach[0], s->d_reach[1], s->Y2, s->XA, s->d_reach[1], st);
+                        s->X, s->d_reach[0], s->d_reach[1], s->Y2, s->XA, s->d_reach[1], st, solve_split(s, nf));
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -624,6 +636,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->fac_wmax = knob("PFR_FAC_WMAX", 16, 1, 16);
   s->us2_small = knob("PFR_US2_SMALL", 110, 0, pfr::MAX_FRONT);
   s->off_small = knob("PFR_OFF_SMALL", 1, 0, 1);
+  s->split_target = knob("PFR_SOLVE_SPLIT", 512, 0, 1 << 20);
   s->check_fused = knob("PFR_CHECK_FUSED", 0, 0, 1);   // measured 2.3 ms against 2 x 0.87 ms per 2,048-frequency chunk
   s->n = S.n;
   s->nnz = S.nnz;
@@ -1306,7 +1319,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
         (void)hipStreamWaitEvent(s->aux, s->lev_ev[l], 0);
         const int nf = s->reach_ptr[0][l + 1] - s->reach_ptr[0][l];
         pfr::launch_solve(0, rmode, true, s->P, s->d_reach_fronts[0] + s->reach_ptr[0][l], nf, solve_W(s, l, nf), ngroups_,
-                          s->F, s->Fc, s->WV, rf, nullptr, s->Y, s->d_reach[0], s->aux);
+                          s->F, s->Fc, s->WV, rf, nullptr, s->Y, s->d_reach[0], s->aux, solve_split(s, nf));
       };
       rc = factor_all(s, 0, nullptr, 0, nv, st, hook);
       if (rc) return rc;

@@ -1150,9 +1150,42 @@ constexpr int SRB = 4, SKC = 8;
 // 16-pivot block cost ~130 dependent memory round trips (~85 us) instead of a few.
 
 
+// V(i) -= L21(i, :) y for the update rows i = i_begin, i_begin + i_step, ... (SRB rows per step; y = the
+// pivot part of the frontal vector, already solved)
+__device__ __forceinline__ void lsolve_rows(const Front& fr, const cplx* __restrict__ base, cplx* __restrict__ wv,
+                                            int64_t Fc, int i_begin, int i_step) {
+  const int f = fr.f, ns = fr.ns;
+#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+#define V(a) wv[(int64_t)(a) * Fc]
+  for (int i0 = i_begin; i0 < f; i0 += i_step) {
+    int ri[SRB];
+    cplx acc[SRB];
+#pragma unroll
+    for (int r = 0; r < SRB; ++r) {
+      ri[r] = min(i0 + r, f - 1);
+      acc[r] = V(ri[r]);
+    }
+    for (int k0 = 0; k0 < ns; k0 += SKC) {
+      cplx y[SKC];
+#pragma unroll
+      for (int u = 0; u < SKC; ++u) y[u] = k0 + u < ns ? V(k0 + u) : make_double2(0.0, 0.0);
+#pragma unroll
+      for (int r = 0; r < SRB; ++r)
+#pragma unroll
+        for (int u = 0; u < SKC; ++u) acc[r] = cfms(acc[r], E(ri[r], min(k0 + u, ns - 1)), y[u]);
+    }
+#pragma unroll
+    for (int r = 0; r < SRB; ++r)
+      if (i0 + r < f) V(i0 + r) = acc[r];
+  }
+#undef E
+#undef V
+}
+
 template <int RHS>
 __global__ __launch_bounds__(512) void k_lsolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
-                               cplx* __restrict__ WV, RhsArgs R, cplx* __restrict__ Y, const int* __restrict__ reach) {
+                               cplx* __restrict__ WV, RhsArgs R, cplx* __restrict__ Y, const int* __restrict__ reach,
+                               int rows_split) {
   int bx;
   const Ctx c = ctx_xcd(bx);
   const Front fr = P.fronts[lvl[bx]];
@@ -1198,30 +1231,24 @@ __global__ __launch_bounds__(512) void k_lsolve_level(DevPattern P, const int* _
       __syncthreads();
     }
   }
-  for (int i0 = ns + SRB * c.w; i0 < f; i0 += SRB * c.W) {
-    int ri[SRB];
-    cplx acc[SRB];
-#pragma unroll
-    for (int r = 0; r < SRB; ++r) {
-      ri[r] = min(i0 + r, f - 1);
-      acc[r] = V(ri[r]);
-    }
-    for (int k0 = 0; k0 < ns; k0 += SKC) {
-      cplx y[SKC];
-#pragma unroll
-      for (int u = 0; u < SKC; ++u) y[u] = k0 + u < ns ? V(k0 + u) : make_double2(0.0, 0.0);
-#pragma unroll
-      for (int r = 0; r < SRB; ++r)
-#pragma unroll
-        for (int u = 0; u < SKC; ++u) acc[r] = cfms(acc[r], E(ri[r], min(k0 + u, ns - 1)), y[u]);
-    }
-#pragma unroll
-    for (int r = 0; r < SRB; ++r)
-      if (i0 + r < f) V(i0 + r) = acc[r];
-  }
+  if (!rows_split) lsolve_rows(fr, base, wv, Fc, ns + SRB * c.w, SRB * c.W);
   for (int a = c.w; a < ns; a += c.W) Y[(int64_t)(fr.col0 + a) * Fc + c.q] = V(a);
 #undef E
 #undef V
+}
+
+// Update rows of the L solve at the top levels, split over S workgroups per (front, frequency group)
+// (launch_solve with split > 1, after k_lsolve_level<..., rows_split = 1> formed the pivot values): at
+// small frequency counts one workgroup per front reads the whole L21 block through one CU, bound by
+// that CU's memory return rate, while most CUs idle.
+__global__ __launch_bounds__(256) void k_lsolve_rows(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F,
+                                                     int64_t Fc, cplx* __restrict__ WV, int S) {
+  int bx;
+  const Ctx c = ctx_xcd(bx);
+  const int slot = bx / S, split = bx % S;
+  const Front fr = P.fronts[lvl[slot]];
+  lsolve_rows(fr, F + fr.off * Fc + c.q, WV + (int64_t)fr.row0 * Fc + c.q, Fc, fr.ns + SRB * (split * c.W + c.w),
+              SRB * c.W * S);
 }
 
 // v - sum_{b in [ns, f)} e[b * es] * X[ix[b]]: the update-row solution values are
@@ -1251,26 +1278,17 @@ __device__ __forceinline__ cplx offdiag_dot(cplx v, const cplx* __restrict__ e, 
 // Pivot rows first take the update-row solution: v_a = y_a - U12(a, :) x_upd, SRB pivot rows
 // per wave sharing each gathered x value (SYM: U12(a, b) = U(a, a) L21(b, a), read from L21);
 // then U11 backward in KBS blocks, the diagonal block by wave 0 in registers.
+// Pivot rows' update part of the U solve: V(a) = y_a + U(a, a) L21(:, a)^T x_upd (SYM) for the pivot
+// rows a = a_begin, a_begin + a_step, ... (SRB per step)
 template <bool SYM>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_usolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
-                               cplx* __restrict__ WV, const cplx* __restrict__ Y, cplx* __restrict__ X,
-                               const int* __restrict__ reach) {
-  int bx;
-  const Ctx c = ctx_xcd(bx);
-  const bool live = !reach || reach[lvl[bx]];   // unreached front: y = 0
-  const Front fr = P.fronts[lvl[bx]];
+__device__ __forceinline__ void usolve_upd(const Front& fr, const int* ix, const cplx* __restrict__ base,
+                                           cplx* __restrict__ wv, const cplx* __restrict__ Y, const cplx* __restrict__ X,
+                                           int64_t Fc, int64_t q, bool live, int a_begin, int a_step) {
   const int f = fr.f, ns = fr.ns;
-  const cplx* __restrict__ base = F + fr.off * Fc + c.q;
-  cplx* __restrict__ wv = WV + (int64_t)fr.row0 * Fc + c.q;
-  // the front's row indices, staged in LDS once: the solution gathers of every pivot row read
-  // them there instead of through dependent global loads
-  __shared__ int six[MAX_FRONT];
-  for (int a = threadIdx.x; a < f; a += blockDim.x) six[a] = P.idx[fr.row0 + a];
-  __syncthreads();
-  const int* ix = six;
+  const Ctx c{0, 0, 0, q};
 #define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
 #define V(a) wv[(int64_t)(a) * Fc]
-  for (int a0 = SRB * c.w; a0 < ns; a0 += SRB * c.W) {
+  for (int a0 = a_begin; a0 < ns; a0 += a_step) {
     int ra[SRB];
     cplx acc[SRB];
 #pragma unroll
@@ -1313,7 +1331,32 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
         V(a0 + r) = SYM ? cadd(y, cmul(E(ra[r], ra[r]), acc[r])) : cadd(y, acc[r]);
       }
   }
+#undef E
+#undef V
+}
+
+template <bool SYM>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_usolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
+                               cplx* __restrict__ WV, const cplx* __restrict__ Y, cplx* __restrict__ X,
+                               const int* __restrict__ reach, int upd_done) {
+  int bx;
+  const Ctx c = ctx_xcd(bx);
+  const bool live = !reach || reach[lvl[bx]];   // unreached front: y = 0
+  const Front fr = P.fronts[lvl[bx]];
+  const int f = fr.f, ns = fr.ns;
+  const cplx* __restrict__ base = F + fr.off * Fc + c.q;
+  cplx* __restrict__ wv = WV + (int64_t)fr.row0 * Fc + c.q;
+  // the front's row indices, staged in LDS once: the solution gathers of every pivot row read
+  // them there instead of through dependent global loads
+  __shared__ int six[MAX_FRONT];
+  if (!upd_done) {
+    for (int a = threadIdx.x; a < f; a += blockDim.x) six[a] = P.idx[fr.row0 + a];
+    __syncthreads();
+    usolve_upd<SYM>(fr, six, base, wv, Y, X, Fc, c.q, live, SRB * c.w, SRB * c.W);
+  }
   __syncthreads();
+#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+#define V(a) wv[(int64_t)(a) * Fc]
   for (int k1 = ns; k1 > 0; k1 -= KBS) {
     const int k0 = max(0, k1 - KBS), kb = k1 - k0;
     if (c.w == 0) {
@@ -1356,6 +1399,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k
 #undef V
 }
 
+// the pivot rows' update part of k_usolve_level split over S workgroups per (front, frequency group)
+template <bool SYM>
+__global__ __launch_bounds__(256) void k_usolve_upd(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F,
+                                                    int64_t Fc, cplx* __restrict__ WV, const cplx* __restrict__ Y,
+                                                    const cplx* __restrict__ X, const int* __restrict__ reach, int S) {
+  int bx;
+  const Ctx c = ctx_xcd(bx);
+  const int slot = bx / S, split = bx % S;
+  const bool live = !reach || reach[lvl[slot]];
+  const Front fr = P.fronts[lvl[slot]];
+  __shared__ int six[MAX_FRONT];
+  for (int a = threadIdx.x; a < fr.f; a += blockDim.x) six[a] = P.idx[fr.row0 + a];
+  __syncthreads();
+  usolve_upd<SYM>(fr, six, F + fr.off * Fc + c.q, WV + (int64_t)fr.row0 * Fc + c.q, Y, X, Fc, c.q, live,
+                  SRB * (split * c.W + c.w), SRB * c.W * S);
+}
+
 // ------------------------------------------------------------------ K3b': two top-down solves in one pass
 // U x = y for two right-hand sides on the same factors (symmetric mode: the forward solution x
 // and the adjoint lambda), each L21 / U11 value loaded once for both.  Vector v is computed on
@@ -1372,25 +1432,17 @@ struct UPair {
 // SR pivot rows per wave sharing each gathered solution value, SK values per chunk, WPE waves per
 // SIMD: (4, 8, 2) for the levels of large fronts; (2, 4, 4) for levels of small fronts, where the
 // many tiny workgroups are latency-bound and occupancy, not per-wave reuse, hides it.
-template <bool SYM, int SR, int SK, int WPE>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void k_usolve2_level(
-    DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc, UPair A, UPair B) {
-  int bx;
-  const Ctx c = ctx_xcd(bx);
-  const int ft = lvl[bx];
-  const bool act[2] = {!A.skip || !A.skip[ft], !B.skip || !B.skip[ft]};
-  const bool live[2] = {!A.reach || A.reach[ft], !B.reach || B.reach[ft]};
-  const cplx* Ys[2] = {A.Y, B.Y};
-  cplx* Xs[2] = {A.X, B.X};
-  const Front fr = P.fronts[ft];
+// the pivot rows' update part of the paired pass: XV(v, a) = y_a + U(a, a) L21(:, a)^T x_upd for
+// a = a_begin, a_begin + a_step, ... (SR per step)
+template <bool SYM, int SR, int SK>
+__device__ __forceinline__ void usolve2_upd(const Front& fr, const int* six, const cplx* __restrict__ base,
+                                            int64_t Fc, int64_t q, const bool (&act)[2], const bool (&live)[2],
+                                            const cplx* const (&Ys)[2], cplx* const (&Xs)[2], int a_begin, int a_step) {
   const int f = fr.f, ns = fr.ns;
-  const cplx* __restrict__ base = F + fr.off * Fc + c.q;
-  __shared__ int six[MAX_FRONT];
-  for (int a = threadIdx.x; a < f; a += blockDim.x) six[a] = P.idx[fr.row0 + a];
-  __syncthreads();
+  const Ctx c{0, 0, 0, q};
 #define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
 #define XV(v, a) Xs[v][(int64_t)(fr.col0 + (a)) * Fc + c.q]
-  for (int a0 = SR * c.w; a0 < ns; a0 += SR * c.W) {
+  for (int a0 = a_begin; a0 < ns; a0 += a_step) {
     int ra[SR];
     cplx acc[2][SR];
 #pragma unroll
@@ -1441,7 +1493,32 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
           }
       }
   }
+#undef E
+#undef XV
+}
+
+template <bool SYM, int SR, int SK, int WPE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void k_usolve2_level(
+    DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc, UPair A, UPair B, int upd_done) {
+  int bx;
+  const Ctx c = ctx_xcd(bx);
+  const int ft = lvl[bx];
+  const bool act[2] = {!A.skip || !A.skip[ft], !B.skip || !B.skip[ft]};
+  const bool live[2] = {!A.reach || A.reach[ft], !B.reach || B.reach[ft]};
+  const cplx* const Ys[2] = {A.Y, B.Y};
+  cplx* const Xs[2] = {A.X, B.X};
+  const Front fr = P.fronts[ft];
+  const int f = fr.f, ns = fr.ns;
+  const cplx* __restrict__ base = F + fr.off * Fc + c.q;
+  __shared__ int six[MAX_FRONT];
+  if (!upd_done) {
+    for (int a = threadIdx.x; a < f; a += blockDim.x) six[a] = P.idx[fr.row0 + a];
+    __syncthreads();
+    usolve2_upd<SYM, SR, SK>(fr, six, base, Fc, c.q, act, live, Ys, Xs, SR * c.w, SR * c.W);
+  }
   __syncthreads();
+#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+#define XV(v, a) Xs[v][(int64_t)(fr.col0 + (a)) * Fc + c.q]
   for (int k1 = ns; k1 > 0; k1 -= KBS) {
     const int k0 = max(0, k1 - KBS), kb = k1 - k0;
     if (c.w == 0) {
@@ -1486,6 +1563,26 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
 #undef E
 #undef XV
+}
+
+// the pivot rows' update part of k_usolve2_level split over S workgroups per (front, frequency group)
+template <bool SYM, int SR, int SK>
+__global__ __launch_bounds__(256) void k_usolve2_upd(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F,
+                                                     int64_t Fc, UPair A, UPair B, int S) {
+  int bx;
+  const Ctx c = ctx_xcd(bx);
+  const int slot = bx / S, split = bx % S;
+  const int ft = lvl[slot];
+  const bool act[2] = {!A.skip || !A.skip[ft], !B.skip || !B.skip[ft]};
+  const bool live[2] = {!A.reach || A.reach[ft], !B.reach || B.reach[ft]};
+  const cplx* const Ys[2] = {A.Y, B.Y};
+  cplx* const Xs[2] = {A.X, B.X};
+  const Front fr = P.fronts[ft];
+  __shared__ int six[MAX_FRONT];
+  for (int a = threadIdx.x; a < fr.f; a += blockDim.x) six[a] = P.idx[fr.row0 + a];
+  __syncthreads();
+  usolve2_upd<SYM, SR, SK>(fr, six, F + fr.off * Fc + c.q, Fc, c.q, act, live, Ys, Xs, SR * (split * c.W + c.w),
+                           SR * c.W * S);
 }
 
 // ------------------------------------------------------------------ K3c: U^T y = g (bottom-up)
@@ -2421,20 +2518,25 @@ static RhsArgs make_rhs(const RhsDesc& d) {
 
 void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups,
                   const double2* F, int64_t Fc, double2* WV, const RhsDesc& rd, const double2* Yin, double2* Out,
-                  const int* reach, hipStream_t st) {
+                  const int* reach, hipStream_t st, int split) {
   if (nfronts <= 0) return;
   dim3 g(nfronts, ngroups), b(64 * W);
+  const dim3 gs(nfronts * split, ngroups), bs(64 * SPLIT_W);
+  const int rs = split > 1;
   RhsArgs R = make_rhs(rd);
   switch (which) {
-    case 0:  // L solve
-      if (rhs_mode == 0) LAUNCH(k_lsolve_level<0>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach);
-      else if (rhs_mode == 1) LAUNCH(k_lsolve_level<1>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach);
-      else if (rhs_mode == 2) LAUNCH(k_lsolve_level<2>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach);
-      else LAUNCH(k_lsolve_level<3>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach);
+    case 0:  // L solve (split > 1: the update rows by k_lsolve_rows over `split` workgroups per front)
+      if (rhs_mode == 0) LAUNCH(k_lsolve_level<0>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach, rs);
+      else if (rhs_mode == 1) LAUNCH(k_lsolve_level<1>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach, rs);
+      else if (rhs_mode == 2) LAUNCH(k_lsolve_level<2>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach, rs);
+      else LAUNCH(k_lsolve_level<3>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach, rs);
+      if (rs) LAUNCH(k_lsolve_rows, gs, bs, st, P, lvl, F, Fc, WV, split);
       break;
-    case 1:  // U solve
-      if (sym) LAUNCH(k_usolve_level<true>, g, b, st, P, lvl, F, Fc, WV, Yin, Out, reach);
-      else LAUNCH(k_usolve_level<false>, g, b, st, P, lvl, F, Fc, WV, Yin, Out, reach);
+    case 1:  // U solve (split > 1: the pivot rows' update part first, by k_usolve_upd)
+      if (rs && sym) LAUNCH(k_usolve_upd<true>, gs, bs, st, P, lvl, F, Fc, WV, Yin, Out, reach, split);
+      else if (rs) LAUNCH(k_usolve_upd<false>, gs, bs, st, P, lvl, F, Fc, WV, Yin, Out, reach, split);
+      if (sym) LAUNCH(k_usolve_level<true>, g, b, st, P, lvl, F, Fc, WV, Yin, Out, reach, rs);
+      else LAUNCH(k_usolve_level<false>, g, b, st, P, lvl, F, Fc, WV, Yin, Out, reach, rs);
       break;
     case 2:  // U^T solve
       if (rhs_mode == 0) LAUNCH(k_utsolve_level<0>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach);
@@ -2449,13 +2551,18 @@ void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const 
 
 void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, bool small, int ngroups,
                     const double2* F, int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0,
-                    const double2* Y1, double2* X1, const int* reach1, hipStream_t st) {
+                    const double2* Y1, double2* X1, const int* reach1, hipStream_t st, int split) {
   if (nfronts <= 0) return;
   UPair a{Y0, X0, reach0, skip0}, b{Y1, X1, reach1, nullptr};
   dim3 g(nfronts, ngroups), bl(64 * W);
+  const int rs = split > 1;
+  // split > 1: the pivot rows' update part over `split` workgroups per front first (the small-front
+  // register shape: many short waves)
+  if (rs) LAUNCH((k_usolve2_upd<true, 2, 4>), dim3(nfronts * split, ngroups), dim3(64 * SPLIT_W), st, P, lvl, F, Fc, a, b,
+                 split);
   // symmetric mode only (the paired top-down pass serves the symmetric loss + gradient sweep)
-  if (small) LAUNCH((k_usolve2_level<true, 2, 4, 4>), g, bl, st, P, lvl, F, Fc, a, b);
-  else LAUNCH((k_usolve2_level<true, 4, 8, 2>), g, bl, st, P, lvl, F, Fc, a, b);
+  if (small) LAUNCH((k_usolve2_level<true, 2, 4, 4>), g, bl, st, P, lvl, F, Fc, a, b, rs);
+  else LAUNCH((k_usolve2_level<true, 4, 8, 2>), g, bl, st, P, lvl, F, Fc, a, b, rs);
 }
 
 void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nrows, const double2* Kd,

@@ -46,14 +46,18 @@ void launch_schur(bool sym, const DevPattern& P, const int4* tiles, int ntiles, 
 void launch_schur_blk(int bc, const DevPattern& P, const int4* blocks, int nblocks, const int* bg1, const int* bgxp,
                       const int2* bgx, int ngroups, double2* F, int64_t Fc, hipStream_t st);
 // which: 0 = L (bottom-up), 1 = U (top-down), 2 = U^T (bottom-up), 3 = L^T (top-down)
+// split > 1 (L and U solves): the update part of every front (L: the update rows; U: the pivot rows'
+// products with the update-row solution) runs first / last over `split` workgroups of SPLIT_W waves per
+// (front, frequency group) -- the top levels' few fronts otherwise pull their L21 blocks through one CU each
+constexpr int SPLIT_W = 4;
 void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups,
                   const double2* F, int64_t Fc, double2* WV, const RhsDesc& rd, const double2* Yin, double2* Out,
-                  const int* reach, hipStream_t st);
+                  const int* reach, hipStream_t st, int split = 1);
 // two top-down U solves in one pass (vector 0 skipped on the fronts flagged in skip0), symmetric
 // mode; small: the low-register variant for levels of small fronts
 void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, bool small, int ngroups,
                     const double2* F, int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0,
-                    const double2* Y1, double2* X1, const int* reach1, hipStream_t st);
+                    const double2* Y1, double2* X1, const int* reach1, hipStream_t st, int split = 1);
 // Hessian sweep: tangent right-hand sides (rows of the permuted matrix, or of its
 // transpose with accumulate = 1) and the directional derivative of the loss cotangent
 void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nrows, const double2* Kd,

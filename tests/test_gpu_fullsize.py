@@ -11,7 +11,8 @@
   is created): PFR_US2_SMALL=0 (every level through the large-front paired top-down solve),
   PFR_US2_SMALL=1024 (every level through the small-front variant), PFR_FAC_WMAX=1 / 16 and
   PFR_SOLVE_WMAX=1 (one-wave and widest LU / solve workgroups), PFR_OFF_SMALL=0 (the bottom
-  levels' off-diagonal rows through the general kernel instead of the no-prefix variant).
+  levels' off-diagonal rows through the general kernel instead of the no-prefix variant),
+  PFR_SOLVE_SPLIT=0 / 1000000 (the solves' update parts never / always split over workgroups).
 
 Tolerances.  These systems are badly scaled (membrane, bending and unit Dirichlet rows) and their
 conditioning grows like (mesh size)^-4.  At C3 the fr of the fp64 problem data is numerically
@@ -154,6 +155,8 @@ def test_c2_forward_sweep_matches_truth():
     {"PFR_FAC_WMAX": "16", "PFR_SOLVE_WMAX": "8"},
     {"PFR_CHECK_FUSED": "1", "PFR_CHECK": "3"},    # the fused walk replaces the checks without the correction
     {"PFR_OFF_SMALL": "0"},
+    {"PFR_SOLVE_SPLIT": "0"},          # every solve launch unsplit (the small meshes split by default)
+    {"PFR_SOLVE_SPLIT": "1000000"},    # every solve launch split 16 ways
 ])
 def test_kernel_variants_match_oracle(env, monkeypatch):
     from oracle.plate_oracle import loss_and_grad
