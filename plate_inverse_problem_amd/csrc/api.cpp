@@ -261,7 +261,7 @@ int solve_W(const pfr_solver* s, int l, int nf) {
 // launch already has split_target workgroups, else enough to reach it (at most 16).
 int solve_split(const pfr_solver* s, int nf) {
   const int64_t wgs = (int64_t)nf * (s->Fc / 64);
-  if (s->split_target <= 0 || wgs >= s->split_target) return 1;
+  if (s->split_target <= 0 || wgs <= 0 || wgs >= s->split_target) return 1;
   return (int)std::min<int64_t>(16, (s->split_target + wgs - 1) / wgs);
 }
 
