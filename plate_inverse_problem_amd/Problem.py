@@ -146,7 +146,10 @@ class _Engine:
         least 64 frequencies; per lane as many frequencies per chunk as fit in its share of ~85 %
         of the free HBM (multiple of 64, <= 4096), in even chunks."""
         n_freqs = max(1, n_freqs)
-        n_lanes = max(1, min(self._lanes_req, -(-n_freqs // 64)))
+        # a lane per 512 frequencies at most: below that a sweep is latency-bound (top-level fronts) and a
+        # second lane only adds its own chains (C4's 512-frequency share: 1 lane 27.1k, 2 lanes 26.4k
+        # freq-solves/s; 1,024: 2 lanes 4 % faster; profiles/r03)
+        n_lanes = max(1, min(self._lanes_req, -(-n_freqs // 512)))
         if self._fixed_batch:
             return n_lanes, int(self._fixed_batch)
         per_lane = -(-n_freqs // n_lanes)
