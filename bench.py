@@ -357,8 +357,10 @@ def main():
                             "frequencies": n_iso},
         "phase_ms": {"factor": phase[0], "fwd_solves": phase[1], "functional": phase[2],
                      "adj_solves": phase[3], "contract": phase[4],
-                     "note": "device ms per step summed over lanes (phases: forward solves include the functional "
-                             "correction's residual walk when on)"},
+                     "note": "device ms per step summed over lanes; fwd_solves = the forward bottom-up pass over "
+                             "the rhs reach + the top-down pass over the loss support's fronts, adj_solves = the "
+                             "adjoint bottom-up + the paired top-down pass, contract = residual walks (checks and "
+                             "the functional correction) + gradient contraction"},
         "loss": val,
         "backward_error": check,
     }
