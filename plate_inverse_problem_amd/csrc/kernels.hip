@@ -1509,7 +1509,86 @@ __device__ __forceinline__ void usolve2_upd(const Front& fr, const int* six, con
 #undef XV
 }
 
-template <bool SYM, int SR, int SK, int WPE, int NP = 1>
+// LDS-staged form of usolve2_upd for one workgroup (all waves): per pass over the pivot rows, the
+// update-row solution values x_upd of both vectors are gathered ONCE per workgroup into LDS in chunks of
+// US2_CH rows and every wave reads them from there (the plain form gathers them once per wave and pass).
+constexpr int US2_CH = 16;
+template <bool SYM, int SR, int SK>
+__device__ __forceinline__ void usolve2_upd_xs(const Front& fr, const int* six, const cplx* __restrict__ base,
+                                               int64_t Fc, int64_t q, const bool (&act)[2], const bool (&live)[2],
+                                               const cplx* const (&Ys)[2], cplx* const (&Xs)[2], int w, int W,
+                                               cplx* __restrict__ sx) {
+  const int f = fr.f, ns = fr.ns, lane = threadIdx.x & 63;
+  const Ctx c{0, 0, 0, q};
+#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+#define XV(v, a) Xs[v][(int64_t)(fr.col0 + (a)) * Fc + c.q]
+  const int npass = (ns + SR * W - 1) / (SR * W);       // the same for every wave of the workgroup
+  const int64_t su = SYM ? (int64_t)f * Fc : Fc;
+  for (int p = 0; p < npass; ++p) {
+    const int a0 = SR * (w + p * W);
+    int ra[SR];
+    cplx acc[2][SR];
+    const cplx* pu[SR];
+#pragma unroll
+    for (int r = 0; r < SR; ++r) {
+      ra[r] = min(a0 + r, ns - 1);
+      acc[0][r] = acc[1][r] = make_double2(0.0, 0.0);
+      pu[r] = base + (SYM ? (int64_t)ra[r] : (int64_t)ra[r] * f) * Fc;
+    }
+    for (int c0 = ns; c0 < f; c0 += US2_CH) {
+      // stage rows c0 .. c0 + US2_CH - 1 of both vectors, 4 row loads per wave and round (clamped rows
+      // past the front are loaded but never read)
+      for (int t0 = 4 * w; t0 < 2 * US2_CH; t0 += 4 * W) {
+        cplx tmp[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int t = min(t0 + u, 2 * US2_CH - 1), v = t / US2_CH, b = t % US2_CH;
+          const int row = __builtin_amdgcn_readfirstlane(six[min(c0 + b, f - 1)]);
+          tmp[u] = Xs[v][(int64_t)row * Fc + c.q];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (t0 + u < 2 * US2_CH) sx[(t0 + u) * 64 + lane] = tmp[u];
+      }
+      __syncthreads();
+      const int nch = min(US2_CH, f - c0);
+      for (int b0 = 0; b0 < nch; b0 += SK) {
+        cplx xv[2][SK], ev[SR][SK];
+#pragma unroll
+        for (int r = 0; r < SR; ++r)
+#pragma unroll
+          for (int u = 0; u < SK; ++u) ev[r][u] = pu[r][min(c0 + b0 + u, f - 1) * su];
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+          for (int u = 0; u < SK; ++u)
+            xv[v][u] = cscale(sx[(v * US2_CH + min(b0 + u, US2_CH - 1)) * 64 + lane], b0 + u < nch ? 1.0 : 0.0);
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+          for (int r = 0; r < SR; ++r)
+#pragma unroll
+            for (int u = 0; u < SK; ++u) acc[v][r] = cfms(acc[v][r], ev[r][u], xv[v][u]);
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int r = 0; r < SR; ++r)
+      if (a0 + r < ns) {
+        const cplx urr = SYM ? E(ra[r], ra[r]) : make_double2(1.0, 0.0);
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+          if (act[v]) {
+            const cplx y = live[v] ? Ys[v][(int64_t)(fr.col0 + a0 + r) * Fc + c.q] : make_double2(0.0, 0.0);
+            XV(v, a0 + r) = SYM ? cadd(y, cmul(urr, acc[v][r])) : cadd(y, acc[v][r]);
+          }
+      }
+  }
+#undef E
+#undef XV
+}
+
+template <bool SYM, int SR, int SK, int WPE, int NP = 1, bool XS = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void k_usolve2_level(
     DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc, UPair A, UPair B, int upd_done) {
   int bx;
@@ -1526,7 +1605,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
   if (!upd_done) {
     for (int a = threadIdx.x; a < f; a += blockDim.x) six[a] = P.idx[fr.row0 + a];
     __syncthreads();
-    usolve2_upd<SYM, SR, SK, NP>(fr, six, base, Fc, c.q, act, live, Ys, Xs, SR * c.w, SR * c.W);
+    if (XS) {
+      __shared__ cplx sx[2 * US2_CH * 64];
+      usolve2_upd_xs<SYM, SR, SK>(fr, six, base, Fc, c.q, act, live, Ys, Xs, c.w, c.W, sx);
+    } else {
+      usolve2_upd<SYM, SR, SK, NP>(fr, six, base, Fc, c.q, act, live, Ys, Xs, SR * c.w, SR * c.W);
+    }
   }
   __syncthreads();
 #define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
@@ -2577,7 +2661,13 @@ void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, boo
     const char* e = getenv("PFR_US2_NP");   // tuning knob: row-group passes sharing each x_upd gather (1, 2)
     return e ? atoi(e) : 1;
   }();
-  if (small && np == 2) LAUNCH((k_usolve2_level<true, 2, 4, 3, 2>), g, bl, st, P, lvl, F, Fc, a, b, rs);
+  static const int xs = [] {
+    const char* e = getenv("PFR_US2_XS");   // tuning knob: x_upd staged in LDS once per workgroup and pass
+    return e ? atoi(e) : 0;
+  }();
+  if (small && xs) LAUNCH((k_usolve2_level<true, 2, 4, 4, 1, true>), g, bl, st, P, lvl, F, Fc, a, b, rs);
+  else if (!small && xs) LAUNCH((k_usolve2_level<true, 4, 8, 2, 1, true>), g, bl, st, P, lvl, F, Fc, a, b, rs);
+  else if (small && np == 2) LAUNCH((k_usolve2_level<true, 2, 4, 3, 2>), g, bl, st, P, lvl, F, Fc, a, b, rs);
   else if (small) LAUNCH((k_usolve2_level<true, 2, 4, 4>), g, bl, st, P, lvl, F, Fc, a, b, rs);
   else LAUNCH((k_usolve2_level<true, 4, 8, 2>), g, bl, st, P, lvl, F, Fc, a, b, rs);
 }
