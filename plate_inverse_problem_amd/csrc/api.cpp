@@ -163,10 +163,9 @@ struct pfr_solver {
   // with its low-register small-front variant)
   int solve_wmax = 8, fac_wmax = 16, us2_small = 110;
   int off_small = 1;                    // PFR_OFF_SMALL: no-prefix off-diagonal variant on levels of ns <= 8
-  int us2_wfit = 0;                     // PFR_US2_WFIT: paired top-down pass with enough waves per workgroup that
-                                        // one pass covers every pivot row (each wave gathers x_upd once)
-  int split_target = 512;               // PFR_SOLVE_SPLIT: solve launches with fewer (front, group) workgroups
-                                        // split their update parts up to about this many workgroups (0: off)
+  int split_target = 256;               // PFR_SOLVE_SPLIT: solve launches with fewer (front, group) workgroups
+                                        // than this (one per CU) split their update parts up to about this
+                                        // many workgroups (0: off)
   int check_fused = 0;                  // PFR_CHECK_FUSED=1: loss sweeps check both solutions in one entry walk
   // backward-error checks (pfr_set_check): PFR_CHECK_* bits, tolerance, optional per-item output;
   // per-frequency maxima scratch, forward and adjoint (kept zero between checks)
@@ -411,9 +410,7 @@ int sym_top_down_pair(pfr_solver* s, hipStream_t st) {
   for (int l = L - 1; l >= 0; --l) {
     const int nf = s->level_ptr[l + 1] - s->level_ptr[l];
     const bool small = s->level_maxf[l] <= s->us2_small;
-    int W = solve_W(s, l, nf);
-    if (s->us2_wfit) W = std::max(W, std::min(8, (s->level_maxns[l] + (small ? 2 : 4) - 1) / (small ? 2 : 4)));
-    pfr::launch_usolve2(s->P, s->d_level_fronts + s->level_ptr[l], nf, W,
+    pfr::launch_usolve2(s->P, s->d_level_fronts + s->level_ptr[l], nf, solve_W(s, l, nf),
                         small, ngroups,
                         s->F, s->Fc, s->Y,
                         s->X, s->d_reach[0], s->d_reach[1], s->Y2, s->XA, s->d_reach[1], st, solve_split(s, nf));
@@ -641,8 +638,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->fac_wmax = knob("PFR_FAC_WMAX", 16, 1, 16);
   s->us2_small = knob("PFR_US2_SMALL", 110, 0, pfr::MAX_FRONT);
   s->off_small = knob("PFR_OFF_SMALL", 1, 0, 1);
-  s->split_target = knob("PFR_SOLVE_SPLIT", 512, 0, 1 << 20);
-  s->us2_wfit = knob("PFR_US2_WFIT", 0, 0, 1);
+  s->split_target = knob("PFR_SOLVE_SPLIT", 256, 0, 1 << 20);
   s->check_fused = knob("PFR_CHECK_FUSED", 0, 0, 1);   // measured 2.3 ms against 2 x 0.87 ms per 2,048-frequency chunk
   s->n = S.n;
   s->nnz = S.nnz;

@@ -1434,10 +1434,7 @@ struct UPair {
 // many tiny workgroups are latency-bound and occupancy, not per-wave reuse, hides it.
 // the pivot rows' update part of the paired pass: XV(v, a) = y_a + U(a, a) L21(:, a)^T x_upd for
 // a = a_begin, a_begin + a_step, ... (SR per step)
-// NP passes over the wave's pivot rows share each gathered update-row solution value (NP = 2: a wave
-// with two row groups gathers x_upd once, not twice; the gathers are otherwise half of the small-front
-// levels' traffic and miss L2, a pass outlasting the L2's turnover)
-template <bool SYM, int SR, int SK, int NP = 1>
+template <bool SYM, int SR, int SK>
 __device__ __forceinline__ void usolve2_upd(const Front& fr, const int* six, const cplx* __restrict__ base,
                                             int64_t Fc, int64_t q, const bool (&act)[2], const bool (&live)[2],
                                             const cplx* const (&Ys)[2], cplx* const (&Xs)[2], int a_begin, int a_step) {
@@ -1445,22 +1442,21 @@ __device__ __forceinline__ void usolve2_upd(const Front& fr, const int* six, con
   const Ctx c{0, 0, 0, q};
 #define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
 #define XV(v, a) Xs[v][(int64_t)(fr.col0 + (a)) * Fc + c.q]
-  for (int a0b = a_begin; a0b < ns; a0b += NP * a_step) {
-    int ra[NP][SR];
-    cplx acc[2][NP][SR];
-    const cplx* pu[NP][SR];
+  for (int a0 = a_begin; a0 < ns; a0 += a_step) {
+    int ra[SR];
+    cplx acc[2][SR];
+#pragma unroll
+    for (int r = 0; r < SR; ++r) {
+      ra[r] = min(a0 + r, ns - 1);
+      acc[0][r] = acc[1][r] = make_double2(0.0, 0.0);
+    }
+    const cplx* pu[SR];
+#pragma unroll
+    for (int r = 0; r < SR; ++r) pu[r] = base + (SYM ? (int64_t)ra[r] : (int64_t)ra[r] * f) * Fc;
     const int64_t su = SYM ? (int64_t)f * Fc : Fc;
-#pragma unroll
-    for (int p = 0; p < NP; ++p)
-#pragma unroll
-      for (int r = 0; r < SR; ++r) {
-        ra[p][r] = min(a0b + p * a_step + r, ns - 1);
-        acc[0][p][r] = acc[1][p][r] = make_double2(0.0, 0.0);
-        pu[p][r] = base + (SYM ? (int64_t)ra[p][r] : (int64_t)ra[p][r] * f) * Fc;
-      }
     for (int b0 = ns; b0 < f; b0 += SK) {
       int iv[SK];
-      cplx xv[2][SK], ev[NP][SR][SK];
+      cplx xv[2][SK], ev[SR][SK];
 #pragma unroll
       for (int u = 0; u < SK; ++u) iv[u] = __builtin_amdgcn_readfirstlane(six[min(b0 + u, f - 1)]);
 #pragma unroll
@@ -1468,13 +1464,11 @@ __device__ __forceinline__ void usolve2_upd(const Front& fr, const int* six, con
 #pragma unroll
         for (int u = 0; u < SK; ++u) xv[v][u] = Xs[v][(int64_t)iv[u] * Fc + c.q];   // inactive: unused
 #pragma unroll
-      for (int p = 0; p < NP; ++p)
+      for (int r = 0; r < SR; ++r)
 #pragma unroll
-        for (int r = 0; r < SR; ++r)
-#pragma unroll
-          for (int u = 0; u < SK; ++u) ev[p][r][u] = pu[p][r][min(b0 + u, f - 1) * su];
-      __builtin_amdgcn_sched_group_barrier(0x020, SK * (NP * SR + 2), 0);   // all vector loads first
-      __builtin_amdgcn_sched_group_barrier(0x002, 8 * SK * NP * SR + 16, 0);
+        for (int u = 0; u < SK; ++u) ev[r][u] = pu[r][min(b0 + u, f - 1) * su];
+      __builtin_amdgcn_sched_group_barrier(0x020, SK * (SR + 2), 0);   // all vector loads first
+      __builtin_amdgcn_sched_group_barrier(0x002, 8 * SK * SR + 16, 0);
 #pragma unroll
       for (int v = 0; v < 2; ++v)
 #pragma unroll
@@ -1483,94 +1477,9 @@ __device__ __forceinline__ void usolve2_upd(const Front& fr, const int* six, con
 #pragma unroll
       for (int v = 0; v < 2; ++v)
 #pragma unroll
-        for (int p = 0; p < NP; ++p)
-#pragma unroll
-          for (int r = 0; r < SR; ++r)
-#pragma unroll
-            for (int u = 0; u < SK; ++u) acc[v][p][r] = cfms(acc[v][p][r], ev[p][r][u], xv[v][u]);
-    }
-#pragma unroll
-    for (int p = 0; p < NP; ++p)
-#pragma unroll
-      for (int r = 0; r < SR; ++r) {
-        const int a = a0b + p * a_step + r;
-        if (a < ns) {
-          const cplx urr = SYM ? E(ra[p][r], ra[p][r]) : make_double2(1.0, 0.0);
-#pragma unroll
-          for (int v = 0; v < 2; ++v)
-            if (act[v]) {
-              const cplx y = live[v] ? Ys[v][(int64_t)(fr.col0 + a) * Fc + c.q] : make_double2(0.0, 0.0);
-              XV(v, a) = SYM ? cadd(y, cmul(urr, acc[v][p][r])) : cadd(y, acc[v][p][r]);
-            }
-        }
-      }
-  }
-#undef E
-#undef XV
-}
-
-// LDS-staged form of usolve2_upd for one workgroup (all waves): per pass over the pivot rows, the
-// update-row solution values x_upd of both vectors are gathered ONCE per workgroup into LDS in chunks of
-// US2_CH rows and every wave reads them from there (the plain form gathers them once per wave and pass).
-constexpr int US2_CH = 16;
-template <bool SYM, int SR, int SK>
-__device__ __forceinline__ void usolve2_upd_xs(const Front& fr, const int* six, const cplx* __restrict__ base,
-                                               int64_t Fc, int64_t q, const bool (&act)[2], const bool (&live)[2],
-                                               const cplx* const (&Ys)[2], cplx* const (&Xs)[2], int w, int W,
-                                               cplx* __restrict__ sx) {
-  const int f = fr.f, ns = fr.ns, lane = threadIdx.x & 63;
-  const Ctx c{0, 0, 0, q};
-#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
-#define XV(v, a) Xs[v][(int64_t)(fr.col0 + (a)) * Fc + c.q]
-  const int npass = (ns + SR * W - 1) / (SR * W);       // the same for every wave of the workgroup
-  const int64_t su = SYM ? (int64_t)f * Fc : Fc;
-  for (int p = 0; p < npass; ++p) {
-    const int a0 = SR * (w + p * W);
-    int ra[SR];
-    cplx acc[2][SR];
-    const cplx* pu[SR];
-#pragma unroll
-    for (int r = 0; r < SR; ++r) {
-      ra[r] = min(a0 + r, ns - 1);
-      acc[0][r] = acc[1][r] = make_double2(0.0, 0.0);
-      pu[r] = base + (SYM ? (int64_t)ra[r] : (int64_t)ra[r] * f) * Fc;
-    }
-    for (int c0 = ns; c0 < f; c0 += US2_CH) {
-      // stage rows c0 .. c0 + US2_CH - 1 of both vectors, 4 row loads per wave and round (clamped rows
-      // past the front are loaded but never read)
-      for (int t0 = 4 * w; t0 < 2 * US2_CH; t0 += 4 * W) {
-        cplx tmp[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int t = min(t0 + u, 2 * US2_CH - 1), v = t / US2_CH, b = t % US2_CH;
-          const int row = __builtin_amdgcn_readfirstlane(six[min(c0 + b, f - 1)]);
-          tmp[u] = Xs[v][(int64_t)row * Fc + c.q];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (t0 + u < 2 * US2_CH) sx[(t0 + u) * 64 + lane] = tmp[u];
-      }
-      __syncthreads();
-      const int nch = min(US2_CH, f - c0);
-      for (int b0 = 0; b0 < nch; b0 += SK) {
-        cplx xv[2][SK], ev[SR][SK];
-#pragma unroll
         for (int r = 0; r < SR; ++r)
 #pragma unroll
-          for (int u = 0; u < SK; ++u) ev[r][u] = pu[r][min(c0 + b0 + u, f - 1) * su];
-#pragma unroll
-        for (int v = 0; v < 2; ++v)
-#pragma unroll
-          for (int u = 0; u < SK; ++u)
-            xv[v][u] = cscale(sx[(v * US2_CH + min(b0 + u, US2_CH - 1)) * 64 + lane], b0 + u < nch ? 1.0 : 0.0);
-#pragma unroll
-        for (int v = 0; v < 2; ++v)
-#pragma unroll
-          for (int r = 0; r < SR; ++r)
-#pragma unroll
-            for (int u = 0; u < SK; ++u) acc[v][r] = cfms(acc[v][r], ev[r][u], xv[v][u]);
-      }
-      __syncthreads();
+          for (int u = 0; u < SK; ++u) acc[v][r] = cfms(acc[v][r], ev[r][u], xv[v][u]);
     }
 #pragma unroll
     for (int r = 0; r < SR; ++r)
@@ -1588,7 +1497,7 @@ __device__ __forceinline__ void usolve2_upd_xs(const Front& fr, const int* six, 
 #undef XV
 }
 
-template <bool SYM, int SR, int SK, int WPE, int NP = 1, bool XS = false>
+template <bool SYM, int SR, int SK, int WPE>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void k_usolve2_level(
     DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc, UPair A, UPair B, int upd_done) {
   int bx;
@@ -1605,12 +1514,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
   if (!upd_done) {
     for (int a = threadIdx.x; a < f; a += blockDim.x) six[a] = P.idx[fr.row0 + a];
     __syncthreads();
-    if (XS) {
-      __shared__ cplx sx[2 * US2_CH * 64];
-      usolve2_upd_xs<SYM, SR, SK>(fr, six, base, Fc, c.q, act, live, Ys, Xs, c.w, c.W, sx);
-    } else {
-      usolve2_upd<SYM, SR, SK, NP>(fr, six, base, Fc, c.q, act, live, Ys, Xs, SR * c.w, SR * c.W);
-    }
+    usolve2_upd<SYM, SR, SK>(fr, six, base, Fc, c.q, act, live, Ys, Xs, SR * c.w, SR * c.W);
   }
   __syncthreads();
 #define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
@@ -2657,18 +2561,7 @@ void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, boo
   if (rs) LAUNCH((k_usolve2_upd<true, 2, 4>), dim3(nfronts * split, ngroups), dim3(64 * SPLIT_W), st, P, lvl, F, Fc, a, b,
                  split);
   // symmetric mode only (the paired top-down pass serves the symmetric loss + gradient sweep)
-  static const int np = [] {
-    const char* e = getenv("PFR_US2_NP");   // tuning knob: row-group passes sharing each x_upd gather (1, 2)
-    return e ? atoi(e) : 1;
-  }();
-  static const int xs = [] {
-    const char* e = getenv("PFR_US2_XS");   // tuning knob: x_upd staged in LDS once per workgroup and pass
-    return e ? atoi(e) : 0;
-  }();
-  if (small && xs) LAUNCH((k_usolve2_level<true, 2, 4, 4, 1, true>), g, bl, st, P, lvl, F, Fc, a, b, rs);
-  else if (!small && xs) LAUNCH((k_usolve2_level<true, 4, 8, 2, 1, true>), g, bl, st, P, lvl, F, Fc, a, b, rs);
-  else if (small && np == 2) LAUNCH((k_usolve2_level<true, 2, 4, 3, 2>), g, bl, st, P, lvl, F, Fc, a, b, rs);
-  else if (small) LAUNCH((k_usolve2_level<true, 2, 4, 4>), g, bl, st, P, lvl, F, Fc, a, b, rs);
+  if (small) LAUNCH((k_usolve2_level<true, 2, 4, 4>), g, bl, st, P, lvl, F, Fc, a, b, rs);
   else LAUNCH((k_usolve2_level<true, 4, 8, 2>), g, bl, st, P, lvl, F, Fc, a, b, rs);
 }
 
