@@ -163,6 +163,8 @@ struct pfr_solver {
   // with its low-register small-front variant)
   int solve_wmax = 8, fac_wmax = 16, us2_small = 110;
   int off_small = 1;                    // PFR_OFF_SMALL: no-prefix off-diagonal variant on levels of ns <= 8
+  int fac_lds = 0;                      // PFR_FAC_LDS: levels whose largest pivot block has at least this many
+                                        // pivots factor A11 in LDS (k_factor_sym_lds; 0: never)
   int split_target = 256;               // PFR_SOLVE_SPLIT: solve launches with fewer (front, group) workgroups
                                         // than this (one per CU) split their update parts up to about this
                                         // many workgroups (0: off)
@@ -292,7 +294,10 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     const int64_t wfill = (4096 + wgs - 1) / wgs;
     const int Wp = (int)std::max<int64_t>(
         1, s->sym ? std::min<int64_t>(fac_wmax, wfill) : std::min<int64_t>(s->level_W[l], wfill));
-    pfr::launch_factor(s->sym, s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st);
+    if (s->sym && s->fac_lds > 0 && s->level_maxns[l] >= s->fac_lds)
+      pfr::launch_factor_lds(s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_maxns[l], s->F, s->Fc, s->flags, st);
+    else
+      pfr::launch_factor(s->sym, s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st);
     mark(l, 2);
     pfr::launch_offdiag(mode, s->P, s->d_items + s->item_ptr[l], s->item_ptr[l + 1] - s->item_ptr[l], s->d_orec,
                         s->d_oxp + s->item_ptr[l], s->d_ox, ngroups, s->F, s->Fc, s->freqs, s->K, s->M, data, ds,
@@ -639,6 +644,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->us2_small = knob("PFR_US2_SMALL", 110, 0, pfr::MAX_FRONT);
   s->off_small = knob("PFR_OFF_SMALL", 1, 0, 1);
   s->split_target = knob("PFR_SOLVE_SPLIT", 256, 0, 1 << 20);
+  s->fac_lds = knob("PFR_FAC_LDS", 0, 0, 64);   // LDS holds the lower triangle of up to 64 pivots x 4 frequencies
   s->check_fused = knob("PFR_CHECK_FUSED", 0, 0, 1);   // measured 2.3 ms against 2 x 0.87 ms per 2,048-frequency chunk
   s->n = S.n;
   s->nnz = S.nnz;

@@ -504,6 +504,113 @@ __global__ __launch_bounds__(PFR_FAC_LB) void k_factor_sym(DevPattern P, const i
 #undef E
 }
 
+// Symmetric A11 LU with the pivot block resident in LDS, for the levels of large pivot blocks (the
+// top of the elimination tree: few fronts, long pivot chains).  Workgroup = one front x QF consecutive
+// frequencies (QF = 4: a 64 B piece of each 128 B line; the workgroups of the two halves of a line are
+// neighbours in dispatch order, i.e. on the same XCD at the same time, so the line is fetched once);
+// the lower triangle of A11 (packed, idx(i, j) = i (i + 1) / 2 + j) is read once into LDS, factored
+// there in 4-pivot blocks (diagonal block, panel rows, trailing update of the lower triangle), and
+// written once: L11 below the diagonal, U11 = diag(U) L11^T above it, U(k, k) on it -- the same
+// entries k_factor_sym writes.  Thread t = (slot t / QF, frequency t % QF).
+__device__ __forceinline__ int tri_row(int e) {
+  int i = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+  if ((i + 1) * (i + 2) / 2 <= e) ++i;
+  else if (i * (i + 1) / 2 > e) --i;
+  return i;
+}
+
+template <int QF>
+__global__ __launch_bounds__(256) void k_factor_sym_lds(DevPattern P, const int* __restrict__ lvl,
+                                                        cplx* __restrict__ F, int64_t Fc, int* __restrict__ flags) {
+  extern __shared__ cplx sA[];
+  const int ngq = (int)(Fc / QF);
+  const int64_t lid = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int slot = (int)(lid / ngq), qg = (int)(lid % ngq);
+  const Front fr = P.fronts[lvl[slot]];
+  const int f = fr.f, ns = fr.ns;
+  const int qq = threadIdx.x % QF, s = threadIdx.x / QF, S = blockDim.x / QF;
+  const int64_t q = (int64_t)qg * QF + qq;
+  cplx* __restrict__ base = F + fr.off * Fc + q;
+  const int nlow = ns * (ns + 1) / 2;
+#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+#define A(i, j) sA[(((i) * ((i) + 1)) / 2 + (j)) * QF + qq]
+  for (int e = s; e < nlow; e += S) {
+    const int i = tri_row(e), j = e - i * (i + 1) / 2;
+    sA[e * QF + qq] = E(i, j);
+  }
+  __syncthreads();
+  for (int k0 = 0; k0 < ns; k0 += KB) {
+    const int kb = min(KB, ns - k0), k1 = k0 + kb;
+    if (s == 0) {
+      // diagonal block: L D L^T of the kb x kb lower triangle, in registers
+      cplx D[KB][KB];
+#pragma unroll
+      for (int i = 0; i < KB; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j) D[i][j] = i < kb ? A(k0 + i, k0 + j) : make_double2(0.0, 0.0);
+#pragma unroll
+      for (int k = 0; k < KB; ++k)
+        if (k < kb) {
+          pivot_check(D[k][k], flags, q);
+          const cplx inv = crecip(D[k][k]);
+#pragma unroll
+          for (int i = k + 1; i < KB; ++i)
+            if (i < kb) {
+              const cplx lik = cmul(D[i][k], inv);
+#pragma unroll
+              for (int j = k + 1; j <= i; ++j) D[i][j] = cfms(D[i][j], lik, D[j][k]);   // D[j][k] still U-scaled
+            }
+#pragma unroll
+          for (int i = k + 1; i < KB; ++i)
+            if (i < kb) D[i][k] = cmul(D[i][k], inv);
+        }
+#pragma unroll
+      for (int i = 0; i < KB; ++i)
+#pragma unroll
+        for (int j = 0; j <= i; ++j)
+          if (i < kb) A(k0 + i, k0 + j) = D[i][j];
+    }
+    __syncthreads();
+    // panel rows: L(i, k0 + t) = (A(i, k0 + t) - sum_{u < t} L(i, k0 + u) U(k0 + u, k0 + t)) / U(k0 + t, k0 + t),
+    // U(u, t) = U(u, u) L(t, u)
+    for (int i = k1 + s; i < ns; i += S) {
+      cplx l[KB];
+#pragma unroll
+      for (int t = 0; t < KB; ++t) l[t] = t < kb ? A(i, k0 + t) : make_double2(0.0, 0.0);
+#pragma unroll
+      for (int t = 0; t < KB; ++t)
+        if (t < kb) {
+#pragma unroll
+          for (int u = 0; u < t; ++u) l[t] = cfms(l[t], l[u], cmul(A(k0 + u, k0 + u), A(k0 + t, k0 + u)));
+          l[t] = cmul(l[t], crecip(A(k0 + t, k0 + t)));
+          A(i, k0 + t) = l[t];
+        }
+    }
+    __syncthreads();
+    // trailing lower triangle: A(i, j) -= sum_t L(i, k0 + t) U(k0 + t, k0 + t) L(j, k0 + t), k1 <= j <= i
+    const int nt = ns - k1, ntl = nt * (nt + 1) / 2;
+    for (int e = s; e < ntl; e += S) {
+      const int ii = tri_row(e), jj = e - ii * (ii + 1) / 2;
+      const int i = k1 + ii, j = k1 + jj;
+      cplx v = A(i, j);
+#pragma unroll
+      for (int t = 0; t < KB; ++t)
+        if (t < kb) v = cfms(v, A(i, k0 + t), cmul(A(k0 + t, k0 + t), A(j, k0 + t)));
+      A(i, j) = v;
+    }
+    __syncthreads();
+  }
+  // write back: L below the diagonal, U(k, k) on it, U(j, i) = U(j, j) L(i, j) above it
+  for (int e = s; e < nlow; e += S) {
+    const int i = tri_row(e), j = e - i * (i + 1) / 2;
+    const cplx v = sA[e * QF + qq];
+    E(i, j) = v;
+    if (j < i) E(j, i) = cmul(A(j, j), v);
+  }
+#undef A
+#undef E
+}
+
 // Off-diagonal panel blocks once A11 = L11 U11 is factored, every row of L21 and
 // every column of U12 independently (read once, written once):
 //   kind 0, row i >= ns:     L(i, :ns) = A(i, :ns) U11^{-1}
@@ -2441,6 +2548,7 @@ __global__ void k_matvec(const int* __restrict__ colptr, const int* __restrict__
 
 // ================================================================== launchers
 #define LAUNCH(kern, grid, block, st, ...) hipLaunchKernelGGL(kern, grid, block, 0, st, __VA_ARGS__)
+#define LAUNCH_DYN(kern, grid, block, lds, st, ...) hipLaunchKernelGGL(kern, grid, block, lds, st, __VA_ARGS__)
 
 void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPack& coef, double2* K, hipStream_t st) {
   LAUNCH(k_combine, dim3((unsigned)((nnz + 255) / 256)), dim3(256), st, stiff, n_stiff, nnz, coef, K);
@@ -2485,6 +2593,18 @@ void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, cons
   dim3 g((nrec / 8 + 3) / 4, ngroups), b(256);
   if (mode == 0) LAUNCH(k_assemble_level<0>, g, b, st, recs, nrec, xptr, xl, F, Fc, freqs, K, M, data, ds, nvalid);
   else LAUNCH(k_assemble_level<1>, g, b, st, recs, nrec, xptr, xl, F, Fc, freqs, K, M, data, ds, nvalid);
+}
+
+void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int maxns, double2* F, int64_t Fc, int* flags,
+                       hipStream_t st) {
+  constexpr int QF = 4;
+  const size_t lds = (size_t)maxns * (maxns + 1) / 2 * QF * sizeof(double2);
+  static const bool attr = [] {   // dynamic LDS beyond the default 64 KiB (up to 64 pivots: 130 KiB)
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_factor_sym_lds<QF>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+  }();
+  (void)attr;
+  LAUNCH_DYN(k_factor_sym_lds<QF>, dim3((unsigned)(nfronts * (Fc / QF))), dim3(256), lds, st, P, lvl, F, Fc, flags);
 }
 
 void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F,

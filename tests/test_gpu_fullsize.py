@@ -157,6 +157,7 @@ def test_c2_forward_sweep_matches_truth():
     {"PFR_OFF_SMALL": "0"},
     {"PFR_SOLVE_SPLIT": "0"},          # every solve launch unsplit (the small meshes split by default)
     {"PFR_SOLVE_SPLIT": "1000000"},    # every solve launch split 16 ways
+    {"PFR_FAC_LDS": "1"},              # every level's A11 LU through the LDS-resident kernel
 ])
 def test_kernel_variants_match_oracle(env, monkeypatch):
     from oracle.plate_oracle import loss_and_grad
