@@ -15,6 +15,7 @@ import argparse
 import gc
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -25,7 +26,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 
-def measure(n_rank, steps, warmup, ny, lanes=None):
+def measure(n_rank, steps, warmup, ny, lanes=None, spread=False):
     import bench
     from plate_inverse_problem_amd.distributed import shard_range
     if lanes is not None:
@@ -36,7 +37,7 @@ def measure(n_rank, steps, warmup, ny, lanes=None):
     world = 4096 // n_rank
     freqs_all = np.linspace(40.0, 600.0, 4096)
     lo, hi = shard_range(4096, 0, world)
-    freqs = freqs_all[lo:hi]
+    freqs = np.linspace(40.0, 600.0, n_rank) if spread else freqs_all[lo:hi]
     ref = prob.solveForward(freqs, theta_true)
     loss_fn = prob.getLossFunction(freqs, ref, "MSE_LOG_AFC")
 
@@ -69,13 +70,26 @@ def main():
     ap.add_argument("--ny", type=int, default=25)
     ap.add_argument("--sizes", default="4096,2048,1024,512")
     ap.add_argument("--lanes", default="", help="comma list of lane counts to try per size (default: engine's)")
+    ap.add_argument("--spread", action="store_true", help="n frequencies over the whole band instead of rank 0's block")
+    ap.add_argument("--one", type=int, nargs=2, default=None, metavar=("N", "LANES"),
+                    help="measure one size in this process (LANES 0: the engine's choice) and print its JSON")
     a = ap.parse_args()
-    torch.cuda.set_device(0)
+    if a.one is not None:
+        torch.cuda.set_device(0)
+        print(json.dumps(measure(a.one[0], a.steps, a.warmup, a.ny, a.one[1] or None, a.spread)), flush=True)
+        return
+    # every size in a fresh process, as every rank is (an engine built after a larger one was freed in the
+    # same process measured up to 12 % slower)
     rows = []
-    lanes_list = [int(v) for v in a.lanes.split(",") if v] or [None]
+    lanes_list = [int(v) for v in a.lanes.split(",") if v] or [0]
     for n in [int(v) for v in a.sizes.split(",")]:
         for ln in lanes_list:
-            r = measure(n, a.steps, a.warmup, a.ny, ln)
+            cmd = [sys.executable, os.path.abspath(__file__), "--one", str(n), str(ln), "--steps", str(a.steps),
+                   "--warmup", str(a.warmup), "--ny", str(a.ny)] + (["--spread"] if a.spread else [])
+            res = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, timeout=600)
+            if res.returncode != 0:
+                sys.exit(res.returncode)
+            r = json.loads(res.stdout.strip().splitlines()[-1])
             rows.append(r)
             print(json.dumps(r), flush=True)
     base = {}
