@@ -513,7 +513,7 @@ __global__ __launch_bounds__(PFR_FAC_LB) void k_factor_sym(DevPattern P, const i
 // written once: L11 below the diagonal, U11 = diag(U) L11^T above it, U(k, k) on it -- the same
 // entries k_factor_sym writes.  Thread t = (slot t / QF, frequency t % QF).
 __device__ __forceinline__ int tri_row(int e) {
-  int i = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+  int i = (int)((sqrtf(8.0f * e + 1.0f) - 1.0f) * 0.5f);
   if ((i + 1) * (i + 2) / 2 <= e) ++i;
   else if (i * (i + 1) / 2 > e) --i;
   return i;
@@ -521,8 +521,10 @@ __device__ __forceinline__ int tri_row(int e) {
 
 template <int QF>
 __global__ __launch_bounds__(256) void k_factor_sym_lds(DevPattern P, const int* __restrict__ lvl,
-                                                        cplx* __restrict__ F, int64_t Fc, int* __restrict__ flags) {
+                                                        cplx* __restrict__ F, int64_t Fc, int* __restrict__ flags,
+                                                        int maxns) {
   extern __shared__ cplx sA[];
+  cplx* __restrict__ sW = sA + (int64_t)maxns * (maxns + 1) / 2 * QF;   // W(i, t) = U(k0 + t, k0 + t) L(i, k0 + t)
   const int ngq = (int)(Fc / QF);
   const int64_t lid = xcd_swizzle(blockIdx.x, gridDim.x);
   const int slot = (int)(lid / ngq), qg = (int)(lid % ngq);
@@ -534,9 +536,20 @@ __global__ __launch_bounds__(256) void k_factor_sym_lds(DevPattern P, const int*
   const int nlow = ns * (ns + 1) / 2;
 #define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
 #define A(i, j) sA[(((i) * ((i) + 1)) / 2 + (j)) * QF + qq]
-  for (int e = s; e < nlow; e += S) {
-    const int i = tri_row(e), j = e - i * (i + 1) / 2;
-    sA[e * QF + qq] = E(i, j);
+#define W(i, t) sW[((i) * KB + (t)) * QF + qq]
+  // UB loads in flight per thread before their LDS stores (a plain loop waits for every load)
+  constexpr int UB = 8;
+  for (int e0 = s; e0 < nlow; e0 += UB * S) {
+    cplx v[UB];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int e = min(e0 + u * S, nlow - 1);
+      const int i = tri_row(e), j = e - i * (i + 1) / 2;
+      v[u] = E(i, j);
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u)
+      if (e0 + u * S < nlow) sA[(e0 + u * S) * QF + qq] = v[u];
   }
   __syncthreads();
   for (int k0 = 0; k0 < ns; k0 += KB) {
@@ -572,30 +585,33 @@ __global__ __launch_bounds__(256) void k_factor_sym_lds(DevPattern P, const int*
     }
     __syncthreads();
     // panel rows: L(i, k0 + t) = (A(i, k0 + t) - sum_{u < t} L(i, k0 + u) U(k0 + u, k0 + t)) / U(k0 + t, k0 + t),
-    // U(u, t) = U(u, u) L(t, u)
+    // U(u, t) = U(u, u) L(t, u); W(i, t) = U(k0 + t, k0 + t) L(i, k0 + t) for the trailing update
     for (int i = k1 + s; i < ns; i += S) {
-      cplx l[KB];
+      cplx l[KB], d[KB];
 #pragma unroll
-      for (int t = 0; t < KB; ++t) l[t] = t < kb ? A(i, k0 + t) : make_double2(0.0, 0.0);
+      for (int t = 0; t < KB; ++t) {
+        l[t] = t < kb ? A(i, k0 + t) : make_double2(0.0, 0.0);
+        d[t] = A(k0 + min(t, kb - 1), k0 + min(t, kb - 1));
+      }
 #pragma unroll
       for (int t = 0; t < KB; ++t)
         if (t < kb) {
 #pragma unroll
-          for (int u = 0; u < t; ++u) l[t] = cfms(l[t], l[u], cmul(A(k0 + u, k0 + u), A(k0 + t, k0 + u)));
-          l[t] = cmul(l[t], crecip(A(k0 + t, k0 + t)));
+          for (int u = 0; u < t; ++u) l[t] = cfms(l[t], l[u], cmul(d[u], A(k0 + t, k0 + u)));
+          l[t] = cmul(l[t], crecip(d[t]));
           A(i, k0 + t) = l[t];
+          W(i, t) = cmul(d[t], l[t]);
         }
     }
     __syncthreads();
-    // trailing lower triangle: A(i, j) -= sum_t L(i, k0 + t) U(k0 + t, k0 + t) L(j, k0 + t), k1 <= j <= i
+    // trailing lower triangle: A(i, j) -= sum_t L(i, k0 + t) W(j, t), k1 <= j <= i
     const int nt = ns - k1, ntl = nt * (nt + 1) / 2;
     for (int e = s; e < ntl; e += S) {
-      const int ii = tri_row(e), jj = e - ii * (ii + 1) / 2;
-      const int i = k1 + ii, j = k1 + jj;
+      const int ii = tri_row(e), i = k1 + ii, j = k1 + e - ii * (ii + 1) / 2;
       cplx v = A(i, j);
 #pragma unroll
       for (int t = 0; t < KB; ++t)
-        if (t < kb) v = cfms(v, A(i, k0 + t), cmul(A(k0 + t, k0 + t), A(j, k0 + t)));
+        if (t < kb) v = cfms(v, A(i, k0 + t), W(j, t));
       A(i, j) = v;
     }
     __syncthreads();
@@ -607,6 +623,7 @@ __global__ __launch_bounds__(256) void k_factor_sym_lds(DevPattern P, const int*
     E(i, j) = v;
     if (j < i) E(j, i) = cmul(A(j, j), v);
   }
+#undef W
 #undef A
 #undef E
 }
@@ -2595,16 +2612,24 @@ void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, cons
   else LAUNCH(k_assemble_level<1>, g, b, st, recs, nrec, xptr, xl, F, Fc, freqs, K, M, data, ds, nvalid);
 }
 
-void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int maxns, double2* F, int64_t Fc, int* flags,
-                       hipStream_t st) {
-  constexpr int QF = 4;
-  const size_t lds = (size_t)maxns * (maxns + 1) / 2 * QF * sizeof(double2);
-  static const bool attr = [] {   // dynamic LDS beyond the default 64 KiB (up to 64 pivots: 130 KiB)
+template <int QF>
+static void launch_factor_lds_q(const DevPattern& P, const int* lvl, int nfronts, int maxns, double2* F, int64_t Fc,
+                                int* flags, hipStream_t st) {
+  const size_t lds = ((size_t)maxns * (maxns + 1) / 2 + (size_t)maxns * KB) * QF * sizeof(double2);
+  static const bool attr = [] {   // dynamic LDS beyond the default 64 KiB (up to 64 pivots x 4 frequencies: 146 KiB)
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_factor_sym_lds<QF>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   }();
   (void)attr;
-  LAUNCH_DYN(k_factor_sym_lds<QF>, dim3((unsigned)(nfronts * (Fc / QF))), dim3(256), lds, st, P, lvl, F, Fc, flags);
+  LAUNCH_DYN(k_factor_sym_lds<QF>, dim3((unsigned)(nfronts * (Fc / QF))), dim3(256), lds, st, P, lvl, F, Fc, flags,
+             maxns);
+}
+
+void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int maxns, int qf, double2* F, int64_t Fc,
+                       int* flags, hipStream_t st) {
+  if (qf == 1) launch_factor_lds_q<1>(P, lvl, nfronts, maxns, F, Fc, flags, st);
+  else if (qf == 2) launch_factor_lds_q<2>(P, lvl, nfronts, maxns, F, Fc, flags, st);
+  else launch_factor_lds_q<4>(P, lvl, nfronts, maxns, F, Fc, flags, st);
 }
 
 void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F,

@@ -36,10 +36,10 @@ void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, cons
                      int64_t ds, int nvalid, hipStream_t st);
 void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F, int64_t Fc,
                    int* flags, hipStream_t st);
-// symmetric A11 LU with the pivot block in LDS (one front x 4 frequencies per workgroup); maxns = the
-// level's largest pivot block (sizes the dynamic LDS: maxns (maxns + 1) / 2 x 64 B)
-void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int maxns, double2* F, int64_t Fc, int* flags,
-                       hipStream_t st);
+// symmetric A11 LU with the pivot block in LDS (one front x qf = 2 or 4 frequencies per workgroup); maxns =
+// the level's largest pivot block (sizes the dynamic LDS: (maxns (maxns + 1) / 2 + 4 maxns) x 16 qf B)
+void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int maxns, int qf, double2* F, int64_t Fc,
+                       int* flags, hipStream_t st);
 // Schur complement A22 -= L21 U12 for a level's tile list (TM x TN = 4 x 4 tiles)
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
                     const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,

@@ -157,7 +157,9 @@ def test_c2_forward_sweep_matches_truth():
     {"PFR_OFF_SMALL": "0"},
     {"PFR_SOLVE_SPLIT": "0"},          # every solve launch unsplit (the small meshes split by default)
     {"PFR_SOLVE_SPLIT": "1000000"},    # every solve launch split 16 ways
-    {"PFR_FAC_LDS": "1"},              # every level's A11 LU through the LDS-resident kernel
+    {"PFR_FAC_LDS": "1"},              # every level's A11 LU through the LDS-resident kernel (1 frequency / workgroup)
+    {"PFR_FAC_LDS": "1", "PFR_FAC_LDS_QF": "4"},   # ... 4 frequencies per workgroup
+    {"PFR_FAC_LDS": "-1"},             # auto: the levels where k_factor_sym would get few workgroups
 ])
 def test_kernel_variants_match_oracle(env, monkeypatch):
     from oracle.plate_oracle import loss_and_grad
@@ -208,6 +210,8 @@ def test_engine_grows_after_small_first_call():
     fr = p.solveForward(freqs)
     eng = p.engine()
     assert eng.n_lanes == 2 and eng.max_batch >= 2048
-    assert np.array_equal(fr[:32], small) or _rel(fr[:32], small) < 1e-13
+    # with PFR_FAC_LDS=-1 the A11 kernel of a level depends on the chunk (the top levels of small chunks
+    # factor in LDS, k_factor_sym_lds): the same frequencies then agree to rounding (measured 6e-12)
+    assert _rel(fr[:32], small) < 1e-10
     p.solveForward(freqs[:100])                     # smaller again: no rebuild
     assert p.engine() is eng and eng.max_batch >= 2048

@@ -12,6 +12,7 @@
 #   bash tools/gpu.sh trace   OUT F [ENV=V ...]       kernel trace of one lanes=1 step of F frequencies in one
 #                                                     chunk + per-level times (tools/level_times.py)
 #   bash tools/gpu.sh env     OUT "ENV=V ..." ...     kernel-class times of one isolated chunk per setting
+#                                                     (FREQS frequencies, STEPS timed steps)
 #   bash tools/gpu.sh strong  OUT                     1-GPU strong-scaling proxy (tools/strong_proxy.py)
 #   bash tools/gpu.sh round   R                       round measurement: tests, traffic (-> profiles/R),
 #                                                     bench, stats, C5, strong proxy
@@ -63,7 +64,7 @@ envs() {
   local i=0 cfg
   for cfg in "$@"; do
     i=$((i + 1))
-    env $cfg timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --steps 3 --freqs "${FREQS:-2048}" \
+    env $cfg timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --steps "${STEPS:-3}" --freqs "${FREQS:-2048}" \
       > "$O/e$i.json" 2> "$O/e$i.err" || { tail -5 "$O/e$i.err"; return 1; }
     python3 -c "import json;d=json.load(open('$O/e$i.json'));f=d['factor_roofline'];p=d['phase_ms'];print('$cfg |', round(d['value']), [round(x,2) for x in f['ms']], {k:round(v,2) for k,v in p.items() if k!='note'})"
   done
