@@ -1,7 +1,8 @@
 """Per-level durations (ms) of every factorisation / solve kernel in the LAST sweep of a
 rocprofv3 --kernel-trace CSV (lanes = 1 runs: the bench's isolated sweep comes last).
 
-Usage: python tools/level_times.py gpurun_out/<dir>/run_kernel_trace.csv [n_levels=17]
+Usage: python tools/level_times.py gpurun_out/<dir>/run_kernel_trace.csv [n_levels=17] [--gaps]
+(--gaps: per sweep, every idle gap above 10 us between consecutive kernels, with its neighbours)
 """
 import csv
 import sys
@@ -42,7 +43,17 @@ def main(path, L=17):
         gap = (t0 - spans[k - 1][1]) / 1e6 if k else float("nan")
         print("sweep %2d: span %7.3f ms  busy %7.3f ms  kernels %4d  idle before %7.3f ms"
               % (k, (t1 - t0) / 1e6, busy / 1e6, nk, gap))
+        if GAPS:
+            a = pads[k]
+            b = pads[k + 1] if k + 1 < len(pads) else len(rows)
+            for i in range(a + 1, b):
+                g = (int(rows[i]["Start_Timestamp"]) - int(rows[i - 1]["End_Timestamp"])) / 1e3
+                if g > 10:
+                    print("    gap %8.1f us  %-24s -> %s" % (g, names[i - 1][:24], names[i][:24]))
 
+
+GAPS = "--gaps" in sys.argv
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 17)
+    args = [a for a in sys.argv[1:] if a != "--gaps"]
+    main(args[0], int(args[1]) if len(args) > 1 else 17)
