@@ -243,12 +243,12 @@ class _Engine:
         (~9 ms) after the first and finished that much later."""
         cur = torch.cuda.current_stream(self.device)
         jobs = []
-        for sv, st, (lo, hi) in zip(self.solvers, self.streams, self._split(n)):
-            if hi <= lo:
-                continue
+        spans = [(sv, st, lo, hi) for sv, st, (lo, hi) in zip(self.solvers, self.streams, self._split(n)) if hi > lo]
+        for sv, st, lo, hi in spans:
             # the lane's accumulation buffers are zero-filled on the current stream BEFORE the lane
-            # stream is ordered after it (k_reduce accumulates into them with +=)
-            bufs = [None if a is None else torch.zeros_like(a) for a in accum]
+            # stream is ordered after it (k_reduce accumulates into them with +=); one lane accumulates
+            # straight into the given tensors
+            bufs = list(accum) if len(spans) == 1 else [None if a is None else torch.zeros_like(a) for a in accum]
             st.wait_stream(cur)
             jobs.append((sv, st, lo, hi, bufs))
 
@@ -280,7 +280,7 @@ class _Engine:
             raise err
         for _, st, _, _, bufs in jobs:
             for a, b in zip(accum, bufs):
-                if a is not None:
+                if a is not None and b is not a:
                     a.add_(b)
 
     def sweep(self, freqs, loss_type=_native.LOSS_NONE, ref=None, scale=1.0, fr=None, loss=None, w=None,
@@ -373,12 +373,15 @@ class _SweepLoss(torch.autograd.Function):
         engine.sweep(freqs, loss_id, ref=torch.view_as_real(ref), scale=1.0 / n_total,
                      loss=loss, w=torch.view_as_real(w), flags=flags, berr=berr)
         engine.last_berr = berr
-        engine.last_flags = _check_flags(flags)
         packed = torch.cat([loss.to(torch.complex128), engine.expand(w)])
         if reduce_fn is not None:
             packed = reduce_fn(packed)
-        ctx.save_for_backward(packed[1:].cpu())
-        return (packed[0].real / n_total).cpu()
+        # one device->host copy per step: loss, gradient partials and the number of flagged frequencies
+        # (the flags themselves are copied only when some are set)
+        host = torch.cat([packed, torch.count_nonzero(flags).to(torch.complex128).reshape(1)]).cpu()
+        engine.last_flags = _check_flags(flags) if host[-1].real != 0 else np.zeros(flags.numel(), np.int32)
+        ctx.save_for_backward(host[1:-1])
+        return host[0].real / n_total
 
     @staticmethod
     def backward(ctx, g):
