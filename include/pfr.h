@@ -60,8 +60,10 @@ typedef struct pfr_symbolic pfr_symbolic;
 typedef struct pfr_solver pfr_solver;
 
 typedef struct pfr_symbolic_options {
-  int32_t leaf_size;   /* nested-dissection leaf size (default 96) */
-  int32_t ordering;    /* 0 nested dissection (default), 1 natural */
+  int32_t leaf_size;   /* nested-dissection leaf size (default 10000): parts at or below it are
+                        * ordered by multiple minimum degree */
+  int32_t ordering;    /* 0 nested dissection + multiple-minimum-degree leaves (default), 1 natural,
+                        * 2 nested dissection + exact minimum-degree leaves (the round 1-3 ordering) */
   int32_t relax_small, relax_mid, relax_big; /* supernode amalgamation (4, 8, 24) */
   double zrelax_mid, zrelax_big;             /* (0.5, 0.1) */
   /* 1: symmetric-structure analysis (default 0).  The caller guarantees that the matrices
@@ -78,6 +80,8 @@ typedef struct pfr_symbolic_options {
   const int32_t* last;
   int32_t max_ns;      /* fundamental supernodes split into pieces of at most max_ns pivots (default 256;
                         * 0 = no split) */
+  int32_t md_delta;    /* multiple minimum degree: each stage eliminates an independent set of the
+                        * nodes of external degree <= minimum + md_delta (default 4) */
 } pfr_symbolic_options;
 
 typedef struct pfr_symbolic_stats {

@@ -98,14 +98,15 @@ class _Engine:
         # (checked on the values): only L is formed, U = diag(U) L^T
         self.symmetric = bool(symmetric) and decoupled_symmetric(rows, cols, vals, n)
         # tuning knobs of the symbolic analysis (defaults in include/pfr.h): PFR_LEAF_SIZE,
-        # PFR_RELAX="small,mid,big" (supernode amalgamation pivot limits), PFR_MAX_NS
-        leaf = os.environ.get("PFR_LEAF_SIZE")
-        relax = os.environ.get("PFR_RELAX")
-        max_ns = os.environ.get("PFR_MAX_NS")
+        # PFR_RELAX="small,mid,big" (supernode amalgamation pivot limits), PFR_MAX_NS, PFR_MD_DELTA,
+        # PFR_ORDERING (2: the exact-minimum-degree leaves of rounds 1-3, for A/B runs)
+        env = lambda k: os.environ.get(k)  # noqa: E731
         self.sym = _native.Symbolic(n, colptr, rows.astype(np.int32), symmetric=self.symmetric,
-                                    leaf_size=int(leaf) if leaf else None,
-                                    relax=tuple(int(v) for v in relax.split(",")) if relax else None,
-                                    max_ns=int(max_ns) if max_ns else None)
+                                    leaf_size=int(env("PFR_LEAF_SIZE")) if env("PFR_LEAF_SIZE") else None,
+                                    ordering=int(env("PFR_ORDERING") or 0),
+                                    relax=tuple(int(v) for v in env("PFR_RELAX").split(",")) if env("PFR_RELAX") else None,
+                                    max_ns=int(env("PFR_MAX_NS")) if env("PFR_MAX_NS") else None,
+                                    md_delta=int(env("PFR_MD_DELTA")) if env("PFR_MD_DELTA") else None)
         self.stats = self.sym.stats()
         self._lanes_req = int(os.environ.get("PFR_LANES", "2")) if lanes is None else int(lanes)
         self._fixed_batch = max_batch

@@ -39,7 +39,7 @@ class SymbolicOptions(C.Structure):
     _fields_ = [("leaf_size", C.c_int32), ("ordering", C.c_int32), ("relax_small", C.c_int32),
                 ("relax_mid", C.c_int32), ("relax_big", C.c_int32), ("zrelax_mid", C.c_double),
                 ("zrelax_big", C.c_double), ("symmetric", C.c_int32), ("n_last", C.c_int32),
-                ("last", C.POINTER(C.c_int32)), ("max_ns", C.c_int32)]
+                ("last", C.POINTER(C.c_int32)), ("max_ns", C.c_int32), ("md_delta", C.c_int32)]
 
 
 class SymbolicStats(C.Structure):
@@ -141,7 +141,7 @@ class Symbolic:
     """Host-only symbolic analysis (nested dissection + supernodal maps)."""
 
     def __init__(self, n: int, colptr, rowind, *, leaf_size=None, ordering=0, relax=None, symmetric=False,
-                 last=None, max_ns=None):
+                 last=None, max_ns=None, md_delta=None):
         L = lib()
         opt = SymbolicOptions()
         L.pfr_symbolic_options_default(C.byref(opt))
@@ -151,6 +151,8 @@ class Symbolic:
         opt.symmetric = int(bool(symmetric))
         if max_ns is not None:
             opt.max_ns = int(max_ns)
+        if md_delta is not None:
+            opt.md_delta = int(md_delta)
         if last is not None and len(last):
             self.last, lp = _i32(last)
             opt.n_last = int(self.last.size)

@@ -110,6 +110,8 @@ struct pfr_solver {
   // Hessian sweep: permuted matrix by rows and by columns ((ptr, index, nz) each),
   // tangent solution / adjoint vectors, combined tangent operators (lazily allocated)
   int32_t *d_rptr = nullptr, *d_ridx = nullptr, *d_rnz = nullptr;
+  int32_t* d_walk = nullptr;            // rows (permuted numbering) in original order: the residual
+                                        // walks' order (mesh-local gathers, whatever the ordering)
   int32_t *d_cptr = nullptr, *d_cidx = nullptr, *d_cnz = nullptr;
   double2 *DX = nullptr, *DL = nullptr, *Kdir = nullptr;
   // fused contraction + checks (k_contract_rows): per permuted row a pseudo-entry (-1, -1, -1, i),
@@ -483,6 +485,7 @@ void check_solution(pfr_solver* s, int which, int mode, int rhs, const pfr::RhsD
   d.b_stride = rd.b_stride;
   d.perm = s->P.perm;
   d.G = rd.G;
+  d.walk = s->d_walk;
   if (R) {   // refinement residual only: no maxima, no flags
     pfr::launch_residual(mode, rhs, d, X, s->Fc, R, nullptr, st);
     return;
@@ -527,6 +530,7 @@ void pfr_symbolic_options_default(pfr_symbolic_options* o) {
   o->n_last = 0;
   o->last = nullptr;
   o->max_ns = d.max_ns;
+  o->md_delta = d.md_delta;
 }
 
 int pfr_symbolic_create(int32_t n, int64_t nnz, const int32_t* colptr, const int32_t* rowind,
@@ -544,6 +548,7 @@ int pfr_symbolic_create(int32_t n, int64_t nnz, const int32_t* colptr, const int
     o.zrelax_big = opt->zrelax_big;
     o.symmetric = opt->symmetric;
     o.max_ns = opt->max_ns;
+    o.md_delta = opt->md_delta;
     if (opt->n_last > 0) {
       if (!opt->last) return fail(PFR_ERR_ARG, "n_last > 0 without last nodes");
       o.last.assign(opt->last, opt->last + opt->n_last);
@@ -974,7 +979,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       return (int)PFR_OK;
     };
     if ((rc = compress(S.prow, S.pcol, &s->d_rptr, &s->d_ridx, &s->d_rnz)) ||
-        (rc = compress(S.pcol, S.prow, &s->d_cptr, &s->d_cidx, &s->d_cnz)))
+        (rc = compress(S.pcol, S.prow, &s->d_cptr, &s->d_cidx, &s->d_cnz)) || (rc = s->up(&s->d_walk, S.iperm)))
       return bail(rc);
     // union row structure of the fused contraction + checks
     std::vector<int64_t> key(S.nnz);
@@ -997,13 +1002,16 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       const int32_t i = S.prow[e], j = S.pcol[e];
       if (find((int64_t)j * S.n + i) < 0) rows[j].push_back(make_int4(i, -1, e, 0));
     }
+    // rows in original order (mesh-local: neighbouring walks gather the same solution rows
+    // whatever the fill-reducing ordering), entries of a row by permuted column
     std::vector<int32_t> uptr(S.n + 1, 0);
     std::vector<int4> uent;
-    for (int i = 0; i < S.n; ++i) {
+    for (int t = 0; t < S.n; ++t) {
+      const int i = S.iperm[t];
       std::sort(rows[i].begin(), rows[i].end(), [](const int4& a, const int4& b) { return a.x < b.x; });
       uent.push_back(make_int4(-1, -1, -1, i));
       for (const int4& v : rows[i]) uent.push_back(make_int4(v.x, v.y, v.z, i));
-      uptr[i + 1] = (int32_t)uent.size();
+      uptr[t + 1] = (int32_t)uent.size();
     }
     std::vector<int32_t> ublk(1, 0);   // entry offsets at row starts
     // enough single-wave workgroups to fill the chip (many short walks: the walk is latency-bound)

@@ -1936,6 +1936,7 @@ struct ResidArgs {
   int64_t b_stride;
   const int* perm;
   const cplx* G;
+  const int* walk;   // rows in walk order (original numbering: mesh-local gathers of X)
 };
 
 __device__ __forceinline__ double cabs1(cplx z) { return fabs(z.x) + fabs(z.y); }
@@ -1971,7 +1972,8 @@ __global__ __launch_bounds__(256) void k_residual(ResidArgs A, const cplx* __res
   double berr = 0.0;
   bool bad = false;         // NaN / Inf residual or a non-zero residual over a zero denominator
   cplx dot = make_double2(0, 0);   // sum_p Mu_p r_p (functional correction, Mu != NULL)
-  for (int p = wave0; p < A.n; p += nwaves) {
+  for (int t = wave0; t < A.n; t += nwaves) {
+    const int p = A.walk[t];
     cplx b;
     if (RHS == 0) {
       const double v = A.rhsP[p];
@@ -2725,7 +2727,7 @@ void launch_residual(int mode, int rhs, const ResidDesc& d, const double2* X, in
   a.ptr = d.ptr; a.idx = d.idx; a.nzs = d.nzs; a.n = d.n;
   a.K = d.K; a.M = d.M; a.freqs = d.freqs; a.data = d.data; a.data_stride = d.data_stride; a.nvalid = d.nvalid;
   a.rhsP = d.rhsP; a.beta_re = d.beta_re; a.beta_im = d.beta_im; a.mass_sum = d.mass_sum;
-  a.B = d.B; a.b_stride = d.b_stride; a.perm = d.perm; a.G = d.G;
+  a.B = d.B; a.b_stride = d.b_stride; a.perm = d.perm; a.G = d.G; a.walk = d.walk;
   const dim3 g((unsigned)residual_parts(d.n), (unsigned)(Fc / 64)), b(256);
   if (mode == 0 && rhs == 0 && Mu) LAUNCH((k_residual<0, 0, true>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
   else if (mode == 0 && rhs == 0) LAUNCH((k_residual<0, 0>), g, b, st, a, X, Fc, R, acc, Mu, cpart);

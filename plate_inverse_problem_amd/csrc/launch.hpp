@@ -125,6 +125,7 @@ struct ResidDesc {
   int64_t b_stride = 0;
   const int* perm = nullptr;
   const double2* G = nullptr;
+  const int* walk = nullptr;   // the n rows (permuted numbering) in walk order
 };
 // Mu != NULL (mode 0, rhs 0): also the functional-correction dot products sum_p Mu_p r_p, one partial
 // per workgroup and frequency in cpart (residual_parts(n) x Fc), summed by launch_correct_finish

@@ -6,11 +6,19 @@
 #include <algorithm>
 #include <array>
 #include <cstring>
+#include <limits>
 #include <numeric>
 #include <stdexcept>
 
 namespace pfr {
 namespace {
+
+uint64_t mix64(uint64_t x) {   // splitmix64 finaliser
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
 
 struct Graph {
   int n = 0;
@@ -103,6 +111,144 @@ class NestedDissection {
   }
 
   void leaf_order(const std::vector<int>& nodes) {
+    if (opt_.ordering == 2) exact_md_order(nodes);
+    else mmd_order(nodes);
+  }
+
+  // Multiple minimum degree (Liu's MMD) on the explicit elimination graph of the leaf, with its
+  // external neighbours (separator nodes of enclosing dissections, eliminated later) kept as
+  // never-eliminated nodes, so every degree is the exact external degree of the constrained
+  // elimination.  Per stage: every node of the current minimum external degree whose
+  // neighbourhood the stage has not touched yet is eliminated (an independent set), then the
+  // touched nodes' degrees are recomputed and indistinguishable ones (equal closed
+  // neighbourhoods) merged into supervariables, eliminated together.
+  void mmd_order(const std::vector<int>& nodes) {
+    const int m = (int)nodes.size();
+    const int id = tag(nodes);
+    for (int i = 0; i < m; ++i) lev_[nodes[i]] = i;
+    // local ids: 0..m-1 leaf nodes, m.. external neighbours
+    std::vector<int> ext_of;   // local external id - m -> global node
+    std::vector<std::vector<int>> adj(m);
+    {
+      for (int i = 0; i < m; ++i) {
+        const int v = nodes[i];
+        for (int k = g_.ptr[v]; k < g_.ptr[v + 1]; ++k) {
+          const int u = g_.adj[k];
+          if (set_[u] == id) {
+            adj[i].push_back(lev_[u]);
+          } else {
+            if (!side_[u]) {
+              ext_of.push_back(u);
+              side_[u] = (int)ext_of.size();
+            }
+            adj[i].push_back(m + side_[u] - 1);
+          }
+        }
+        std::sort(adj[i].begin(), adj[i].end());
+      }
+      for (int u : ext_of) side_[u] = 0;
+    }
+    const int tot = m + (int)ext_of.size();
+    std::vector<int> w(tot, 1), deg(m, 0);
+    std::vector<char> alive(m, 1), touched(m, 0);
+    std::vector<std::vector<int>> members(m);
+    for (int i = 0; i < m; ++i) {
+      members[i].push_back(nodes[i]);
+      deg[i] = (int)adj[i].size();
+    }
+    int remaining = m;
+    std::vector<int> cand, hit, merged;
+    std::vector<std::pair<uint64_t, int>> keys;
+    while (remaining > 0) {
+      int dmin = std::numeric_limits<int>::max();
+      for (int i = 0; i < m; ++i)
+        if (alive[i] && deg[i] < dmin) dmin = deg[i];
+      cand.clear();
+      for (int i = 0; i < m; ++i)
+        if (alive[i] && deg[i] <= dmin + opt_.md_delta) cand.push_back(i);
+      std::stable_sort(cand.begin(), cand.end(), [&](int a, int b) { return deg[a] < deg[b]; });
+      hit.clear();
+      for (int v : cand) {
+        if (touched[v] || !alive[v]) continue;
+        alive[v] = 0;
+        touched[v] = 1;
+        remaining -= (int)members[v].size();
+        for (int x : members[v]) order_.push_back(x);
+        const std::vector<int> nb = std::move(adj[v]);
+        adj[v].clear();
+        for (int a : nb) {
+          if (a >= m) continue;
+          merged.clear();
+          std::set_union(adj[a].begin(), adj[a].end(), nb.begin(), nb.end(), std::back_inserter(merged));
+          adj[a].clear();
+          for (int x : merged)
+            if (x != a && x != v) adj[a].push_back(x);
+          if (!touched[a]) {
+            touched[a] = 1;
+            hit.push_back(a);
+          }
+        }
+      }
+      // degrees of the touched nodes, then supervariable detection among them
+      keys.clear();
+      for (int a : hit) {
+        if (!alive[a]) continue;
+        // hash of the closed neighbourhood adj[a] + {a}
+        uint64_t h = mix64((uint64_t)a);
+        for (int x : adj[a]) h += mix64((uint64_t)x);
+        keys.emplace_back(h, a);
+      }
+      std::sort(keys.begin(), keys.end());
+      for (size_t s = 0; s < keys.size();) {
+        size_t e = s + 1;
+        while (e < keys.size() && keys[e].first == keys[s].first) ++e;
+        for (size_t i = s; i < e; ++i) {
+          const int a = keys[i].second;
+          if (!alive[a]) continue;
+          for (size_t j = i + 1; j < e; ++j) {
+            const int b = keys[j].second;
+            if (!alive[b] || adj[a].size() != adj[b].size()) continue;
+            // closed neighbourhoods equal: adj[a] - {b} == adj[b] - {a}, with a in adj[b]
+            if (!std::binary_search(adj[a].begin(), adj[a].end(), b)) continue;
+            bool same = true;
+            for (size_t p = 0, q = 0; p < adj[a].size() || q < adj[b].size();) {
+              if (p < adj[a].size() && adj[a][p] == b) { ++p; continue; }
+              if (q < adj[b].size() && adj[b][q] == a) { ++q; continue; }
+              if (p >= adj[a].size() || q >= adj[b].size() || adj[a][p] != adj[b][q]) { same = false; break; }
+              ++p;
+              ++q;
+            }
+            if (!same) continue;
+            // merge b into a
+            alive[b] = 0;
+            w[a] += w[b];
+            members[a].insert(members[a].end(), members[b].begin(), members[b].end());
+            members[b].clear();
+            for (int x : adj[b]) {
+              if (x >= m || x == a) continue;
+              auto it = std::lower_bound(adj[x].begin(), adj[x].end(), b);
+              if (it != adj[x].end() && *it == b) adj[x].erase(it);
+            }
+            adj[b].clear();
+            adj[a].erase(std::lower_bound(adj[a].begin(), adj[a].end(), b));
+          }
+        }
+        s = e;
+      }
+      // weights changed by merges: recompute the touched nodes' degrees exactly
+      for (int a : hit)
+        if (alive[a]) {
+          int d = 0;
+          for (int x : adj[a]) d += w[x];
+          deg[a] = d;
+        }
+      for (int v : cand) touched[v] = 0;
+      for (int a : hit) touched[a] = 0;
+    }
+    for (int v : nodes) set_[v] = -1;
+  }
+
+  void exact_md_order(const std::vector<int>& nodes) {
     // exact minimum degree on the induced subgraph; external neighbours count
     // once towards the degree (they are eliminated later, as separator nodes)
     const int m = (int)nodes.size();

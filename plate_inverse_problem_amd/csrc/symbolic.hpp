@@ -17,13 +17,15 @@
 namespace pfr {
 
 struct SymbolicOptions {
-  int leaf_size = 96;        // nested-dissection leaves at or below this size use minimum degree
+  int leaf_size = 10000;     // nested-dissection parts at or below this size are ordered by minimum degree
   int relax_small = 4;       // always amalgamate supernodes with <= this many pivots
   int relax_mid = 8;         // ... with <= this many pivots when zero fraction < zrelax_mid
   int relax_big = 24;        // ... with <= this many pivots when zero fraction < zrelax_big
   double zrelax_mid = 0.5;
   double zrelax_big = 0.1;
-  int ordering = 0;          // 0 = nested dissection, 1 = natural (tests)
+  int ordering = 0;          // 0 = nested dissection + multiple minimum degree leaves, 1 = natural
+                             // (tests), 2 = nested dissection + exact minimum degree leaves (round 1-3)
+  int md_delta = 4;          // multiple minimum degree: eliminate nodes of degree <= min + md_delta
   int symmetric = 0;         // 1 = symmetric-structure analysis with decoupled Dirichlet nodes
   std::vector<int> last;     // nodes eliminated last, together (they form the root front)
   int max_ns = 256;          // > 0: fundamental supernodes are split into pieces of at most this many pivots
