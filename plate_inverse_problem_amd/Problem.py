@@ -101,13 +101,14 @@ class _Engine:
         # PFR_RELAX="small,mid,big" (supernode amalgamation pivot limits), PFR_MAX_NS, PFR_MD_DELTA,
         # PFR_ORDERING (2: the exact-minimum-degree leaves of rounds 1-3, for A/B runs)
         env = lambda k: os.environ.get(k)  # noqa: E731
-        self.sym = _native.Symbolic(n, colptr, rows.astype(np.int32), symmetric=self.symmetric,
-                                    leaf_size=int(env("PFR_LEAF_SIZE")) if env("PFR_LEAF_SIZE") else None,
-                                    ordering=int(env("PFR_ORDERING") or 0),
-                                    relax=tuple(int(v) for v in env("PFR_RELAX").split(",")) if env("PFR_RELAX") else None,
-                                    max_ns=int(env("PFR_MAX_NS")) if env("PFR_MAX_NS") else None,
-                                    md_delta=int(env("PFR_MD_DELTA")) if env("PFR_MD_DELTA") else None)
-        self.stats = self.sym.stats()
+        self._sym_args = (n, colptr, rows.astype(np.int32))
+        self._sym_kw = dict(symmetric=self.symmetric, ordering=int(env("PFR_ORDERING") or 0),
+                            relax=tuple(int(v) for v in env("PFR_RELAX").split(",")) if env("PFR_RELAX") else None,
+                            max_ns=int(env("PFR_MAX_NS")) if env("PFR_MAX_NS") else None,
+                            md_delta=int(env("PFR_MD_DELTA")) if env("PFR_MD_DELTA") else None)
+        self._leaf_env = int(env("PFR_LEAF_SIZE")) if env("PFR_LEAF_SIZE") else None
+        self._syms = {}
+        self._use_symbolic(n_freqs)
         self._lanes_req = int(os.environ.get("PFR_LANES", "2")) if lanes is None else int(lanes)
         self._fixed_batch = max_batch
         self.solvers, self.streams, self._pool = [], [], None
@@ -142,6 +143,29 @@ class _Engine:
         self.check_tol = float(os.environ.get("PFR_CHECK_TOL", "1e-10"))
         self.ensure(n_freqs)
 
+    def leaf_size_for(self, n_freqs: int) -> int:
+        """Nested-dissection leaf size of the ordering for a sweep of ``n_freqs`` frequencies (DESIGN.md
+        section 8, round 3).  Parts of at most this many nodes are ordered by multiple minimum degree:
+        10,000 (one dissection at C3) gives the least fill and Schur-complement traffic but a deep tree
+        (38 levels), whose per-level chains cost nothing when each level has thousands of workgroups
+        and dominate the sparse solve passes of narrow sweeps; those get the shallower trees of more
+        dissection levels (C3, freq-solves/s: 512 frequencies 23.8k / 28.8k at leaf 10,000 / 96, 1,024
+        36.4k / 38.6k at 10,000 / 500, 2,048 50.6k / 47.2k at 10,000 / 500)."""
+        if self._leaf_env is not None:
+            return self._leaf_env
+        n_freqs = max(1, n_freqs)
+        return 96 if n_freqs <= 512 else 500 if n_freqs <= 1024 else 10000
+
+    def _use_symbolic(self, n_freqs: int) -> bool:
+        """Select (building once) the symbolic analysis for a sweep width; True if it changed."""
+        leaf = self.leaf_size_for(n_freqs)
+        if leaf not in self._syms:
+            self._syms[leaf] = _native.Symbolic(*self._sym_args, leaf_size=leaf, **self._sym_kw)
+        changed = getattr(self, "sym", None) is not self._syms[leaf]
+        self.sym = self._syms[leaf]
+        self.stats = self.sym.stats()
+        return changed
+
     def _shape_for(self, n_freqs: int):
         """(lanes, frequencies per chunk) for a sweep of ``n_freqs``: up to ``lanes`` lanes of at
         least 64 frequencies; per lane as many frequencies per chunk as fit in its share of ~85 %
@@ -171,8 +195,11 @@ class _Engine:
                                               and per_lane <= self.max_batch):
                 return
         self._sized_for.add(n_freqs)
+        old = self.sym
+        if self.solvers:
+            self._use_symbolic(n_freqs)   # a rebuild for a wider sweep may take a deeper ordering
         lanes, batch = self._shape_for(n_freqs)
-        if self.solvers and lanes <= self.n_lanes and batch <= self.max_batch:
+        if self.solvers and lanes <= self.n_lanes and batch <= self.max_batch and self.sym is old:
             return
         lanes = max(lanes, self.n_lanes)
         batch = max(batch, self.max_batch if self.solvers else 0)

@@ -46,11 +46,12 @@ def _active_pattern(p):
     return idx, np.cumsum(colptr).astype(np.int32), rows.astype(np.int32)
 
 
-@pytest.mark.parametrize("material,leaf", [("isotropic", 96), ("sol", 16), ("orthotropic", 8)])
-def test_symbolic_invariants(material, leaf):
+@pytest.mark.parametrize("material,leaf,ordering", [("isotropic", 96, 0), ("sol", 16, 0), ("orthotropic", 8, 0),
+                                                    ("orthotropic", 10000, 0), ("sol", 10000, 0), ("isotropic", 96, 2)])
+def test_symbolic_invariants(material, leaf, ordering):
     p = make_problem(material, ny=3)
     idx, colptr, rowind = _active_pattern(p)
-    sym = _native.Symbolic(p.mat_size, colptr, rowind, leaf_size=leaf)
+    sym = _native.Symbolic(p.mat_size, colptr, rowind, leaf_size=leaf, ordering=ordering)
     st = sym.stats()
     perm, iperm = sym.export("PERM"), sym.export("IPERM")
     assert np.array_equal(np.sort(perm), np.arange(p.mat_size))
@@ -68,12 +69,13 @@ def test_symbolic_invariants(material, leaf):
     assert np.array_equal(np.sort(asm_nz), np.arange(rowind.size))   # every entry assembled once
 
 
-@pytest.mark.parametrize("material", ["isotropic", "sol", "orthotropic_d4"])
-def test_multifrontal_model_matches_dense(material):
+@pytest.mark.parametrize("material,leaf", [("isotropic", 16), ("sol", 16), ("orthotropic_d4", 16),
+                                           ("orthotropic_d4", 10000)])
+def test_multifrontal_model_matches_dense(material, leaf):
     """Factor + forward/transpose solves through the exported maps == dense solve."""
     p = make_problem(material, ny=3)
     idx, colptr, rowind = _active_pattern(p)
-    sym = _native.Symbolic(p.mat_size, colptr, rowind, leaf_size=16)
+    sym = _native.Symbolic(p.mat_size, colptr, rowind, leaf_size=leaf)
     orc = oracle_for(p)
     c = orc.coefficients(p.parameters)
     data = (orc.mass_values() * -(2 * np.pi * 317.0) ** 2 + c @ p.mats[:18])[idx]
@@ -95,6 +97,18 @@ def test_nested_dissection_beats_natural_fill():
     nat = _native.Symbolic(p.mat_size, colptr, rowind, ordering=1).stats()
     assert nd["nnz_lu"] < 0.7 * nat["nnz_lu"]
     assert nd["factor_flops"] < 0.5 * nat["factor_flops"]
+
+
+def test_multiple_minimum_degree_beats_exact_minimum_degree():
+    """The MMD leaves (supervariables, independent sets of minimum external degree, delta 4) against
+    the exact minimum degree of rounds 1-3 on the same dissection (C3 figures: DESIGN.md section 8)."""
+    p = make_problem("orthotropic", ny=12)
+    idx, colptr, rowind = _active_pattern(p)
+    for leaf in (96, 10000):
+        mmd = _native.Symbolic(p.mat_size, colptr, rowind, leaf_size=leaf).stats()
+        emd = _native.Symbolic(p.mat_size, colptr, rowind, leaf_size=leaf, ordering=2, md_delta=0).stats()
+        assert mmd["factor_flops"] < emd["factor_flops"]
+        assert mmd["nnz_lu"] < emd["nnz_lu"]
 
 
 def test_workspace_estimate_scales_with_batch():
