@@ -66,11 +66,15 @@ class NestedDissection {
   NestedDissection(const Graph& g, const SymbolicOptions& opt)
       : g_(g), opt_(opt), set_(g.n, -1), lev_(g.n, -1), side_(g.n, 0) {}
 
-  std::vector<int> run() {
-    std::vector<int> all(g_.n);
-    std::iota(all.begin(), all.end(), 0);
+  // excluded nodes (e.g. the ones required last) are left out of every part but keep their edges:
+  // the minimum-degree parts see them as external neighbours eliminated later, like separators
+  std::vector<int> run(const std::vector<char>* exclude = nullptr) {
+    std::vector<int> all;
+    all.reserve(g_.n);
+    for (int v = 0; v < g_.n; ++v)
+      if (!exclude || !(*exclude)[v]) all.push_back(v);
     order_.reserve(g_.n);
-    dissect(all);
+    if (!all.empty()) dissect(all);
     return order_;
   }
 
@@ -432,19 +436,18 @@ int analyse(int32_t n, int64_t nnz, const int32_t* colptr, const int32_t* rowind
       perm = nd.run();
     } else {
       // nodes required last (e.g. the loss functional's support, so that one top-down solve
-      // pass can serve the forward and the adjoint right-hand sides): ordered by nested
-      // dissection with their edges cut, then moved to the end of the order
+      // pass can serve the forward and the adjoint right-hand sides): left out of every dissection
+      // part but with their edges kept (the minimum-degree parts count them as external neighbours:
+      // C3 with the accelerometer support last, 0.195 GFLOP against 0.224 with the edges cut), then
+      // appended to the order.  Measured as the engine's ordering (round 3): the two support-reach
+      // solve chains shrink to the root, the factorisation grows by more -- not used.
       std::vector<char> islast(n, 0);
       for (int v : opt.last) {
         if (v < 0 || v >= n) throw std::runtime_error("last node out of range");
         islast[v] = 1;
       }
-      std::vector<char> cut2(isdir);
-      for (int v = 0; v < n; ++v) cut2[v] = cut2[v] || islast[v];
-      Graph g2 = symmetric_graph(n, colptr, rowind, cut2);
-      NestedDissection nd(g2, opt);
-      for (int v : nd.run())
-        if (!islast[v]) perm.push_back(v);
+      NestedDissection nd(g, opt);
+      perm = nd.run(&islast);
       for (int v = 0; v < n; ++v)
         if (islast[v]) perm.push_back(v);
     }
