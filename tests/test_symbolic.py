@@ -194,4 +194,5 @@ def test_last_nodes_and_max_ns_options():
     b = np.random.default_rng(2).standard_normal(p.mat_size) + 0j
     mf = MFModel(sym)
     x = mf.solve_sym(mf.factor(data), b, sym, data)
-    assert np.linalg.norm(x - np.linalg.solve(A, b)) / np.linalg.norm(x) < 1e-10
+    # cond(A) = 3.8e10 (kappa * u = 8e-6): the static order with the support last lands at 1.3e-10
+    assert np.linalg.norm(x - np.linalg.solve(A, b)) / np.linalg.norm(x) < 1e-9
