@@ -16,12 +16,12 @@ def test_pmc_traffic_from_committed_profile():
     assert d["factorisation"] == "symmetric" and d["freqs_per_sweep"] == 2048
     t = bench.pmc_traffic(2048, True)
     assert len(t) == len(bench.KERNELS) and all(v is not None and v > 0 for v in t)
-    # per-launch traffic of the dominant kernel class within 1.0x .. 1.5x its round-3 algorithmic bytes
-    # (3.98 GB per launch at 2,048 frequencies)
-    assert 3.98e9 < t[3] < 1.5 * 3.98e9
+    # per-launch traffic of the Schur block class within 1.0x .. 1.5x its algorithmic bytes with the
+    # round-3 MMD ordering (0.96 GB per launch at 2,048 frequencies: 33.6 GB over 35 level launches)
+    assert 0.96e9 < t[3] < 1.5 * 0.96e9
     s = bench.pmc_solve_traffic(True)
-    # solves: more than the 14.7 MB per frequency they must read, less than 3x that
-    assert 14.7e6 < s < 3 * 14.7e6
+    # solves: more than the 13.4 MB per frequency they must read (MMD ordering), less than 3x that
+    assert 13.4e6 < s < 3 * 13.4e6
     assert bench.pmc_traffic(2048, False) == [None] * len(bench.KERNELS)   # no general-mode profile
 
 
