@@ -97,6 +97,24 @@ struct pfr_solver {
   // whose bottom-up solve can be non-zero (per-front flags + the fronts level by level)
   std::vector<int32_t> front_of_col, front_parent, level_fronts_host, front_ns, front_f;
   std::vector<char> reach_host[2];
+  // functional from the bottom-up passes (symmetric loss / correction sweeps, PFR_FN_DOT, default on):
+  // slices 1-3 of the forward bottom-up chain solve L w_k = a_k over the support's reach; F_k = w_k^T
+  // diag(U)^-1 y; the adjoint's bottom-up result = sum_k c_k w_k -- no top-down pass over the support's
+  // fronts and no separate adjoint bottom-up pass
+  int fn_dot = 1;
+  bool fn_ready = false;                // row lists below match the current reaches
+  std::vector<int32_t> front_off, front_col0;
+  std::vector<double> a_perm;           // 3 x n: a_k at the permuted support rows
+  double* d_aP = nullptr;               // device copy of a_perm
+  int32_t* d_noslot = nullptr;          // n x -1 (no coupling slot: slices 1-3)
+  int2* d_fn_rows = nullptr;            // (row, factor element of U(row, row)): pivot rows in both reaches
+  int n_fn_rows = 0;
+  int32_t* d_sup_rows = nullptr;        // pivot rows of the support-reach fronts
+  int n_sup_rows = 0;
+  double2* WVk = nullptr;               // 3 x total_rows x Fc (slices 1-3 work vectors)
+  double2* YVk = nullptr;               // 2 x n x Fc (slices 2, 3 solutions; slice 1's is Y2)
+  double2* fn_parts = nullptr;          // FN_PARTS x 3 x Fc
+  double2* fcoef = nullptr;             // 3 x Fc
   // side stream for the forward bottom-up solve over the rhs reach, overlapped with the
   // factorisation level by level (symmetric loss + gradient sweeps)
   hipStream_t aux = nullptr;
@@ -218,6 +236,8 @@ int64_t workspace_bytes(const Symbolic& S, int64_t Fc) {
   b += 6 * (int64_t)S.n * Fc * 16;   // X, Y, XA, G, Y2, XR
   b += Fc * (8 + 8 + 4 + 16);        // freqs, loss terms, flags, tq
   b += Fc * (8 + 8) + (int64_t)pfr::residual_parts(S.n) * Fc * 16;   // fr0, mscale, cpart
+  if (S.symmetric)   // functional from the bottom-up passes: WVk, YVk, fn_parts, fcoef
+    b += (3 * S.total_rows + 2 * (int64_t)S.n + 3 * pfr::FN_PARTS_HOST + 3) * Fc * 16;
   return b;
 }
 
@@ -405,6 +425,78 @@ int adjoint_solve(pfr_solver* s, const pfr::RhsDesc& rg, double2* Out, hipStream
   return solve_all(s, 3, 0, rg, s->Y, Out, st, subset);
 }
 
+// Row lists and buffers of the functional-from-bottom-up path (allocated on first use, lists rebuilt
+// whenever a reach changed)
+int fn_setup(pfr_solver* s) {
+  int rc;
+  const int64_t Fc = s->Fc, n = s->n;
+  if (!s->WVk) {
+    int64_t rows = 0;
+    for (size_t t = 0; t < s->front_f.size(); ++t) rows += s->front_f[t];
+    if ((rc = s->alloc(&s->WVk, 3 * rows * Fc)) || (rc = s->alloc(&s->YVk, 2 * n * Fc)) ||
+        (rc = s->alloc(&s->fn_parts, 3 * (int64_t)pfr::FN_PARTS_HOST * Fc)) || (rc = s->alloc(&s->fcoef, 3 * Fc)) ||
+        (rc = s->up(&s->d_noslot, std::vector<int32_t>(n, -1))) || (rc = s->alloc(&s->d_aP, 3 * n)) ||
+        (rc = s->alloc(&s->d_fn_rows, n)) || (rc = s->alloc(&s->d_sup_rows, n)))
+      return rc;
+    HIP_TRY(hipMemcpy(s->d_aP, s->a_perm.data(), s->a_perm.size() * 8, hipMemcpyHostToDevice));
+  }
+  if (s->fn_ready) return PFR_OK;
+  std::vector<int2> both;
+  std::vector<int32_t> sup;
+  for (size_t t = 0; t < s->front_ns.size(); ++t) {
+    if (!s->reach_host[1][t]) continue;
+    for (int a = 0; a < s->front_ns[t]; ++a) {
+      const int32_t row = s->front_col0[t] + a;
+      sup.push_back(row);
+      if (s->reach_host[0][t])
+        both.push_back(make_int2(row, s->front_off[t] + a * s->front_f[t] + a));
+    }
+  }
+  s->n_fn_rows = (int)both.size();
+  s->n_sup_rows = (int)sup.size();
+  // at most n rows each (pivot rows are distinct): into the buffers allocated for n
+  if (!both.empty()) HIP_TRY(hipMemcpy(s->d_fn_rows, both.data(), both.size() * sizeof(int2), hipMemcpyHostToDevice));
+  if (!sup.empty()) HIP_TRY(hipMemcpy(s->d_sup_rows, sup.data(), sup.size() * 4, hipMemcpyHostToDevice));
+  s->fn_ready = true;
+  return PFR_OK;
+}
+
+// forward bottom-up over the rhs reach (slice 0) and L w_k = a_k over the support reach (slices 1-3),
+// one launch chain
+int fn_bottom_up(pfr_solver* s, int rhs_mode, const pfr::RhsDesc& rf, hipStream_t st) {
+  const int L = (int)s->level_ptr.size() - 1;
+  const int ngroups = (int)(s->Fc / 64);
+  int64_t total_rows = 0;
+  for (size_t t = 0; t < s->front_f.size(); ++t) total_rows += s->front_f[t];
+  pfr::RhsDesc rd[4] = {rf, rf, rf, rf};
+  double2* WV[4] = {s->WV, s->WVk, s->WVk + total_rows * s->Fc, s->WVk + 2 * total_rows * s->Fc};
+  double2* Y[4] = {s->Y, s->Y2, s->YVk, s->YVk + (int64_t)s->n * s->Fc};
+  const int* reach[4] = {s->d_reach[0], s->d_reach[1], s->d_reach[1], s->d_reach[1]};
+  for (int k = 1; k < 4; ++k) {
+    rd[k].rhsP = s->d_aP + (int64_t)(k - 1) * s->n;
+    rd[k].mass_sum = 0.0;
+    rd[k].beta_re = 1.0;
+    rd[k].beta_im = 0.0;
+    rd[k].cslot = s->d_noslot;
+  }
+  for (int l = 0; l < L; ++l) {
+    const int* lvl[4];
+    int nf[4];
+    lvl[0] = s->d_reach_fronts[0] + s->reach_ptr[0][l];
+    nf[0] = s->reach_ptr[0][l + 1] - s->reach_ptr[0][l];
+    for (int k = 1; k < 4; ++k) {
+      lvl[k] = s->d_reach_fronts[1] + s->reach_ptr[1][l];
+      nf[k] = s->reach_ptr[1][l + 1] - s->reach_ptr[1][l];
+    }
+    const int nmax = std::max(nf[0], nf[1]);
+    if (nmax == 0) continue;
+    pfr::launch_lsolve_multi(rhs_mode, s->P, 4, lvl, nf, solve_W(s, l, nmax), ngroups, s->F, s->Fc, WV, rd, Y, reach,
+                             st, solve_split(s, nf[0] + 3 * nf[1]));
+  }
+  HIP_TRY(hipGetLastError());
+  return PFR_OK;
+}
+
 // Symmetric mode, loss + gradient: the forward top-down pass first over the fronts the loss
 // support reaches only (they hold every support row), then -- once the loss cotangent is known
 // and its bottom-up pass (same fronts) done -- ONE top-down pass computes the adjoint on every
@@ -421,7 +513,7 @@ int sym_top_down_support(pfr_solver* s, const pfr::RhsDesc& rd, hipStream_t st) 
   return PFR_OK;
 }
 
-int sym_top_down_pair(pfr_solver* s, hipStream_t st) {
+int sym_top_down_pair(pfr_solver* s, hipStream_t st, bool fwd_all = false) {
   const int L = (int)s->level_ptr.size() - 1;
   const int ngroups = (int)(s->Fc / 64);
   for (int l = L - 1; l >= 0; --l) {
@@ -430,7 +522,8 @@ int sym_top_down_pair(pfr_solver* s, hipStream_t st) {
     pfr::launch_usolve2(s->P, s->d_level_fronts + s->level_ptr[l], nf, solve_W(s, l, nf),
                         small, ngroups,
                         s->F, s->Fc, s->Y,
-                        s->X, s->d_reach[0], s->d_reach[1], s->Y2, s->XA, s->d_reach[1], st, solve_split(s, nf));
+                        s->X, s->d_reach[0], fwd_all ? nullptr : s->d_reach[1], s->Y2, s->XA, s->d_reach[1], st,
+                        solve_split(s, nf));
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -453,6 +546,7 @@ int set_reach(pfr_solver* s, int which, const std::vector<int32_t>& prows) {
     s->reach_ptr[which].push_back((int32_t)list.size());
   }
   s->reach_host[which].assign(mark.begin(), mark.end());
+  s->fn_ready = false;
   HIP_TRY(hipMemcpy(s->d_reach[which], mark.data(), nf * 4, hipMemcpyHostToDevice));
   if (!list.empty()) HIP_TRY(hipMemcpy(s->d_reach_fronts[which], list.data(), list.size() * 4, hipMemcpyHostToDevice));
   return PFR_OK;
@@ -663,7 +757,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->fac_lds_wg = knob("PFR_FAC_LDS_WG", 160, 0, 1 << 20);
   s->fac_lds_qf = knob("PFR_FAC_LDS_QF", 1, 1, 4);
   if (s->fac_lds_qf == 3) s->fac_lds_qf = 4;
-  s->check_fused = knob("PFR_CHECK_FUSED", 0, 0, 1);   // measured 2.3 ms against 2 x 0.87 ms per 2,048-frequency chunk
+  s->check_fused = knob("PFR_CHECK_FUSED", 0, 0, 1);
+  s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);   // measured 2.3 ms against 2 x 0.87 ms per 2,048-frequency chunk
   s->n = S.n;
   s->nnz = S.nnz;
   s->Fc = round64(max_batch);
@@ -1037,6 +1132,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       s->front_parent[t] = F.parent;
       s->front_ns.push_back(F.ns);
       s->front_f.push_back(F.f);
+      s->front_off.push_back((int32_t)F.off);
+      s->front_col0.push_back(F.col0);
       for (int a = 0; a < F.ns; ++a) s->front_of_col[F.col0 + a] = t;
     }
     s->level_fronts_host = S.level_fronts;
@@ -1275,6 +1372,10 @@ int pfr_set_functional(pfr_solver* s, int32_t n_support, const int32_t* index, c
   int rc;
   if ((rc = s->up(&d_idx, pidx)) || (rc = s->up(&d_a, av))) return rc;
   if ((rc = set_reach(s, 1, pidx))) return rc;        // loss adjoint reach: functional support
+  s->a_perm.assign(3 * (size_t)s->n, 0.0);
+  for (int k = 0; k < 3; ++k)
+    for (int i = 0; i < n_support; ++i) s->a_perm[(size_t)k * s->n + pidx[i]] += av[(size_t)k * n_support + i];
+  if (s->d_aP) HIP_TRY(hipMemcpy(s->d_aP, s->a_perm.data(), s->a_perm.size() * 8, hipMemcpyHostToDevice));
   s->fn.n_support = n_support;
   s->fn.pidx = d_idx;
   s->fn.a = d_a;
@@ -1305,6 +1406,9 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
   const bool adj = reverse || correct;                 // an adjoint solve runs
   const bool paired = s->sym && adj && !refine;        // one top-down pass for both solutions
   const bool fwd_late = paired || correct;             // forward residual walk after the adjoint
+  const bool fn_fast = paired && !s->aux && s->fn_dot; // functional from the bottom-up passes
+  if (fn_fast)
+    if (int rc0 = fn_setup(s)) return rc0;
   bool used[5] = {true, true, true, adj, adj};
   // K may have been recombined since the last sweep (pfr_combine, any solver): refresh the entry-ordered
   // copy the fused contraction + checks read (2.6 % of one chunk's traffic at C3, once per call) -- only
@@ -1333,7 +1437,11 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
       rf.Bc = s->Bc;
       if ((rc = factor_all(s, 0, nullptr, 0, nv, st))) return rc;
       record(s, 1, st);   // the forward bottom-up pass belongs to the solve phases (sptrsv_roofline)
-      if ((rc = solve_all(s, 0, s->n_crow > 0 ? 3 : 0, rf, nullptr, s->Y, st, 0))) return rc;
+      if (fn_fast) {
+        if ((rc = fn_bottom_up(s, s->n_crow > 0 ? 3 : 0, rf, st))) return rc;
+      } else if ((rc = solve_all(s, 0, s->n_crow > 0 ? 3 : 0, rf, nullptr, s->Y, st, 0))) {
+        return rc;
+      }
     } else if (paired) {
       // forward bottom-up solve over the rhs reach on the side stream, level l as soon as level
       // l's L factor is formed (it needs nothing else), overlapping the factorisation
@@ -1364,7 +1472,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
     // symmetric mode with an adjoint: forward top-down only over the loss support's fronts, then one
     // combined top-down pass (sym_top_down_pair); otherwise the full forward solve first
     if (paired) {
-      if ((rc = sym_top_down_support(s, rf, st))) return rc;
+      if (!fn_fast && (rc = sym_top_down_support(s, rf, st))) return rc;
     } else {
       if ((rc = forward_solve(s, 0, rd, s->X, st, 0))) return rc;
       if (refine) {
@@ -1384,7 +1492,14 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
     fa.ref = reinterpret_cast<const double2*>(ref_dev);
     fa.scale = scale;
     if (adj) HIP_TRY(hipMemsetAsync(s->G, 0, (size_t)s->n * Fc * 16, st));
-    if (correct) {
+    if (fn_fast) {
+      const double2* Yk[3] = {s->Y2, s->YVk, s->YVk + (int64_t)s->n * Fc};
+      pfr::launch_fn_dot(s->d_fn_rows, s->n_fn_rows, s->F, s->Y, Yk, Fc, s->fn_parts, st);
+      pfr::FunctionalArgs fs = fa;
+      if (correct) fs.fr0 = s->fr0;
+      pfr::launch_functional_fn(fs, s->fn_parts, Fc, nv, q0, correct ? nullptr : fr_dev, correct ? nullptr : s->loss_terms,
+                                s->G, s->fcoef, st);
+    } else if (correct) {
       pfr::FunctionalArgs fs = fa;
       fs.fr0 = s->fr0;          // seed: fr of this solve kept, G = d fr / d x
       pfr::launch_functional(fs, s->X, Fc, nv, q0, nullptr, nullptr, s->G, st);
@@ -1395,7 +1510,19 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
     if (adj) {
       pfr::RhsDesc rg;
       rg.G = s->G;
-      if (paired) {
+      if (fn_fast) {
+        double2* Yk[3] = {s->Y2, s->YVk, s->YVk + (int64_t)s->n * Fc};
+        pfr::launch_fn_combine(s->d_sup_rows, s->n_sup_rows, s->fcoef, Yk, Fc, st);
+        if ((rc = sym_top_down_pair(s, st, true))) return rc;
+        pfr::launch_dirichlet_post(dir_desc(s), s->n_dir, s->XA, s->Fc, st);
+        if (correct) {
+          // the correction fr(x) + Re(mu^T r) needs fr OF the solution x whose residual r is walked (the
+          // dot product's fr has its own rounding error, which the correction does not see): fr0 from x
+          pfr::FunctionalArgs fs = fa;
+          fs.fr0 = s->fr0;
+          pfr::launch_functional(fs, s->X, Fc, nv, q0, nullptr, nullptr, nullptr, st);
+        }
+      } else if (paired) {
         if ((rc = solve_all(s, 0, 2, rg, nullptr, s->Y2, st, 1)) || (rc = sym_top_down_pair(s, st))) return rc;
         pfr::launch_dirichlet_post(dir_desc(s), s->n_dir, s->XA, s->Fc, st);
       } else {

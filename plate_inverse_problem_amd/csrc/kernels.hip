@@ -1161,6 +1161,16 @@ struct RhsArgs {
   const cplx* Bc;         // RHS 3: Dirichlet corrections, slot-major (slot * Fc + q)
 };
 
+constexpr int MAX_SLICES = 4;
+struct LSlices {          // k_lsolve_level_z / k_lsolve_rows_z: one bottom-up solve per slice
+  const int* lvl[MAX_SLICES];     // the level's fronts of the slice
+  int nf[MAX_SLICES];
+  cplx* WV[MAX_SLICES];           // frontal work vectors (total_rows x Fc each)
+  cplx* Y[MAX_SLICES];            // solution (permuted, n x Fc)
+  const int* reach[MAX_SLICES];
+  RhsArgs R[MAX_SLICES];
+};
+
 template <int RHS>
 __device__ __forceinline__ cplx rhs_value(const DevPattern& P, const RhsArgs& R, int p, int64_t q, int64_t Fc) {
   if (RHS == 0 || RHS == 3) {
@@ -1307,12 +1317,9 @@ __device__ __forceinline__ void lsolve_rows(const Front& fr, const cplx* __restr
 }
 
 template <int RHS>
-__global__ __launch_bounds__(512) void k_lsolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
-                               cplx* __restrict__ WV, RhsArgs R, cplx* __restrict__ Y, const int* __restrict__ reach,
-                               int rows_split) {
-  int bx;
-  const Ctx c = ctx_xcd(bx);
-  const Front fr = P.fronts[lvl[bx]];
+__device__ __forceinline__ void lsolve_front(const DevPattern& P, const Front& fr, const cplx* __restrict__ F, int64_t Fc,
+                                             cplx* __restrict__ WV, const RhsArgs& R, cplx* __restrict__ Y,
+                                             const int* __restrict__ reach, int rows_split, const Ctx& c) {
   const int f = fr.f, ns = fr.ns;
   const cplx* __restrict__ base = F + fr.off * Fc + c.q;
   cplx* __restrict__ wv = WV + (int64_t)fr.row0 * Fc + c.q;
@@ -1361,6 +1368,31 @@ __global__ __launch_bounds__(512) void k_lsolve_level(DevPattern P, const int* _
 #undef V
 }
 
+template <int RHS>
+__global__ __launch_bounds__(512) void k_lsolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
+                               cplx* __restrict__ WV, RhsArgs R, cplx* __restrict__ Y, const int* __restrict__ reach,
+                               int rows_split) {
+  int bx;
+  const Ctx c = ctx_xcd(bx);
+  lsolve_front<RHS>(P, P.fronts[lvl[bx]], F, Fc, WV, R, Y, reach, rows_split, c);
+}
+
+// Several bottom-up L solves in ONE chain of launches (blockIdx.z = slice): in a loss sweep the forward
+// right-hand side over its reach and the three functional vectors aU, aV, aW over theirs (real
+// coefficients: the slices' RhsArgs carry rhsP = a_k, mass_sum = 0, beta = 1, no coupling slots), so
+// that fr comes from  a_k^T x = (L^-1 a_k)^T diag(U)^-1 (L^-1 b)  without a top-down pass over the
+// support's fronts, and the adjoint's bottom-up result is a combination of the slices' (k_fn_combine).
+// Workgroups past a slice's front count return at once (the grid is sized for the largest slice).
+template <int RHS>
+__global__ __launch_bounds__(512) void k_lsolve_level_z(DevPattern P, LSlices S, const cplx* __restrict__ F, int64_t Fc,
+                                                        int rows_split) {
+  int bx;
+  const Ctx c = ctx_xcd(bx);
+  const int z = blockIdx.z;
+  if (bx >= S.nf[z]) return;
+  lsolve_front<RHS>(P, P.fronts[S.lvl[z][bx]], F, Fc, S.WV[z], S.R[z], S.Y[z], S.reach[z], rows_split, c);
+}
+
 // Update rows of the L solve at the top levels, split over S workgroups per (front, frequency group)
 // (launch_solve with split > 1, after k_lsolve_level<..., rows_split = 1> formed the pivot values): at
 // small frequency counts one workgroup per front reads the whole L21 block through one CU, bound by
@@ -1373,6 +1405,18 @@ __global__ __launch_bounds__(256) void k_lsolve_rows(DevPattern P, const int* __
   const Front fr = P.fronts[lvl[slot]];
   lsolve_rows(fr, F + fr.off * Fc + c.q, WV + (int64_t)fr.row0 * Fc + c.q, Fc, fr.ns + SRB * (split * c.W + c.w),
               SRB * c.W * S);
+}
+
+__global__ __launch_bounds__(256) void k_lsolve_rows_z(DevPattern P, LSlices S, const cplx* __restrict__ F, int64_t Fc,
+                                                       int split) {
+  int bx;
+  const Ctx c = ctx_xcd(bx);
+  const int z = blockIdx.z;
+  const int slot = bx / split, part = bx % split;
+  if (slot >= S.nf[z]) return;
+  const Front fr = P.fronts[S.lvl[z][slot]];
+  lsolve_rows(fr, F + fr.off * Fc + c.q, S.WV[z] + (int64_t)fr.row0 * Fc + c.q, Fc, fr.ns + SRB * (part * c.W + c.w),
+              SRB * c.W * split);
 }
 
 // v - sum_{b in [ns, f)} e[b * es] * X[ix[b]]: the update-row solution values are
@@ -2216,6 +2260,7 @@ __global__ void k_functional(FunctionalArgs A, const cplx* __restrict__ X, int64
     loss_terms[q] = term;
     s = valid && fr > 0.0 ? dl * A.scale / fr : 0.0;
   }
+  if (!G) return;             // fr0 only (the functional-from-bottom-up path: fr of the final x)
   const cplx cU = make_double2(s * ts2 * U.x, -s * ts2 * U.y);
   const cplx cV = make_double2(s * ts2 * Vv.x, -s * ts2 * Vv.y);
   const cplx cW = make_double2(s * W.x, -s * W.y);
@@ -2225,6 +2270,94 @@ __global__ void k_functional(FunctionalArgs A, const cplx* __restrict__ X, int64
     g.x = au * cU.x + av * cV.x + aw * cW.x;
     g.y = au * cU.y + av * cV.y + aw * cW.y;
     G[(int64_t)A.pidx[t] * Fc + q] = g;
+  }
+}
+
+// ------------------------------------------------------------------ K4': functional from the bottom-up passes
+// F_k = a_k^T x = sum_i (L^-1 a_k)_i (L^-1 b)_i / U(i, i) over the pivot rows i reached by both the rhs
+// and the support (rows: (permuted row, factor element of U(i, i))).  Per frequency group FN_PARTS
+// workgroups, each one partial per frequency (deterministic; k_functional_fn sums them in order).
+constexpr int FN_PARTS = 16;
+__global__ __launch_bounds__(256) void k_fn_dot(const int2* __restrict__ rows, int nrows, const cplx* __restrict__ F,
+                                                const cplx* __restrict__ Yb, const cplx* __restrict__ Y0,
+                                                const cplx* __restrict__ Y1, const cplx* __restrict__ Y2, int64_t Fc,
+                                                cplx* __restrict__ parts) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t q = (int64_t)blockIdx.y * 64 + lane;
+  const int part = blockIdx.x;
+  cplx s0 = make_double2(0, 0), s1 = s0, s2 = s0;
+  for (int t = part * 4 + w; t < nrows; t += FN_PARTS * 4) {
+    const int2 r = rows[t];
+    const int64_t o = (int64_t)r.x * Fc + q;
+    const cplx yb = cmul(Yb[o], crecip(F[(int64_t)r.y * Fc + q]));
+    s0 = cadd(s0, cmul(Y0[o], yb));
+    s1 = cadd(s1, cmul(Y1[o], yb));
+    s2 = cadd(s2, cmul(Y2[o], yb));
+  }
+  __shared__ cplx sh[3][4][64];
+  sh[0][w][lane] = s0;
+  sh[1][w][lane] = s1;
+  sh[2][w][lane] = s2;
+  __syncthreads();
+  if (w < 3) {
+    const cplx v = cadd(cadd(sh[w][0][lane], sh[w][1][lane]), cadd(sh[w][2][lane], sh[w][3][lane]));
+    parts[((int64_t)part * 3 + w) * Fc + q] = v;
+  }
+}
+
+// k_functional with U, V, W from k_fn_dot's partials; also the cotangent coefficients (c_U, c_V, c_W)
+// per frequency (fcoef, 3 x Fc) for k_fn_combine.  G (zeroed) gets the adjoint rhs at the support rows.
+__global__ void k_functional_fn(FunctionalArgs A, const cplx* __restrict__ parts, int64_t Fc, int nvalid,
+                                int64_t q_global0, double* __restrict__ fr_out, double* __restrict__ loss_terms,
+                                cplx* __restrict__ G, cplx* __restrict__ fcoef) {
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Fc) return;
+  cplx U = make_double2(0, 0), Vv = U, W = U;
+  for (int p = 0; p < FN_PARTS; ++p) {
+    U = cadd(U, parts[((int64_t)p * 3 + 0) * Fc + q]);
+    Vv = cadd(Vv, parts[((int64_t)p * 3 + 1) * Fc + q]);
+    W = cadd(W, parts[((int64_t)p * 3 + 2) * Fc + q]);
+  }
+  const double ts2 = A.ts * A.ts;
+  const double fr = sqrt(ts2 * (U.x * U.x + U.y * U.y) + ts2 * (Vv.x * Vv.x + Vv.y * Vv.y) + W.x * W.x + W.y * W.y);
+  const bool valid = q < nvalid;
+  double s = 0.0;
+  if (A.fr0) {
+    A.fr0[q] = valid ? fr : 0.0;
+    s = valid && fr > 0.0 ? 1.0 / fr : 0.0;
+  } else {
+    if (valid && fr_out) fr_out[q_global0 + q] = fr;
+    if (A.loss_type >= 0) {
+      double term = 0.0, dl = 0.0;
+      if (valid) loss_term(A.loss_type, fr, A.ref[q_global0 + q], term, dl);
+      loss_terms[q] = term;
+      s = valid && fr > 0.0 ? dl * A.scale / fr : 0.0;
+    }
+  }
+  const cplx cU = make_double2(s * ts2 * U.x, -s * ts2 * U.y);
+  const cplx cV = make_double2(s * ts2 * Vv.x, -s * ts2 * Vv.y);
+  const cplx cW = make_double2(s * W.x, -s * W.y);
+  fcoef[q] = cU;
+  fcoef[Fc + q] = cV;
+  fcoef[2 * Fc + q] = cW;
+  for (int t = 0; t < A.n_support; ++t) {
+    const double au = A.a[t], av = A.a[A.n_support + t], aw = A.a[2 * A.n_support + t];
+    G[(int64_t)A.pidx[t] * Fc + q] =
+        make_double2(au * cU.x + av * cV.x + aw * cW.x, au * cU.y + av * cV.y + aw * cW.y);
+  }
+}
+
+// The adjoint's bottom-up result over the support's fronts: L^-1 g = sum_k c_k (L^-1 a_k), in place in Y0
+// (rows: the pivot rows of the support-reach fronts, permuted)
+__global__ __launch_bounds__(256) void k_fn_combine(const int* __restrict__ rows, int nrows, const cplx* __restrict__ fcoef,
+                                                    cplx* __restrict__ Y0, const cplx* __restrict__ Y1,
+                                                    const cplx* __restrict__ Y2, int64_t Fc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.y * 64 + lane;
+  const cplx c0 = fcoef[q], c1 = fcoef[Fc + q], c2 = fcoef[2 * Fc + q];
+  for (int t = blockIdx.x * 4 + (threadIdx.x >> 6); t < nrows; t += gridDim.x * 4) {
+    const int64_t o = (int64_t)rows[t] * Fc + q;
+    Y0[o] = cadd(cadd(cmul(c0, Y0[o]), cmul(c1, Y1[o])), cmul(c2, Y2[o]));
   }
 }
 
@@ -2694,6 +2827,45 @@ void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const 
       LAUNCH(k_ltsolve_level, g, b, st, P, lvl, F, Fc, WV, Yin, Out, reach);
       break;
   }
+}
+
+void launch_lsolve_multi(int rhs_mode, const DevPattern& P, int nslices, const int* const* lvl, const int* nf, int W,
+                         int ngroups, const double2* F, int64_t Fc, double2* const* WV, const RhsDesc* rd,
+                         double2* const* Y, const int* const* reach, hipStream_t st, int split) {
+  LSlices S{};
+  int nmax = 0;
+  for (int z = 0; z < nslices; ++z) {
+    S.lvl[z] = lvl[z];
+    S.nf[z] = nf[z];
+    S.WV[z] = WV[z];
+    S.Y[z] = Y[z];
+    S.reach[z] = reach[z];
+    S.R[z] = make_rhs(rd[z]);
+    nmax = std::max(nmax, nf[z]);
+  }
+  if (nmax <= 0) return;
+  const dim3 g(nmax, ngroups, nslices), b(64 * W);
+  const int rs = split > 1;
+  if (rhs_mode == 0) LAUNCH(k_lsolve_level_z<0>, g, b, st, P, S, F, Fc, rs);
+  else LAUNCH(k_lsolve_level_z<3>, g, b, st, P, S, F, Fc, rs);
+  if (rs) LAUNCH(k_lsolve_rows_z, dim3(nmax * split, ngroups, nslices), dim3(64 * SPLIT_W), st, P, S, F, Fc, split);
+}
+
+void launch_fn_dot(const int2* rows, int nrows, const double2* F, const double2* Yb, const double2* const* Yk, int64_t Fc,
+                   double2* parts, hipStream_t st) {
+  LAUNCH(k_fn_dot, dim3(FN_PARTS, (unsigned)(Fc / 64)), dim3(256), st, rows, nrows, F, Yb, Yk[0], Yk[1], Yk[2], Fc, parts);
+}
+
+void launch_functional_fn(const FunctionalArgs& A, const double2* parts, int64_t Fc, int nvalid, int64_t q0,
+                          double* fr_out, double* loss_terms, double2* G, double2* fcoef, hipStream_t st) {
+  LAUNCH(k_functional_fn, dim3((unsigned)((Fc + 63) / 64)), dim3(64), st, A, parts, Fc, nvalid, q0, fr_out, loss_terms,
+         G, fcoef);
+}
+
+void launch_fn_combine(const int* rows, int nrows, const double2* fcoef, double2* const* Yk, int64_t Fc, hipStream_t st) {
+  if (nrows <= 0) return;
+  const unsigned nb = (unsigned)std::min(64, (nrows + 3) / 4);
+  LAUNCH(k_fn_combine, dim3(nb, (unsigned)(Fc / 64)), dim3(256), st, rows, nrows, fcoef, Yk[0], Yk[1], Yk[2], Fc);
 }
 
 void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, bool small, int ngroups,

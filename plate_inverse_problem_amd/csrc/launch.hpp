@@ -57,6 +57,19 @@ constexpr int SPLIT_W = 4;
 void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups,
                   const double2* F, int64_t Fc, double2* WV, const RhsDesc& rd, const double2* Yin, double2* Out,
                   const int* reach, hipStream_t st, int split = 1);
+// nslices (<= 4) bottom-up L solves as one chain of launches (blockIdx.z = slice; slice z: the fronts
+// lvl[z][0 .. nf[z]), its work vectors WV[z], rhs rd[z] (rhs_mode 0 or 3 for every slice), solution Y[z])
+void launch_lsolve_multi(int rhs_mode, const DevPattern& P, int nslices, const int* const* lvl, const int* nf, int W,
+                         int ngroups, const double2* F, int64_t Fc, double2* const* WV, const RhsDesc* rd,
+                         double2* const* Y, const int* const* reach, hipStream_t st, int split);
+// functional from the bottom-up passes: partial dot products (FN_PARTS x 3 x Fc), the functional / loss
+// / cotangent from them (fcoef: 3 x Fc, G at the support rows), and L^-1 g = sum_k c_k L^-1 a_k in Yk[0]
+constexpr int FN_PARTS_HOST = 16;
+void launch_fn_dot(const int2* rows, int nrows, const double2* F, const double2* Yb, const double2* const* Yk, int64_t Fc,
+                   double2* parts, hipStream_t st);
+void launch_functional_fn(const FunctionalArgs& A, const double2* parts, int64_t Fc, int nvalid, int64_t q0,
+                          double* fr_out, double* loss_terms, double2* G, double2* fcoef, hipStream_t st);
+void launch_fn_combine(const int* rows, int nrows, const double2* fcoef, double2* const* Yk, int64_t Fc, hipStream_t st);
 // two top-down U solves in one pass (vector 0 skipped on the fronts flagged in skip0), symmetric
 // mode; small: the low-register variant for levels of small fronts
 void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, bool small, int ngroups,
