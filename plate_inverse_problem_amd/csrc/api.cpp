@@ -757,8 +757,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->fac_lds_wg = knob("PFR_FAC_LDS_WG", 160, 0, 1 << 20);
   s->fac_lds_qf = knob("PFR_FAC_LDS_QF", 1, 1, 4);
   if (s->fac_lds_qf == 3) s->fac_lds_qf = 4;
-  s->check_fused = knob("PFR_CHECK_FUSED", 0, 0, 1);
-  s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);   // measured 2.3 ms against 2 x 0.87 ms per 2,048-frequency chunk
+  s->check_fused = knob("PFR_CHECK_FUSED", 0, 0, 1);   // measured 2.3 ms against 2 x 0.87 ms per 2,048-frequency chunk
+  s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);   // functional from the bottom-up passes (symmetric paired sweeps)
   s->n = S.n;
   s->nnz = S.nnz;
   s->Fc = round64(max_batch);
