@@ -66,7 +66,9 @@ KERNELS = (("k_assemble_level",), ("k_factor_level", "k_factor_sym"), ("k_offdia
            ("k_schur_level", "k_schur_sym_level"))
 KERNEL_NAMES = ("k_assemble_level", "k_factor_level", "k_offdiag_level", "k_schur_sym_blk",
                 "k_schur_sym_level / k_schur_level")
-SOLVE_KERNELS = ("k_lsolve_level", "k_usolve_level", "k_usolve2_level")
+# every launch of the triangular solves: level passes, split update parts, the sliced bottom-up chain and
+# the combination of its functional slices
+SOLVE_KERNELS = ("k_lsolve", "k_usolve", "k_fn_combine")
 
 
 def _pmc():
@@ -94,12 +96,12 @@ def pmc_traffic(chunk, symmetric):
 
 def pmc_solve_traffic(symmetric):
     """Measured HBM bytes per frequency of one sweep's triangular solves (every launch of the solve
-    kernels; sweeps counted by their k_functional launches)."""
+    kernels; chunks counted by their k_pad_freqs launches, one per chunk of freqs_per_sweep)."""
     d = _pmc()
     if d is None or d.get("factorisation") != ("symmetric" if symmetric else "general"):
         return None
     k = d["kernels"]
-    sweeps = sum(e["dispatches"] for n, e in k.items() if n.startswith("k_functional") and "tangent" not in n)
+    sweeps = sum(e["dispatches"] for n, e in k.items() if n == "k_pad_freqs")
     if not sweeps:
         return None
     byts = sum(e["read_bytes"] + e["write_bytes"] for n, e in k.items() if n.startswith(SOLVE_KERNELS))
@@ -350,17 +352,20 @@ def main():
                             "fp64_TFLOPs": fact_tfs, "fp64_frac": fact_tfs / FP64_PEAK_TFLOPS,
                             "concurrent_ms_per_step": kms.tolist()},
         "sptrsv_roofline": {"bound": "hbm",
-                            "kernel": "k_lsolve_level + k_usolve_level + k_usolve2_level (forward and adjoint)",
+                            "kernel": "k_lsolve_level_z / k_lsolve_rows_z (one bottom-up chain: forward rhs + "
+                                      "the functional's three vectors) + k_usolve2_level / k_usolve2_upd (paired "
+                                      "top-down) + k_fn_combine",
                             "achieved": trsv_gbs, "alg_bytes": trsv_bytes, "alg_bytes_per_freq": sb.tolist(),
                             "ms": trsv_ms, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": trsv_gbs / HBM_PEAK_GBS,
                             "traffic": None if trsv_traffic is None else trsv_traffic * n_iso,
                             "frequencies": n_iso},
         "phase_ms": {"factor": phase[0], "fwd_solves": phase[1], "functional": phase[2],
                      "adj_solves": phase[3], "contract": phase[4],
-                     "note": "device ms per step summed over lanes; fwd_solves = the forward bottom-up pass over "
-                             "the rhs reach + the top-down pass over the loss support's fronts, adj_solves = the "
-                             "adjoint bottom-up + the paired top-down pass, contract = residual walks (checks and "
-                             "the functional correction) + gradient contraction"},
+                     "note": "device ms per step summed over lanes; fwd_solves = the bottom-up chain over the "
+                             "rhs reach and the loss support's reach (forward rhs + the functional's three vectors), "
+                             "functional = its dot products + loss terms, adj_solves = the adjoint's bottom-up "
+                             "combination + the paired top-down pass, contract = residual walks (checks and the "
+                             "functional correction) + gradient contraction"},
         "loss": val,
         "backward_error": check,
     }

@@ -249,7 +249,9 @@ PFR_API int pfr_solver_alg_bytes(const pfr_solver* s, int64_t* bytes_out /* 5 */
 
 /* Algorithmic HBM bytes per frequency of the triangular solves of one loss pfr_sweep under the
  * solver's current check mode: factor entries each pass must read (16 B each) plus rhs in / solution
- * out.  Symmetric mode without refinement (the paired passes): [0] forward bottom-up over the fronts
+ * out.  Symmetric mode without refinement, functional from the bottom-up passes (PFR_FN_DOT, default):
+ * [0] the one bottom-up chain over the fronts the rhs or the loss support reach, [1] the paired top-down
+ * pass over every front.  With PFR_FN_DOT=0 (the paired passes): [0] forward bottom-up over the fronts
  * the rhs reaches + forward top-down over the fronts the loss support reaches, [1] adjoint bottom-up
  * over that reach + the single top-down pass that reads every U value once for the adjoint and the
  * rest of the forward solution.  Otherwise [0] / [1] forward / adjoint pair (reached bottom-up + full

@@ -1239,13 +1239,15 @@ int pfr_solver_solve_bytes(const pfr_solver* s, int64_t* bytes) {
   if (!s || !bytes) return fail(PFR_ERR_ARG, "null argument");
   // factor entries each pass reads once: lower[w] = L11 + L21 of the fronts reach w holds (the
   // bottom-up pass of rhs w), upper_r[w] = U11 + U12 of those fronts, upper / lower_all = every front
-  int64_t lower[2] = {0, 0}, upper_r[2] = {0, 0}, upper = 0, lower_all = 0;
+  int64_t lower[2] = {0, 0}, upper_r[2] = {0, 0}, upper = 0, lower_all = 0, lower_union = 0, sup_rows = 0;
   for (size_t t = 0; t < s->front_ns.size(); ++t) {
     const int64_t ns = s->front_ns[t], r = s->front_f[t] - ns;
     const int64_t u = ns * (ns + 1) / 2 + r * ns;             // U11 + U12 (symmetric: diag(U) L^T)
     const int64_t l = ns * (ns - 1) / 2 + r * ns;             // L11 (unit diagonal) + L21
     upper += u;
     lower_all += l;
+    if (s->reach_host[0][t] || s->reach_host[1][t]) lower_union += l;
+    if (s->reach_host[1][t]) sup_rows += ns;
     for (int w = 0; w < 2; ++w)
       if (s->reach_host[w][t]) {
         lower[w] += l;
@@ -1254,7 +1256,13 @@ int pfr_solver_solve_bytes(const pfr_solver* s, int64_t* bytes) {
   }
   const int64_t vec = 2 * 16 * (int64_t)s->n;                 // rhs in, solution out
   const bool refine = (s->check_mode & PFR_CHECK_REFINE) != 0;
-  if (s->sym && !refine) {
+  if (s->sym && !refine && s->fn_dot) {
+    // loss sweep, functional from the bottom-up passes: ONE bottom-up chain over the rhs reach and the
+    // support reach together (the support's three vectors share each L value of their fronts) + the
+    // paired top-down pass over every front (each U value once for the adjoint and the forward solution)
+    bytes[0] = 16 * lower_union + vec + 3 * 32 * sup_rows;
+    bytes[1] = 16 * upper + 2 * vec;
+  } else if (s->sym && !refine) {
     // loss sweep, paired: forward bottom-up over its reach + forward top-down over the fronts the loss
     // support reaches; adjoint bottom-up over that reach + ONE top-down pass over every front that
     // forms the adjoint and the rest of the forward solution together (each U value loaded once)
