@@ -115,6 +115,10 @@ struct pfr_solver {
   double2* YVk = nullptr;               // 2 x n x Fc (slices 2, 3 solutions; slice 1's is Y2)
   double2* fn_parts = nullptr;          // FN_PARTS x 3 x Fc
   double2* fcoef = nullptr;             // 3 x Fc
+  // the gradient contraction fused into the forward residual walk (PFR_CONTRACT_WALK, default on; needs
+  // the functional correction's walk): per (workgroup, k, frequency) sums, reduced with m_q by k_reduce_q
+  int contract_walk = 1;
+  double2* kpart = nullptr;
   // side stream for the forward bottom-up solve over the rhs reach, overlapped with the
   // factorisation level by level (symmetric loss + gradient sweeps)
   hipStream_t aux = nullptr;
@@ -238,6 +242,7 @@ int64_t workspace_bytes(const Symbolic& S, int64_t Fc) {
   b += Fc * (8 + 8) + (int64_t)pfr::residual_parts(S.n) * Fc * 16;   // fr0, mscale, cpart
   if (S.symmetric)   // functional from the bottom-up passes: WVk, YVk, fn_parts, fcoef
     b += (3 * S.total_rows + 2 * (int64_t)S.n + 3 * pfr::FN_PARTS_HOST + 3) * Fc * 16;
+  b += (int64_t)pfr::residual_parts(S.n) * 18 * Fc * 16;   // kpart (contraction in the forward walk)
   return b;
 }
 
@@ -559,7 +564,7 @@ int set_reach(pfr_solver* s, int which, const std::vector<int32_t>& prows) {
 // b - A x is written there (the refinement step), nothing is checked.
 void check_solution(pfr_solver* s, int which, int mode, int rhs, const pfr::RhsDesc& rd, const double2* data,
                     int64_t ds, int nvalid, const double2* X, double2* R, int64_t q0, hipStream_t st,
-                    const double2* Mu = nullptr, bool check = true) {
+                    const double2* Mu = nullptr, bool check = true, bool contract = false) {
   pfr::ResidDesc d;
   d.ptr = which == 0 ? s->d_rptr : s->d_cptr;
   d.idx = which == 0 ? s->d_ridx : s->d_cidx;
@@ -580,6 +585,11 @@ void check_solution(pfr_solver* s, int which, int mode, int rhs, const pfr::RhsD
   d.perm = s->P.perm;
   d.G = rd.G;
   d.walk = s->d_walk;
+  if (contract) {
+    d.se = s->stiff;
+    d.n_stiff = s->n_stiff;
+    d.kpart = s->kpart;
+  }
   if (R) {   // refinement residual only: no maxima, no flags
     pfr::launch_residual(mode, rhs, d, X, s->Fc, R, nullptr, st);
     return;
@@ -758,7 +768,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->fac_lds_qf = knob("PFR_FAC_LDS_QF", 1, 1, 4);
   if (s->fac_lds_qf == 3) s->fac_lds_qf = 4;
   s->check_fused = knob("PFR_CHECK_FUSED", 0, 0, 1);   // measured 2.3 ms against 2 x 0.87 ms per 2,048-frequency chunk
-  s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);   // functional from the bottom-up passes (symmetric paired sweeps)
+  s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);
+  s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);   // functional from the bottom-up passes (symmetric paired sweeps)
   s->n = S.n;
   s->nnz = S.nnz;
   s->Fc = round64(max_batch);
@@ -1547,16 +1558,25 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
       record(s, 4, st);
       bool want_f = fwd_late && (s->check_mode & PFR_CHECK_FORWARD);
       bool want_a = (s->check_mode & PFR_CHECK_ADJOINT) != 0;
+      // the gradient contraction rides on the forward residual walk (loss sweeps with the correction)
+      const bool cwalk = reverse && correct && s->contract_walk && !fused_checks &&
+                         (s->n_stiff == 12 || s->n_stiff == 18);
+      if (cwalk && !s->kpart) {
+        if ((rc = s->alloc(&s->kpart, (int64_t)pfr::residual_parts(s->n) * 18 * Fc))) return rc;
+      }
       if (correct) {
         // the forward residual walk: backward error (when checked) + the correction's dot products,
         // then the corrected fr, its loss terms and the per-frequency cotangent scales
-        check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st, s->XA, want_f);
+        check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st, s->XA, want_f, cwalk);
         want_f = false;
         pfr::launch_correct_finish(fa, s->fr0, s->cpart, pfr::residual_parts(s->n), Fc, nv, q0, fr_dev, s->loss_terms,
                                    s->mscale, st);
       }
       const double* msc = correct ? s->mscale : nullptr;
-      if (reverse) pfr::launch_contract_eg(s->d_uent, s->n_uent, s->d_se, s->n_stiff, s->XA, s->X, Fc, nv, s->partial, st, msc);
+      if (cwalk)
+        pfr::launch_reduce_q(s->kpart, pfr::residual_parts(s->n), s->n_stiff, msc, nv, Fc, s->partial, st);
+      else if (reverse)
+        pfr::launch_contract_eg(s->d_uent, s->n_uent, s->d_se, s->n_stiff, s->XA, s->X, Fc, nv, s->partial, st, msc);
       if (fused_checks && (want_f || want_a)) {
         // gradient contraction's row walk fused with both checks (PFR_CHECK_FUSED=1)
         pfr::RowCheckDesc cd;
@@ -1585,8 +1605,8 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
       }
       if (reverse) {
         pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st, msc);
-        pfr::launch_reduce(s->partial, pfr::contract_eg_parts(s->n_uent), s->n_stiff, s->tq, s->e, s->loss_terms, nv, Fc,
-                           reinterpret_cast<double2*>(w_dev), loss_dev, st);
+        pfr::launch_reduce(s->partial, cwalk ? 1 : pfr::contract_eg_parts(s->n_uent), s->n_stiff, s->tq, s->e,
+                           s->loss_terms, nv, Fc, reinterpret_cast<double2*>(w_dev), loss_dev, st);
       }
     } else {
       record(s, 4, st);

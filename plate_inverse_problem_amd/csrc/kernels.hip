@@ -1981,6 +1981,8 @@ struct ResidArgs {
   const int* perm;
   const cplx* G;
   const int* walk;   // rows in walk order (original numbering: mesh-local gathers of X)
+  const double* se;  // NSK > 0: stiffness values, nz-major (se[nz * NSK + k])
+  cplx* kpart;       // NSK > 0: per (workgroup, k, frequency) sums of S_k(nz) mu_row x_col
 };
 
 __device__ __forceinline__ double cabs1(cplx z) { return fabs(z.x) + fabs(z.y); }
@@ -1994,7 +1996,12 @@ __device__ __forceinline__ cplx resid_entry(const ResidArgs& A, const cplx* __re
   return dq[nz];
 }
 
-template <int MODE, int RHS, bool DOT = false>
+// NSK > 0 (with DOT, the loss sweep's forward walk under the functional correction): the gradient
+// contraction rides on the walk -- every entry (p, j, nz) it visits has x_j gathered and mu_p loaded
+// already, so s_k(q) += S_k(nz) mu_p x_j per lane (frequency), per workgroup; the loss cotangent scale
+// m_q is only known after this walk (k_correct_finish), so the partials stay per frequency and
+// k_reduce_q applies m_q.  Replaces k_contract_eg's separate entry walk.
+template <int MODE, int RHS, bool DOT = false, int NSK = 0>
 __global__ __launch_bounds__(256) void k_residual(ResidArgs A, const cplx* __restrict__ X, int64_t Fc,
                                                   cplx* __restrict__ R, double* __restrict__ acc,
                                                   const cplx* __restrict__ Mu, cplx* __restrict__ cpart) {
@@ -2016,8 +2023,13 @@ __global__ __launch_bounds__(256) void k_residual(ResidArgs A, const cplx* __res
   double berr = 0.0;
   bool bad = false;         // NaN / Inf residual or a non-zero residual over a zero denominator
   cplx dot = make_double2(0, 0);   // sum_p Mu_p r_p (functional correction, Mu != NULL)
+  cplx ks[NSK > 0 ? NSK : 1];
+#pragma unroll
+  for (int k = 0; k < (NSK > 0 ? NSK : 1); ++k) ks[k] = make_double2(0, 0);
   for (int t = wave0; t < A.n; t += nwaves) {
     const int p = A.walk[t];
+    cplx mup = make_double2(0, 0);
+    if (NSK > 0) mup = Mu[(int64_t)p * Fc + q];
     cplx b;
     if (RHS == 0) {
       const double v = A.rhsP[p];
@@ -2043,16 +2055,37 @@ __global__ __launch_bounds__(256) void k_residual(ResidArgs A, const cplx* __res
         r = cfms(r, a[u], x[u]);
         den = fma(cabs1(a[u]), cabs1(x[u]), den);
       }
+      if (NSK > 0) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const cplx mx = cmul(mup, x[u]);
+          const double* sk = A.se + (int64_t)A.nzs[e + u] * NSK;
+#pragma unroll
+          for (int k = 0; k < NSK; ++k) {
+            ks[k].x = fma(sk[k], mx.x, ks[k].x);
+            ks[k].y = fma(sk[k], mx.y, ks[k].y);
+          }
+        }
+      }
     }
     for (; e < e1; ++e) {
       const cplx a = resid_entry<MODE>(A, dq, A.nzs[e], om2);
       const cplx x = X[(int64_t)A.idx[e] * Fc + q];
       r = cfms(r, a, x);
       den = fma(cabs1(a), cabs1(x), den);
+      if (NSK > 0) {
+        const cplx mx = cmul(mup, x);
+        const double* sk = A.se + (int64_t)A.nzs[e] * NSK;
+#pragma unroll
+        for (int k = 0; k < NSK; ++k) {
+          ks[k].x = fma(sk[k], mx.x, ks[k].x);
+          ks[k].y = fma(sk[k], mx.y, ks[k].y);
+        }
+      }
     }
     if (R) R[(int64_t)p * Fc + q] = r;
     if (DOT) {
-      const cplx m = Mu[(int64_t)p * Fc + q];
+      const cplx m = NSK > 0 ? mup : Mu[(int64_t)p * Fc + q];
       dot = cadd(dot, cmul(m, r));
     }
     const double cr = cabs1(r);
@@ -2070,6 +2103,20 @@ __global__ __launch_bounds__(256) void k_residual(ResidArgs A, const cplx* __res
       cplx t = sdot[0][lane];
       for (int k = 1; k < (int)(blockDim.x >> 6); ++k) t = cadd(t, sdot[k][lane]);
       cpart[(int64_t)bx * Fc + q] = t;
+    }
+  }
+  if (NSK > 0) {
+    // the waves' contraction sums in LDS, added in wave order: one partial per (workgroup, k, frequency)
+    __shared__ cplx sks[4][64];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < NSK; ++k) {
+      __syncthreads();
+      sks[w][lane] = ks[k];
+      __syncthreads();
+      if (w == 0)
+        A.kpart[((int64_t)bx * NSK + k) * Fc + q] =
+            cadd(cadd(sks[0][lane], sks[1][lane]), cadd(sks[2][lane], sks[3][lane]));
     }
   }
   if (!acc) return;          // residual only (refinement step / correction without a check)
@@ -2622,6 +2669,38 @@ __global__ void k_rhs_dot(const int* __restrict__ sup, const double* __restrict_
 
 // Deterministic reduction over (blocks, valid frequencies):
 //   w[k] += sum_q ( -sum_blk partial[blk][k][q] + e_k * t_q ),  loss += sum_q loss_terms[q]
+// partial[k] = sum_q m_q sum_b kpart[b][k][q] (fixed order): the fused walk's contraction in
+// k_contract_eg's partial layout (one part), so that k_reduce completes it unchanged
+__global__ __launch_bounds__(1024) void k_reduce_q(const cplx* __restrict__ kpart, int nparts, int n_stiff,
+                                                   const double* __restrict__ msc, int nvalid, int64_t Fc,
+                                                   cplx* __restrict__ partial) {
+  __shared__ double sre[1024], sim[1024];
+  const int k = blockIdx.x;
+  double re = 0, im = 0;
+  for (int q = threadIdx.x; q < nvalid; q += blockDim.x) {
+    double pr = 0, pi = 0;
+    for (int b = 0; b < nparts; ++b) {
+      const cplx v = kpart[((int64_t)b * n_stiff + k) * Fc + q];
+      pr += v.x;
+      pi += v.y;
+    }
+    const double m = msc ? msc[q] : 1.0;
+    re = fma(m, pr, re);
+    im = fma(m, pi, im);
+  }
+  sre[threadIdx.x] = re;
+  sim[threadIdx.x] = im;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      sre[threadIdx.x] += sre[threadIdx.x + s];
+      sim[threadIdx.x] += sim[threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[k] = make_double2(sre[0], sim[0]);
+}
+
 __global__ void k_reduce(const cplx* __restrict__ partial, int nparts, int n_stiff, const cplx* __restrict__ t_q,
                          CoefPack e, const double* __restrict__ loss_terms, int nvalid, int64_t Fc,
                          cplx* __restrict__ w_out, double* __restrict__ loss_out) {
@@ -2900,8 +2979,13 @@ void launch_residual(int mode, int rhs, const ResidDesc& d, const double2* X, in
   a.K = d.K; a.M = d.M; a.freqs = d.freqs; a.data = d.data; a.data_stride = d.data_stride; a.nvalid = d.nvalid;
   a.rhsP = d.rhsP; a.beta_re = d.beta_re; a.beta_im = d.beta_im; a.mass_sum = d.mass_sum;
   a.B = d.B; a.b_stride = d.b_stride; a.perm = d.perm; a.G = d.G; a.walk = d.walk;
+  a.se = d.se; a.kpart = d.kpart;
   const dim3 g((unsigned)residual_parts(d.n), (unsigned)(Fc / 64)), b(256);
-  if (mode == 0 && rhs == 0 && Mu) LAUNCH((k_residual<0, 0, true>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
+  if (mode == 0 && rhs == 0 && Mu && d.kpart && d.n_stiff == 12)
+    LAUNCH((k_residual<0, 0, true, 12>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
+  else if (mode == 0 && rhs == 0 && Mu && d.kpart && d.n_stiff == 18)
+    LAUNCH((k_residual<0, 0, true, 18>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
+  else if (mode == 0 && rhs == 0 && Mu) LAUNCH((k_residual<0, 0, true>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
   else if (mode == 0 && rhs == 0) LAUNCH((k_residual<0, 0>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
   else if (mode == 0) LAUNCH((k_residual<0, 2>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
   else if (rhs == 1) LAUNCH((k_residual<1, 1>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
@@ -2972,6 +3056,11 @@ void launch_contract_eg(const int4* ent, int nent, const double* se, int n_stiff
 void launch_rhs_dot(const int* sup, const double* val, int n_sup, const double2* Lam, int64_t Fc, double2* t_out,
                     hipStream_t st, const double* msc) {
   LAUNCH(k_rhs_dot, dim3((unsigned)((Fc + 63) / 64)), dim3(64), st, sup, val, n_sup, Lam, Fc, msc, t_out);
+}
+
+void launch_reduce_q(const double2* kpart, int nparts, int n_stiff, const double* msc, int nvalid, int64_t Fc,
+                     double2* partial, hipStream_t st) {
+  LAUNCH(k_reduce_q, dim3(n_stiff), dim3(1024), st, kpart, nparts, n_stiff, msc, nvalid, Fc, partial);
 }
 
 void launch_reduce(const double2* partial, int nparts, int n_stiff, const double2* t_q, const CoefPack& e,

@@ -139,10 +139,18 @@ struct ResidDesc {
   const int* perm = nullptr;
   const double2* G = nullptr;
   const int* walk = nullptr;   // the n rows (permuted numbering) in walk order
+  // the gradient contraction fused into the forward walk (mode 0, rhs 0, Mu != NULL): stiffness values
+  // nz-major (n_stiff 12 or 18 per nz) and the per (workgroup, k, frequency) output
+  const double* se = nullptr;
+  int n_stiff = 0;
+  double2* kpart = nullptr;
 };
 // Mu != NULL (mode 0, rhs 0): also the functional-correction dot products sum_p Mu_p r_p, one partial
 // per workgroup and frequency in cpart (residual_parts(n) x Fc), summed by launch_correct_finish
 int residual_parts(int n);
+// partial[k] = sum_q msc[q] sum_b kpart[b][k][q] (msc NULL: 1): the fused walk's contraction as one part
+void launch_reduce_q(const double2* kpart, int nparts, int n_stiff, const double* msc, int nvalid, int64_t Fc,
+                     double2* partial, hipStream_t st);
 void launch_residual(int mode, int rhs, const ResidDesc& d, const double2* X, int64_t Fc, double2* R, double* acc,
                      hipStream_t st, const double2* Mu = nullptr, double2* cpart = nullptr);
 // corrected fr (fr_out, global index; may be NULL), loss terms and cotangent scales of a chunk
