@@ -244,7 +244,12 @@ class _Engine:
         if self.n_stiff == 18:
             return v
         out = torch.zeros(v.shape[:-1] + (18,), dtype=v.dtype, device=v.device)
-        out[..., torch.as_tensor(self.kidx, device=v.device)] = v
+        # the index on the device once: a per-call host->device copy of it blocked the host until the
+        # sweep had finished, so the small kernels after the sweep were only enqueued then
+        key = str(v.device)
+        if getattr(self, "_kidx_dev", (None, None))[0] != key:
+            self._kidx_dev = (key, torch.as_tensor(self.kidx, device=v.device))
+        out[..., self._kidx_dev[1]] = v
         return out
 
     def set_coefficients(self, c: np.ndarray):
