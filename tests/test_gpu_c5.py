@@ -8,9 +8,11 @@
   Tolerance: the GPU gradient matches the oracle's to ~5e-7 at C3 (tests/test_gpu_fullsize.py), and
   the badly identified directions (E2, nu12, b2..b4: docs in DESIGN.md section 7 / profiles/r03
   c5_identifiability.json) carry gradient components of ~1e-6 of the largest, so the quasi-Newton
-  steps agree closely (measured 4.3e-9 in x); x within 1e-7, f within 1e-6 of the starting loss (the losses fall ~100x
-  over the iterations, and each side's fr carries its own ~1e-7 error, so late losses differ by more
-  than 1e-6 relative to themselves: measured 5.5e-6).
+  steps agree closely (measured 4.3e-9 in x); x within 1e-7; the GPU loss at each GPU iterate within 1e-6
+  of the starting loss of the oracle's loss at the same point (the losses fall ~100x over the iterations,
+  and each side's fr carries its own ~1e-7 error, so late losses differ by more than 1e-6 relative to
+  themselves: measured 5.5e-6; comparing the two trajectories' losses instead adds the loss change
+  across their ~1e-8 differences in x, which measured up to 1.2e-6 of the starting loss).
 (The reference has no L-BFGS; its optimisers' trajectories are pinned at ny = 3 in
 tests/test_gpu_reference_run.py.)
 """
@@ -61,14 +63,18 @@ def test_c5_full_mesh_iterates_match_oracle_driven(c5):
     ref = c5.solveForward(freqs)
     th0 = np.asarray(c5.parameters) * (1 + REL0)
     runs = []
-    for f in (c5.getLossFunction(freqs, ref, "MSE_LOG_AFC", th0),
-              oracle_loss_fn(oracle_for(c5), freqs, ref, "MSE_LOG_AFC", scaling=th0, n_workers=8)):
+    orc_fn = oracle_loss_fn(oracle_for(c5), freqs, ref, "MSE_LOG_AFC", scaling=th0, n_workers=8)
+    for f in (c5.getLossFunction(freqs, ref, "MSE_LOG_AFC", th0), orc_fn):
         res = Optimizers.optimize_lbfgs(f, np.ones(8), N_steps=3)
         runs.append((np.array([np.asarray(v, dtype=np.float64) for v in res.x_history + [res.x]]),
                      np.array([float(v) for v in res.f_history + [res.f]])))
     (xg, fg), (xo, fo) = runs
+    # the GPU losses against the oracle's at the SAME points (the GPU iterates): the loss functions agree,
+    # independently of how the two trajectories' ~1e-8 differences in x move the losses
+    fo_at_xg = np.array([float(orc_fn(torch.as_tensor(x))) for x in xg])
     report("c5_full_mesh_vs_oracle", x_max_abs=np.max(np.abs(xg - xo)) if xg.shape == xo.shape else -1.0,
-           f_max_rel=np.max(np.abs(fg / fo - 1)) if fg.shape == fo.shape else -1.0)
+           f_max_rel=np.max(np.abs(fg / fo - 1)) if fg.shape == fo.shape else -1.0,
+           f_same_x_max_abs=float(np.max(np.abs(fg - fo_at_xg))), f0=float(fo_at_xg[0]))
     assert xg.shape == xo.shape and len(xg) >= 3
     assert np.max(np.abs(xg - xo)) < 1e-7
-    assert np.max(np.abs(fg - fo)) < 1e-6 * fo[0]
+    assert np.max(np.abs(fg - fo_at_xg)) < 1e-6 * fo_at_xg[0]
