@@ -242,20 +242,21 @@ def main():
     freqs, ref, lo, hi, step = workload(n_total)
     eng = prob.engine()
     solver = eng.solver
-    # timed region: per-phase HIP events only (bracketing every launch costs host time that delays
-    # the second lane's launches); per-launch events in one extra untimed step afterwards
-    eng.set_timing(True, kernels=False)
-    phase = np.zeros(5)
+    # timed region: no device timing at all; per-phase HIP events in one extra untimed step, per-launch
+    # events (which cost host time that delays the second lane's launches) in another
+    eng.set_timing(False)
     n_coll0 = pdist.N_COLLECTIVES
     last = {}
 
     def step_acc():
         last["val"], last["grad"] = step()
-        phase[:] += eng.last_timings()
 
     elapsed = timed(step_acc, args.steps, args.warmup, world, device)
-    phase *= 1.0 / (args.steps + args.warmup)
     collectives = (pdist.N_COLLECTIVES - n_coll0) / (args.steps + args.warmup)
+    eng.set_timing(True, kernels=False)
+    step()
+    torch.cuda.synchronize()
+    phase = np.asarray(eng.last_timings(), dtype=np.float64)
     val = last["val"]
     # backward errors of the last timed step's solves (checked on the device in every sweep)
     berr = eng.last_berr.cpu().numpy()

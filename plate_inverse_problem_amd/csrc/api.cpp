@@ -1605,7 +1605,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
       }
       if (reverse) {
         pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st, msc);
-        pfr::launch_reduce(s->partial, cwalk ? 1 : pfr::contract_eg_parts(s->n_uent), s->n_stiff, s->tq, s->e,
+        pfr::launch_reduce(s->partial, cwalk ? (int)(Fc / 64) : pfr::contract_eg_parts(s->n_uent), s->n_stiff, s->tq, s->e,
                            s->loss_terms, nv, Fc, reinterpret_cast<double2*>(w_dev), loss_dev, st);
       }
     } else {

@@ -2669,36 +2669,37 @@ __global__ void k_rhs_dot(const int* __restrict__ sup, const double* __restrict_
 
 // Deterministic reduction over (blocks, valid frequencies):
 //   w[k] += sum_q ( -sum_blk partial[blk][k][q] + e_k * t_q ),  loss += sum_q loss_terms[q]
-// partial[k] = sum_q m_q sum_b kpart[b][k][q] (fixed order): the fused walk's contraction in
-// k_contract_eg's partial layout (one part), so that k_reduce completes it unchanged
-__global__ __launch_bounds__(1024) void k_reduce_q(const cplx* __restrict__ kpart, int nparts, int n_stiff,
-                                                   const double* __restrict__ msc, int nvalid, int64_t Fc,
-                                                   cplx* __restrict__ partial) {
-  __shared__ double sre[1024], sim[1024];
-  const int k = blockIdx.x;
-  double re = 0, im = 0;
-  for (int q = threadIdx.x; q < nvalid; q += blockDim.x) {
-    double pr = 0, pi = 0;
-    for (int b = 0; b < nparts; ++b) {
-      const cplx v = kpart[((int64_t)b * n_stiff + k) * Fc + q];
-      pr += v.x;
-      pi += v.y;
-    }
-    const double m = msc ? msc[q] : 1.0;
-    re = fma(m, pr, re);
-    im = fma(m, pi, im);
+// partial[t * n_stiff + k] = sum_{q in tile t} m_q sum_b kpart[b][k][q] (fixed order; tile = 64 frequencies):
+// the fused walk's contraction in k_contract_eg's partial layout (one part per tile), so that k_reduce
+// completes it unchanged.  Block = (k, tile), 4 waves splitting the workgroup partials b.
+__global__ __launch_bounds__(256) void k_reduce_q(const cplx* __restrict__ kpart, int nparts, int n_stiff,
+                                                  const double* __restrict__ msc, int nvalid, int64_t Fc,
+                                                  cplx* __restrict__ partial) {
+  __shared__ double sre[4][64], sim[4][64];
+  const int k = blockIdx.x, tile = blockIdx.y;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t q = (int64_t)tile * 64 + lane;
+  double pr = 0, pi = 0;
+#pragma unroll 8
+  for (int b = w; b < nparts; b += 4) {
+    const cplx v = kpart[((int64_t)b * n_stiff + k) * Fc + q];
+    pr += v.x;
+    pi += v.y;
   }
-  sre[threadIdx.x] = re;
-  sim[threadIdx.x] = im;
+  sre[w][lane] = pr;
+  sim[w][lane] = pi;
   __syncthreads();
-  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-    if (threadIdx.x < s) {
-      sre[threadIdx.x] += sre[threadIdx.x + s];
-      sim[threadIdx.x] += sim[threadIdx.x + s];
+  if (w == 0) {
+    const double m = q < nvalid ? (msc ? msc[q] : 1.0) : 0.0;
+    double re = m * ((sre[0][lane] + sre[1][lane]) + (sre[2][lane] + sre[3][lane]));
+    double im = m * ((sim[0][lane] + sim[1][lane]) + (sim[2][lane] + sim[3][lane]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      re += __shfl_xor(re, o);
+      im += __shfl_xor(im, o);
     }
-    __syncthreads();
+    if (lane == 0) partial[(int64_t)tile * n_stiff + k] = make_double2(re, im);
   }
-  if (threadIdx.x == 0) partial[k] = make_double2(sre[0], sim[0]);
 }
 
 __global__ void k_reduce(const cplx* __restrict__ partial, int nparts, int n_stiff, const cplx* __restrict__ t_q,
@@ -3060,7 +3061,7 @@ void launch_rhs_dot(const int* sup, const double* val, int n_sup, const double2*
 
 void launch_reduce_q(const double2* kpart, int nparts, int n_stiff, const double* msc, int nvalid, int64_t Fc,
                      double2* partial, hipStream_t st) {
-  LAUNCH(k_reduce_q, dim3(n_stiff), dim3(1024), st, kpart, nparts, n_stiff, msc, nvalid, Fc, partial);
+  LAUNCH(k_reduce_q, dim3(n_stiff, (unsigned)(Fc / 64)), dim3(256), st, kpart, nparts, n_stiff, msc, nvalid, Fc, partial);
 }
 
 void launch_reduce(const double2* partial, int nparts, int n_stiff, const double2* t_q, const CoefPack& e,

@@ -148,7 +148,8 @@ struct ResidDesc {
 // Mu != NULL (mode 0, rhs 0): also the functional-correction dot products sum_p Mu_p r_p, one partial
 // per workgroup and frequency in cpart (residual_parts(n) x Fc), summed by launch_correct_finish
 int residual_parts(int n);
-// partial[k] = sum_q msc[q] sum_b kpart[b][k][q] (msc NULL: 1): the fused walk's contraction as one part
+// partial[t * n_stiff + k] = sum_{q in tile t} msc[q] sum_b kpart[b][k][q] (msc NULL: 1; tiles of 64
+// frequencies): the fused walk's contraction as Fc / 64 parts
 void launch_reduce_q(const double2* kpart, int nparts, int n_stiff, const double* msc, int nvalid, int64_t Fc,
                      double2* partial, hipStream_t st);
 void launch_residual(int mode, int rhs, const ResidDesc& d, const double2* X, int64_t Fc, double2* R, double* acc,
