@@ -188,8 +188,9 @@ struct pfr_solver {
   int solve_wmax = 8, fac_wmax = 16, us2_small = 110;
   int off_small = 1;                    // PFR_OFF_SMALL: no-prefix off-diagonal variant on levels of ns <= 8
   int fac_lds_qf = 1;                   // PFR_FAC_LDS_QF: frequencies per k_factor_sym_lds workgroup (1, 2 or 4)
-  int fac_lds = 0;                      // PFR_FAC_LDS: which levels factor A11 in LDS (k_factor_sym_lds): n > 0
+  int fac_lds = -1;                     // PFR_FAC_LDS: which levels factor A11 in LDS (k_factor_sym_lds): n > 0
                                         // those whose largest pivot block has at least n pivots, 0 none, -1 auto
+                                        // (default since round 3: 512-frequency sweeps +2.6 %, 4,096 unchanged)
   int fac_lds_wg = 160;                 // PFR_FAC_LDS_WG: auto mode threshold (workgroups of k_factor_sym)
   int split_target = 256;               // PFR_SOLVE_SPLIT: solve launches with fewer (front, group) workgroups
                                         // than this (one per CU) split their update parts up to about this
@@ -325,8 +326,8 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
         1, s->sym ? std::min<int64_t>(fac_wmax, wfill) : std::min<int64_t>(s->level_W[l], wfill));
     // A11 in LDS: PFR_FAC_LDS = n > 0: levels whose largest pivot block has >= n pivots; -1: levels on which the
     // global-memory kernel would get fewer than PFR_FAC_LDS_WG workgroups (the top of the tree in small chunks:
-    // 512 frequencies levels 10-16, 2,048 level 16 -- faster per level there, slower elsewhere; off by default:
-    // the timed sweeps do not gain)
+    // 512 frequencies levels 10-16, 2,048 level 16 -- faster per level there, slower elsewhere; the default
+    // since the MMD ordering: 512-frequency sweeps 31.8k -> 32.6k freq-solves/s, 4,096 unchanged)
     const bool lds = s->sym && s->level_maxns[l] <= 64 &&
                      (s->fac_lds > 0 ? s->level_maxns[l] >= s->fac_lds
                                      : s->fac_lds < 0 && s->level_maxns[l] >= 16 && wgs < s->fac_lds_wg);
@@ -763,7 +764,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->us2_small = knob("PFR_US2_SMALL", 110, 0, pfr::MAX_FRONT);
   s->off_small = knob("PFR_OFF_SMALL", 1, 0, 1);
   s->split_target = knob("PFR_SOLVE_SPLIT", 256, 0, 1 << 20);
-  s->fac_lds = knob("PFR_FAC_LDS", 0, -1, 64);   // LDS holds the lower triangle of up to 64 pivots x 4 frequencies
+  s->fac_lds = knob("PFR_FAC_LDS", -1, -1, 64);   // LDS holds the lower triangle of up to 64 pivots x 4 frequencies
   s->fac_lds_wg = knob("PFR_FAC_LDS_WG", 160, 0, 1 << 20);
   s->fac_lds_qf = knob("PFR_FAC_LDS_QF", 1, 1, 4);
   if (s->fac_lds_qf == 3) s->fac_lds_qf = 4;
