@@ -3,7 +3,7 @@ sys.path.insert(0, os.getcwd())
 import numpy as np, torch
 from bench import build_problem
 p = build_problem(25, torch.device("cuda", 0))
-freqs = np.linspace(40.0, 600.0, 4096)
+freqs = np.linspace(40.0, 600.0, int(os.environ.get("HP_FREQS", "4096")))
 th = p.parameters.copy()
 ref = p.solveForward(freqs, th)
 loss_fn = p.getLossFunction(freqs, ref, "MSE_LOG_AFC")
@@ -20,4 +20,4 @@ for _ in range(5): step()
 pr.disable()
 torch.cuda.synchronize()
 print("ms/step", (time.perf_counter()-t0)/5*1e3)
-pstats.Stats(pr).sort_stats("tottime").print_stats(18)
+pstats.Stats(pr).sort_stats(os.environ.get("HP_SORT", "tottime")).print_stats(30)
