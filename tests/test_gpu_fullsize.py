@@ -160,6 +160,12 @@ def test_c2_forward_sweep_matches_truth():
     {"PFR_FAC_LDS": "1"},              # every level's A11 LU through the LDS-resident kernel (1 frequency / workgroup)
     {"PFR_FAC_LDS": "1", "PFR_FAC_LDS_QF": "4"},   # ... 4 frequencies per workgroup
     {"PFR_FAC_LDS": "-1"},             # auto: the levels where k_factor_sym would get few workgroups
+    {"PFR_FAC_LDS": "0"},              # never (the global-memory A11 LU on every level)
+    {"PFR_FN_DOT": "0"},               # fr from the top-down pass over the support's fronts
+    {"PFR_CONTRACT_WALK": "0"},        # the gradient contraction as k_contract_eg's own walk
+    {"PFR_FN_DOT": "0", "PFR_CONTRACT_WALK": "0"},
+    {"PFR_LEAF_SIZE": "10000"},        # the deep MMD tree on a narrow sweep
+    {"PFR_ORDERING": "2", "PFR_LEAF_SIZE": "96", "PFR_MD_DELTA": "0"},   # the rounds 1-3 ordering
 ])
 def test_kernel_variants_match_oracle(env, monkeypatch):
     from oracle.plate_oracle import loss_and_grad
