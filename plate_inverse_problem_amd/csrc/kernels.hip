@@ -2960,11 +2960,7 @@ void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, boo
   if (rs) LAUNCH((k_usolve2_upd<true, 2, 4>), dim3(nfronts * split, ngroups), dim3(64 * SPLIT_W), st, P, lvl, F, Fc, a, b,
                  split);
   // symmetric mode only (the paired top-down pass serves the symmetric loss + gradient sweep)
-  static const int xmid = getenv("XUS2") ? atoi(getenv("XUS2")) : 0;
-  if (small && xmid == 1) LAUNCH((k_usolve2_level<true, 4, 4, 3>), g, bl, st, P, lvl, F, Fc, a, b, rs);
-  else if (small && xmid == 2) LAUNCH((k_usolve2_level<true, 4, 4, 4>), g, bl, st, P, lvl, F, Fc, a, b, rs);
-  else if (small && xmid == 3) LAUNCH((k_usolve2_level<true, 2, 8, 3>), g, bl, st, P, lvl, F, Fc, a, b, rs);
-  else if (small) LAUNCH((k_usolve2_level<true, 2, 4, 4>), g, bl, st, P, lvl, F, Fc, a, b, rs);
+  if (small) LAUNCH((k_usolve2_level<true, 2, 4, 4>), g, bl, st, P, lvl, F, Fc, a, b, rs);
   else LAUNCH((k_usolve2_level<true, 4, 8, 2>), g, bl, st, P, lvl, F, Fc, a, b, rs);
 }
 
