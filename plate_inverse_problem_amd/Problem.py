@@ -149,12 +149,13 @@ class _Engine:
         10,000 (one dissection at C3) gives the least fill and Schur-complement traffic but a deep tree
         (38 levels), whose per-level chains cost nothing when each level has thousands of workgroups
         and dominate the sparse solve passes of narrow sweeps; those get the shallower trees of more
-        dissection levels (C3, freq-solves/s: 512 frequencies 23.8k / 28.8k at leaf 10,000 / 96, 1,024
-        36.4k / 38.6k at 10,000 / 500, 2,048 50.6k / 47.2k at 10,000 / 500)."""
+        dissection levels.  C3, freq-solves/s at leaf 96 / 500 / 3,000 / 10,000 (late round 3, with the
+        functional from the bottom-up passes): 512 frequencies 32.7k / 33.0k / 31.3k / 30.5k, 1,024
+        41.1k / 42.8k / 43.5k / 44.0k, 2,048 - / 49.8k / 51.4k / 52.7k."""
         if self._leaf_env is not None:
             return self._leaf_env
         n_freqs = max(1, n_freqs)
-        return 96 if n_freqs <= 512 else 500 if n_freqs <= 1024 else 10000
+        return 96 if n_freqs <= 512 else 10000
 
     def _use_symbolic(self, n_freqs: int) -> bool:
         """Select (building once) the symbolic analysis for a sweep width; True if it changed."""
