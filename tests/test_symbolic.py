@@ -196,3 +196,54 @@ def test_last_nodes_and_max_ns_options():
     x = mf.solve_sym(mf.factor(data), b, sym, data)
     # cond(A) = 3.8e10 (kappa * u = 8e-6): the static order with the support last lands at 1.3e-10
     assert np.linalg.norm(x - np.linalg.solve(A, b)) / np.linalg.norm(x) < 1e-9
+
+
+def _bottom_up(mf, F, vec_perm):
+    """L y = v over every front (the model's symmetric bottom-up pass), v and y in permuted numbering."""
+    WV = np.zeros(int(mf.fr[:, 1].sum()), dtype=complex)
+    Y = np.zeros(mf.n, dtype=complex)
+    for lvl in mf.levels():
+        for t in lvl:
+            ns, f, row0, col0 = (int(v) for v in mf.fr[t, :4])
+            w = mf._gather(F, WV, t, vec_perm)
+            for k in range(ns):
+                w[k + 1:] -= F[t][k + 1:, k] * w[k]
+            WV[row0:row0 + f] = w
+            Y[col0:col0 + ns] = w[:ns]
+    return Y
+
+
+@pytest.mark.parametrize("leaf", [16, 10000])
+def test_functional_from_bottom_up_passes(leaf):
+    """The identity the loss sweeps use (PFR_FN_DOT, csrc/kernels.hip k_fn_dot): with A = L U,
+    U = diag(U) L^T, a^T A^-1 b = (L^-1 a)^T diag(U)^-1 (L^-1 b) -- checked on the symmetric model
+    against the model's full solve, for the accelerometer's three functional vectors."""
+    p = make_problem("orthotropic", ny=3)
+    idx, colptr, rowind = _active_pattern(p)
+    sym = _native.Symbolic(p.mat_size, colptr, rowind, leaf_size=leaf, symmetric=True)
+    orc = oracle_for(p)
+    c = orc.coefficients(p.parameters)
+    data = (orc.mass_values() * -(2 * np.pi * 233.0) ** 2 + c @ p.mats[:18])[idx]
+    mf = MFModel(sym)
+    F = mf.factor(data)
+    rng = np.random.default_rng(3)
+    b = rng.standard_normal(p.mat_size) + 1j * rng.standard_normal(p.mat_size)
+    # Dirichlet columns moved to the rhs (k_dirichlet_rhs), as the forward pass does
+    dirs, cpl = sym.export("DIRICHLET"), sym.export("COUPLING")
+    bp = b[mf.perm].astype(complex)
+    for p_i, ds, nz in cpl:
+        p_d, nz_dd = dirs[ds]
+        bp[p_i] -= data[nz] * bp[p_d] / data[nz_dd]
+    x = mf.solve_sym(F, b, sym, data)
+    yb = _bottom_up(mf, F, bp)
+    diag = np.empty(mf.n, dtype=complex)
+    for t, (ns, f, row0, col0, *_r) in enumerate(mf.fr):
+        diag[col0:col0 + ns] = np.diag(F[t])[:ns]
+    dir_rows = set(int(v) for v in dirs[:, 0])
+    for a in p.averaging_vectors():
+        ap = np.asarray(a, dtype=np.float64)[mf.perm].astype(complex)
+        assert not any(ap[r] != 0 for r in dir_rows)          # the support holds no Dirichlet node
+        wa = _bottom_up(mf, F, ap)
+        lhs = np.sum(wa * yb / diag)
+        ref = np.dot(np.asarray(a, dtype=np.float64), x)
+        assert abs(lhs - ref) <= 1e-10 * max(abs(ref), np.abs(a).sum() * np.abs(x).max())
