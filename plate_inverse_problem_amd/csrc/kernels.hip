@@ -47,7 +47,10 @@ __device__ __forceinline__ void pivot_check(cplx p, int* flags, int64_t q) {
 }
 
 constexpr int KB = 4;    // factorisation pivot block
-constexpr int KBS = 8;   // triangular-solve block (its lower triangle: 28 loads, all in flight)
+#ifndef PFR_KBS
+#define PFR_KBS 8
+#endif
+constexpr int KBS = PFR_KBS;   // triangular-solve block (its lower triangle: 28 loads, all in flight)
 
 // ------------------------------------------------------------------ helpers
 // XCD-aware workgroup order: the dispatcher deals workgroups round-robin over
