@@ -1999,13 +1999,16 @@ __device__ __forceinline__ cplx resid_entry(const ResidArgs& A, const cplx* __re
   return dq[nz];
 }
 
+#ifndef PFR_RES_WPE
+#define PFR_RES_WPE 5   // the fused walk at 96 VGPRs (5 waves/SIMD): its phase 9.5 -> 8.0 ms per step, lane-summed
+#endif
 // NSK > 0 (with DOT, the loss sweep's forward walk under the functional correction): the gradient
 // contraction rides on the walk -- every entry (p, j, nz) it visits has x_j gathered and mu_p loaded
 // already, so s_k(q) += S_k(nz) mu_p x_j per lane (frequency), per workgroup; the loss cotangent scale
 // m_q is only known after this walk (k_correct_finish), so the partials stay per frequency and
 // k_reduce_q applies m_q.  Replaces k_contract_eg's separate entry walk.
 template <int MODE, int RHS, bool DOT = false, int NSK = 0>
-__global__ __launch_bounds__(256) void k_residual(ResidArgs A, const cplx* __restrict__ X, int64_t Fc,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSK > 0 ? PFR_RES_WPE : 1))) void k_residual(ResidArgs A, const cplx* __restrict__ X, int64_t Fc,
                                                   cplx* __restrict__ R, double* __restrict__ acc,
                                                   const cplx* __restrict__ Mu, cplx* __restrict__ cpart) {
   // XCD-aware order: the workgroups of one 64-frequency group run together on one XCD, so the
