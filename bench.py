@@ -17,10 +17,10 @@ sharded across the N GPUs.
 * ``value`` = all frequencies of all ranks / (max-over-ranks seconds per step);
 * each GPU runs ``lanes`` (default 2) solvers on their own HIP streams over
   contiguous halves of its frequencies, concurrently;
-* ``roofline``: the dominant kernel class by device time -- at C3 ``k_schur_sym_blk``
-  (Schur complement of the large update blocks of the multifrontal factorisation;
-  HBM-bound): algorithmic bytes per launch (the solver's count: A22 stores +
-  gathered children's entries + L21 read once, 16 B per complex entry) / average
+* ``roofline``: the dominant kernel class by device time -- at C3 with the MMD ordering
+  ``k_offdiag_level`` (the L21 rows of the multifrontal factorisation, HBM-bound; within a few
+  % of ``k_schur_sym_blk``): algorithmic bytes per launch (the solver's count: L21 stores +
+  gathered children's entries + L11/U11 read, 16 B per complex entry) / average
   launch time, from HIP events that libpfr records around every launch on the
   lane's stream during one isolated lane-0 sweep of a full chunk right after the
   timed region (inside the timed region the lanes overlap, so a launch's duration
@@ -258,7 +258,8 @@ def main():
     torch.cuda.synchronize()
     phase = np.asarray(eng.last_timings(), dtype=np.float64)
     val = last["val"]
-    # backward errors of the last timed step's solves (checked on the device in every sweep)
+    # backward errors of the solves of this untimed step (same workload and theta as the timed steps;
+    # checked on the device in every sweep)
     berr = eng.last_berr.cpu().numpy()
     check = {"measure": "componentwise backward error max_i |b - A x|_i / (|A||x| + |b|)_i per frequency "
                         "(UMFPACK's omega1), on the device in every sweep",

@@ -177,9 +177,10 @@ PFR_API int pfr_matvec(pfr_solver* s, int32_t batch, const double* data_dev, int
 /* K_out_dev = sum_k coef_k * S_k  (S registered by pfr_set_stiffness), complex nnz.  n_stiff is 18
  * (A, B, D coefficient matrices of Problem.py:440-445) or 12 (A and D only: the B coefficients vanish
  * for mid-plane symmetric laminates, so their matrices and gradient partials are left out).
- * pfr_set_stiffness registers stiff_dev for pfr_combine (read at every call) AND takes a copy of its
- * values for the gradient contraction: after the caller changes the buffer's values it must call
- * pfr_set_stiffness again (the call returns once the copy is made). */
+ * pfr_set_stiffness registers stiff_dev: pfr_combine, the Hessian sweep and the gradient contraction of
+ * every loss sweep (fused into the forward residual walk by default) read it at every call, so the
+ * buffer must stay alive and unchanged while the solver uses it (an entry-ordered copy is also taken
+ * for the k_contract_eg path; after changing the values, call pfr_set_stiffness again). */
 PFR_API int pfr_set_stiffness(pfr_solver* s, int32_t n_stiff, const double* stiff_dev /* (nnz, n_stiff) */,
                               const double* rhs_weights /* host, n_stiff: e_k */);
 PFR_API int pfr_combine(pfr_solver* s, const double* coef /* host complex n_stiff */, double* K_out_dev,
@@ -226,7 +227,9 @@ PFR_API int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_
  * in symmetric mode inside the paired top-down pass -- and the forward residual walk (the forward
  * check) accumulates the correction; in a loss sweep that adjoint is the loss adjoint up to one
  * scalar per frequency, so the correction costs only the residual walk.  pfr_hessian_sweep applies
- * the correction (its loss and gradient equal pfr_sweep's), not the checks. */
+ * the correction to its loss and gradient (they equal pfr_sweep's), not the checks; its second-order
+ * seeds (the directional derivatives of the loss cotangent) are formed from the uncorrected fr, so its
+ * Hessian is that of the uncorrected functional (the two differ by the solve's first-order error). */
 PFR_API int pfr_set_check(pfr_solver* s, int32_t mode, double tol, double* berr_dev);
 
 /* Per-phase device times [ms] of the last pfr_sweep/pfr_solve call on this solver, measured with HIP

@@ -167,15 +167,19 @@ class _Engine:
         self.stats = self.sym.stats()
         return changed
 
+    def _lanes_for(self, n_freqs: int) -> int:
+        """Solver lanes for a sweep of ``n_freqs``: a lane per 512 frequencies at most -- below that a
+        sweep is latency-bound (top-level fronts) and a second lane only adds its own chains (C4's
+        512-frequency share: 1 lane 27.1k, 2 lanes 26.4k freq-solves/s; 1,024: 2 lanes 4 % faster;
+        profiles/r03)."""
+        return max(1, min(self._lanes_req, -(-max(1, n_freqs) // 512)))
+
     def _shape_for(self, n_freqs: int):
         """(lanes, frequencies per chunk) for a sweep of ``n_freqs``: up to ``lanes`` lanes of at
         least 64 frequencies; per lane as many frequencies per chunk as fit in its share of ~85 %
         of the free HBM (multiple of 64, <= 4096), in even chunks."""
         n_freqs = max(1, n_freqs)
-        # a lane per 512 frequencies at most: below that a sweep is latency-bound (top-level fronts) and a
-        # second lane only adds its own chains (C4's 512-frequency share: 1 lane 27.1k, 2 lanes 26.4k
-        # freq-solves/s; 1,024: 2 lanes 4 % faster; profiles/r03)
-        n_lanes = max(1, min(self._lanes_req, -(-n_freqs // 512)))
+        n_lanes = self._lanes_for(n_freqs)
         if self._fixed_batch:
             return n_lanes, int(self._fixed_batch)
         per_lane = -(-n_freqs // n_lanes)
@@ -189,11 +193,13 @@ class _Engine:
         """Size the lanes for a sweep of ``n_freqs`` frequencies.  The solvers are rebuilt only when
         the sweep needs more lanes or larger chunks than the current ones have (a small first call
         must not pin 1 lane and 64-frequency chunks on every later large sweep); smaller sweeps run
-        on the existing solvers."""
+        on the existing solvers -- with their lanes and their ordering: the widest sweep so far fixes the
+        elimination tree (a C4 rank, whose engine is first sized for its 512-frequency share, gets the
+        shallow narrow-sweep tree; a 512-frequency sweep after a 4,096-frequency one runs on the deep
+        tree, correct but slower)."""
         if self.solvers:
             per_lane = -(-max(1, n_freqs) // self.n_lanes)
-            if n_freqs in self._sized_for or (min(self._lanes_req, -(-max(1, n_freqs) // 64)) <= self.n_lanes
-                                              and per_lane <= self.max_batch):
+            if n_freqs in self._sized_for or (self._lanes_for(n_freqs) <= self.n_lanes and per_lane <= self.max_batch):
                 return
         self._sized_for.add(n_freqs)
         old = self.sym

@@ -1298,7 +1298,10 @@ int pfr_set_stiffness(pfr_solver* s, int32_t n_stiff, const double* stiff_dev, c
   for (int k = 0; k < n_stiff; ++k) s->e.re[k] = w[k];
   HIP_TRY(hipSetDevice(s->device));
   if (!s->partial) {
-    int rc = s->alloc(&s->partial, (int64_t)pfr::contract_eg_parts(s->n_uent) * 18);
+    // written by k_contract_eg (contract_eg_parts(n_uent) parts) and by k_reduce_q (one part per 64-frequency
+    // tile of the chunk: Fc / 64), 18 partials each
+    const int64_t parts = std::max<int64_t>(pfr::contract_eg_parts(s->n_uent), s->Fc / 64);
+    int rc = s->alloc(&s->partial, parts * 18);
     if (rc) return rc;
   }
   if (!s->d_se) {
