@@ -8,11 +8,17 @@
   Tolerance: the GPU gradient matches the oracle's to ~5e-7 at C3 (tests/test_gpu_fullsize.py), and
   the badly identified directions (E2, nu12, b2..b4: docs in DESIGN.md section 7 / profiles/r03
   c5_identifiability.json) carry gradient components of ~1e-6 of the largest, so the quasi-Newton
-  steps agree closely (measured 4.3e-9 in x); x within 1e-7; the GPU loss at each GPU iterate within 1e-6
-  of the starting loss of the oracle's loss at the same point (the losses fall ~100x over the iterations,
-  and each side's fr carries its own ~1e-7 error, so late losses differ by more than 1e-6 relative to
-  themselves: measured 5.5e-6; comparing the two trajectories' losses instead adds the loss change
-  across their ~1e-8 differences in x, which measured up to 1.2e-6 of the starting loss).
+  steps agree closely (measured 4.3e-9 in x); x within 1e-7.
+* the losses, per iterate and relative to THAT iterate's loss: MSE_LOG_AFC is the mean of d_q^2 with
+  d_q = log fr_q - log |ref_q|, so relative fr errors e_q on the two sides move a term by at most
+  2 |d_q| (e_gpu + e_orc) + (e_gpu + e_orc)^2.  With the fr errors measured against the
+  extended-precision truth at C3 (GPU with the functional correction <= 1e-7, the oracle's refined
+  SuperLU <= 1.7e-7: tests/golden/c3_grad_truth.npz) the GPU loss at each GPU iterate must lie within
+  mean_q [2 |d_q| 3e-7 + 9e-14] of the oracle's loss at the same point -- a per-iterate bound that
+  tightens as the fit converges, ~4e-5 of the loss at the last iterates here (|d_q| ~ 1e-2), where a
+  fixed 1e-6 would be below what the two fp64 solvers determine about a loss that is a small
+  difference; and the two trajectories' loss histories within that bound plus 1e-7 relative (their x
+  differ by ~1e-8).
 (The reference has no L-BFGS; its optimisers' trajectories are pinned at ny = 3 in
 tests/test_gpu_reference_run.py.)
 """
@@ -72,9 +78,17 @@ def test_c5_full_mesh_iterates_match_oracle_driven(c5):
     # the GPU losses against the oracle's at the SAME points (the GPU iterates): the loss functions agree,
     # independently of how the two trajectories' ~1e-8 differences in x move the losses
     fo_at_xg = np.array([float(orc_fn(torch.as_tensor(x))) for x in xg])
+    # per-iterate bound from the two sides' fr errors (docstring): d_q from the GPU fr at each iterate
+    E_FR = 1e-7 + 1.7e-7
+    bound = np.array([np.mean(2 * np.abs(np.log(c5.solveForward(freqs, x * th0)) - np.log(np.abs(ref))) * E_FR
+                              + E_FR ** 2) for x in xg])
+    rel_same_x = np.abs(fg - fo_at_xg) / fo_at_xg
     report("c5_full_mesh_vs_oracle", x_max_abs=np.max(np.abs(xg - xo)) if xg.shape == xo.shape else -1.0,
            f_max_rel=np.max(np.abs(fg / fo - 1)) if fg.shape == fo.shape else -1.0,
-           f_same_x_max_abs=float(np.max(np.abs(fg - fo_at_xg))), f0=float(fo_at_xg[0]))
+           f_same_x_max_abs=float(np.max(np.abs(fg - fo_at_xg))), f0=float(fo_at_xg[0]),
+           f_same_x_max_rel=float(rel_same_x.max()), bound_max_rel=float(np.max(bound / fo_at_xg)),
+           f_same_x_over_bound=float(np.max(np.abs(fg - fo_at_xg) / bound)))
     assert xg.shape == xo.shape and len(xg) >= 3
     assert np.max(np.abs(xg - xo)) < 1e-7
-    assert np.max(np.abs(fg - fo_at_xg)) < 1e-6 * fo_at_xg[0]
+    assert np.all(np.abs(fg - fo_at_xg) <= bound), (np.abs(fg - fo_at_xg), bound)
+    assert np.all(np.abs(fg - fo) <= bound + 1e-7 * fo), (np.abs(fg - fo), bound)
