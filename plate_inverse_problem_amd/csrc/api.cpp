@@ -79,6 +79,9 @@ struct pfr_solver {
   int32_t* d_asm_xp = nullptr;          // per 8-record chunk: range of further child sources in d_asm_x
   int2* d_asm_x = nullptr;              // (record within chunk, child element id)
   std::vector<int32_t> asm_ptr;         // record offset of each level (multiple of 8)
+  int32_t* d_rec0 = nullptr;            // per front: its first A11 assembly record (fused assembly)
+  int fuse_asm = 1;                     // PFR_FUSE_ASM: A11 gathered by k_factor_sym itself (symmetric mode,
+                                        // levels on the global-memory A11 LU)
   int32_t* d_colptr = nullptr;
   int32_t* d_rowind = nullptr;
   // symmetric mode (options.symmetric): U never formed; Dirichlet nodes decoupled
@@ -180,6 +183,8 @@ struct pfr_solver {
   std::vector<ChunkEvents> tev;
   int n_tev = 0;                        // chunks recorded by the last call
   int64_t alg_bytes[5]{};               // algorithmic HBM bytes per frequency of each class (one sweep)
+  // per level: A11 assembly, A11 LU, and the fused class (children's entries gathered + L11 / U11 written)
+  std::vector<int64_t> lev_asm_bytes, lev_lu_bytes, lev_fused_bytes;
   // launch-shape tuning knobs, read from the environment when the solver is created (so that a
   // process can build solvers with different settings, e.g. tests forcing each kernel variant):
   // PFR_SOLVE_WMAX (waves per solve workgroup, at most), PFR_FAC_WMAX (waves per A11 LU
@@ -298,6 +303,21 @@ int solve_split(const pfr_solver* s, int nf) {
   return (int)std::min<int64_t>(16, (s->split_target + wgs - 1) / wgs);
 }
 
+// A11 of level l factored in LDS (k_factor_sym_lds): PFR_FAC_LDS = n > 0: levels whose largest pivot block has
+// >= n pivots; -1: levels on which the global-memory kernel would get fewer than PFR_FAC_LDS_WG workgroups (the
+// top of the tree in small chunks: 512 frequencies levels 10-16, 2,048 level 16 -- faster per level there, slower
+// elsewhere; the default since the MMD ordering: 512-frequency sweeps 31.8k -> 32.6k freq-solves/s, 4,096
+// unchanged)
+bool level_lds(const pfr_solver* s, int l) {
+  const int64_t wgs = (int64_t)(s->level_ptr[l + 1] - s->level_ptr[l]) * (s->Fc / 64) * pfr::FAC_G;
+  return s->sym && s->level_maxns[l] <= 64 &&
+         (s->fac_lds > 0 ? s->level_maxns[l] >= s->fac_lds
+                         : s->fac_lds < 0 && s->level_maxns[l] >= 16 && wgs < s->fac_lds_wg);
+}
+
+// A11 of level l gathered by k_factor_sym itself (PFR_FUSE_ASM; operator-form sweeps of a symmetric analysis)
+bool level_fused(const pfr_solver* s, int l, int mode) { return s->sym && s->fuse_asm && mode == 0 && !level_lds(s, l); }
+
 // after_panel(l): called once level l's L21 panel is launched (its L factor complete in stream order)
 int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nvalid, hipStream_t st,
                const std::function<void(int)>& after_panel = nullptr) {
@@ -311,10 +331,6 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
   for (int l = 0; l < L; ++l) {
     int nf = s->level_ptr[l + 1] - s->level_ptr[l];
     mark(l, 0);
-    pfr::launch_assemble(mode, s->d_asm + s->asm_ptr[l], s->asm_ptr[l + 1] - s->asm_ptr[l],
-                         s->d_asm_xp + s->asm_ptr[l] / 8, s->d_asm_x, ngroups, s->F, s->Fc, s->freqs, s->K, s->M,
-                         data, ds, nvalid, st);
-    mark(l, 1);
     // panel: enough workgroups (front x 16 frequencies) to fill the chip -> one wave
     // each (no idle waves at the block barriers); few large fronts -> more waves
     // (symmetric kernel: up to 16 waves -- the top levels' few fronts are latency-bound, every
@@ -328,14 +344,30 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     // global-memory kernel would get fewer than PFR_FAC_LDS_WG workgroups (the top of the tree in small chunks:
     // 512 frequencies levels 10-16, 2,048 level 16 -- faster per level there, slower elsewhere; the default
     // since the MMD ordering: 512-frequency sweeps 31.8k -> 32.6k freq-solves/s, 4,096 unchanged)
-    const bool lds = s->sym && s->level_maxns[l] <= 64 &&
-                     (s->fac_lds > 0 ? s->level_maxns[l] >= s->fac_lds
-                                     : s->fac_lds < 0 && s->level_maxns[l] >= 16 && wgs < s->fac_lds_wg);
+    const bool lds = level_lds(s, l);
+    // the A11 assembly fused into the global-memory LU (k_factor_sym gathers its own pivot block)
+    const bool fused = level_fused(s, l, mode);
+    if (!fused)
+      pfr::launch_assemble(mode, s->d_asm + s->asm_ptr[l], s->asm_ptr[l + 1] - s->asm_ptr[l],
+                           s->d_asm_xp + s->asm_ptr[l] / 8, s->d_asm_x, ngroups, s->F, s->Fc, s->freqs, s->K, s->M,
+                           data, ds, nvalid, st);
+    mark(l, 1);
+    pfr::AsmArgs asmb;
+    if (fused) {
+      asmb.recs = s->d_asm;
+      asmb.rec0 = s->d_rec0;
+      asmb.xptr = s->d_asm_xp;
+      asmb.xl = s->d_asm_x;
+      asmb.freqs = s->freqs;
+      asmb.K = s->K;
+      asmb.M = s->M;
+    }
     if (lds)
       pfr::launch_factor_lds(s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_maxns[l], s->fac_lds_qf, s->F, s->Fc,
                              s->flags, st);
     else
-      pfr::launch_factor(s->sym, s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st);
+      pfr::launch_factor(s->sym, s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st,
+                         asmb);
     mark(l, 2);
     pfr::launch_offdiag(mode, s->P, s->d_items + s->item_ptr[l], s->item_ptr[l + 1] - s->item_ptr[l], s->d_orec,
                         s->d_oxp + s->item_ptr[l], s->d_ox, ngroups, s->F, s->Fc, s->freqs, s->K, s->M, data, ds,
@@ -770,7 +802,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   if (s->fac_lds_qf == 3) s->fac_lds_qf = 4;
   s->check_fused = knob("PFR_CHECK_FUSED", 0, 0, 1);   // measured 2.3 ms against 2 x 0.87 ms per 2,048-frequency chunk
   s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);
-  s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);   // functional from the bottom-up passes (symmetric paired sweeps)
+  s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);
+  s->fuse_asm = knob("PFR_FUSE_ASM", 1, 0, 1);   // functional from the bottom-up passes (symmetric paired sweeps)
   s->n = S.n;
   s->nnz = S.nnz;
   s->Fc = round64(max_batch);
@@ -925,7 +958,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     std::vector<int2> ax, orec, ox;
     s->asm_ptr.assign(1, 0);
     s->item_ptr.assign(1, 0);
-    std::vector<int32_t> nzm, s1m;
+    std::vector<int32_t> nzm, s1m, rec0(S.fronts.size(), 0);
     std::vector<std::pair<int32_t, int32_t>> morem;   // (a * f + b, id)
     for (int l = 0; l < L; ++l) {
       for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
@@ -965,6 +998,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
           for (; lo != morem.end() && lo->first == a * f + b; ++lo) out.push_back(lo->second);
           return out;
         };
+        rec0[t] = (int32_t)av.size();
         for (int a = 0; a < ns; ++a)
           for (int b = 0; b < (sym ? a + 1 : ns); ++b) {   // symmetric: A11's lower triangle only
             const int k = (int)(av.size() % 8);
@@ -1022,6 +1056,24 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       g_s[1] += (int64_t)gxp.back();                       // gx may hold a placeholder
       s->alg_bytes[0] = 16 * (s_a11 + g_a11);             // A11 (symmetric: lower) stores + child entries gathered
       s->alg_bytes[1] = 16 * (s_a11 + s_ns2);             // A11 read + L11/U11 write
+      // the same per level, and the fused form (children's entries gathered + L11/U11 written: A11 itself
+      // never makes a round trip through HBM)
+      s->lev_asm_bytes.assign(L, 0);
+      s->lev_lu_bytes.assign(L, 0);
+      s->lev_fused_bytes.assign(L, 0);
+      for (const Front& F : S.fronts) {
+        const int64_t a11 = sym ? (int64_t)F.ns * (F.ns + 1) / 2 : (int64_t)F.ns * F.ns;
+        s->lev_asm_bytes[F.level] += 16 * a11;
+        s->lev_lu_bytes[F.level] += 16 * (a11 + (int64_t)F.ns * F.ns);
+        s->lev_fused_bytes[F.level] += 16 * (int64_t)F.ns * F.ns;
+      }
+      for (int l = 0; l < L; ++l) {
+        int64_t g = 0;
+        for (int r = s->asm_ptr[l]; r < s->asm_ptr[l + 1]; ++r) g += av[r].z >= 0;
+        g += axp[s->asm_ptr[l + 1] / 8] - axp[s->asm_ptr[l] / 8];
+        s->lev_asm_bytes[l] += 16 * g;
+        s->lev_fused_bytes[l] += 16 * g;
+      }
       s->alg_bytes[2] = 16 * (s_rns + g_off + s_ns2);     // L21/U12 stores + gathered children + L11/U11 read
       for (int k = 0; k < 2; ++k)                         // A22 stores + gathered children + L21/U12 read
         s->alg_bytes[3 + k] = 16 * (s_r2[k] + g_s[k] + s_rns2[k]);
@@ -1033,7 +1085,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     if (ox.empty()) ox.push_back(make_int2(0, 0));
     if ((rc = s->up(&s->d_asm, av)) || (rc = s->up(&s->d_asm_xp, axp)) || (rc = s->up(&s->d_asm_x, ax)) ||
         (rc = s->up(&s->d_items, iv)) || (rc = s->up(&s->d_orec, orec)) || (rc = s->up(&s->d_oxp, oxp)) ||
-        (rc = s->up(&s->d_ox, ox)))
+        (rc = s->up(&s->d_ox, ox)) || (rc = s->up(&s->d_rec0, rec0)))
       return bail(rc);
   }
   std::vector<int32_t> cp(colptr, colptr + S.n + 1), ri(rowind, rowind + S.nnz);
@@ -1227,7 +1279,7 @@ int pfr_last_kernel_timings(const pfr_solver* s, double* ms, int64_t* launches) 
   for (int c = 0; c < s->n_tev; ++c) {
     if (!s->tev[c].used[0]) continue;
     for (int l = 0; l < L; ++l) {
-      const int work[5] = {s->asm_ptr[l + 1] - s->asm_ptr[l], s->level_ptr[l + 1] - s->level_ptr[l],
+      const int work[5] = {level_fused(s, l, 0) ? 0 : s->asm_ptr[l + 1] - s->asm_ptr[l], s->level_ptr[l + 1] - s->level_ptr[l],
                            s->item_ptr[l + 1] - s->item_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
                            s->tile_ptr[l + 1] - s->tile_ptr[l]};
       for (int k = 0; k < 5; ++k) {
@@ -1244,6 +1296,17 @@ int pfr_last_kernel_timings(const pfr_solver* s, double* ms, int64_t* launches) 
 int pfr_solver_alg_bytes(const pfr_solver* s, int64_t* bytes) {
   if (!s || !bytes) return fail(PFR_ERR_ARG, "null argument");
   for (int i = 0; i < 5; ++i) bytes[i] = s->alg_bytes[i];
+  // levels whose A11 assembly is fused into the LU (operator-form sweeps): class 0 empty there, class 1 the
+  // fused form
+  bytes[0] = bytes[1] = 0;
+  for (int l = 0; l + 1 < (int)s->level_ptr.size(); ++l) {
+    if (level_fused(s, l, 0)) {
+      bytes[1] += s->lev_fused_bytes[l];
+    } else {
+      bytes[0] += s->lev_asm_bytes[l];
+      bytes[1] += s->lev_lu_bytes[l];
+    }
+  }
   return PFR_OK;
 }
 

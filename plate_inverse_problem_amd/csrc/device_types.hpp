@@ -69,6 +69,21 @@ struct CoefPack {
   double im[COEF_MAX];
 };
 
+// The A11 assembly fused into the symmetric A11 LU (k_factor_sym prologue, PFR_FUSE_ASM): the
+// assembly records of the level (dst, nz, first child source, -) with each front's first record at
+// rec0[front] (its ns (ns + 1) / 2 records, lower triangle row by row), the overflow lists of further
+// child sources per 8-record chunk (xptr / xl, global chunk numbering), and the operator K - omega^2 M.
+// recs == NULL: A11 was assembled by k_assemble_level.
+struct AsmArgs {
+  const int4* recs = nullptr;
+  const int32_t* rec0 = nullptr;
+  const int32_t* xptr = nullptr;
+  const int2* xl = nullptr;
+  const double* freqs = nullptr;
+  const double2* K = nullptr;
+  const double* M = nullptr;
+};
+
 struct FunctionalArgs {
   int32_t n_support;
   const int32_t* pidx;    // permuted DOF index of each support entry (device)

@@ -392,8 +392,57 @@ __device__ __forceinline__ void row_updateR(const cplx* __restrict__ rd, cplx* _
 #define PFR_FAC_SB 2          // 4-pivot blocks per super-block (rank of the trailing update / 4)
 #endif
 
+// A11's lower triangle gathered by the LU workgroup itself (PFR_FUSE_ASM): per entry the original
+// K - omega^2 M value plus the first child update-matrix entry, one store each (the (row, lane group)
+// slots of the workgroup take the front's records in turn, 4 in flight); then the rare further child
+// entries (overflow lists of the records' 8-record chunks) added by one lane group in list order.  The
+// workgroup's own later loads of these entries are served by its XCD's L2 (written moments before), so
+// A11 no longer makes a store -> HBM -> reload trip between two launches, and the level's
+// k_assemble_level launch is gone.  Loads unconditional from clamped indices, masked arithmetically.
+__device__ __forceinline__ void factor_gather_a11(const AsmArgs& A, int front, int ns, cplx* __restrict__ F, int64_t Fc,
+                                                  int64_t q, int e0, int es, bool lead) {
+  const int R0 = A.rec0[front], nr = ns * (ns + 1) / 2;
+  const double om = 6.283185307179586 * A.freqs[q];
+  const double om2 = om * om;
+  constexpr int U = 4;
+  for (int e = e0; e < nr; e += U * es) {
+    int4 r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) r[u] = A.recs[R0 + min(e + u * es, nr - 1)];
+    cplx o[U], ch[U];
+    double mm[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      o[u] = A.K[max(r[u].y, 0)];
+      mm[u] = A.M[max(r[u].y, 0)];
+      ch[u] = F[(int64_t)max(r[u].z, 0) * Fc + q];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const double so = r[u].y >= 0 ? 1.0 : 0.0, sc = r[u].z >= 0 ? 1.0 : 0.0;
+      const cplx v = make_double2(fma(so, fma(-om2, mm[u], o[u].x), sc * ch[u].x), fma(so, o[u].y, sc * ch[u].y));
+      if (e + u * es < nr) F[(int64_t)r[u].x * Fc + q] = v;
+    }
+  }
+  __syncthreads();
+  if (lead) {
+    const int c0 = R0 >> 3, c1 = (R0 + nr - 1) >> 3;
+    for (int ck = c0; ck <= c1; ++ck) {
+      const int x1 = A.xptr[ck + 1];
+      for (int x = A.xptr[ck]; x < x1; ++x) {
+        const int2 g = A.xl[x];
+        const int rec = ck * 8 + g.x;
+        if (rec < R0 || rec >= R0 + nr) continue;
+        cplx* d = F + (int64_t)A.recs[rec].x * Fc + q;
+        *d = cadd(*d, F[(int64_t)g.y * Fc + q]);
+      }
+    }
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(PFR_FAC_LB) void k_factor_sym(DevPattern P, const int* __restrict__ lvl, cplx* __restrict__ F,
-                                                     int64_t Fc, int* __restrict__ flags) {
+                                                     int64_t Fc, int* __restrict__ flags, AsmArgs asmb) {
   Ctx c;
   c.lane = threadIdx.x & 63;
   c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -401,10 +450,12 @@ __global__ __launch_bounds__(PFR_FAC_LB) void k_factor_sym(DevPattern P, const i
   constexpr int QG = 64 / FAC_G;     // frequencies per lane group
   c.q = (int64_t)blockIdx.y * QG + c.lane % QG;
   const int sub = c.lane / QG;
-  const Front fr = P.fronts[lvl[blockIdx.x]];
+  const int front = lvl[blockIdx.x];
+  const Front fr = P.fronts[front];
   const int f = fr.f, ns = fr.ns;
   cplx* __restrict__ base = F + fr.off * Fc + c.q;
   const int r0 = FAC_G * c.w + sub, rs = FAC_G * c.W;   // this lane's first row offset, row stride
+  if (asmb.recs) factor_gather_a11(asmb, front, ns, F, Fc, c.q, r0, rs, c.w == 0 && sub == 0);
 #define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
   // 4-pivot diagonal block at k0 (kb pivots): one load burst from the lower triangle, LU in
   // registers (U = diag(U) L^T up to rounding), one store burst
@@ -2854,8 +2905,8 @@ void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int max
 }
 
 void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F,
-                   int64_t Fc, int* flags, hipStream_t st) {
-  if (sym) LAUNCH(k_factor_sym, dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
+                   int64_t Fc, int* flags, hipStream_t st, const AsmArgs& asmb) {
+  if (sym) LAUNCH(k_factor_sym, dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags, asmb);
   else LAUNCH(k_factor_level<true>, dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
 }
 

@@ -34,8 +34,9 @@ void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPac
 void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, const int2* xl, int ngroups, double2* F,
                      int64_t Fc, const double* freqs, const double2* K, const double* M, const double2* data,
                      int64_t ds, int nvalid, hipStream_t st);
+// asmb.recs != NULL (symmetric mode): A11 gathered by the LU kernel itself (no k_assemble_level launch)
 void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F, int64_t Fc,
-                   int* flags, hipStream_t st);
+                   int* flags, hipStream_t st, const AsmArgs& asmb = AsmArgs());
 // symmetric A11 LU with the pivot block in LDS (one front x qf = 2 or 4 frequencies per workgroup); maxns =
 // the level's largest pivot block (sizes the dynamic LDS: (maxns (maxns + 1) / 2 + 4 maxns) x 16 qf B)
 void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int maxns, int qf, double2* F, int64_t Fc,
