@@ -201,6 +201,10 @@ struct pfr_solver {
                                         // than this (one per CU) split their update parts up to about this
                                         // many workgroups (0: off)
   int check_fused = 0;                  // PFR_CHECK_FUSED=1: loss sweeps check both solutions in one entry walk
+  // dependency-driven paired top-down pass over the narrow top of the tree (PFR_FLOW, k_usolve2_flow): the
+  // levels from the root down while a level has fewer than PFR_FLOW_WG (front, frequency group) workgroups
+  int flow = 0, flow_wg = 1024, flow_lcut = 0;
+  pfr::FlowDesc fd{};
   // backward-error checks (pfr_set_check): PFR_CHECK_* bits, tolerance, optional per-item output;
   // per-frequency maxima scratch, forward and adjoint (kept zero between checks)
   int check_mode = 0;
@@ -554,7 +558,16 @@ int sym_top_down_support(pfr_solver* s, const pfr::RhsDesc& rd, hipStream_t st) 
 int sym_top_down_pair(pfr_solver* s, hipStream_t st, bool fwd_all = false) {
   const int L = (int)s->level_ptr.size() - 1;
   const int ngroups = (int)(s->Fc / 64);
-  for (int l = L - 1; l >= 0; --l) {
+  int l_hi = L - 1;
+  if (s->flow && s->fd.ntasks > 0) {
+    // the narrow top in one dependency-driven launch, the wide levels below it level by level
+    pfr::FlowDesc d = s->fd;
+    d.flags = s->flags;
+    pfr::launch_usolve2_flow(s->P, d, ngroups, s->F, s->Fc, s->Y, s->X, s->d_reach[0], fwd_all ? nullptr : s->d_reach[1],
+                             s->Y2, s->XA, s->d_reach[1], st);
+    l_hi = s->flow_lcut - 1;
+  }
+  for (int l = l_hi; l >= 0; --l) {
     const int nf = s->level_ptr[l + 1] - s->level_ptr[l];
     const bool small = s->level_maxf[l] <= s->us2_small;
     pfr::launch_usolve2(s->P, s->d_level_fronts + s->level_ptr[l], nf, solve_W(s, l, nf),
@@ -803,7 +816,9 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->check_fused = knob("PFR_CHECK_FUSED", 0, 0, 1);   // measured 2.3 ms against 2 x 0.87 ms per 2,048-frequency chunk
   s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);
   s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);
-  s->fuse_asm = knob("PFR_FUSE_ASM", 1, 0, 1);   // functional from the bottom-up passes (symmetric paired sweeps)
+  s->fuse_asm = knob("PFR_FUSE_ASM", 1, 0, 1);
+  s->flow = knob("PFR_FLOW", 0, 0, 1);
+  s->flow_wg = knob("PFR_FLOW_WG", 1024, 0, 1 << 20);   // functional from the bottom-up passes (symmetric paired sweeps)
   s->n = S.n;
   s->nnz = S.nnz;
   s->Fc = round64(max_batch);
@@ -1216,6 +1231,50 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       (rc = s->alloc(&s->mscale, Fc)) || (rc = s->alloc(&s->cpart, (int64_t)pfr::residual_parts(S.n) * Fc)))
     return bail(rc);
   HIP_TRY(hipMemset(s->d_berr_acc, 0, 2 * Fc * sizeof(double)));
+  if (s->sym && s->flow) {
+    // task list of the dependency-driven top-down pass: levels from the root down while narrow; per level its
+    // fronts' update parts (S per front: every wave of a part at least one SR-row group), then their
+    // triangular parts -- a topological order (a front after its parent's triangular part, its triangular
+    // part after its own update parts)
+    const int L = (int)S.level_ptr.size() - 1, ng = (int)(Fc / 64);
+    constexpr int SR = 4, W = 4;
+    int lcut = L;
+    while (lcut > 0 && (int64_t)(S.level_ptr[lcut] - S.level_ptr[lcut - 1]) * ng < s->flow_wg) --lcut;
+    std::vector<int32_t> slot(S.fronts.size(), -1), pslot(S.fronts.size(), -1);
+    std::vector<int4> tasks;
+    int nslots = 0;
+    for (int l = L - 1; l >= lcut; --l) {
+      for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
+        const int t = S.level_fronts[e];
+        const Front& F = S.fronts[t];
+        slot[t] = nslots++;
+        const int parts = std::max(1, std::min(16, (F.ns + SR * W - 1) / (SR * W)));
+        for (int p = 0; p < parts; ++p) tasks.push_back(make_int4(t, p, parts, slot[t]));
+      }
+      for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
+        const int t = S.level_fronts[e];
+        const Front& F = S.fronts[t];
+        const int parts = std::max(1, std::min(16, (F.ns + SR * W - 1) / (SR * W)));
+        tasks.push_back(make_int4(t, -1, parts, slot[t]));
+      }
+    }
+    for (size_t t = 0; t < S.fronts.size(); ++t)
+      if (slot[t] >= 0 && S.fronts[t].parent >= 0) pslot[t] = slot[S.fronts[t].parent];
+    s->flow_lcut = lcut;
+    if (!tasks.empty()) {
+      int4* dt;
+      int32_t* dp;
+      unsigned* dw;
+      const int64_t nw = (1 + 2 * (int64_t)nslots * ng + 3) / 4 * 4;   // memset block: a multiple of 16 B
+      if ((rc = s->up(&dt, tasks)) || (rc = s->up(&dp, pslot)) || (rc = s->alloc(&dw, nw))) return bail(rc);
+      s->fd.tasks = dt;
+      s->fd.ntasks = (int)tasks.size();
+      s->fd.pslot = dp;
+      s->fd.nslots = nslots;
+      s->fd.words = dw;
+      s->fd.words_bytes = (size_t)nw * sizeof(unsigned);
+    }
+  }
   // PFR_AUX=1: run the forward sparse L-solve on a side stream, level by level behind the
   // factorisation (+2% with one solver lane; with two lanes the extra queues cost more than it saves)
   const char* aux_env = getenv("PFR_AUX");

@@ -1719,26 +1719,11 @@ __device__ __forceinline__ void usolve2_upd(const Front& fr, const int* six, con
 #undef XV
 }
 
-template <bool SYM, int SR, int SK, int WPE>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void k_usolve2_level(
-    DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc, UPair A, UPair B, int upd_done) {
-  int bx;
-  const Ctx c = ctx_xcd(bx);
-  const int ft = lvl[bx];
-  const bool act[2] = {!A.skip || !A.skip[ft], !B.skip || !B.skip[ft]};
-  const bool live[2] = {!A.reach || A.reach[ft], !B.reach || B.reach[ft]};
-  const cplx* const Ys[2] = {A.Y, B.Y};
-  cplx* const Xs[2] = {A.X, B.X};
-  const Front fr = P.fronts[ft];
+// U11 backward for the pivot values XV(v, 0 .. ns) the update part left there: KBS blocks, the diagonal
+// block by wave 0 in registers, the rows above updated by all waves
+__device__ __forceinline__ void usolve2_tri(const Front& fr, const cplx* __restrict__ base, int64_t Fc, const Ctx& c,
+                                            const bool (&act)[2], cplx* const (&Xs)[2]) {
   const int f = fr.f, ns = fr.ns;
-  const cplx* __restrict__ base = F + fr.off * Fc + c.q;
-  __shared__ int six[MAX_FRONT];
-  if (!upd_done) {
-    for (int a = threadIdx.x; a < f; a += blockDim.x) six[a] = P.idx[fr.row0 + a];
-    __syncthreads();
-    usolve2_upd<SYM, SR, SK>(fr, six, base, Fc, c.q, act, live, Ys, Xs, SR * c.w, SR * c.W);
-  }
-  __syncthreads();
 #define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
 #define XV(v, a) Xs[v][(int64_t)(fr.col0 + (a)) * Fc + c.q]
   for (int k1 = ns; k1 > 0; k1 -= KBS) {
@@ -1787,6 +1772,30 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
 #undef XV
 }
 
+
+template <bool SYM, int SR, int SK, int WPE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void k_usolve2_level(
+    DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc, UPair A, UPair B, int upd_done) {
+  int bx;
+  const Ctx c = ctx_xcd(bx);
+  const int ft = lvl[bx];
+  const bool act[2] = {!A.skip || !A.skip[ft], !B.skip || !B.skip[ft]};
+  const bool live[2] = {!A.reach || A.reach[ft], !B.reach || B.reach[ft]};
+  const cplx* const Ys[2] = {A.Y, B.Y};
+  cplx* const Xs[2] = {A.X, B.X};
+  const Front fr = P.fronts[ft];
+  const int f = fr.f;
+  const cplx* __restrict__ base = F + fr.off * Fc + c.q;
+  __shared__ int six[MAX_FRONT];
+  if (!upd_done) {
+    for (int a = threadIdx.x; a < f; a += blockDim.x) six[a] = P.idx[fr.row0 + a];
+    __syncthreads();
+    usolve2_upd<SYM, SR, SK>(fr, six, base, Fc, c.q, act, live, Ys, Xs, SR * c.w, SR * c.W);
+  }
+  __syncthreads();
+  usolve2_tri(fr, base, Fc, c, act, Xs);
+}
+
 // the pivot rows' update part of k_usolve2_level split over S workgroups per (front, frequency group)
 template <bool SYM, int SR, int SK>
 __global__ __launch_bounds__(256) void k_usolve2_upd(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F,
@@ -1805,6 +1814,110 @@ __global__ __launch_bounds__(256) void k_usolve2_upd(DevPattern P, const int* __
   __syncthreads();
   usolve2_upd<SYM, SR, SK>(fr, six, F + fr.off * Fc + c.q, Fc, c.q, act, live, Ys, Xs, SR * (split * c.W + c.w),
                            SR * c.W * S);
+}
+
+// ------------------------------------------------------------------ dependency-driven passes (narrow top)
+// The narrow top of the elimination tree -- levels of a few fronts, whose per-level launches give a few
+// workgroups each and drain the chip at every level boundary -- as ONE launch in which every workgroup
+// takes the next task ticket and waits only for the tasks it depends on:
+//  * tickets are issued by an atomic counter in a topological order of the tasks (the host's list), so a
+//    workgroup waits only on tasks with smaller tickets, which running workgroups hold: no dependence on
+//    dispatch order, residency or placement, whatever the grid size;
+//  * hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): the producer's waves retire their
+//    stores, one lane fences release at agent scope (the XCD L2's dirty lines written back) and stores /
+//    adds the flag word by an agent-scope atomic; the consumer's one lane polls the word relaxed (s_sleep
+//    between polls), fences acquire at agent scope (its CU's L1 dropped) and releases the workgroup at a
+//    barrier; every polled word is zeroed by a memset on the stream before the launch;
+//  * spins are bounded (~1 s): a timeout flags the group's frequencies (PFR_FLAG_BAD_PIVOT) and goes on, so
+//    a broken schedule ends in flagged results, never in a hung GPU.
+struct FlowArgs {
+  const int4* tasks;     // (front, part (-1: the triangular part), parts S, region slot of the front)
+  int ntasks;
+  const int* pslot;      // per front: region slot of its parent, -1 when the front has no parent in the region
+  unsigned* ticket;      // the task counter
+  unsigned* done;        // per (slot, group): 1 once the front's pass is complete
+  unsigned* cnt;         // per (slot, group): update parts complete
+  int* flags;            // per frequency of the chunk
+};
+
+__device__ __forceinline__ bool flow_wait(unsigned* w, unsigned want) {
+  __shared__ int s_ok;
+  if (threadIdx.x == 0) {
+    int ok = 1;
+    unsigned spins = 0;
+    while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 24)) {
+        ok = 0;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    s_ok = ok;
+  }
+  __syncthreads();
+  return s_ok != 0;
+}
+
+__device__ __forceinline__ void flow_publish(unsigned* w, bool add) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its stores retired
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // keep: the release's own wait can be dropped (ROCm 7.2)
+    if (add)
+      __hip_atomic_fetch_add(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      __hip_atomic_store(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__device__ __forceinline__ int flow_ticket(unsigned* ticket) {
+  __shared__ int s_t;
+  if (threadIdx.x == 0) s_t = (int)__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  return s_t;
+}
+
+// The paired top-down pass (k_usolve2_level + k_usolve2_upd) over the narrow top: per front and
+// 64-frequency group, S update-part tasks (pivot rows a = SR (p W + w) + k SR W S, after the parent's pass)
+// and one triangular task (after the front's S update parts).
+template <int SR, int SK>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_usolve2_flow(
+    DevPattern P, const cplx* __restrict__ F, int64_t Fc, UPair A, UPair B, FlowArgs G, int ngroups) {
+  const int tk = flow_ticket(G.ticket);
+  if (tk >= G.ntasks * ngroups) return;
+  const int task = tk / ngroups, g = tk - task * ngroups;
+  const int4 T = G.tasks[task];
+  Ctx c;
+  c.lane = threadIdx.x & 63;
+  c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  c.W = blockDim.x >> 6;
+  c.q = (int64_t)g * 64 + c.lane;
+  const int ft = T.x;
+  const bool act[2] = {!A.skip || !A.skip[ft], !B.skip || !B.skip[ft]};
+  const bool live[2] = {!A.reach || A.reach[ft], !B.reach || B.reach[ft]};
+  const cplx* const Ys[2] = {A.Y, B.Y};
+  cplx* const Xs[2] = {A.X, B.X};
+  const Front fr = P.fronts[ft];
+  const cplx* __restrict__ base = F + fr.off * Fc + c.q;
+  __shared__ int six[MAX_FRONT];
+  bool ok = true;
+  if (T.y >= 0) {
+    for (int a = threadIdx.x; a < fr.f; a += blockDim.x) six[a] = P.idx[fr.row0 + a];
+    const int ps = G.pslot[ft];
+    if (ps >= 0) ok = flow_wait(G.done + (int64_t)ps * ngroups + g, 1u);
+    else __syncthreads();
+    usolve2_upd<true, SR, SK>(fr, six, base, Fc, c.q, act, live, Ys, Xs, SR * (T.y * c.W + c.w), SR * c.W * T.z);
+    if (!ok) atomicOr(G.flags + c.q, PFR_FLAG_BAD_PIVOT);
+    flow_publish(G.cnt + (int64_t)T.w * ngroups + g, true);
+  } else {
+    ok = flow_wait(G.cnt + (int64_t)T.w * ngroups + g, (unsigned)T.z);
+    usolve2_tri(fr, base, Fc, c, act, Xs);
+    if (!ok) atomicOr(G.flags + c.q, PFR_FLAG_BAD_PIVOT);
+    flow_publish(G.done + (int64_t)T.w * ngroups + g, false);
+  }
 }
 
 // ------------------------------------------------------------------ K3c: U^T y = g (bottom-up)
@@ -3019,6 +3132,16 @@ void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, boo
   // symmetric mode only (the paired top-down pass serves the symmetric loss + gradient sweep)
   if (small) LAUNCH((k_usolve2_level<true, 2, 4, 4>), g, bl, st, P, lvl, F, Fc, a, b, rs);
   else LAUNCH((k_usolve2_level<true, 4, 8, 2>), g, bl, st, P, lvl, F, Fc, a, b, rs);
+}
+
+void launch_usolve2_flow(const DevPattern& P, const FlowDesc& d, int ngroups, const double2* F, int64_t Fc,
+                         const double2* Y0, double2* X0, const int* reach0, const int* skip0, const double2* Y1,
+                         double2* X1, const int* reach1, hipStream_t st) {
+  if (d.ntasks <= 0) return;
+  UPair a{Y0, X0, reach0, skip0}, b{Y1, X1, reach1, nullptr};
+  FlowArgs G{d.tasks, d.ntasks, d.pslot, d.words, d.words + 1, d.words + 1 + (int64_t)d.nslots * ngroups, d.flags};
+  (void)hipMemsetAsync(d.words, 0, d.words_bytes, st);
+  LAUNCH((k_usolve2_flow<4, 8>), dim3((unsigned)(d.ntasks * ngroups)), dim3(256), st, P, F, Fc, a, b, G, ngroups);
 }
 
 void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nrows, const double2* Kd,

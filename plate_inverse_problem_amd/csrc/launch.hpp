@@ -76,6 +76,21 @@ void launch_fn_combine(const int* rows, int nrows, const double2* fcoef, double2
 void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, bool small, int ngroups,
                     const double2* F, int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0,
                     const double2* Y1, double2* X1, const int* reach1, hipStream_t st, int split = 1);
+// dependency-driven pass over the narrow top of the elimination tree (one launch, task tickets, per-front
+// completion words): the task list and its words (ticket, done, cnt: 1 + 2 nslots ngroups unsigned,
+// zeroed by the launcher), flags per frequency (a spin timeout sets PFR_FLAG_BAD_PIVOT)
+struct FlowDesc {
+  const int4* tasks = nullptr;
+  int ntasks = 0;
+  const int* pslot = nullptr;
+  int nslots = 0;
+  unsigned* words = nullptr;
+  size_t words_bytes = 0;
+  int* flags = nullptr;
+};
+void launch_usolve2_flow(const DevPattern& P, const FlowDesc& d, int ngroups, const double2* F, int64_t Fc,
+                         const double2* Y0, double2* X0, const int* reach0, const int* skip0, const double2* Y1,
+                         double2* X1, const int* reach1, hipStream_t st);
 // Hessian sweep: tangent right-hand sides (rows of the permuted matrix, or of its
 // transpose with accumulate = 1) and the directional derivative of the loss cotangent
 void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nrows, const double2* Kd,
