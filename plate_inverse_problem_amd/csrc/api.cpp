@@ -201,10 +201,16 @@ struct pfr_solver {
                                         // than this (one per CU) split their update parts up to about this
                                         // many workgroups (0: off)
   int check_fused = 0;                  // PFR_CHECK_FUSED=1: loss sweeps check both solutions in one entry walk
-  // dependency-driven paired top-down pass over the narrow top of the tree (PFR_FLOW, k_usolve2_flow): the
-  // levels from the root down while a level has fewer than PFR_FLOW_WG (front, frequency group) workgroups
+  // dependency-driven passes over the narrow top of the tree (PFR_FLOW bits: 1 the paired top-down pass,
+  // k_usolve2_flow; 2 the sliced bottom-up chain, k_lsolve_flow): the levels from the root down while a level
+  // has fewer than PFR_FLOW_WG (front, frequency group) workgroups
   int flow = 0, flow_wg = 1024, flow_lcut = 0;
   pfr::FlowDesc fd{};
+  // ... and the sliced bottom-up chain over the same levels (task list rebuilt whenever a reach changes)
+  std::vector<int32_t> flow_slot;       // per front: region slot or -1
+  pfr::LFlowDesc lfd{};
+  int4* d_lf_tasks = nullptr;
+  int32_t *d_lf_cptr = nullptr, *d_lf_cslot = nullptr, *d_lf_parts = nullptr;
   // backward-error checks (pfr_set_check): PFR_CHECK_* bits, tolerance, optional per-item output;
   // per-frequency maxima scratch, forward and adjoint (kept zero between checks)
   int check_mode = 0;
@@ -467,6 +473,75 @@ int adjoint_solve(pfr_solver* s, const pfr::RhsDesc& rg, double2* Out, hipStream
   return solve_all(s, 3, 0, rg, s->Y, Out, st, subset);
 }
 
+// Task list of the dependency-driven bottom-up chain (k_lsolve_flow) for the current reaches: levels from
+// flow_lcut up; per level the pivot tasks of every (front, slice) reached (slice 0: the forward rhs reach, slices
+// 1-3: the functional support's reach), then their update-row tasks
+int lflow_build(pfr_solver* s) {
+  constexpr int SRB = 4, W = 4, NZ = 4;
+  const int L = (int)s->level_ptr.size() - 1, ng = (int)(s->Fc / 64);
+  const int nslots = s->fd.nslots;
+  s->lfd.ntasks = 0;
+  if (!(s->flow & 2) || nslots == 0) return PFR_OK;
+  int rc;
+  if (!s->d_lf_tasks) {
+    const int64_t nw = (1 + 2 * (int64_t)nslots * NZ * ng + 3) / 4 * 4;
+    unsigned* dw;
+    if ((rc = s->alloc(&s->d_lf_tasks, (int64_t)nslots * NZ * 17)) || (rc = s->alloc(&s->d_lf_cptr, (int64_t)nslots * NZ + 1)) ||
+        (rc = s->alloc(&s->d_lf_cslot, (int64_t)nslots * NZ + 1)) || (rc = s->alloc(&s->d_lf_parts, nslots)) ||
+        (rc = s->alloc(&dw, nw)))
+      return rc;
+    s->lfd.words = dw;
+    s->lfd.words_bytes = (size_t)nw * sizeof(unsigned);
+  }
+  auto reached = [&](int t, int z) { return s->reach_host[z == 0 ? 0 : 1][t] != 0; };
+  std::vector<int32_t> parts(nslots, 0), cptr(1, 0), cslot;
+  std::vector<std::vector<int>> kids(nslots);
+  for (size_t t = 0; t < s->flow_slot.size(); ++t) {
+    const int sl = s->flow_slot[t];
+    if (sl < 0) continue;
+    const int r = s->front_f[t] - s->front_ns[t];
+    parts[sl] = r == 0 ? 0 : std::max(1, std::min(16, (r + SRB * W - 1) / (SRB * W)));
+    const int p = s->front_parent[t];
+    if (p >= 0 && s->flow_slot[p] >= 0) kids[s->flow_slot[p]].push_back((int)t);
+  }
+  std::vector<int> slot_front(nslots);
+  for (size_t t = 0; t < s->flow_slot.size(); ++t)
+    if (s->flow_slot[t] >= 0) slot_front[s->flow_slot[t]] = (int)t;
+  for (int sl = 0; sl < nslots; ++sl)
+    for (int z = 0; z < NZ; ++z) {
+      for (int c : kids[sl])
+        if (reached(c, z) && parts[s->flow_slot[c]] > 0) cslot.push_back(s->flow_slot[c]);
+      cptr.push_back((int32_t)cslot.size());
+    }
+  std::vector<int4> tasks;
+  for (int l = s->flow_lcut; l < L; ++l) {
+    for (int e = s->level_ptr[l]; e < s->level_ptr[l + 1]; ++e) {
+      const int t = s->level_fronts_host[e];
+      for (int z = 0; z < NZ; ++z)
+        if (reached(t, z)) tasks.push_back(make_int4(t, z, -1, s->flow_slot[t]));
+    }
+    for (int e = s->level_ptr[l]; e < s->level_ptr[l + 1]; ++e) {
+      const int t = s->level_fronts_host[e];
+      for (int z = 0; z < NZ; ++z)
+        if (reached(t, z))
+          for (int p = 0; p < parts[s->flow_slot[t]]; ++p) tasks.push_back(make_int4(t, z, p, s->flow_slot[t]));
+    }
+  }
+  if (cslot.empty()) cslot.push_back(0);
+  HIP_TRY(hipMemcpy(s->d_lf_cptr, cptr.data(), cptr.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s->d_lf_cslot, cslot.data(), cslot.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s->d_lf_parts, parts.data(), parts.size() * 4, hipMemcpyHostToDevice));
+  if (!tasks.empty()) HIP_TRY(hipMemcpy(s->d_lf_tasks, tasks.data(), tasks.size() * sizeof(int4), hipMemcpyHostToDevice));
+  s->lfd.tasks = s->d_lf_tasks;
+  s->lfd.ntasks = (int)tasks.size();
+  s->lfd.cptr = s->d_lf_cptr;
+  s->lfd.cslot = s->d_lf_cslot;
+  s->lfd.parts = s->d_lf_parts;
+  s->lfd.nslots = nslots;
+  (void)ng;
+  return PFR_OK;
+}
+
 // Row lists and buffers of the functional-from-bottom-up path (allocated on first use, lists rebuilt
 // whenever a reach changed)
 int fn_setup(pfr_solver* s) {
@@ -499,6 +574,7 @@ int fn_setup(pfr_solver* s) {
   // at most n rows each (pivot rows are distinct): into the buffers allocated for n
   if (!both.empty()) HIP_TRY(hipMemcpy(s->d_fn_rows, both.data(), both.size() * sizeof(int2), hipMemcpyHostToDevice));
   if (!sup.empty()) HIP_TRY(hipMemcpy(s->d_sup_rows, sup.data(), sup.size() * 4, hipMemcpyHostToDevice));
+  if ((rc = lflow_build(s))) return rc;
   s->fn_ready = true;
   return PFR_OK;
 }
@@ -521,7 +597,10 @@ int fn_bottom_up(pfr_solver* s, int rhs_mode, const pfr::RhsDesc& rf, hipStream_
     rd[k].beta_im = 0.0;
     rd[k].cslot = s->d_noslot;
   }
-  for (int l = 0; l < L; ++l) {
+  // the narrow top in one dependency-driven launch after the wide levels (PFR_FLOW)
+  const bool flow = (s->flow & 2) && s->lfd.ntasks > 0;
+  const int l_end = flow ? s->flow_lcut : L;
+  for (int l = 0; l < l_end; ++l) {
     const int* lvl[4];
     int nf[4];
     lvl[0] = s->d_reach_fronts[0] + s->reach_ptr[0][l];
@@ -534,6 +613,11 @@ int fn_bottom_up(pfr_solver* s, int rhs_mode, const pfr::RhsDesc& rf, hipStream_
     if (nmax == 0) continue;
     pfr::launch_lsolve_multi(rhs_mode, s->P, 4, lvl, nf, solve_W(s, l, nmax), ngroups, s->F, s->Fc, WV, rd, Y, reach,
                              st, solve_split(s, nf[0] + 3 * nf[1]));
+  }
+  if (flow) {
+    pfr::LFlowDesc d = s->lfd;
+    d.flags = s->flags;
+    pfr::launch_lsolve_flow(rhs_mode, s->P, d, ngroups, s->F, s->Fc, WV, rd, Y, reach, st);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -559,7 +643,7 @@ int sym_top_down_pair(pfr_solver* s, hipStream_t st, bool fwd_all = false) {
   const int L = (int)s->level_ptr.size() - 1;
   const int ngroups = (int)(s->Fc / 64);
   int l_hi = L - 1;
-  if (s->flow && s->fd.ntasks > 0) {
+  if ((s->flow & 1) && s->fd.ntasks > 0) {
     // the narrow top in one dependency-driven launch, the wide levels below it level by level
     pfr::FlowDesc d = s->fd;
     d.flags = s->flags;
@@ -817,7 +901,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);
   s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);
   s->fuse_asm = knob("PFR_FUSE_ASM", 1, 0, 1);
-  s->flow = knob("PFR_FLOW", 0, 0, 1);
+  s->flow = knob("PFR_FLOW", 0, 0, 3);   // bit 0: paired top-down pass, bit 1: bottom-up chain
   s->flow_wg = knob("PFR_FLOW_WG", 1024, 0, 1 << 20);   // functional from the bottom-up passes (symmetric paired sweeps)
   s->n = S.n;
   s->nnz = S.nnz;
@@ -1261,6 +1345,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     for (size_t t = 0; t < S.fronts.size(); ++t)
       if (slot[t] >= 0 && S.fronts[t].parent >= 0) pslot[t] = slot[S.fronts[t].parent];
     s->flow_lcut = lcut;
+    s->flow_slot = slot;
     if (!tasks.empty()) {
       int4* dt;
       int32_t* dp;

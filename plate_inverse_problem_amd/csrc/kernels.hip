@@ -1920,6 +1920,61 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   }
 }
 
+// The sliced bottom-up chain (k_lsolve_level_z + k_lsolve_rows_z) over the narrow top, level by level
+// upwards: per (front, slice) reached, a pivot task (frontal vector gathered from the rhs and the children's
+// update vectors, pivot blocks, y; after every in-region child's update rows of that slice) and S_t update-row
+// tasks (rows ns + SRB (p W + w) + k SRB W S, after the front's pivot task).
+struct LFlowArgs {
+  const int4* tasks;     // (front, slice, part (-1: the pivot task), region slot of the front)
+  int ntasks;
+  const int* cptr;       // per (slot, slice): its in-region children reached in the slice, cslot[cptr[4 slot + z] ..]
+  const int* cslot;      //   (only children with update rows: the others contribute nothing to the gather)
+  const int* parts;      // per slot: update-row tasks S of the front (0: no update rows)
+  unsigned* ticket;
+  unsigned* pdone;       // per (slot, slice, group): pivot task complete
+  unsigned* rcnt;        // per (slot, slice, group): update-row tasks complete
+  int* flags;
+};
+
+template <int RHS>
+__global__ __launch_bounds__(256) void k_lsolve_flow(DevPattern P, LSlices S, const cplx* __restrict__ F, int64_t Fc,
+                                                     LFlowArgs G, int ngroups) {
+  const int tk = flow_ticket(G.ticket);
+  if (tk >= G.ntasks * ngroups) return;
+  const int task = tk / ngroups, g = tk - task * ngroups;
+  const int4 T = G.tasks[task];
+  Ctx c;
+  c.lane = threadIdx.x & 63;
+  c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  c.W = blockDim.x >> 6;
+  c.q = (int64_t)g * 64 + c.lane;
+  const int z = T.y, sl = T.w;
+  const Front fr = P.fronts[T.x];
+  const int64_t wz = ((int64_t)sl * MAX_SLICES + z) * ngroups + g;
+  bool ok = true;
+  if (T.z < 0) {
+    // every in-region child of this slice: its update rows complete (children outside the region were
+    // solved by earlier launches; unreached children are skipped by the gather itself)
+    const int key = sl * MAX_SLICES + z;
+    const int c1 = G.cptr[key + 1];
+    for (int k = G.cptr[key]; k < c1; ++k) {
+      const int cs = G.cslot[k];
+      ok = flow_wait(G.rcnt + ((int64_t)cs * MAX_SLICES + z) * ngroups + g, (unsigned)G.parts[cs]) && ok;
+    }
+    if (c1 == G.cptr[key]) __syncthreads();
+    lsolve_front<RHS>(P, fr, F, Fc, S.WV[z], S.R[z], S.Y[z], S.reach[z], 1, c);
+    if (!ok) atomicOr(G.flags + c.q, PFR_FLAG_BAD_PIVOT);
+    flow_publish(G.pdone + wz, false);
+  } else {
+    ok = flow_wait(G.pdone + wz, 1u);
+    const int Sp = G.parts[sl];
+    lsolve_rows(fr, F + fr.off * Fc + c.q, S.WV[z] + (int64_t)fr.row0 * Fc + c.q, Fc, fr.ns + SRB * (T.z * c.W + c.w),
+                SRB * c.W * Sp);
+    if (!ok) atomicOr(G.flags + c.q, PFR_FLAG_BAD_PIVOT);
+    flow_publish(G.rcnt + wz, true);
+  }
+}
+
 // ------------------------------------------------------------------ K3c: U^T y = g (bottom-up)
 template <int RHS>
 __global__ __launch_bounds__(512) void k_utsolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
@@ -3142,6 +3197,23 @@ void launch_usolve2_flow(const DevPattern& P, const FlowDesc& d, int ngroups, co
   FlowArgs G{d.tasks, d.ntasks, d.pslot, d.words, d.words + 1, d.words + 1 + (int64_t)d.nslots * ngroups, d.flags};
   (void)hipMemsetAsync(d.words, 0, d.words_bytes, st);
   LAUNCH((k_usolve2_flow<4, 8>), dim3((unsigned)(d.ntasks * ngroups)), dim3(256), st, P, F, Fc, a, b, G, ngroups);
+}
+
+void launch_lsolve_flow(int rhs_mode, const DevPattern& P, const LFlowDesc& d, int ngroups, const double2* F, int64_t Fc,
+                        double2* const* WV, const RhsDesc* rd, double2* const* Y, const int* const* reach, hipStream_t st) {
+  if (d.ntasks <= 0) return;
+  LSlices S{};
+  for (int z = 0; z < MAX_SLICES; ++z) {
+    S.WV[z] = WV[z];
+    S.Y[z] = Y[z];
+    S.reach[z] = reach[z];
+    S.R[z] = make_rhs(rd[z]);
+  }
+  const int64_t per = (int64_t)d.nslots * MAX_SLICES * ngroups;
+  LFlowArgs G{d.tasks, d.ntasks, d.cptr, d.cslot, d.parts, d.words, d.words + 1, d.words + 1 + per, d.flags};
+  (void)hipMemsetAsync(d.words, 0, d.words_bytes, st);
+  if (rhs_mode == 0) LAUNCH(k_lsolve_flow<0>, dim3((unsigned)(d.ntasks * ngroups)), dim3(256), st, P, S, F, Fc, G, ngroups);
+  else LAUNCH(k_lsolve_flow<3>, dim3((unsigned)(d.ntasks * ngroups)), dim3(256), st, P, S, F, Fc, G, ngroups);
 }
 
 void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nrows, const double2* Kd,

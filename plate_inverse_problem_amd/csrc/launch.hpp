@@ -91,6 +91,22 @@ struct FlowDesc {
 void launch_usolve2_flow(const DevPattern& P, const FlowDesc& d, int ngroups, const double2* F, int64_t Fc,
                          const double2* Y0, double2* X0, const int* reach0, const int* skip0, const double2* Y1,
                          double2* X1, const int* reach1, hipStream_t st);
+// the sliced bottom-up chain over the narrow top (4 slices as launch_lsolve_multi; words: ticket, pdone, rcnt:
+// 1 + 2 nslots 4 ngroups unsigned).  cptr / cslot: per slot its in-region children REACHED in each slice
+// are waited for -- the host lists, per (slot, slice), the children of that slice (cptr indexed slot * 4 + z)
+struct LFlowDesc {
+  const int4* tasks = nullptr;
+  int ntasks = 0;
+  const int* cptr = nullptr;
+  const int* cslot = nullptr;
+  const int* parts = nullptr;
+  int nslots = 0;
+  unsigned* words = nullptr;
+  size_t words_bytes = 0;
+  int* flags = nullptr;
+};
+void launch_lsolve_flow(int rhs_mode, const DevPattern& P, const LFlowDesc& d, int ngroups, const double2* F, int64_t Fc,
+                        double2* const* WV, const RhsDesc* rd, double2* const* Y, const int* const* reach, hipStream_t st);
 // Hessian sweep: tangent right-hand sides (rows of the permuted matrix, or of its
 // transpose with accumulate = 1) and the directional derivative of the loss cotangent
 void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nrows, const double2* Kd,
