@@ -1841,23 +1841,20 @@ struct FlowArgs {
 };
 
 __device__ __forceinline__ bool flow_wait(unsigned* w, unsigned want) {
-  __shared__ int s_ok;
+  int bad = 0;
   if (threadIdx.x == 0) {
-    int ok = 1;
     unsigned spins = 0;
     while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
       __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 24)) {
-        ok = 0;
+      if (++spins > (1u << 21)) {   // ~2 s of polls: give up (flagged), never hang the GPU
+        bad = 1;
         break;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    s_ok = ok;
   }
-  __syncthreads();
-  return s_ok != 0;
+  return !__syncthreads_or(bad);   // the barrier after the acquire releases the other waves' loads
 }
 
 __device__ __forceinline__ void flow_publish(unsigned* w, bool add) {
@@ -1961,7 +1958,6 @@ __global__ __launch_bounds__(256) void k_lsolve_flow(DevPattern P, LSlices S, co
       const int cs = G.cslot[k];
       ok = flow_wait(G.rcnt + ((int64_t)cs * MAX_SLICES + z) * ngroups + g, (unsigned)G.parts[cs]) && ok;
     }
-    if (c1 == G.cptr[key]) __syncthreads();
     lsolve_front<RHS>(P, fr, F, Fc, S.WV[z], S.R[z], S.Y[z], S.reach[z], 1, c);
     if (!ok) atomicOr(G.flags + c.q, PFR_FLAG_BAD_PIVOT);
     flow_publish(G.pdone + wz, false);
