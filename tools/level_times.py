@@ -1,24 +1,36 @@
 """Per-level durations (ms) of every factorisation / solve kernel in the LAST sweep of a
 rocprofv3 --kernel-trace CSV (lanes = 1 runs: the bench's isolated sweep comes last).
 
-Usage: python tools/level_times.py gpurun_out/<dir>/run_kernel_trace.csv [n_levels=17] [--gaps]
+Usage: python tools/level_times.py gpurun_out/<dir>/run_kernel_trace.csv [n_levels (default: the last sweep's)] [--gaps]
 (--gaps: per sweep, every idle gap above 10 us between consecutive kernels, with its neighbours)
 """
 import csv
 import sys
 
 
-def main(path, L=17):
+LU = ("k_factor_sym", "k_factor_sym_lds", "k_factor_level")
+
+
+def main(path, L=None):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     names = [r["Kernel_Name"].split("(")[0].replace("void ", "").replace("pfr::", "").split("<")[0] for r in rows]
-    asm = [i for i, n in enumerate(names) if n == "k_assemble_level"]
-    st = asm[-L]
+    # one A11 LU launch per level (the assembly may be fused into it): the level marker; the level count is
+    # that of the last sweep (k_pad_freqs starts every chunk)
+    pads = [i for i, n in enumerate(names) if n == "k_pad_freqs"]
+    lus = [i for i, n in enumerate(names) if n in LU]
+    if L is None:
+        L = sum(1 for i in lus if i > pads[-1]) if pads else 17
+    st = lus[-L]
+    # the level's assembly launch (unfused levels) precedes its LU launch
+    if st > 0 and names[st - 1] == "k_assemble_level":
+        st -= 1
     end = len(rows)
     tab, lvl = {}, -1
-    for r, n in zip(rows[st:end], names[st:end]):
-        if n == "k_assemble_level":
-            lvl += 1
+    for i, (r, n) in enumerate(zip(rows[st:end], names[st:end])):
+        if n in LU or (n == "k_assemble_level" and (st + i + 1 >= end or names[st + i + 1] in LU)):
+            if not (n in LU and i > 0 and names[st + i - 1] == "k_assemble_level"):
+                lvl += 1
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
         t = tab.setdefault(n, {})
         key = lvl if n.startswith(("k_assemble", "k_factor", "k_offdiag", "k_schur")) else "x"
@@ -56,4 +68,4 @@ GAPS = "--gaps" in sys.argv
 
 if __name__ == "__main__":
     args = [a for a in sys.argv[1:] if a != "--gaps"]
-    main(args[0], int(args[1]) if len(args) > 1 else 17)
+    main(args[0], int(args[1]) if len(args) > 1 else None)
