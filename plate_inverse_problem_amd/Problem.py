@@ -28,6 +28,7 @@ import scipy.sparse as sp
 import torch
 
 from . import _native
+from ._abd_jet import coeffs18 as _jet_coeffs18
 from .Accelerometer import Accelerometer, AccelerometerParams
 from .Geometry import Geometry, GeometryParams
 from .Material import Material, get_material
@@ -359,6 +360,9 @@ class _Engine:
         return sum(ms), sum(n)
 
 
+_JET_TYPES = ('isotropic', 'orthotropic', 'orthotropic_d4', 'sol', 'symm_sol')
+
+
 def _coeffs18(transform, params: torch.Tensor) -> torch.Tensor:
     A, B, D = transform(params)
     return torch.cat([A, B, D]).to(torch.complex128)
@@ -595,6 +599,14 @@ class Problem:
     def _transform(self):
         return self.material.get_ABD_transform(self.geometry.height)
 
+    def _coeffs(self, transform, p: torch.Tensor) -> torch.Tensor:
+        """c(theta) (18 complex) differentiable in theta: the jet transform (value and Jacobian in one numpy
+        pass, backward one product: _abd_jet.py) for the material types of Material.py, torch autograd
+        through ``transform`` otherwise."""
+        if self.material.atype in _JET_TYPES:
+            return _jet_coeffs18(self.material, self.geometry.height, p)
+        return _coeffs18(transform, p)
+
     def _freqs(self, freqs) -> torch.Tensor:
         return torch.as_tensor(np.asarray(freqs, dtype=np.float64) if not isinstance(freqs, torch.Tensor)
                                else freqs, dtype=torch.float64, device=self.device).contiguous()
@@ -612,7 +624,7 @@ class Problem:
         def fr_function(freqs, params):
             f = self._freqs(freqs)
             p = params if isinstance(params, torch.Tensor) else torch.as_tensor(np.asarray(params, dtype=np.float64))
-            c = _coeffs18(transform, p.to(torch.float64).cpu())
+            c = self._coeffs(transform, p.to(torch.float64).cpu())
             return _SweepFR.apply(c, self.engine(f.numel()), f)
 
         self._fr_function = weakref.ref(fr_function)    # no Problem <-> closure reference cycle
@@ -696,7 +708,7 @@ class Problem:
 
         def loss(params):
             p = params if isinstance(params, torch.Tensor) else torch.as_tensor(np.asarray(params, dtype=np.float64))
-            c = _coeffs18(transform, p.to(torch.float64).cpu() * scaling)
+            c = self._coeffs(transform, p.to(torch.float64).cpu() * scaling)
             return _SweepLoss.apply(c, self.engine(max(1, hi - lo)), f_local, ref_local, loss_id, n_total, reduce_fn)
 
         return loss
