@@ -9,3 +9,4 @@ timeout -k 10 300 python3 -u tools/grad_err_groups.py --out gpurun_out/r4a/grad_
 STEPS=3 bash tools/gpu.sh trace r4a_t512 512 || exit $?
 STEPS=3 bash tools/gpu.sh trace r4a_t512deep 512 PFR_LEAF_SIZE=10000 || exit $?
 STEPS=2 bash tools/gpu.sh trace r4a_t2048 2048 || exit $?
+timeout -k 10 300 python3 -u tools/grad_err_groups.py --check 15 --out gpurun_out/r4a/grad_groups_refine.json > gpurun_out/r4a/grad_groups_refine.log 2>&1 || exit $?
