@@ -441,16 +441,10 @@ __device__ __forceinline__ void factor_gather_a11(const AsmArgs& A, int front, i
   __syncthreads();
 }
 
-__global__ __launch_bounds__(PFR_FAC_LB) void k_factor_sym(DevPattern P, const int* __restrict__ lvl, cplx* __restrict__ F,
-                                                     int64_t Fc, int* __restrict__ flags, AsmArgs asmb) {
-  Ctx c;
-  c.lane = threadIdx.x & 63;
-  c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  c.W = blockDim.x >> 6;
-  constexpr int QG = 64 / FAC_G;     // frequencies per lane group
-  c.q = (int64_t)blockIdx.y * QG + c.lane % QG;
-  const int sub = c.lane / QG;
-  const int front = lvl[blockIdx.x];
+// One front's A11 LU for the 64 / FAC_G frequencies of c.q's lane group: c.w / c.W the wave's index and count
+// among the waves working on these frequencies (every wave of the workgroup reaches the same barriers)
+__device__ __forceinline__ void factor_sym_front(const DevPattern& P, int front, cplx* __restrict__ F, int64_t Fc,
+                                                 int* __restrict__ flags, const AsmArgs& asmb, const Ctx& c, int sub) {
   const Front fr = P.fronts[front];
   const int f = fr.f, ns = fr.ns;
   cplx* __restrict__ base = F + fr.off * Fc + c.q;
@@ -556,6 +550,17 @@ __global__ __launch_bounds__(PFR_FAC_LB) void k_factor_sym(DevPattern P, const i
     }
   }
 #undef E
+}
+
+__global__ __launch_bounds__(PFR_FAC_LB) void k_factor_sym(DevPattern P, const int* __restrict__ lvl, cplx* __restrict__ F,
+                                                     int64_t Fc, int* __restrict__ flags, AsmArgs asmb) {
+  Ctx c;
+  c.lane = threadIdx.x & 63;
+  c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  c.W = blockDim.x >> 6;
+  constexpr int QG = 64 / FAC_G;     // frequencies per lane group
+  c.q = (int64_t)blockIdx.y * QG + c.lane % QG;
+  factor_sym_front(P, lvl[blockIdx.x], F, Fc, flags, asmb, c, c.lane / QG);
 }
 
 // Symmetric A11 LU with the pivot block resident in LDS, for the levels of large pivot blocks (the
@@ -799,18 +804,16 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
 // the prefix loop is not needed (96 VGPRs: 5 waves/SIMD against 4) -- the bottom levels'
 // rows are short and their waves bound by the latency of their item -> front -> record -> source
 // load chain, which more resident waves overlap.
+// One item (OFF_G OFF_RPL rows / columns of a front) of the panel for the frequency group `by`: the wave's
+// own work, no barrier
 template <int MODE, bool SMALL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMALL ? 5 : 1))) void k_offdiag_level(DevPattern P, const int4* __restrict__ items, int nitems,
-                                                        const int2* __restrict__ orec, const int* __restrict__ oxp,
-                                                        const int2* __restrict__ ox, cplx* __restrict__ F, int64_t Fc,
-                                                        const double* __restrict__ freqs, const cplx* __restrict__ K,
-                                                        const double* __restrict__ M, const cplx* __restrict__ data,
-                                                        int64_t data_stride, int nvalid) {
+__device__ __forceinline__ void offdiag_item(const DevPattern& P, const int4* __restrict__ items, int wid,
+                                             const int2* __restrict__ orec, const int* __restrict__ oxp,
+                                             const int2* __restrict__ ox, cplx* __restrict__ F, int64_t Fc,
+                                             const double* __restrict__ freqs, const cplx* __restrict__ K,
+                                             const double* __restrict__ M, const cplx* __restrict__ data,
+                                             int64_t data_stride, int nvalid, int by) {
   const int lane = threadIdx.x & 63;
-  const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
-  const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
-  const int wid = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
-  if (wid >= nitems) return;
   constexpr int QG = 64 / OFF_G;                  // frequencies per lane group
   const int sub = lane / QG;
   const int64_t q = (int64_t)by * QG + lane % QG;
@@ -868,6 +871,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMALL ? 5 :
 #undef TAIL
     default: break;
   }
+}
+
+template <int MODE, bool SMALL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMALL ? 5 : 1))) void k_offdiag_level(DevPattern P, const int4* __restrict__ items, int nitems,
+                                                        const int2* __restrict__ orec, const int* __restrict__ oxp,
+                                                        const int2* __restrict__ ox, cplx* __restrict__ F, int64_t Fc,
+                                                        const double* __restrict__ freqs, const cplx* __restrict__ K,
+                                                        const double* __restrict__ M, const cplx* __restrict__ data,
+                                                        int64_t data_stride, int nvalid) {
+  const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
+  const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
+  const int wid = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  if (wid >= nitems) return;
+  offdiag_item<MODE, SMALL>(P, items, wid, orec, oxp, ox, F, Fc, freqs, K, M, data, data_stride, nvalid, by);
 }
 
 // ------------------------------------------------------------------ K2b: Schur complement
@@ -1041,19 +1058,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PFR_SCHUR_W
 // NB LDS buffers of KC pivots each.  NB = 2: plain double buffering, one __syncthreads per
 // stage (it drains the next stage's copies).  NB >= 3: the copies of NB - 1 stages ahead stay in
 // flight across a raw s_barrier, each stage retired by a counted vmcnt.
+// block `bid` for the frequency group `by` (the workgroup's BC waves; barriers inside)
 template <int NB, int KC, int BC>
-__global__ __launch_bounds__(64 * BC) void k_schur_sym_blk(DevPattern P, const int4* __restrict__ blocks, int nblocks,
-                                                         const int* __restrict__ bg1, const int* __restrict__ bgxp,
-                                                         const int2* __restrict__ bgx, cplx* __restrict__ F,
-                                                         int64_t Fc) {
+__device__ __forceinline__ void schur_blk_body(const DevPattern& P, int bid, int by, const int4* __restrict__ blocks,
+                                               const int* __restrict__ bg1, const int* __restrict__ bgxp,
+                                               const int2* __restrict__ bgx, cplx* __restrict__ F, int64_t Fc) {
   constexpr int BR = SCHUR_BLK, NW = BC, TCW = BC / 4;   // block rows, waves, tile columns
   constexpr int BROWS = BR + BC + 1;      // LDS rows per pivot: row operands, column operands, U(k, k)
   __shared__ cplx sop[NB][KC][BROWS][64];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
-  const int bid = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
-  if (bid >= nblocks) return;                // whole workgroup: uniform
   const int64_t q = (int64_t)by * 64 + lane;
   const int4 bk = blocks[bid];
   const Front fr = P.fronts[bk.x];
@@ -1195,6 +1209,17 @@ __global__ __launch_bounds__(64 * BC) void k_schur_sym_blk(DevPattern P, const i
         if (i < r && j <= i) base[((int64_t)(ns + i) * f + ns + j) * Fc] = acc[m][n];
       }
   }
+}
+
+template <int NB, int KC, int BC>
+__global__ __launch_bounds__(64 * BC) void k_schur_sym_blk(DevPattern P, const int4* __restrict__ blocks, int nblocks,
+                                                         const int* __restrict__ bg1, const int* __restrict__ bgxp,
+                                                         const int2* __restrict__ bgx, cplx* __restrict__ F,
+                                                         int64_t Fc) {
+  const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
+  const int bid = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
+  if (bid >= nblocks) return;                // whole workgroup: uniform
+  schur_blk_body<NB, KC, BC>(P, bid, by, blocks, bg1, bgxp, bgx, F, Fc);
 }
 
 // ------------------------------------------------------------------ right-hand sides
