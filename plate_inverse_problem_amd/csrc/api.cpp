@@ -209,6 +209,11 @@ struct pfr_solver {
   // ... and the sliced bottom-up chain over the same levels (task list rebuilt whenever a reach changes)
   std::vector<int32_t> flow_slot;       // per front: region slot or -1
   pfr::LFlowDesc lfd{};
+  // the factorisation's narrow top in one dependency-driven launch (PFR_FLOW bit 2, k_factor_flow): levels
+  // [fflow_lcut, L) -- from the root down while a level has fewer than PFR_FLOW_FWG (front, group) A11 tasks
+  int fflow_lcut = 0, flow_fwg = 256;
+  int timed_levels = 0;                 // levels the last factorisation launched level by level (class timings)
+  pfr::FactorFlowDesc ffd{};
   int4* d_lf_tasks = nullptr;
   int32_t *d_lf_cptr = nullptr, *d_lf_cslot = nullptr, *d_lf_parts = nullptr;
   // backward-error checks (pfr_set_check): PFR_CHECK_* bits, tolerance, optional per-item output;
@@ -338,7 +343,11 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
   auto mark = [&](int l, int c) {
     if (kt) (void)hipEventRecord(kev[6 * l + c], st);
   };
-  for (int l = 0; l < L; ++l) {
+  // the narrow top as one dependency-driven launch (PFR_FLOW bit 2; operator-form sweeps of a symmetric analysis)
+  const bool fflow = (s->flow & 4) && s->ffd.ntasks > 0 && mode == 0 && s->sym && s->schur_bc == 16 && !after_panel;
+  const int l_end = fflow ? s->fflow_lcut : L;
+  s->timed_levels = l_end;
+  for (int l = 0; l < l_end; ++l) {
     int nf = s->level_ptr[l + 1] - s->level_ptr[l];
     mark(l, 0);
     // panel: enough workgroups (front x 16 frequencies) to fill the chip -> one wave
@@ -394,6 +403,19 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
                       s->d_gx, ngroups, s->F,
                       s->Fc, st);
     mark(l, 5);
+  }
+  if (fflow) {
+    pfr::FactorFlowDesc d = s->ffd;
+    d.flags = s->flags;
+    pfr::AsmArgs asmb;
+    asmb.recs = s->d_asm;
+    asmb.rec0 = s->d_rec0;
+    asmb.xptr = s->d_asm_xp;
+    asmb.xl = s->d_asm_x;
+    asmb.freqs = s->freqs;
+    asmb.K = s->K;
+    asmb.M = s->M;
+    pfr::launch_factor_flow(s->P, d, ngroups, s->F, s->Fc, asmb, st);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -901,7 +923,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);
   s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);
   s->fuse_asm = knob("PFR_FUSE_ASM", 1, 0, 1);
-  s->flow = knob("PFR_FLOW", 0, 0, 3);   // bit 0: paired top-down pass, bit 1: bottom-up chain
+  s->flow = knob("PFR_FLOW", 0, 0, 7);   // bit 0: paired top-down pass, bit 1: bottom-up chain, bit 2: factorisation
+  s->flow_fwg = knob("PFR_FLOW_FWG", 256, 0, 1 << 20);
   s->flow_wg = knob("PFR_FLOW_WG", 1024, 0, 1 << 20);   // functional from the bottom-up passes (symmetric paired sweeps)
   s->n = S.n;
   s->nnz = S.nnz;
@@ -949,6 +972,14 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     const char* be = getenv("PFR_SCHUR_BLK_MIN");
     const int blk_min = be ? atoi(be) : 24;
     const int L = (int)S.level_ptr.size() - 1;
+    // the factorisation flow's region: every update block there goes through the block kernel (its Schur tasks)
+    s->fflow_lcut = L;
+    if (sym && (s->flow & 4)) {
+      const int64_t ng = s->Fc / 64;
+      while (s->fflow_lcut > 0 && (int64_t)(S.level_ptr[s->fflow_lcut] - S.level_ptr[s->fflow_lcut - 1]) * ng < s->flow_fwg)
+        --s->fflow_lcut;
+    }
+    std::vector<int32_t> blk_begin(S.fronts.size(), 0), blk_end(S.fronts.size(), 0);
     for (int l = 0; l < L; ++l) {
       for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
         const int t = S.level_fronts[e];
@@ -977,7 +1008,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
           }
         }
         std::sort(more.begin(), more.end());
-        if (sym && blk_min > 0 && r >= blk_min) {
+        blk_begin[t] = blk_end[t] = (int32_t)bv.size();
+        if (sym && ((blk_min > 0 && r >= blk_min) || (F.level >= s->fflow_lcut && r > 0))) {
           // 16 x BC blocks touching the lower triangle; wave w owns the 4 x 4 tile (w / tcw, w % tcw)
           constexpr int B = pfr::SCHUR_BLK;
           const int BC = s->schur_bc, tcw = BC / 4;
@@ -999,6 +1031,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
               bgxp.push_back((int32_t)bgx.size());
             }
           blk_front[t] = 1;
+          blk_end[t] = (int32_t)bv.size();
           continue;
         }
         // super-tiles of (SCHUR_TM SCHUR_SR) x (SCHUR_TN SCHUR_SC): lane group `sub` owns the
@@ -1057,7 +1090,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     std::vector<int2> ax, orec, ox;
     s->asm_ptr.assign(1, 0);
     s->item_ptr.assign(1, 0);
-    std::vector<int32_t> nzm, s1m, rec0(S.fronts.size(), 0);
+    std::vector<int32_t> nzm, s1m, rec0(S.fronts.size(), 0), item_begin(S.fronts.size(), 0);
     std::vector<std::pair<int32_t, int32_t>> morem;   // (a * f + b, id)
     for (int l = 0; l < L; ++l) {
       for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
@@ -1106,6 +1139,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
             for (int32_t id : extras(a, b)) ax.push_back(make_int2(k, id));
             if (av.size() % 8 == 0) axp.push_back((int32_t)ax.size());
           }
+        item_begin[t] = (int32_t)iv.size();
         for (int kind = 0; kind < (sym ? 1 : 2); ++kind)   // symmetric: U12 = diag(U11) L21^T implicit
           for (int i0 = ns; i0 < f; i0 += pfr::OFF_G * pfr::OFF_RPL) {
             iv.push_back(make_int4(t, i0, kind, (int32_t)orec.size()));
@@ -1186,6 +1220,79 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
         (rc = s->up(&s->d_items, iv)) || (rc = s->up(&s->d_orec, orec)) || (rc = s->up(&s->d_oxp, oxp)) ||
         (rc = s->up(&s->d_ox, ox)) || (rc = s->up(&s->d_rec0, rec0)))
       return bail(rc);
+    if (s->fflow_lcut < L) {
+      // task list of the factorisation flow, levels upwards: per level the A11 tasks, then 16-item L21 tasks,
+      // then one task per update block
+      std::vector<int32_t> slot(S.fronts.size(), -1), item_end, nb, nc, cptr(1, 0), cslot;
+      std::vector<int4> tasks;
+      int nslots = 0;
+      for (int l = s->fflow_lcut; l < L; ++l)
+        for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) slot[S.level_fronts[e]] = nslots++;
+      item_end.resize(nslots);
+      nb.resize(nslots);
+      nc.resize(nslots);
+      std::vector<std::vector<int>> kids(nslots);
+      for (size_t t = 0; t < S.fronts.size(); ++t) {
+        if (slot[t] < 0) continue;
+        const int sl = slot[t];
+        nc[sl] = blk_end[t] - blk_begin[t];
+        if (S.fronts[t].parent >= 0 && slot[S.fronts[t].parent] >= 0) kids[slot[S.fronts[t].parent]].push_back((int)t);
+      }
+      // item ranges: a front's items are consecutive, the next front's (in level order) start where it ends
+      for (int l = s->fflow_lcut; l < L; ++l)
+        for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
+          const int t = S.level_fronts[e];
+          const int end = e + 1 < S.level_ptr[l + 1] ? item_begin[S.level_fronts[e + 1]] : s->item_ptr[l + 1];
+          item_end[slot[t]] = end;
+          nb[slot[t]] = (end - item_begin[t] + 15) / 16;
+        }
+      for (int sl = 0; sl < nslots; ++sl) {
+        for (int c : kids[sl])
+          if (nc[slot[c]] > 0) cslot.push_back(slot[c]);
+        cptr.push_back((int32_t)cslot.size());
+      }
+      for (int l = s->fflow_lcut; l < L; ++l) {
+        for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
+          const int t = S.level_fronts[e];
+          tasks.push_back(make_int4(0, t, 0, slot[t]));
+        }
+        for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
+          const int t = S.level_fronts[e];
+          for (int it = item_begin[t]; it < item_end[slot[t]]; it += 16) tasks.push_back(make_int4(1, t, it, slot[t]));
+        }
+        for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
+          const int t = S.level_fronts[e];
+          for (int b = blk_begin[t]; b < blk_end[t]; ++b) tasks.push_back(make_int4(2, t, b, slot[t]));
+        }
+      }
+      if (cslot.empty()) cslot.push_back(0);
+      int4* dt;
+      int32_t *dcp, *dcs, *die, *dnb, *dnc;
+      unsigned* dw;
+      const int64_t nw = (1 + 3 * (int64_t)nslots * (s->Fc / 64) + 3) / 4 * 4;
+      if ((rc = s->up(&dt, tasks)) || (rc = s->up(&dcp, cptr)) || (rc = s->up(&dcs, cslot)) || (rc = s->up(&die, item_end)) ||
+          (rc = s->up(&dnb, nb)) || (rc = s->up(&dnc, nc)) || (rc = s->alloc(&dw, nw)))
+        return bail(rc);
+      pfr::FactorFlowDesc& d = s->ffd;
+      d.tasks = dt;
+      d.ntasks = (int)tasks.size();
+      d.cptr = dcp;
+      d.cslot = dcs;
+      d.item_end = die;
+      d.nb = dnb;
+      d.nc = dnc;
+      d.nslots = nslots;
+      d.words = dw;
+      d.words_bytes = (size_t)nw * sizeof(unsigned);
+      d.items = s->d_items;
+      d.orec = s->d_orec;
+      d.oxp = s->d_oxp;
+      d.ox = s->d_ox;
+      d.blocks = s->d_blocks;
+      d.bg1 = s->d_bg1;
+      d.bgxp = s->d_bgxp;
+      d.bgx = s->d_bgx;
+    }
   }
   std::vector<int32_t> cp(colptr, colptr + S.n + 1), ri(rowind, rowind + S.nnz);
   if ((rc = s->up(&s->d_colptr, cp)) || (rc = s->up(&s->d_rowind, ri))) return bail(rc);
@@ -1419,7 +1526,7 @@ int pfr_last_kernel_timings(const pfr_solver* s, double* ms, int64_t* launches) 
   }
   if (!(s->timing & 2) || s->n_tev == 0) return PFR_OK;
   HIP_TRY(hipEventSynchronize(s->tev[s->n_tev - 1].ev[5]));
-  const int L = (int)s->level_ptr.size() - 1;
+  const int L = std::min((int)s->level_ptr.size() - 1, s->timed_levels);   // the flow region has no level events
   for (int c = 0; c < s->n_tev; ++c) {
     if (!s->tev[c].used[0]) continue;
     for (int l = 0; l < L; ++l) {

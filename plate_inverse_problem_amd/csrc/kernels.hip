@@ -1895,11 +1895,18 @@ __device__ __forceinline__ void flow_publish(unsigned* w, bool add) {
   }
 }
 
+// the task record, wave-uniform (scalar registers: its indices address whole-workgroup data)
+__device__ __forceinline__ int4 flow_task(const int4* tasks, int task) {
+  const int4 t = tasks[task];
+  return make_int4(__builtin_amdgcn_readfirstlane(t.x), __builtin_amdgcn_readfirstlane(t.y),
+                   __builtin_amdgcn_readfirstlane(t.z), __builtin_amdgcn_readfirstlane(t.w));
+}
+
 __device__ __forceinline__ int flow_ticket(unsigned* ticket) {
   __shared__ int s_t;
   if (threadIdx.x == 0) s_t = (int)__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  return s_t;
+  return __builtin_amdgcn_readfirstlane(s_t);   // uniform: the task's indices live in scalar registers
 }
 
 // The paired top-down pass (k_usolve2_level + k_usolve2_upd) over the narrow top: per front and
@@ -1911,7 +1918,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   const int tk = flow_ticket(G.ticket);
   if (tk >= G.ntasks * ngroups) return;
   const int task = tk / ngroups, g = tk - task * ngroups;
-  const int4 T = G.tasks[task];
+  const int4 T = flow_task(G.tasks, task);
   Ctx c;
   c.lane = threadIdx.x & 63;
   c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1964,7 +1971,7 @@ __global__ __launch_bounds__(256) void k_lsolve_flow(DevPattern P, LSlices S, co
   const int tk = flow_ticket(G.ticket);
   if (tk >= G.ntasks * ngroups) return;
   const int task = tk / ngroups, g = tk - task * ngroups;
-  const int4 T = G.tasks[task];
+  const int4 T = flow_task(G.tasks, task);
   Ctx c;
   c.lane = threadIdx.x & 63;
   c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1993,6 +2000,94 @@ __global__ __launch_bounds__(256) void k_lsolve_flow(DevPattern P, LSlices S, co
                 SRB * c.W * Sp);
     if (!ok) atomicOr(G.flags + c.q, PFR_FLAG_BAD_PIVOT);
     flow_publish(G.rcnt + wz, true);
+  }
+}
+
+// The factorisation's narrow top (symmetric mode) as ONE dependency-driven launch of 16-wave workgroups, per
+// front and 64-frequency group three kinds of task (ticket order: per level upwards its A tasks, B tasks,
+// C tasks -- topological):
+//  A  the A11 LU with the assembly gathered in (factor_sym_front; waves 0-7 the first 32 frequencies, 8-15
+//     the second), after every in-region child's C tasks (their update matrices feed the gather);
+//  B  16 consecutive items of the front's L21 rows (offdiag_item, one per wave), after the front's A task;
+//  C  one 16 x 16 block of the update matrix (schur_blk_body; every update block of the region goes through
+//     the block kernel), after all the front's B tasks.
+// Hand-offs as the solve passes' (flow_wait / flow_publish).
+struct FFlowArgs {
+  const int4* tasks;     // (kind, front, first item / block, region slot)
+  int ntasks;
+  const int* cptr;       // per slot: in-region children with update blocks, cslot[cptr[slot] .. cptr[slot + 1])
+  const int* cslot;
+  const int* item_end;   // per slot: end of the front's items (global item index)
+  const int* nb;         // per slot: B tasks of the front
+  const int* nc;         // per slot: C tasks (update blocks) of the front
+  unsigned* ticket;
+  unsigned* a_done;      // per (slot, group)
+  unsigned* b_cnt;
+  unsigned* c_cnt;
+  int* flags;
+  const int4* items;
+  const int2* orec;
+  const int* oxp;
+  const int2* ox;
+  const int4* blocks;
+  const int* bg1;
+  const int* bgxp;
+  const int2* bgx;
+  AsmArgs asmb;
+};
+
+// the A and B task bodies out of line: each gets the register budget to itself (inlined into one kernel the
+// three bodies' live ranges added up and spilled).  Arguments by value: a reference would put the kernel's
+// argument block in per-lane memory, and every index loaded from it would count as divergent.
+static __device__ __noinline__ void fflow_a(DevPattern P, int front, cplx* F, int64_t Fc, int* flags, AsmArgs asmb, int g,
+                                            int lane, int w) {
+  Ctx c;
+  c.lane = lane;
+  c.w = w & 7;
+  c.W = 8;
+  constexpr int QG = 64 / FAC_G;
+  c.q = (int64_t)(FAC_G * g + (w >> 3)) * QG + lane % QG;
+  factor_sym_front(P, front, F, Fc, flags, asmb, c, lane / QG);
+}
+
+static __device__ __noinline__ void fflow_b(DevPattern P, const int4* items, const int2* orec, const int* oxp,
+                                            const int2* ox, int wid, cplx* F, int64_t Fc, const double* freqs,
+                                            const cplx* K, const double* M, int g) {
+  offdiag_item<0, false>(P, items, wid, orec, oxp, ox, F, Fc, freqs, K, M, nullptr, 0, 1, g);
+}
+
+__global__ __launch_bounds__(1024) void k_factor_flow(DevPattern P, cplx* __restrict__ F, int64_t Fc, FFlowArgs G,
+                                                      int ngroups) {
+  const int tk = flow_ticket(G.ticket);
+  if (tk >= G.ntasks * ngroups) return;
+  const int task = tk / ngroups, g = tk - task * ngroups;
+  const int4 T = flow_task(G.tasks, task);
+  const int sl = T.w;
+  const int64_t wg = (int64_t)sl * ngroups + g;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  bool ok = true;
+  if (T.x == 0) {
+    const int c1 = G.cptr[sl + 1];
+    for (int k = G.cptr[sl]; k < c1; ++k) {
+      const int cs = G.cslot[k];
+      ok = flow_wait(G.c_cnt + (int64_t)cs * ngroups + g, (unsigned)G.nc[cs]) && ok;
+    }
+    fflow_a(P, T.y, F, Fc, G.flags, G.asmb, g, lane, w);
+    if (!ok) atomicOr(G.flags + (int64_t)g * 64 + lane, PFR_FLAG_BAD_PIVOT);
+    flow_publish(G.a_done + wg, false);
+  } else if (T.x == 1) {
+    ok = flow_wait(G.a_done + wg, 1u);
+    const int wid = T.z + w;
+    if (wid < G.item_end[sl])
+      fflow_b(P, G.items, G.orec, G.oxp, G.ox, wid, F, Fc, G.asmb.freqs, G.asmb.K, G.asmb.M, g);
+    if (!ok) atomicOr(G.flags + (int64_t)g * 64 + lane, PFR_FLAG_BAD_PIVOT);
+    flow_publish(G.b_cnt + wg, true);
+  } else {
+    ok = flow_wait(G.b_cnt + wg, (unsigned)G.nb[sl]);
+    schur_blk_body<4, 1, 16>(P, T.z, g, G.blocks, G.bg1, G.bgxp, G.bgx, F, Fc);
+    if (!ok) atomicOr(G.flags + (int64_t)g * 64 + lane, PFR_FLAG_BAD_PIVOT);
+    flow_publish(G.c_cnt + wg, true);
   }
 }
 
@@ -3235,6 +3330,16 @@ void launch_lsolve_flow(int rhs_mode, const DevPattern& P, const LFlowDesc& d, i
   (void)hipMemsetAsync(d.words, 0, d.words_bytes, st);
   if (rhs_mode == 0) LAUNCH(k_lsolve_flow<0>, dim3((unsigned)(d.ntasks * ngroups)), dim3(256), st, P, S, F, Fc, G, ngroups);
   else LAUNCH(k_lsolve_flow<3>, dim3((unsigned)(d.ntasks * ngroups)), dim3(256), st, P, S, F, Fc, G, ngroups);
+}
+
+void launch_factor_flow(const DevPattern& P, const FactorFlowDesc& d, int ngroups, double2* F, int64_t Fc,
+                        const AsmArgs& asmb, hipStream_t st) {
+  if (d.ntasks <= 0) return;
+  const int64_t per = (int64_t)d.nslots * ngroups;
+  FFlowArgs G{d.tasks, d.ntasks, d.cptr, d.cslot, d.item_end, d.nb, d.nc, d.words, d.words + 1, d.words + 1 + per,
+              d.words + 1 + 2 * per, d.flags, d.items, d.orec, d.oxp, d.ox, d.blocks, d.bg1, d.bgxp, d.bgx, asmb};
+  (void)hipMemsetAsync(d.words, 0, d.words_bytes, st);
+  LAUNCH(k_factor_flow, dim3((unsigned)(d.ntasks * ngroups)), dim3(1024), st, P, F, Fc, G, ngroups);
 }
 
 void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nrows, const double2* Kd,

@@ -107,6 +107,32 @@ struct LFlowDesc {
 };
 void launch_lsolve_flow(int rhs_mode, const DevPattern& P, const LFlowDesc& d, int ngroups, const double2* F, int64_t Fc,
                         double2* const* WV, const RhsDesc* rd, double2* const* Y, const int* const* reach, hipStream_t st);
+// the factorisation's narrow top (symmetric mode, operator form) in one launch: tasks (kind 0 A11 LU, 1 L21
+// items, 2 Schur blocks; front; first item / block; slot), words ticket, a_done, b_cnt, c_cnt (1 + 3 nslots
+// ngroups unsigned, zeroed by the launcher)
+struct FactorFlowDesc {
+  const int4* tasks = nullptr;
+  int ntasks = 0;
+  const int* cptr = nullptr;
+  const int* cslot = nullptr;
+  const int* item_end = nullptr;
+  const int* nb = nullptr;
+  const int* nc = nullptr;
+  int nslots = 0;
+  unsigned* words = nullptr;
+  size_t words_bytes = 0;
+  int* flags = nullptr;
+  const int4* items = nullptr;
+  const int2* orec = nullptr;
+  const int* oxp = nullptr;
+  const int2* ox = nullptr;
+  const int4* blocks = nullptr;
+  const int* bg1 = nullptr;
+  const int* bgxp = nullptr;
+  const int2* bgx = nullptr;
+};
+void launch_factor_flow(const DevPattern& P, const FactorFlowDesc& d, int ngroups, double2* F, int64_t Fc,
+                        const AsmArgs& asmb, hipStream_t st);
 // Hessian sweep: tangent right-hand sides (rows of the permuted matrix, or of its
 // transpose with accumulate = 1) and the directional derivative of the loss cotangent
 void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nrows, const double2* Kd,

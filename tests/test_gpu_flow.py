@@ -1,0 +1,68 @@
+"""GPU: the dependency-driven passes over the narrow top of the elimination tree (PFR_FLOW bits: 1 the paired
+top-down solve, 2 the sliced bottom-up chain, 4 the factorisation) at C3 size against the level-by-level
+launches and the extended-precision truth.
+
+C4's per-rank workload (512 frequencies of the C3 sweep, the block with the resonance) and a 2,048-frequency
+chunk: with every flow the loss, the 18 gradient partials and fr must equal the level-launch results to
+rounding (the same arithmetic per entry; only the A11 LU's row-to-wave map and the Schur kernel of the small
+update blocks differ: measured ~1e-15), and fr at the fixture frequencies inside the block must stay within
+the C3 tolerance of the truth (1e-7, test_gpu_fullsize.py).
+"""
+import gc
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import make_problem, report
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _run(monkeypatch, flow, lo, hi):
+    from plate_inverse_problem_amd import _native
+    from plate_inverse_problem_amd.Problem import _coeffs18
+    monkeypatch.setenv("PFR_FLOW", str(flow))
+    T = np.load(os.path.join(GOLDEN, "c3_grad_truth.npz"))
+    p = make_problem("orthotropic", ny=25, device="cuda:0")
+    try:
+        sel = np.arange(lo, hi)
+        f, ref = T["freqs"][sel], T["ref"][sel]
+        eng = p.engine(sel.size)
+        c = _coeffs18(p._transform(), torch.as_tensor(T["theta"])).detach().numpy()
+        eng.set_coefficients(c)
+        dev = eng.device
+        w = torch.zeros(eng.n_stiff, dtype=torch.complex128, device=dev)
+        loss = torch.zeros(1, dtype=torch.float64, device=dev)
+        flags = torch.zeros(sel.size, dtype=torch.int32, device=dev)
+        eng.sweep(torch.as_tensor(f, device=dev), _native.LOSS_MSE_LOG_AFC,
+                  ref=torch.view_as_real(torch.as_tensor(ref.astype(np.complex128), device=dev)), scale=1.0 / sel.size,
+                  loss=loss, w=torch.view_as_real(w), flags=flags)
+        F = np.load(os.path.join(GOLDEN, "c3_truth.npz"))
+        inside = (F["index"] >= lo) & (F["index"] < hi)
+        fr = p.solveForward(F["freqs"][inside])
+        out = (float(loss.item()), eng.expand(w).cpu().numpy(), fr, F["fr_true"][inside], int(flags.count_nonzero()))
+        return out
+    finally:
+        p._engine = None
+        del p
+        gc.collect()
+        torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("lo,hi", [(1024, 1536), (0, 2048)])
+def test_flows_match_level_launches(monkeypatch, lo, hi):
+    base = _run(monkeypatch, 0, lo, hi)
+    for flow in (1, 2, 4, 7):
+        got = _run(monkeypatch, flow, lo, hi)
+        dl = abs(got[0] / base[0] - 1)
+        dw = float(np.max(np.abs(got[1] - base[1])) / np.max(np.abs(base[1])))
+        dfr = float(np.max(np.abs(got[2] / base[2] - 1)))
+        err = float(np.max(np.abs(got[2] / got[3] - 1)))
+        report(f"flow{flow}_{lo}_{hi}", loss_rel=dl, w_rel=dw, fr_rel=dfr, fr_vs_truth=err, flagged=got[4])
+        assert got[4] == 0, (flow, got[4])
+        assert dl < 1e-11 and dw < 1e-10 and dfr < 1e-11, (flow, dl, dw, dfr)
+        assert err < 1e-7, (flow, err)

@@ -173,6 +173,8 @@ def test_c2_forward_sweep_matches_truth():
     {"PFR_FLOW": "3"},                 # both solve passes dependency-driven (every level narrow at this size)
     {"PFR_FLOW": "3", "PFR_FLOW_WG": "16"},   # ... only the top levels, the rest level by level
     {"PFR_FLOW": "2"},                 # the bottom-up chain only
+    {"PFR_FLOW": "7"},                 # the factorisation's narrow top too (every level at this size)
+    {"PFR_FLOW": "7", "PFR_FLOW_FWG": "8", "PFR_FLOW_WG": "8"},   # ... only the topmost levels
 ])
 def test_kernel_variants_match_oracle(env, monkeypatch):
     from oracle.plate_oracle import loss_and_grad
