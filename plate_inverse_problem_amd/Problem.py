@@ -748,9 +748,16 @@ class Problem:
         def model(params):
             p = torch.as_tensor(np.asarray(params, dtype=np.float64)).detach()
             n = p.numel()
-            c = _coeffs18(transform, p * scaling).detach().numpy()
-            jac = torch.autograd.functional.jacobian(c_real, p).numpy().reshape(18, 2, n)
-            dc = jac[:, 0] + 1j * jac[:, 1]                                                # (18, n)
+            if self.material.atype in _JET_TYPES:
+                # the same c (to the bit) as getLossFunction's jet transform, and its Jacobian in p
+                from ._abd_jet import abd_and_jacobian
+                sc = np.broadcast_to(np.asarray(scaling, dtype=np.float64), (n,))
+                c, J = abd_and_jacobian(self.material, self.geometry.height, (p * scaling).numpy())
+                dc = J * sc[None, :]                                                      # (18, n)
+            else:
+                c = _coeffs18(transform, p * scaling).detach().numpy()
+                jac = torch.autograd.functional.jacobian(c_real, p).numpy().reshape(18, 2, n)
+                dc = jac[:, 0] + 1j * jac[:, 1]                                            # (18, n)
             d2 = np.stack([torch.autograd.functional.hessian(lambda x, m=m: c_real(x)[m], p).numpy()
                            for m in range(36)]).reshape(18, 2, n, n)
             d2c = d2[:, 0] + 1j * d2[:, 1]                                                 # (18, n, n)

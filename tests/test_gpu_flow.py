@@ -3,10 +3,14 @@ top-down solve, 2 the sliced bottom-up chain, 4 the factorisation) at C3 size ag
 launches and the extended-precision truth.
 
 C4's per-rank workload (512 frequencies of the C3 sweep, the block with the resonance) and a 2,048-frequency
-chunk: with every flow the loss, the 18 gradient partials and fr must equal the level-launch results to
-rounding (the same arithmetic per entry; only the A11 LU's row-to-wave map and the Schur kernel of the small
-update blocks differ: measured ~1e-15), and fr at the fixture frequencies inside the block must stay within
-the C3 tolerance of the truth (1e-7, test_gpu_fullsize.py).
+chunk, with the global-memory A11 LU on every level (PFR_FAC_LDS=0: the flow's A11 tasks use it, and the LDS
+LU of the level launches rounds differently): with every flow the loss, the 18 gradient partials and fr must
+EQUAL the level-launch results -- the same operations per entry in the same order (the A11 LU's row-to-wave
+map and, for the small update blocks, the Schur kernel differ, not the arithmetic), so any hand-off that let a
+task read a stale or unfinished value shows as a difference.  With the default LDS LU on the level launches,
+fr at the fixture frequencies inside the block must lie within the accuracy class of the reference's refined
+solves against the truth (2e-7: the oracle's refined SuperLU is within 1.65e-7 over the 4,096 frequencies,
+c3_grad_truth.npz; the corrected static-pivot fr moves by ~1e-7 with the rounding of the pivot-block LU).
 """
 import gc
 import os
@@ -22,10 +26,11 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def _run(monkeypatch, flow, lo, hi):
+def _run(monkeypatch, flow, lo, hi, fac_lds="0"):
     from plate_inverse_problem_amd import _native
     from plate_inverse_problem_amd.Problem import _coeffs18
     monkeypatch.setenv("PFR_FLOW", str(flow))
+    monkeypatch.setenv("PFR_FAC_LDS", fac_lds)
     T = np.load(os.path.join(GOLDEN, "c3_grad_truth.npz"))
     p = make_problem("orthotropic", ny=25, device="cuda:0")
     try:
@@ -64,5 +69,19 @@ def test_flows_match_level_launches(monkeypatch, lo, hi):
         err = float(np.max(np.abs(got[2] / got[3] - 1)))
         report(f"flow{flow}_{lo}_{hi}", loss_rel=dl, w_rel=dw, fr_rel=dfr, fr_vs_truth=err, flagged=got[4])
         assert got[4] == 0, (flow, got[4])
-        assert dl < 1e-11 and dw < 1e-10 and dfr < 1e-11, (flow, dl, dw, dfr)
-        assert err < 1e-7, (flow, err)
+        assert dl == 0 and dw == 0 and dfr == 0, (flow, dl, dw, dfr)
+        assert err < 2e-7, (flow, err)
+
+
+def test_factor_flow_default_lds_accuracy(monkeypatch):
+    """The factorisation flow against the default level launches (LDS A11 LU on their few-workgroup levels):
+    both within the refined solves' accuracy class of the truth, loss and partials to that class too."""
+    base = _run(monkeypatch, 0, 1024, 1536, fac_lds="-1")
+    got = _run(monkeypatch, 7, 1024, 1536, fac_lds="-1")
+    e0 = float(np.max(np.abs(base[2] / base[3] - 1)))
+    e1 = float(np.max(np.abs(got[2] / got[3] - 1)))
+    dl = abs(got[0] / base[0] - 1)
+    dw = float(np.max(np.abs(got[1] - base[1])) / np.max(np.abs(base[1])))
+    report("flow7_default_lds", fr_vs_truth_level=e0, fr_vs_truth_flow=e1, loss_rel=dl, w_rel=dw)
+    assert got[4] == 0 and e0 < 2e-7 and e1 < 2e-7
+    assert dl < 1e-7 and dw < 4e-7
