@@ -48,6 +48,14 @@ extern "C" {
                                * accuracy the reference's refined UMFPACK solves give; the loss, its
                                * cotangent and the gradient are formed from the corrected fr */
 
+#define PFR_CHECK_REFINE_ADJ 16 /* selective adjoint refinement (loss sweeps with PFR_CHECK_CORRECT, symmetric
+                               * mode): after the forward residual walk, the 64-frequency groups holding a frequency
+                               * whose functional correction exceeds the tolerance (pfr_set_refine_tol; the
+                               * first-order fr error estimate, large next to a resonance) get one refinement step
+                               * of the fr adjoint, mu += A^-T (d fr / d x - A^T mu), and their gradient contraction
+                               * and correction are redone with it: the gradient of those frequencies to the
+                               * accuracy of the reference's refined solves, the other groups untouched */
+
 /* loss types (Problem.py:948-975) */
 #define PFR_LOSS_NONE -1
 #define PFR_LOSS_MSE 0
@@ -231,6 +239,8 @@ PFR_API int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_
  * seeds (the directional derivatives of the loss cotangent) are formed from the uncorrected fr, so its
  * Hessian is that of the uncorrected functional (the two differ by the solve's first-order error). */
 PFR_API int pfr_set_check(pfr_solver* s, int32_t mode, double tol, double* berr_dev);
+/* PFR_CHECK_REFINE_ADJ threshold: refine the groups where |Re(mu^T r)| > tol |fr| (default 2e-8) */
+PFR_API int pfr_set_refine_tol(pfr_solver* s, double tol);
 
 /* Per-phase device times [ms] of the last pfr_sweep/pfr_solve call on this solver, measured with HIP
  * events on the call's stream (0 = factor, 1 = forward solves, 2 = functional, 3 = adjoint solves,

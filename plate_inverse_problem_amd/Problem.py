@@ -140,8 +140,10 @@ class _Engine:
         # second order in the solve's error, the accuracy of the reference's refined UMFPACK solves) by
         # default; PFR_CHECK=<PFR_CHECK_* bits> / PFR_CHECK_TOL override; refinement (bit 4) off by default
         self.check_mode = int(os.environ.get("PFR_CHECK", str(_native.PFR_CHECK_FORWARD | _native.PFR_CHECK_ADJOINT
-                                                              | _native.PFR_CHECK_CORRECT)))
+                                                              | _native.PFR_CHECK_CORRECT | _native.PFR_CHECK_REFINE_ADJ)))
         self.check_tol = float(os.environ.get("PFR_CHECK_TOL", "1e-10"))
+        # the selective adjoint refinement's group threshold (first-order fr error estimate)
+        self.refine_tol = float(os.environ.get("PFR_REFINE_TOL", "2e-8"))
         self.ensure(n_freqs)
 
     def leaf_size_for(self, n_freqs: int) -> int:
@@ -228,6 +230,7 @@ class _Engine:
             sv.set_operator(torch.view_as_real(self.K), self.mass)      # K(theta) shared by the lanes
             sv.set_functional(self._sup, self._a3, self._ts)
             sv.set_check(self.check_mode, self.check_tol)
+            sv.set_refine_tol(self.refine_tol)
         self._coef_key = None          # new solvers: rhs scale not set yet
 
     def set_check(self, mode: int | None = None, tol: float | None = None):

@@ -24,6 +24,7 @@ PFR_FLAG_BAD_PIVOT = 1
 PFR_FLAG_BACKWARD_ERROR = 2
 PFR_FLAG_BACKWARD_ERROR_ADJ = 4
 PFR_CHECK_FORWARD, PFR_CHECK_ADJOINT, PFR_CHECK_REFINE, PFR_CHECK_CORRECT = 1, 2, 4, 8
+PFR_CHECK_REFINE_ADJ = 16
 LOSS_NONE, LOSS_MSE, LOSS_RMSE, LOSS_MSE_AFC, LOSS_MSE_LOG_AFC, LOSS_COTANGENT = -1, 0, 1, 2, 3, 4
 LOSS_IDS = {"MSE": LOSS_MSE, "RMSE": LOSS_RMSE, "MSE_AFC": LOSS_MSE_AFC, "MSE_LOG_AFC": LOSS_MSE_LOG_AFC}
 
@@ -78,6 +79,7 @@ _PROTOS = {
     "pfr_hessian_sweep": (C.c_int, [_P, C.c_int32, _P, C.c_int32, _P, C.c_double, C.c_int32, _P, _P, _P, _P, _P,
                                     _P]),
     "pfr_set_check": (C.c_int, [_P, C.c_int32, C.c_double, _P]),
+    "pfr_set_refine_tol": (C.c_int, [_P, C.c_double]),
     "pfr_set_timing": (C.c_int, [_P, C.c_int32]),
     "pfr_last_timings": (C.c_int, [_P, _DP]),
     "pfr_last_kernel_timings": (C.c_int, [_P, _DP, _P]),
@@ -296,6 +298,11 @@ class Solver:
                                int(bool(transpose)), self._stream(y)), "pfr_matvec")
 
     # ---- backward-error checks
+    def set_refine_tol(self, tol: float):
+        """Threshold of the selective adjoint refinement (PFR_CHECK_REFINE_ADJ): groups where the functional
+        correction exceeds tol |fr| get one refinement step of the fr adjoint."""
+        check(lib().pfr_set_refine_tol(self._h, float(tol)), "pfr_set_refine_tol")
+
     def set_check(self, mode: int, tol: float, berr=None):
         """PFR_CHECK_* bits, flag tolerance; ``berr`` (device float64, 2 per frequency of each later
         call, or None) receives the componentwise backward errors (forward, adjoint)."""

@@ -80,7 +80,7 @@ struct pfr_solver {
   int2* d_asm_x = nullptr;              // (record within chunk, child element id)
   std::vector<int32_t> asm_ptr;         // record offset of each level (multiple of 8)
   int32_t* d_rec0 = nullptr;            // per front: its first A11 assembly record (fused assembly)
-  int fuse_asm = 1;                     // PFR_FUSE_ASM: A11 gathered by k_factor_sym itself (symmetric mode,
+  int fuse_asm = 0;                     // PFR_FUSE_ASM: A11 gathered by k_factor_sym itself (symmetric mode,
                                         // levels on the global-memory A11 LU)
   int32_t* d_colptr = nullptr;
   int32_t* d_rowind = nullptr;
@@ -220,6 +220,8 @@ struct pfr_solver {
   // per-frequency maxima scratch, forward and adjoint (kept zero between checks)
   int check_mode = 0;
   double check_tol = 1e-10;
+  double refine_tol = 2e-8;             // PFR_CHECK_REFINE_ADJ group threshold (pfr_set_refine_tol)
+  int32_t* gmask = nullptr;             // per 64-frequency group of the chunk: refine its adjoint
   double* berr_out = nullptr;
   double* d_berr_acc = nullptr;
 
@@ -425,7 +427,7 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
 // subset (0 forward rhs, 1 loss adjoint, -1 none): bottom-up passes visit only the reached
 // fronts; top-down passes treat the pivot values of unreached fronts as zero
 int solve_all(pfr_solver* s, int which, int rhs_mode, const pfr::RhsDesc& rd, const double2* Yin, double2* Out,
-              hipStream_t st, int subset = -1) {
+              hipStream_t st, int subset = -1, const int* gmask = nullptr) {
   const int L = (int)s->level_ptr.size() - 1;
   const int ngroups = (int)(s->Fc / 64);
   const bool up = (which == 0 || which == 2);
@@ -441,7 +443,7 @@ int solve_all(pfr_solver* s, int which, int rhs_mode, const pfr::RhsDesc& rd, co
     // the update parts split over several workgroups: L solves, and U solves in symmetric mode
     const int split = (which == 0 || (which == 1 && s->sym)) ? solve_split(s, nf) : 1;
     pfr::launch_solve(which, rhs_mode, s->sym, s->P, lvl, nf, solve_W(s, l, nf), ngroups, s->F, s->Fc, s->WV, rd, Yin, Out,
-                      reach, st, split);
+                      reach, st, split, gmask);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -483,12 +485,14 @@ int forward_solve(pfr_solver* s, int rhs_mode, pfr::RhsDesc rd, double2* Out, hi
 
 // A^T l = g (g = rg.G, permuted), l -> Out.  Symmetric mode: the decoupled matrix is symmetric,
 // so L and U = diag(U) L^T again, then the Dirichlet rows of l are corrected.
-int adjoint_solve(pfr_solver* s, const pfr::RhsDesc& rg, double2* Out, hipStream_t st, int subset = -1) {
+int adjoint_solve(pfr_solver* s, const pfr::RhsDesc& rg, double2* Out, hipStream_t st, int subset = -1,
+                  const int* gmask = nullptr) {
   int rc;
   if (s->sym) {
-    if ((rc = solve_all(s, 0, 2, rg, nullptr, s->Y, st, subset)) || (rc = solve_all(s, 1, 0, rg, s->Y, Out, st, subset)))
+    if ((rc = solve_all(s, 0, 2, rg, nullptr, s->Y, st, subset, gmask)) ||
+        (rc = solve_all(s, 1, 0, rg, s->Y, Out, st, subset, gmask)))
       return rc;
-    pfr::launch_dirichlet_post(dir_desc(s), s->n_dir, Out, s->Fc, st);
+    pfr::launch_dirichlet_post(dir_desc(s), s->n_dir, Out, s->Fc, st, gmask);
     return PFR_OK;
   }
   if ((rc = solve_all(s, 2, 2, rg, nullptr, s->Y, st, subset))) return rc;
@@ -716,7 +720,7 @@ int set_reach(pfr_solver* s, int which, const std::vector<int32_t>& prows) {
 // b - A x is written there (the refinement step), nothing is checked.
 void check_solution(pfr_solver* s, int which, int mode, int rhs, const pfr::RhsDesc& rd, const double2* data,
                     int64_t ds, int nvalid, const double2* X, double2* R, int64_t q0, hipStream_t st,
-                    const double2* Mu = nullptr, bool check = true, bool contract = false) {
+                    const double2* Mu = nullptr, bool check = true, bool contract = false, const int* gmask = nullptr) {
   pfr::ResidDesc d;
   d.ptr = which == 0 ? s->d_rptr : s->d_cptr;
   d.idx = which == 0 ? s->d_ridx : s->d_cidx;
@@ -737,6 +741,7 @@ void check_solution(pfr_solver* s, int which, int mode, int rhs, const pfr::RhsD
   d.perm = s->P.perm;
   d.G = rd.G;
   d.walk = s->d_walk;
+  d.gmask = gmask;
   if (contract) {
     d.se = s->stiff;
     d.n_stiff = s->n_stiff;
@@ -922,7 +927,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->check_fused = knob("PFR_CHECK_FUSED", 0, 0, 1);   // measured 2.3 ms against 2 x 0.87 ms per 2,048-frequency chunk
   s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);
   s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);
-  s->fuse_asm = knob("PFR_FUSE_ASM", 1, 0, 1);
+  s->fuse_asm = knob("PFR_FUSE_ASM", 0, 0, 1);   // measured slower (2,048-frequency chunk: A11 classes 4.1 -> 6.6 ms)
   s->flow = knob("PFR_FLOW", 0, 0, 7);   // bit 0: paired top-down pass, bit 1: bottom-up chain, bit 2: factorisation
   s->flow_fwg = knob("PFR_FLOW_FWG", 256, 0, 1 << 20);
   s->flow_wg = knob("PFR_FLOW_WG", 1024, 0, 1 << 20);   // functional from the bottom-up passes (symmetric paired sweeps)
@@ -1419,7 +1424,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       (rc = s->alloc(&s->Y2, (int64_t)S.n * Fc)) || (rc = s->alloc(&s->XR, (int64_t)S.n * Fc)) ||
       (rc = s->alloc(&s->freqs, Fc)) || (rc = s->alloc(&s->loss_terms, Fc)) || (rc = s->alloc(&s->flags, Fc)) ||
       (rc = s->alloc(&s->tq, Fc)) || (rc = s->alloc(&s->d_berr_acc, 2 * Fc)) || (rc = s->alloc(&s->fr0, Fc)) ||
-      (rc = s->alloc(&s->mscale, Fc)) || (rc = s->alloc(&s->cpart, (int64_t)pfr::residual_parts(S.n) * Fc)))
+      (rc = s->alloc(&s->mscale, Fc)) || (rc = s->alloc(&s->cpart, (int64_t)pfr::residual_parts(S.n) * Fc)) ||
+      (rc = s->alloc(&s->gmask, Fc / 64)))
     return bail(rc);
   HIP_TRY(hipMemset(s->d_berr_acc, 0, 2 * Fc * sizeof(double)));
   if (s->sym && s->flow) {
@@ -1496,8 +1502,14 @@ int pfr_set_timing(pfr_solver* s, int32_t enable) {
   return PFR_OK;
 }
 
+int pfr_set_refine_tol(pfr_solver* s, double tol) {
+  if (!s || !(tol >= 0.0)) return fail(PFR_ERR_ARG, "bad refine tolerance");
+  s->refine_tol = tol;
+  return PFR_OK;
+}
+
 int pfr_set_check(pfr_solver* s, int32_t mode, double tol, double* berr_dev) {
-  if (!s || mode < 0 || mode > 15 || !(tol >= 0.0)) return fail(PFR_ERR_ARG, "bad check arguments");
+  if (!s || mode < 0 || mode > 31 || !(tol >= 0.0)) return fail(PFR_ERR_ARG, "bad check arguments");
   s->check_mode = mode;
   s->check_tol = tol;
   s->berr_out = berr_dev;
@@ -1882,11 +1894,26 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
       if (cwalk && !s->kpart) {
         if ((rc = s->alloc(&s->kpart, (int64_t)pfr::residual_parts(s->n) * 18 * Fc))) return rc;
       }
+      // selective adjoint refinement (PFR_CHECK_REFINE_ADJ): the groups next to a resonance, where the unrefined
+      // solves' first-order error dominates the gradient, get one refinement step of mu
+      const bool refine_adj = reverse && correct && cwalk && fn_fast && (s->check_mode & PFR_CHECK_REFINE_ADJ);
       if (correct) {
         // the forward residual walk: backward error (when checked) + the correction's dot products,
         // then the corrected fr, its loss terms and the per-frequency cotangent scales
         check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st, s->XA, want_f, cwalk);
         want_f = false;
+        pfr::launch_correct_finish(fa, s->fr0, s->cpart, pfr::residual_parts(s->n), Fc, nv, q0, fr_dev, s->loss_terms,
+                                   s->mscale, st, refine_adj ? s->gmask : nullptr, s->refine_tol);
+      }
+      if (refine_adj) {
+        // mu += A^-T (G - A^T mu) on the marked groups (G: the fr seed d fr / d x the adjoint solved), then their
+        // correction dot products and gradient contraction again with the refined mu, and their fr / m_q
+        check_solution(s, 1, 0, 2, rg, nullptr, 0, nv, s->XA, s->XR, q0, st, nullptr, false, false, s->gmask);
+        pfr::RhsDesc rr;
+        rr.G = s->XR;
+        if ((rc = adjoint_solve(s, rr, s->Y2, st, -1, s->gmask))) return rc;
+        pfr::launch_axpy_vec(s->XA, s->Y2, (int64_t)s->n * Fc, st, s->gmask, Fc);
+        check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st, s->XA, false, true, s->gmask);
         pfr::launch_correct_finish(fa, s->fr0, s->cpart, pfr::residual_parts(s->n), Fc, nv, q0, fr_dev, s->loss_terms,
                                    s->mscale, st);
       }

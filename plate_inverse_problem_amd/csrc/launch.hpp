@@ -55,9 +55,10 @@ void launch_schur_blk(int bc, const DevPattern& P, const int4* blocks, int nbloc
 // products with the update-row solution) runs first / last over `split` workgroups of SPLIT_W waves per
 // (front, frequency group) -- the top levels' few fronts otherwise pull their L21 blocks through one CU each
 constexpr int SPLIT_W = 4;
+// gmask (may be NULL): per 64-frequency group, solve it (the selective adjoint refinement's solves)
 void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups,
                   const double2* F, int64_t Fc, double2* WV, const RhsDesc& rd, const double2* Yin, double2* Out,
-                  const int* reach, hipStream_t st, int split = 1);
+                  const int* reach, hipStream_t st, int split = 1, const int* gmask = nullptr);
 // nslices (<= 4) bottom-up L solves as one chain of launches (blockIdx.z = slice; slice z: the fronts
 // lvl[z][0 .. nf[z]), its work vectors WV[z], rhs rd[z] (rhs_mode 0 or 3 for every slice), solution Y[z])
 void launch_lsolve_multi(int rhs_mode, const DevPattern& P, int nslices, const int* const* lvl, const int* nf, int W,
@@ -174,7 +175,7 @@ void launch_reduce(const double2* partial, int nparts, int n_stiff, const double
 // place) and the adjoint's Dirichlet rows (X in place)
 void launch_dirichlet_rhs(int src, const DirDesc& d, int n_crow, const RhsDesc& rd, double2* G, double2* Bc,
                           int64_t Fc, hipStream_t st);
-void launch_dirichlet_post(const DirDesc& d, int n_dir, double2* X, int64_t Fc, hipStream_t st);
+void launch_dirichlet_post(const DirDesc& d, int n_dir, double2* X, int64_t Fc, hipStream_t st, const int* gmask = nullptr);
 // Backward-error check: the original system's rows (forward) or columns (adjoint) in the permuted
 // numbering, A = K - omega^2 M (mode 0) or the explicit batch (mode 1); rhs 0 operator, 1 explicit
 // B, 2 vector G.  The per-frequency componentwise backward error accumulates in acc (max, zero on
@@ -202,6 +203,7 @@ struct ResidDesc {
   const double* se = nullptr;
   int n_stiff = 0;
   double2* kpart = nullptr;
+  const int* gmask = nullptr;  // per 64-frequency group: walk it (NULL: every group)
 };
 // Mu != NULL (mode 0, rhs 0): also the functional-correction dot products sum_p Mu_p r_p, one partial
 // per workgroup and frequency in cpart (residual_parts(n) x Fc), summed by launch_correct_finish
@@ -213,13 +215,15 @@ void launch_reduce_q(const double2* kpart, int nparts, int n_stiff, const double
 void launch_residual(int mode, int rhs, const ResidDesc& d, const double2* X, int64_t Fc, double2* R, double* acc,
                      hipStream_t st, const double2* Mu = nullptr, double2* cpart = nullptr);
 // corrected fr (fr_out, global index; may be NULL), loss terms and cotangent scales of a chunk
+// gmask != NULL: per 64-frequency group, 1 when some frequency's |correction| > tol |fr| (refine its adjoint)
 void launch_correct_finish(const FunctionalArgs& A, const double* fr0, const double2* cpart, int nparts, int64_t Fc,
                            int nvalid, int64_t q0, double* fr_out, double* loss_terms, double* mscale,
-                           hipStream_t st);
+                           hipStream_t st, int* gmask = nullptr, double tol = 0.0);
 // flags |= flag where acc[q] > tol (or not finite); acc cleared
 void launch_berr_finish(double* acc, int64_t Fc, int nvalid, double tol, int flag, int* flags, double* berr_out,
                         int64_t q0, int which, hipStream_t st);
-void launch_axpy_vec(double2* X, const double2* D, int64_t count, hipStream_t st);
+void launch_axpy_vec(double2* X, const double2* D, int64_t count, hipStream_t st, const int* gmask = nullptr,
+                     int64_t Fc = 64);
 void launch_scale_vec(double2* X, const double* m, int n, int64_t Fc, hipStream_t st);
 void launch_unpermute(const int* perm, int n, const double2* X, int64_t Fc, int nvalid, double2* out, hipStream_t st);
 void launch_matvec(const int* colptr, const int* rowind, int n, const double2* data, int64_t ds, const double2* x,
