@@ -191,6 +191,7 @@ struct pfr_solver {
   // workgroup, at most), PFR_US2_SMALL (largest front of a level the paired top-down solve treats
   // with its low-register small-front variant)
   int solve_wmax = 8, fac_wmax = 16, us2_small = 110;
+  int us2_cfg = 0;                      // PFR_US2_CFG: register shape of the small-front paired top-down pass
   int off_small = 1;                    // PFR_OFF_SMALL: no-prefix off-diagonal variant on levels of ns <= 8
   int fac_lds_qf = 1;                   // PFR_FAC_LDS_QF: frequencies per k_factor_sym_lds workgroup (1, 2 or 4)
   int fac_lds = -1;                     // PFR_FAC_LDS: which levels factor A11 in LDS (k_factor_sym_lds): n > 0
@@ -684,7 +685,7 @@ int sym_top_down_pair(pfr_solver* s, hipStream_t st, bool fwd_all = false) {
                         small, ngroups,
                         s->F, s->Fc, s->Y,
                         s->X, s->d_reach[0], fwd_all ? nullptr : s->d_reach[1], s->Y2, s->XA, s->d_reach[1], st,
-                        solve_split(s, nf));
+                        solve_split(s, nf), s->us2_cfg);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -918,6 +919,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->solve_wmax = knob("PFR_SOLVE_WMAX", 8, 1, 8);
   s->fac_wmax = knob("PFR_FAC_WMAX", 16, 1, 16);
   s->us2_small = knob("PFR_US2_SMALL", 110, 0, pfr::MAX_FRONT);
+  s->us2_cfg = knob("PFR_US2_CFG", 0, 0, 2);
   s->off_small = knob("PFR_OFF_SMALL", 1, 0, 1);
   s->split_target = knob("PFR_SOLVE_SPLIT", 256, 0, 1 << 20);
   s->fac_lds = knob("PFR_FAC_LDS", -1, -1, 64);   // LDS holds the lower triangle of up to 64 pivots x 4 frequencies

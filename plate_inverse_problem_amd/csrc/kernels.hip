@@ -3309,7 +3309,7 @@ void launch_fn_combine(const int* rows, int nrows, const double2* fcoef, double2
 
 void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, bool small, int ngroups,
                     const double2* F, int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0,
-                    const double2* Y1, double2* X1, const int* reach1, hipStream_t st, int split) {
+                    const double2* Y1, double2* X1, const int* reach1, hipStream_t st, int split, int small_cfg) {
   if (nfronts <= 0) return;
   UPair a{Y0, X0, reach0, skip0}, b{Y1, X1, reach1, nullptr};
   dim3 g(nfronts, ngroups), bl(64 * W);
@@ -3318,8 +3318,12 @@ void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, boo
   // register shape: many short waves)
   if (rs) LAUNCH((k_usolve2_upd<true, 2, 4>), dim3(nfronts * split, ngroups), dim3(64 * SPLIT_W), st, P, lvl, F, Fc, a, b,
                  split);
-  // symmetric mode only (the paired top-down pass serves the symmetric loss + gradient sweep)
-  if (small) LAUNCH((k_usolve2_level<true, 2, 4, 4>), g, bl, st, P, lvl, F, Fc, a, b, rs);
+  // symmetric mode only (the paired top-down pass serves the symmetric loss + gradient sweep).  Small-front levels:
+  // SR pivot rows per pass share each gathered update-row value (small_cfg 0: 2 rows x 4 values at 4 waves/SIMD;
+  // 1: 4 x 4 at 3; 2: 8 x 2 at 3 -- more rows per pass, fewer re-gathers of the update-row solution)
+  if (small && small_cfg == 1) LAUNCH((k_usolve2_level<true, 4, 4, 3>), g, bl, st, P, lvl, F, Fc, a, b, rs);
+  else if (small && small_cfg == 2) LAUNCH((k_usolve2_level<true, 8, 2, 3>), g, bl, st, P, lvl, F, Fc, a, b, rs);
+  else if (small) LAUNCH((k_usolve2_level<true, 2, 4, 4>), g, bl, st, P, lvl, F, Fc, a, b, rs);
   else LAUNCH((k_usolve2_level<true, 4, 8, 2>), g, bl, st, P, lvl, F, Fc, a, b, rs);
 }
 

@@ -170,6 +170,8 @@ def test_c2_forward_sweep_matches_truth():
     {"PFR_LEAF_SIZE": "10000"},        # the deep MMD tree on a narrow sweep
     {"PFR_ORDERING": "2", "PFR_LEAF_SIZE": "96", "PFR_MD_DELTA": "0"},   # the rounds 1-3 ordering
     {"PFR_FUSE_ASM": "1"},             # A11 gathered by the A11 LU kernel itself (no k_assemble_level launches)
+    {"PFR_US2_CFG": "1", "PFR_US2_SMALL": "1024"},   # small-front paired top-down pass, 4 rows x 4 values
+    {"PFR_US2_CFG": "2", "PFR_US2_SMALL": "1024"},   # ... 8 rows x 2 values
     {"PFR_FLOW": "3"},                 # both solve passes dependency-driven (every level narrow at this size)
     {"PFR_FLOW": "3", "PFR_FLOW_WG": "16"},   # ... only the top levels, the rest level by level
     {"PFR_FLOW": "2"},                 # the bottom-up chain only
