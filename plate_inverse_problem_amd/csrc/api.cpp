@@ -222,7 +222,9 @@ struct pfr_solver {
   int check_mode = 0;
   double check_tol = 1e-10;
   double refine_tol = 2e-8;             // PFR_CHECK_REFINE_ADJ group threshold (pfr_set_refine_tol)
-  int32_t* gmask = nullptr;             // per 64-frequency group of the chunk: refine its adjoint
+  double* gind = nullptr;               // per 64-frequency group: largest |correction| / |fr| of the chunk
+  int32_t* glist = nullptr;             // the groups whose adjoint is refined (REFINE_CAP, -1: none)
+  double2* Gx = nullptr;                // the fr seed of the forward solution (support rows; zero elsewhere)
   double* berr_out = nullptr;
   double* d_berr_acc = nullptr;
 
@@ -428,9 +430,9 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
 // subset (0 forward rhs, 1 loss adjoint, -1 none): bottom-up passes visit only the reached
 // fronts; top-down passes treat the pivot values of unreached fronts as zero
 int solve_all(pfr_solver* s, int which, int rhs_mode, const pfr::RhsDesc& rd, const double2* Yin, double2* Out,
-              hipStream_t st, int subset = -1, const int* gmask = nullptr) {
+              hipStream_t st, int subset = -1, const int* glist = nullptr) {
   const int L = (int)s->level_ptr.size() - 1;
-  const int ngroups = (int)(s->Fc / 64);
+  const int ngroups = glist ? pfr::REFINE_CAP : (int)(s->Fc / 64);
   const bool up = (which == 0 || which == 2);
   const int* reach = subset >= 0 ? s->d_reach[subset] : nullptr;
   for (int t = 0; t < L; ++t) {
@@ -444,7 +446,7 @@ int solve_all(pfr_solver* s, int which, int rhs_mode, const pfr::RhsDesc& rd, co
     // the update parts split over several workgroups: L solves, and U solves in symmetric mode
     const int split = (which == 0 || (which == 1 && s->sym)) ? solve_split(s, nf) : 1;
     pfr::launch_solve(which, rhs_mode, s->sym, s->P, lvl, nf, solve_W(s, l, nf), ngroups, s->F, s->Fc, s->WV, rd, Yin, Out,
-                      reach, st, split, gmask);
+                      reach, st, split, glist);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -487,13 +489,13 @@ int forward_solve(pfr_solver* s, int rhs_mode, pfr::RhsDesc rd, double2* Out, hi
 // A^T l = g (g = rg.G, permuted), l -> Out.  Symmetric mode: the decoupled matrix is symmetric,
 // so L and U = diag(U) L^T again, then the Dirichlet rows of l are corrected.
 int adjoint_solve(pfr_solver* s, const pfr::RhsDesc& rg, double2* Out, hipStream_t st, int subset = -1,
-                  const int* gmask = nullptr) {
+                  const int* glist = nullptr) {
   int rc;
   if (s->sym) {
-    if ((rc = solve_all(s, 0, 2, rg, nullptr, s->Y, st, subset, gmask)) ||
-        (rc = solve_all(s, 1, 0, rg, s->Y, Out, st, subset, gmask)))
+    if ((rc = solve_all(s, 0, 2, rg, nullptr, s->Y, st, subset, glist)) ||
+        (rc = solve_all(s, 1, 0, rg, s->Y, Out, st, subset, glist)))
       return rc;
-    pfr::launch_dirichlet_post(dir_desc(s), s->n_dir, Out, s->Fc, st, gmask);
+    pfr::launch_dirichlet_post(dir_desc(s), s->n_dir, Out, s->Fc, st, glist);
     return PFR_OK;
   }
   if ((rc = solve_all(s, 2, 2, rg, nullptr, s->Y, st, subset))) return rc;
@@ -721,7 +723,7 @@ int set_reach(pfr_solver* s, int which, const std::vector<int32_t>& prows) {
 // b - A x is written there (the refinement step), nothing is checked.
 void check_solution(pfr_solver* s, int which, int mode, int rhs, const pfr::RhsDesc& rd, const double2* data,
                     int64_t ds, int nvalid, const double2* X, double2* R, int64_t q0, hipStream_t st,
-                    const double2* Mu = nullptr, bool check = true, bool contract = false, const int* gmask = nullptr) {
+                    const double2* Mu = nullptr, bool check = true, bool contract = false, const int* glist = nullptr) {
   pfr::ResidDesc d;
   d.ptr = which == 0 ? s->d_rptr : s->d_cptr;
   d.idx = which == 0 ? s->d_ridx : s->d_cidx;
@@ -742,7 +744,7 @@ void check_solution(pfr_solver* s, int which, int mode, int rhs, const pfr::RhsD
   d.perm = s->P.perm;
   d.G = rd.G;
   d.walk = s->d_walk;
-  d.gmask = gmask;
+  d.glist = glist;
   if (contract) {
     d.se = s->stiff;
     d.n_stiff = s->n_stiff;
@@ -1427,7 +1429,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       (rc = s->alloc(&s->freqs, Fc)) || (rc = s->alloc(&s->loss_terms, Fc)) || (rc = s->alloc(&s->flags, Fc)) ||
       (rc = s->alloc(&s->tq, Fc)) || (rc = s->alloc(&s->d_berr_acc, 2 * Fc)) || (rc = s->alloc(&s->fr0, Fc)) ||
       (rc = s->alloc(&s->mscale, Fc)) || (rc = s->alloc(&s->cpart, (int64_t)pfr::residual_parts(S.n) * Fc)) ||
-      (rc = s->alloc(&s->gmask, Fc / 64)))
+      (rc = s->alloc(&s->gind, Fc / 64)) || (rc = s->alloc(&s->glist, pfr::REFINE_CAP)))
     return bail(rc);
   HIP_TRY(hipMemset(s->d_berr_acc, 0, 2 * Fc * sizeof(double)));
   if (s->sym && s->flow) {
@@ -1905,17 +1907,29 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
         check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st, s->XA, want_f, cwalk);
         want_f = false;
         pfr::launch_correct_finish(fa, s->fr0, s->cpart, pfr::residual_parts(s->n), Fc, nv, q0, fr_dev, s->loss_terms,
-                                   s->mscale, st, refine_adj ? s->gmask : nullptr, s->refine_tol);
+                                   s->mscale, st, refine_adj ? s->gind : nullptr);
       }
       if (refine_adj) {
-        // mu += A^-T (G - A^T mu) on the marked groups (G: the fr seed d fr / d x the adjoint solved), then their
-        // correction dot products and gradient contraction again with the refined mu, and their fr / m_q
-        check_solution(s, 1, 0, 2, rg, nullptr, 0, nv, s->XA, s->XR, q0, st, nullptr, false, false, s->gmask);
+        // the listed groups (largest first-order fr error estimates above the tolerance, at most REFINE_CAP):
+        // mu += A^-T (G - A^T mu) with the fr seed G = d fr / d x of THIS x (k_functional seed mode; the adjoint
+        // was solved for the seed of the bottom-up dot products, whose rounding differs), then their correction
+        // dot products and gradient contraction again with the refined mu, and their fr / m_q
+        pfr::launch_select_groups(s->gind, (int)(Fc / 64), s->refine_tol, s->glist, st);
+        if (!s->Gx) {
+          if ((rc = s->alloc(&s->Gx, (int64_t)s->n * Fc))) return rc;
+          HIP_TRY(hipMemsetAsync(s->Gx, 0, (size_t)s->n * Fc * 16, st));   // only the support rows are ever written
+        }
+        pfr::FunctionalArgs fs = fa;
+        fs.fr0 = s->fr0;
+        pfr::launch_functional(fs, s->X, Fc, nv, q0, nullptr, nullptr, s->Gx, st);
+        pfr::RhsDesc rgx;
+        rgx.G = s->Gx;
+        check_solution(s, 1, 0, 2, rgx, nullptr, 0, nv, s->XA, s->XR, q0, st, nullptr, false, false, s->glist);
         pfr::RhsDesc rr;
         rr.G = s->XR;
-        if ((rc = adjoint_solve(s, rr, s->Y2, st, -1, s->gmask))) return rc;
-        pfr::launch_axpy_vec(s->XA, s->Y2, (int64_t)s->n * Fc, st, s->gmask, Fc);
-        check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st, s->XA, false, true, s->gmask);
+        if ((rc = adjoint_solve(s, rr, s->Y2, st, -1, s->glist))) return rc;
+        pfr::launch_axpy_vec(s->XA, s->Y2, (int64_t)s->n * Fc, st, s->glist, Fc);
+        check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st, s->XA, false, true, s->glist);
         pfr::launch_correct_finish(fa, s->fr0, s->cpart, pfr::residual_parts(s->n), Fc, nv, q0, fr_dev, s->loss_terms,
                                    s->mscale, st);
       }

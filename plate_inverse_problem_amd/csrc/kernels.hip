@@ -66,6 +66,15 @@ struct Ctx {
   int lane, w, W;
   int64_t q;
 };
+// With a group list (the selective adjoint refinement: a few 64-frequency groups of the chunk, the launch's grid
+// rows indexing the list) the workgroup's frequencies are the listed group's; false: no group (list entry -1).
+__device__ __forceinline__ bool pick_group(Ctx& c, const int* __restrict__ glist) {
+  if (!glist) return true;
+  const int g = glist[c.q >> 6];
+  if (g < 0) return false;
+  c.q = (int64_t)g * 64 + c.lane;
+  return true;
+}
 // ctx() for the level-solve kernels with the XCD-aware workgroup order: the workgroups of one
 // 64-frequency group run on one XCD, so the solution rows that many fronts of a level gather
 // (their common ancestors' pivots) are fetched into one L2, not eight.  bx: the front slot.
@@ -1450,10 +1459,10 @@ __device__ __forceinline__ void lsolve_front(const DevPattern& P, const Front& f
 template <int RHS>
 __global__ __launch_bounds__(512) void k_lsolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
                                cplx* __restrict__ WV, RhsArgs R, cplx* __restrict__ Y, const int* __restrict__ reach,
-                               int rows_split, const int* __restrict__ gmask) {
+                               int rows_split, const int* __restrict__ glist) {
   int bx;
-  const Ctx c = ctx_xcd(bx);
-  if (gmask && !gmask[c.q >> 6]) return;
+  Ctx c = ctx_xcd(bx);
+  if (!pick_group(c, glist)) return;
   lsolve_front<RHS>(P, P.fronts[lvl[bx]], F, Fc, WV, R, Y, reach, rows_split, c);
 }
 
@@ -1478,10 +1487,10 @@ __global__ __launch_bounds__(512) void k_lsolve_level_z(DevPattern P, LSlices S,
 // small frequency counts one workgroup per front reads the whole L21 block through one CU, bound by
 // that CU's memory return rate, while most CUs idle.
 __global__ __launch_bounds__(256) void k_lsolve_rows(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F,
-                                                     int64_t Fc, cplx* __restrict__ WV, int S, const int* __restrict__ gmask) {
+                                                     int64_t Fc, cplx* __restrict__ WV, int S, const int* __restrict__ glist) {
   int bx;
-  const Ctx c = ctx_xcd(bx);
-  if (gmask && !gmask[c.q >> 6]) return;
+  Ctx c = ctx_xcd(bx);
+  if (!pick_group(c, glist)) return;
   const int slot = bx / S, split = bx % S;
   const Front fr = P.fronts[lvl[slot]];
   lsolve_rows(fr, F + fr.off * Fc + c.q, WV + (int64_t)fr.row0 * Fc + c.q, Fc, fr.ns + SRB * (split * c.W + c.w),
@@ -1587,10 +1596,10 @@ __device__ __forceinline__ void usolve_upd(const Front& fr, const int* ix, const
 template <bool SYM>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void k_usolve_level(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F, int64_t Fc,
                                cplx* __restrict__ WV, const cplx* __restrict__ Y, cplx* __restrict__ X,
-                               const int* __restrict__ reach, int upd_done, const int* __restrict__ gmask) {
+                               const int* __restrict__ reach, int upd_done, const int* __restrict__ glist) {
   int bx;
-  const Ctx c = ctx_xcd(bx);
-  if (gmask && !gmask[c.q >> 6]) return;
+  Ctx c = ctx_xcd(bx);
+  if (!pick_group(c, glist)) return;
   const bool live = !reach || reach[lvl[bx]];   // unreached front: y = 0
   const Front fr = P.fronts[lvl[bx]];
   const int f = fr.f, ns = fr.ns;
@@ -1654,10 +1663,10 @@ template <bool SYM>
 __global__ __launch_bounds__(256) void k_usolve_upd(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F,
                                                     int64_t Fc, cplx* __restrict__ WV, const cplx* __restrict__ Y,
                                                     const cplx* __restrict__ X, const int* __restrict__ reach, int S,
-                                                    const int* __restrict__ gmask) {
+                                                    const int* __restrict__ glist) {
   int bx;
-  const Ctx c = ctx_xcd(bx);
-  if (gmask && !gmask[c.q >> 6]) return;
+  Ctx c = ctx_xcd(bx);
+  if (!pick_group(c, glist)) return;
   const int slot = bx / S, split = bx % S;
   const bool live = !reach || reach[lvl[slot]];
   const Front fr = P.fronts[lvl[slot]];
@@ -2241,10 +2250,11 @@ __global__ __launch_bounds__(64) void k_dirichlet_rhs(DirArgs D, RhsArgs R, cplx
 }
 
 __global__ __launch_bounds__(64) void k_dirichlet_post(DirArgs D, cplx* __restrict__ X, int64_t Fc,
-                                                        const int* __restrict__ gmask) {
-  if (gmask && !gmask[blockIdx.y]) return;
+                                                        const int* __restrict__ glist) {
+  const int gy = glist ? glist[blockIdx.y] : (int)blockIdx.y;
+  if (gy < 0) return;
   const int slot = blockIdx.x;
-  const int64_t q = (int64_t)blockIdx.y * 64 + threadIdx.x;
+  const int64_t q = (int64_t)gy * 64 + threadIdx.x;
   const double om = 6.283185307179586 * D.freqs[q];
   const double om2 = om * om;
   const int2 d = D.dir[slot];
@@ -2328,7 +2338,7 @@ struct ResidArgs {
   const int* walk;   // rows in walk order (original numbering: mesh-local gathers of X)
   const double* se;  // NSK > 0: stiffness values, nz-major (se[nz * NSK + k])
   cplx* kpart;       // NSK > 0: per (workgroup, k, frequency) sums of S_k(nz) mu_row x_col
-  const int* gmask;  // per 64-frequency group: walk it (NULL: every group)
+  const int* glist;  // the groups to walk, indexed by grid row (-1: none; NULL: grid row = group)
 };
 
 __device__ __forceinline__ double cabs1(cplx z) { return fabs(z.x) + fabs(z.y); }
@@ -2358,8 +2368,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSK > 0 ? P
   // solution rows their window of rows gathers (~2 MB) stay in that XCD's L2 instead of every
   // XCD's L2 holding windows of eight groups
   const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
-  const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
-  if (A.gmask && !A.gmask[by]) return;      // group not selected (the selective adjoint refinement)
+  const int bx = (int)(lid % gridDim.x), by = A.glist ? A.glist[lid / gridDim.x] : (int)(lid / gridDim.x);
+  if (by < 0) return;                       // no listed group (the selective adjoint refinement)
   const int64_t q = (int64_t)by * 64 + (threadIdx.x & 63);
   const int wave0 = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
   const int nwaves = gridDim.x * (blockDim.x >> 6);
@@ -2515,13 +2525,13 @@ __device__ __forceinline__ void loss_term(int loss_type, double fr, cplx r, doub
 // reference's fr, for one dot product per row folded into the residual walk.  Per frequency: the
 // corrected fr (fr_out, global index), the loss term of it and the cotangent scale
 // m_q = scale * d term / d fr (lambda = m_q mu: the gradient contraction and k_rhs_dot take it).
-// gmask != NULL: also mark the 64-frequency groups whose first-order fr error estimate |Re(mu^T r)| / fr exceeds
-// tol for the selective adjoint refinement (the estimate is the correction itself; large next to a resonance)
+// gind != NULL: also each 64-frequency group's largest first-order fr error estimate |Re(mu^T r)| / fr (the
+// correction itself; large next to a resonance), from which k_select_groups picks the groups to refine
 __global__ __launch_bounds__(256) void k_correct_finish(FunctionalArgs A, const double* __restrict__ fr0,
                                                         const cplx* __restrict__ cpart, int nparts, int64_t Fc,
                                                         int nvalid, int64_t q_global0, double* __restrict__ fr_out,
                                                         double* __restrict__ loss_terms, double* __restrict__ mscale,
-                                                        int* __restrict__ gmask, double tol) {
+                                                        double* __restrict__ gind) {
   // 4 waves per 64 frequencies: wave w sums the partials b = w, w + 4, ... (8 loads in flight), then
   // wave 0 adds the four in order -- a fixed summation order (deterministic)
   __shared__ cplx sd[4][64];
@@ -2536,10 +2546,12 @@ __global__ __launch_bounds__(256) void k_correct_finish(FunctionalArgs A, const 
   d = cadd(cadd(sd[0][lane], sd[1][lane]), cadd(sd[2][lane], sd[3][lane]));
   const bool valid = q < nvalid;
   const double fr = fr0[q] + d.x;
-  if (gmask) {
-    const bool big = valid && !(fabs(d.x) <= tol * fabs(fr));     // NaN / Inf: refine (and get flagged)
-    const int any = __any(big);
-    if (lane == 0) gmask[blockIdx.x] = any;
+  if (gind) {
+    double v = valid ? fabs(d.x) / fabs(fr) : 0.0;
+    if (!(v <= 1e300)) v = 1e300;                                  // NaN / Inf: refine first
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+    if (lane == 0) gind[blockIdx.x] = v;
   }
   if (valid && fr_out) fr_out[q_global0 + q] = fr;
   if (A.loss_type < 0) return;
@@ -2568,10 +2580,40 @@ __global__ void k_scale_vec(cplx* __restrict__ X, const double* __restrict__ m, 
 }
 
 // X += D over a permuted frequency-minor vector (iterative refinement)
-__global__ void k_axpy_vec(cplx* __restrict__ X, const cplx* __restrict__ D, int64_t count, const int* __restrict__ gmask,
+// glist != NULL: count = rows x REFINE_CAP x 64, element (row, list slot, lane) of the listed group
+__global__ void k_axpy_vec(cplx* __restrict__ X, const cplx* __restrict__ D, int64_t count, const int* __restrict__ glist,
                            int64_t Fc) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < count && (!gmask || gmask[(i % Fc) >> 6])) X[i] = cadd(X[i], D[i]);
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  if (glist) {
+    const int64_t row = i / (REFINE_CAP * 64), r = i % (REFINE_CAP * 64);
+    const int g = glist[r >> 6];
+    if (g < 0) return;
+    i = row * Fc + (int64_t)g * 64 + (r & 63);
+  }
+  X[i] = cadd(X[i], D[i]);
+}
+
+// The (at most REFINE_CAP) groups with the largest indicators above tol, largest first; -1 past them.  One wave.
+__global__ __launch_bounds__(64) void k_select_groups(const double* __restrict__ gind, int ngroups, double tol,
+                                                      int* __restrict__ glist) {
+  const int t = threadIdx.x;
+  double v = t < ngroups ? gind[t] : -1.0;
+  for (int k = 0; k < REFINE_CAP; ++k) {
+    double m = v;
+    int who = t;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      const double mo = __shfl_xor(m, off);
+      const int wo = __shfl_xor(who, off);
+      if (mo > m || (mo == m && wo < who)) {
+        m = mo;
+        who = wo;
+      }
+    }
+    if (t == 0) glist[k] = m > tol ? who : -1;
+    if (t == who) v = -1.0;
+  }
 }
 
 // Directional derivative of the loss cotangent G (k_functional) along dx:
@@ -3237,7 +3279,7 @@ static RhsArgs make_rhs(const RhsDesc& d) {
 
 void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups,
                   const double2* F, int64_t Fc, double2* WV, const RhsDesc& rd, const double2* Yin, double2* Out,
-                  const int* reach, hipStream_t st, int split, const int* gmask) {
+                  const int* reach, hipStream_t st, int split, const int* glist) {
   if (nfronts <= 0) return;
   dim3 g(nfronts, ngroups), b(64 * W);
   const dim3 gs(nfronts * split, ngroups), bs(64 * SPLIT_W);
@@ -3245,17 +3287,17 @@ void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const 
   RhsArgs R = make_rhs(rd);
   switch (which) {
     case 0:  // L solve (split > 1: the update rows by k_lsolve_rows over `split` workgroups per front)
-      if (rhs_mode == 0) LAUNCH(k_lsolve_level<0>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach, rs, gmask);
-      else if (rhs_mode == 1) LAUNCH(k_lsolve_level<1>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach, rs, gmask);
-      else if (rhs_mode == 2) LAUNCH(k_lsolve_level<2>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach, rs, gmask);
-      else LAUNCH(k_lsolve_level<3>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach, rs, gmask);
-      if (rs) LAUNCH(k_lsolve_rows, gs, bs, st, P, lvl, F, Fc, WV, split, gmask);
+      if (rhs_mode == 0) LAUNCH(k_lsolve_level<0>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach, rs, glist);
+      else if (rhs_mode == 1) LAUNCH(k_lsolve_level<1>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach, rs, glist);
+      else if (rhs_mode == 2) LAUNCH(k_lsolve_level<2>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach, rs, glist);
+      else LAUNCH(k_lsolve_level<3>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach, rs, glist);
+      if (rs) LAUNCH(k_lsolve_rows, gs, bs, st, P, lvl, F, Fc, WV, split, glist);
       break;
     case 1:  // U solve (split > 1: the pivot rows' update part first, by k_usolve_upd)
-      if (rs && sym) LAUNCH(k_usolve_upd<true>, gs, bs, st, P, lvl, F, Fc, WV, Yin, Out, reach, split, gmask);
-      else if (rs) LAUNCH(k_usolve_upd<false>, gs, bs, st, P, lvl, F, Fc, WV, Yin, Out, reach, split, gmask);
-      if (sym) LAUNCH(k_usolve_level<true>, g, b, st, P, lvl, F, Fc, WV, Yin, Out, reach, rs, gmask);
-      else LAUNCH(k_usolve_level<false>, g, b, st, P, lvl, F, Fc, WV, Yin, Out, reach, rs, gmask);
+      if (rs && sym) LAUNCH(k_usolve_upd<true>, gs, bs, st, P, lvl, F, Fc, WV, Yin, Out, reach, split, glist);
+      else if (rs) LAUNCH(k_usolve_upd<false>, gs, bs, st, P, lvl, F, Fc, WV, Yin, Out, reach, split, glist);
+      if (sym) LAUNCH(k_usolve_level<true>, g, b, st, P, lvl, F, Fc, WV, Yin, Out, reach, rs, glist);
+      else LAUNCH(k_usolve_level<false>, g, b, st, P, lvl, F, Fc, WV, Yin, Out, reach, rs, glist);
       break;
     case 2:  // U^T solve
       if (rhs_mode == 0) LAUNCH(k_utsolve_level<0>, g, b, st, P, lvl, F, Fc, WV, R, Out, reach);
@@ -3380,8 +3422,8 @@ void launch_residual(int mode, int rhs, const ResidDesc& d, const double2* X, in
   a.K = d.K; a.M = d.M; a.freqs = d.freqs; a.data = d.data; a.data_stride = d.data_stride; a.nvalid = d.nvalid;
   a.rhsP = d.rhsP; a.beta_re = d.beta_re; a.beta_im = d.beta_im; a.mass_sum = d.mass_sum;
   a.B = d.B; a.b_stride = d.b_stride; a.perm = d.perm; a.G = d.G; a.walk = d.walk;
-  a.se = d.se; a.kpart = d.kpart; a.gmask = d.gmask;
-  const dim3 g((unsigned)residual_parts(d.n), (unsigned)(Fc / 64)), b(256);
+  a.se = d.se; a.kpart = d.kpart; a.glist = d.glist;
+  const dim3 g((unsigned)residual_parts(d.n), (unsigned)(d.glist ? REFINE_CAP : Fc / 64)), b(256);
   if (mode == 0 && rhs == 0 && Mu && d.kpart && d.n_stiff == 12)
     LAUNCH((k_residual<0, 0, true, 12>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
   else if (mode == 0 && rhs == 0 && Mu && d.kpart && d.n_stiff == 18)
@@ -3395,9 +3437,9 @@ void launch_residual(int mode, int rhs, const ResidDesc& d, const double2* X, in
 
 void launch_correct_finish(const FunctionalArgs& A, const double* fr0, const double2* cpart, int nparts, int64_t Fc,
                            int nvalid, int64_t q0, double* fr_out, double* loss_terms, double* mscale,
-                           hipStream_t st, int* gmask, double tol) {
+                           hipStream_t st, double* gind) {
   LAUNCH(k_correct_finish, dim3((unsigned)(Fc / 64)), dim3(256), st, A, fr0, cpart, nparts, Fc, nvalid, q0,
-         fr_out, loss_terms, mscale, gmask, tol);
+         fr_out, loss_terms, mscale, gind);
 }
 
 void launch_berr_finish(double* acc, int64_t Fc, int nvalid, double tol, int flag, int* flags, double* berr_out,
@@ -3411,8 +3453,13 @@ void launch_scale_vec(double2* X, const double* m, int n, int64_t Fc, hipStream_
   LAUNCH(k_scale_vec, dim3((unsigned)((count + 255) / 256)), dim3(256), st, X, m, n, Fc);
 }
 
-void launch_axpy_vec(double2* X, const double2* D, int64_t count, hipStream_t st, const int* gmask, int64_t Fc) {
-  LAUNCH(k_axpy_vec, dim3((unsigned)((count + 255) / 256)), dim3(256), st, X, D, count, gmask, Fc);
+void launch_axpy_vec(double2* X, const double2* D, int64_t count, hipStream_t st, const int* glist, int64_t Fc) {
+  if (glist) count = count / Fc * REFINE_CAP * 64;   // rows x the listed groups
+  LAUNCH(k_axpy_vec, dim3((unsigned)((count + 255) / 256)), dim3(256), st, X, D, count, glist, Fc);
+}
+
+void launch_select_groups(const double* gind, int ngroups, double tol, int* glist, hipStream_t st) {
+  LAUNCH(k_select_groups, dim3(1), dim3(64), st, gind, ngroups, tol, glist);
 }
 
 void launch_functional_tangent(const FunctionalArgs& A, const double2* X, const double2* DX, int64_t Fc, int nvalid,
@@ -3496,9 +3543,9 @@ void launch_dirichlet_rhs(int src, const DirDesc& d, int n_crow, const RhsDesc& 
   else LAUNCH(k_dirichlet_rhs<2>, g, b, st, make_dir(d), make_rhs(rd), G, Bc, Fc);
 }
 
-void launch_dirichlet_post(const DirDesc& d, int n_dir, double2* X, int64_t Fc, hipStream_t st, const int* gmask) {
+void launch_dirichlet_post(const DirDesc& d, int n_dir, double2* X, int64_t Fc, hipStream_t st, const int* glist) {
   if (n_dir <= 0) return;
-  LAUNCH(k_dirichlet_post, dim3(n_dir, (unsigned)(Fc / 64)), dim3(64), st, make_dir(d), X, Fc, gmask);
+  LAUNCH(k_dirichlet_post, dim3(n_dir, (unsigned)(glist ? REFINE_CAP : Fc / 64)), dim3(64), st, make_dir(d), X, Fc, glist);
 }
 
 // fill padded frequency slots with the last valid frequency (keeps padded lanes well-posed)

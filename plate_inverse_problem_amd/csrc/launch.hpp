@@ -5,6 +5,10 @@
 
 namespace pfr {
 
+// The selective adjoint refinement works on at most this many 64-frequency groups per chunk (a compacted list;
+// its launches have this many grid rows instead of one per group)
+constexpr int REFINE_CAP = 4;
+
 struct RhsDesc {
   const double* rhsP = nullptr;   // RHS 0: permuted Dirichlet vector (device)
   double beta_re = 0, beta_im = 0, mass_sum = 0;
@@ -55,10 +59,11 @@ void launch_schur_blk(int bc, const DevPattern& P, const int4* blocks, int nbloc
 // products with the update-row solution) runs first / last over `split` workgroups of SPLIT_W waves per
 // (front, frequency group) -- the top levels' few fronts otherwise pull their L21 blocks through one CU each
 constexpr int SPLIT_W = 4;
-// gmask (may be NULL): per 64-frequency group, solve it (the selective adjoint refinement's solves)
+// glist (may be NULL): the groups to solve, REFINE_CAP of them (-1: none), indexed by grid row (pass
+// ngroups = REFINE_CAP); the selective adjoint refinement's solves
 void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups,
                   const double2* F, int64_t Fc, double2* WV, const RhsDesc& rd, const double2* Yin, double2* Out,
-                  const int* reach, hipStream_t st, int split = 1, const int* gmask = nullptr);
+                  const int* reach, hipStream_t st, int split = 1, const int* glist = nullptr);
 // nslices (<= 4) bottom-up L solves as one chain of launches (blockIdx.z = slice; slice z: the fronts
 // lvl[z][0 .. nf[z]), its work vectors WV[z], rhs rd[z] (rhs_mode 0 or 3 for every slice), solution Y[z])
 void launch_lsolve_multi(int rhs_mode, const DevPattern& P, int nslices, const int* const* lvl, const int* nf, int W,
@@ -176,7 +181,7 @@ void launch_reduce(const double2* partial, int nparts, int n_stiff, const double
 // place) and the adjoint's Dirichlet rows (X in place)
 void launch_dirichlet_rhs(int src, const DirDesc& d, int n_crow, const RhsDesc& rd, double2* G, double2* Bc,
                           int64_t Fc, hipStream_t st);
-void launch_dirichlet_post(const DirDesc& d, int n_dir, double2* X, int64_t Fc, hipStream_t st, const int* gmask = nullptr);
+void launch_dirichlet_post(const DirDesc& d, int n_dir, double2* X, int64_t Fc, hipStream_t st, const int* glist = nullptr);
 // Backward-error check: the original system's rows (forward) or columns (adjoint) in the permuted
 // numbering, A = K - omega^2 M (mode 0) or the explicit batch (mode 1); rhs 0 operator, 1 explicit
 // B, 2 vector G.  The per-frequency componentwise backward error accumulates in acc (max, zero on
@@ -204,7 +209,7 @@ struct ResidDesc {
   const double* se = nullptr;
   int n_stiff = 0;
   double2* kpart = nullptr;
-  const int* gmask = nullptr;  // per 64-frequency group: walk it (NULL: every group)
+  const int* glist = nullptr;  // the groups to walk (REFINE_CAP, -1: none; NULL: every group)
 };
 // Mu != NULL (mode 0, rhs 0): also the functional-correction dot products sum_p Mu_p r_p, one partial
 // per workgroup and frequency in cpart (residual_parts(n) x Fc), summed by launch_correct_finish
@@ -216,14 +221,16 @@ void launch_reduce_q(const double2* kpart, int nparts, int n_stiff, const double
 void launch_residual(int mode, int rhs, const ResidDesc& d, const double2* X, int64_t Fc, double2* R, double* acc,
                      hipStream_t st, const double2* Mu = nullptr, double2* cpart = nullptr);
 // corrected fr (fr_out, global index; may be NULL), loss terms and cotangent scales of a chunk
-// gmask != NULL: per 64-frequency group, 1 when some frequency's |correction| > tol |fr| (refine its adjoint)
+// gind != NULL: per 64-frequency group its largest |correction| / |fr| (launch_select_groups picks from them)
 void launch_correct_finish(const FunctionalArgs& A, const double* fr0, const double2* cpart, int nparts, int64_t Fc,
                            int nvalid, int64_t q0, double* fr_out, double* loss_terms, double* mscale,
-                           hipStream_t st, int* gmask = nullptr, double tol = 0.0);
+                           hipStream_t st, double* gind = nullptr);
+// glist[0 .. REFINE_CAP): the groups with the largest indicators above tol, largest first, -1 past them
+void launch_select_groups(const double* gind, int ngroups, double tol, int* glist, hipStream_t st);
 // flags |= flag where acc[q] > tol (or not finite); acc cleared
 void launch_berr_finish(double* acc, int64_t Fc, int nvalid, double tol, int flag, int* flags, double* berr_out,
                         int64_t q0, int which, hipStream_t st);
-void launch_axpy_vec(double2* X, const double2* D, int64_t count, hipStream_t st, const int* gmask = nullptr,
+void launch_axpy_vec(double2* X, const double2* D, int64_t count, hipStream_t st, const int* glist = nullptr,
                      int64_t Fc = 64);
 void launch_scale_vec(double2* X, const double* m, int n, int64_t Fc, hipStream_t st);
 void launch_unpermute(const int* perm, int n, const double2* X, int64_t Fc, int nvalid, double2* out, hipStream_t st);
