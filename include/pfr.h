@@ -46,15 +46,19 @@ extern "C" {
 #define PFR_CHECK_CORRECT 8   /* functional correction (pfr_sweep): fr += Re(mu^T (b - A x)) with mu the adjoint
                                * of fr (A^T mu = d fr / d x) -- fr to second order in the solve's error, the
                                * accuracy the reference's refined UMFPACK solves give; the loss, its
-                               * cotangent and the gradient are formed from the corrected fr */
+                               * cotangent and the gradient are formed from the corrected fr; in loss sweeps
+                               * the cotangent also carries the solve-error scale fr / (mu^T A x) (complex; the
+                               * static-pivot solves' error next to a resonance is a complex multiple of the
+                               * solution itself, which this divides out of the gradient contraction; env
+                               * PFR_SCALE_CORR=0 turns it off) */
 
 #define PFR_CHECK_REFINE_ADJ 16 /* selective adjoint refinement (loss sweeps with PFR_CHECK_CORRECT, symmetric
                                * mode): after the forward residual walk, the 64-frequency groups holding a frequency
                                * whose functional correction exceeds the tolerance (pfr_set_refine_tol; the
                                * first-order fr error estimate, large next to a resonance) get one refinement step
                                * of the fr adjoint, mu += A^-T (d fr / d x - A^T mu), and their gradient contraction
-                               * and correction are redone with it: the gradient of those frequencies to the
-                               * accuracy of the reference's refined solves, the other groups untouched */
+                               * and correction are redone with it (opt-in: with the solve-error scale of
+                               * PFR_CHECK_CORRECT the gradient is already within the oracle's accuracy) */
 
 /* loss types (Problem.py:948-975) */
 #define PFR_LOSS_NONE -1
@@ -241,6 +245,11 @@ PFR_API int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_
 PFR_API int pfr_set_check(pfr_solver* s, int32_t mode, double tol, double* berr_dev);
 /* PFR_CHECK_REFINE_ADJ threshold: refine the groups where |Re(mu^T r)| > tol |fr| (default 2e-8) */
 PFR_API int pfr_set_refine_tol(pfr_solver* s, double tol);
+
+/* Diagnostic: the last chunk's solution vectors of pfr_sweep for chunk lane q (which 0: the forward solution x,
+ * 1: the adjoint (mu, the adjoint of fr, under PFR_CHECK_CORRECT; lambda otherwise)), caller numbering, n complex
+ * into out_host.  Synchronises the device. */
+PFR_API int pfr_debug_solution(pfr_solver* s, int32_t which, int32_t q, double* out_host);
 
 /* Per-phase device times [ms] of the last pfr_sweep/pfr_solve call on this solver, measured with HIP
  * events on the call's stream (0 = factor, 1 = forward solves, 2 = functional, 3 = adjoint solves,

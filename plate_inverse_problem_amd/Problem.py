@@ -138,9 +138,9 @@ class _Engine:
         self.last_flags = None         # its status flags (host)
         # backward-error checks of every solve (pfr_set_check) and the functional correction (fr to
         # second order in the solve's error, the accuracy of the reference's refined UMFPACK solves) by
-        # default; PFR_CHECK=<PFR_CHECK_* bits> / PFR_CHECK_TOL override; refinement (bit 4) off by default
+        # default; PFR_CHECK=<PFR_CHECK_* bits> / PFR_CHECK_TOL override; refinement (bits 4, 16) off by default
         self.check_mode = int(os.environ.get("PFR_CHECK", str(_native.PFR_CHECK_FORWARD | _native.PFR_CHECK_ADJOINT
-                                                              | _native.PFR_CHECK_CORRECT | _native.PFR_CHECK_REFINE_ADJ)))
+                                                              | _native.PFR_CHECK_CORRECT)))
         self.check_tol = float(os.environ.get("PFR_CHECK_TOL", "1e-10"))
         # the selective adjoint refinement's group threshold (first-order fr error estimate)
         self.refine_tol = float(os.environ.get("PFR_REFINE_TOL", "2e-8"))

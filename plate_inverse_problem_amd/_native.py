@@ -80,6 +80,7 @@ _PROTOS = {
                                     _P]),
     "pfr_set_check": (C.c_int, [_P, C.c_int32, C.c_double, _P]),
     "pfr_set_refine_tol": (C.c_int, [_P, C.c_double]),
+    "pfr_debug_solution": (C.c_int, [_P, C.c_int32, C.c_int32, _DP]),
     "pfr_set_timing": (C.c_int, [_P, C.c_int32]),
     "pfr_last_timings": (C.c_int, [_P, _DP]),
     "pfr_last_kernel_timings": (C.c_int, [_P, _DP, _P]),
@@ -298,6 +299,12 @@ class Solver:
                                int(bool(transpose)), self._stream(y)), "pfr_matvec")
 
     # ---- backward-error checks
+    def debug_solution(self, which: int, q: int) -> np.ndarray:
+        """The last chunk's forward solution (0) or adjoint (1) of chunk lane q, caller numbering (diagnostic)."""
+        out = np.zeros(2 * self.sym.stats()["n"], dtype=np.float64)
+        check(lib().pfr_debug_solution(self._h, int(which), int(q), out.ctypes.data_as(_DP)), "pfr_debug_solution")
+        return out[0::2] + 1j * out[1::2]
+
     def set_refine_tol(self, tol: float):
         """Threshold of the selective adjoint refinement (PFR_CHECK_REFINE_ADJ): groups where the functional
         correction exceeds tol |fr| get one refinement step of the fr adjoint."""

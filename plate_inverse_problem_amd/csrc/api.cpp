@@ -152,8 +152,9 @@ struct pfr_solver {
   double *freqs = nullptr, *loss_terms = nullptr;
   // functional correction (PFR_CHECK_CORRECT): fr of the solve, per-frequency cotangent scale, and
   // the residual walk's per-workgroup dot-product partials (residual_parts(n) x Fc)
-  double *fr0 = nullptr, *mscale = nullptr;
-  double2* cpart = nullptr;
+  double* fr0 = nullptr;
+  double2 *mscale = nullptr, *cpart = nullptr;     // mscale complex: the solve-error scale (k_correct_finish)
+  int scale_corr = 1;                   // PFR_SCALE_CORR: the solve-error scale of the loss sweeps' cotangent
   int32_t* flags = nullptr;
   // operator / rhs / functional / stiffness state
   const double2* K = nullptr;
@@ -265,7 +266,7 @@ int64_t workspace_bytes(const Symbolic& S, int64_t Fc) {
   b += S.total_rows * Fc * 16;       // WV
   b += 6 * (int64_t)S.n * Fc * 16;   // X, Y, XA, G, Y2, XR
   b += Fc * (8 + 8 + 4 + 16);        // freqs, loss terms, flags, tq
-  b += Fc * (8 + 8) + (int64_t)pfr::residual_parts(S.n) * Fc * 16;   // fr0, mscale, cpart
+  b += Fc * (8 + 16) + (int64_t)pfr::residual_parts(S.n) * Fc * 16;   // fr0, mscale, cpart
   if (S.symmetric)   // functional from the bottom-up passes: WVk, YVk, fn_parts, fcoef
     b += (3 * S.total_rows + 2 * (int64_t)S.n + 3 * pfr::FN_PARTS_HOST + 3) * Fc * 16;
   b += (int64_t)pfr::residual_parts(S.n) * 18 * Fc * 16;   // kpart (contraction in the forward walk)
@@ -931,6 +932,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->check_fused = knob("PFR_CHECK_FUSED", 0, 0, 1);   // measured 2.3 ms against 2 x 0.87 ms per 2,048-frequency chunk
   s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);
   s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);
+  s->scale_corr = knob("PFR_SCALE_CORR", 1, 0, 1);
   s->fuse_asm = knob("PFR_FUSE_ASM", 0, 0, 1);   // measured slower (2,048-frequency chunk: A11 classes 4.1 -> 6.6 ms)
   s->flow = knob("PFR_FLOW", 0, 0, 7);   // bit 0: paired top-down pass, bit 1: bottom-up chain, bit 2: factorisation
   s->flow_fwg = knob("PFR_FLOW_FWG", 256, 0, 1 << 20);
@@ -1506,6 +1508,21 @@ int pfr_set_timing(pfr_solver* s, int32_t enable) {
   return PFR_OK;
 }
 
+int pfr_debug_solution(pfr_solver* s, int32_t which, int32_t q, double* out) {
+  if (!s || !out || which < 0 || which > 1 || q < 0 || q >= s->Fc) return fail(PFR_ERR_ARG, "bad debug arguments");
+  HIP_TRY(hipSetDevice(s->device));
+  HIP_TRY(hipDeviceSynchronize());
+  std::vector<double2> col((size_t)s->n);
+  const double2* src = which == 0 ? s->X : s->XA;
+  HIP_TRY(hipMemcpy2D(col.data(), sizeof(double2), src + q, (size_t)s->Fc * sizeof(double2), sizeof(double2), s->n,
+                      hipMemcpyDeviceToHost));
+  for (int p = 0; p < s->n; ++p) {       // permuted row p holds caller row perm[p]
+    out[2 * (int64_t)s->perm[p]] = col[p].x;
+    out[2 * (int64_t)s->perm[p] + 1] = col[p].y;
+  }
+  return PFR_OK;
+}
+
 int pfr_set_refine_tol(pfr_solver* s, double tol) {
   if (!s || !(tol >= 0.0)) return fail(PFR_ERR_ARG, "bad refine tolerance");
   s->refine_tol = tol;
@@ -1901,13 +1918,21 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
       // selective adjoint refinement (PFR_CHECK_REFINE_ADJ): the groups next to a resonance, where the unrefined
       // solves' first-order error dominates the gradient, get one refinement step of mu
       const bool refine_adj = reverse && correct && cwalk && fn_fast && (s->check_mode & PFR_CHECK_REFINE_ADJ);
+      // the solve-error scale of the cotangent (k_correct_finish): t_q = mu^T rhsP in, m_q t_q out
+      const bool scorr = reverse && correct && s->scale_corr;
+      pfr::RhsScale bsc;
+      bsc.freqs = s->freqs;
+      bsc.mass_sum = s->mass_sum;
+      bsc.beta_re = s->beta_re;
+      bsc.beta_im = s->beta_im;
       if (correct) {
         // the forward residual walk: backward error (when checked) + the correction's dot products,
         // then the corrected fr, its loss terms and the per-frequency cotangent scales
         check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st, s->XA, want_f, cwalk);
         want_f = false;
+        if (scorr) pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st);
         pfr::launch_correct_finish(fa, s->fr0, s->cpart, pfr::residual_parts(s->n), Fc, nv, q0, fr_dev, s->loss_terms,
-                                   s->mscale, st, refine_adj ? s->gind : nullptr);
+                                   s->mscale, st, refine_adj ? s->gind : nullptr, scorr ? s->tq : nullptr, bsc);
       }
       if (refine_adj) {
         // the listed groups (largest first-order fr error estimates above the tolerance, at most REFINE_CAP):
@@ -1930,10 +1955,11 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
         if ((rc = adjoint_solve(s, rr, s->Y2, st, -1, s->glist))) return rc;
         pfr::launch_axpy_vec(s->XA, s->Y2, (int64_t)s->n * Fc, st, s->glist, Fc);
         check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st, s->XA, false, true, s->glist);
+        if (scorr) pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st);
         pfr::launch_correct_finish(fa, s->fr0, s->cpart, pfr::residual_parts(s->n), Fc, nv, q0, fr_dev, s->loss_terms,
-                                   s->mscale, st);
+                                   s->mscale, st, nullptr, scorr ? s->tq : nullptr, bsc);
       }
-      const double* msc = correct ? s->mscale : nullptr;
+      const double2* msc = correct ? s->mscale : nullptr;
       if (cwalk)
         pfr::launch_reduce_q(s->kpart, pfr::residual_parts(s->n), s->n_stiff, msc, nv, Fc, s->partial, st);
       else if (reverse)
@@ -1965,7 +1991,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
         if (want_a) check_solution(s, 1, 0, 2, rg, nullptr, 0, nv, s->XA, nullptr, q0, st);
       }
       if (reverse) {
-        pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st, msc);
+        if (!scorr) pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st, msc);
         pfr::launch_reduce(s->partial, cwalk ? (int)(Fc / 64) : pfr::contract_eg_parts(s->n_uent), s->n_stiff, s->tq, s->e,
                            s->loss_terms, nv, Fc, reinterpret_cast<double2*>(w_dev), loss_dev, st);
       }

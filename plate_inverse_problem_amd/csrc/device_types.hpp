@@ -84,6 +84,12 @@ struct AsmArgs {
   const double* M = nullptr;
 };
 
+// b = rhsP * (beta_re - omega^2 mass_sum + i beta_im) per frequency (the rhs of a sweep's solves)
+struct RhsScale {
+  const double* freqs = nullptr;   // chunk-local frequencies [Hz]
+  double mass_sum = 0, beta_re = 0, beta_im = 0;
+};
+
 struct FunctionalArgs {
   int32_t n_support;
   const int32_t* pidx;    // permuted DOF index of each support entry (device)

@@ -2526,12 +2526,21 @@ __device__ __forceinline__ void loss_term(int loss_type, double fr, cplx r, doub
 // corrected fr (fr_out, global index), the loss term of it and the cotangent scale
 // m_q = scale * d term / d fr (lambda = m_q mu: the gradient contraction and k_rhs_dot take it).
 // gind != NULL: also each 64-frequency group's largest first-order fr error estimate |Re(mu^T r)| / fr (the
-// correction itself; large next to a resonance), from which k_select_groups picks the groups to refine
+// correction itself; large next to a resonance), from which k_select_groups picks the groups to refine.
+//
+// tq != NULL (the solve-error scale, on in loss sweeps): tq holds t_q = mu^T rhsP on entry and m_q t_q on exit,
+// and m_q is complex, dl * scale * fr / (mu^T A x).  Next to a resonance the static-pivot solves' error is
+// almost all along the resonant mode, i.e. along the solution itself: x = (1 + dx) x*, mu = (1 + dm) mu*
+// with complex scalars dx, dm of up to ~cond * eps.  The gradient contraction mu^T S_k x then carries
+// (1 + dx)(1 + dm), whose imaginary part the real gradient does not forgive (the partials cancel by 1e7-1e9
+// over the sweep); fr = mu*^T A x* = mu*^T b, so mu^T A x = (1 + dx)(1 + dm) fr to first order, and
+// mu^T A x = mu^T b - mu^T r is two dot products the sweep has already formed (k_rhs_dot, the correction's
+// walk): dividing by it removes both factors with no further solve
 __global__ __launch_bounds__(256) void k_correct_finish(FunctionalArgs A, const double* __restrict__ fr0,
                                                         const cplx* __restrict__ cpart, int nparts, int64_t Fc,
                                                         int nvalid, int64_t q_global0, double* __restrict__ fr_out,
-                                                        double* __restrict__ loss_terms, double* __restrict__ mscale,
-                                                        double* __restrict__ gind) {
+                                                        double* __restrict__ loss_terms, cplx* __restrict__ mscale,
+                                                        double* __restrict__ gind, cplx* __restrict__ tq, RhsScale bsc) {
   // 4 waves per 64 frequencies: wave w sums the partials b = w, w + 4, ... (8 loads in flight), then
   // wave 0 adds the four in order -- a fixed summation order (deterministic)
   __shared__ cplx sd[4][64];
@@ -2558,7 +2567,23 @@ __global__ __launch_bounds__(256) void k_correct_finish(FunctionalArgs A, const 
   double term = 0.0, dl = 0.0;
   if (valid) loss_term(A.loss_type, fr, A.ref[q_global0 + q], term, dl);
   loss_terms[q] = term;
-  mscale[q] = valid ? dl * A.scale : 0.0;
+  cplx m = make_double2(valid ? dl * A.scale : 0.0, 0.0);
+  if (tq) {
+    const cplx t0 = tq[q];
+    if (valid) {
+      const double om = 6.283185307179586 * bsc.freqs[q];
+      const cplx bs = make_double2(fma(-om * om, bsc.mass_sum, bsc.beta_re), bsc.beta_im);
+      const cplx bt = cmul(bs, t0);
+      const cplx den = make_double2(bt.x - d.x, bt.y - d.y);        // mu^T A x
+      const double dd = den.x * den.x + den.y * den.y;
+      if (dd > 0.0 && isfinite(dd)) {
+        const double f = m.x * fr / dd;                             // m fr / den = m fr conj(den) / |den|^2
+        m = make_double2(f * den.x, -f * den.y);
+      }
+    }
+    tq[q] = cmul(m, t0);
+  }
+  mscale[q] = m;
 }
 
 // flag the frequencies whose backward error exceeds tol; optional per-frequency output (global
@@ -2574,9 +2599,9 @@ __global__ void k_berr_finish(double* __restrict__ acc, int64_t Fc, int nvalid, 
 }
 
 // X[p, q] *= m[q] over a permuted frequency-minor vector (lambda = m_q mu, functional correction)
-__global__ void k_scale_vec(cplx* __restrict__ X, const double* __restrict__ m, int n, int64_t Fc) {
+__global__ void k_scale_vec(cplx* __restrict__ X, const cplx* __restrict__ m, int n, int64_t Fc) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < (int64_t)n * Fc) X[i] = cscale(X[i], m[i % Fc]);
+  if (i < (int64_t)n * Fc) X[i] = cmul(X[i], m[i % Fc]);
 }
 
 // X += D over a permuted frequency-minor vector (iterative refinement)
@@ -2994,7 +3019,7 @@ template <int NS, int EW, bool MS>
 __global__ __launch_bounds__(256) void k_contract_eg(const int4* __restrict__ ent, int nent,
                                                      const double* __restrict__ se, const cplx* __restrict__ Lam,
                                                      const cplx* __restrict__ X, int64_t Fc, int nvalid,
-                                                     const double* __restrict__ msc, cplx* __restrict__ partial) {
+                                                     const cplx* __restrict__ msc, cplx* __restrict__ partial) {
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
   const int e0 = min(wv * EW, nent - 1);     // waves past the end: clamped entries, masked below
@@ -3015,9 +3040,9 @@ __global__ __launch_bounds__(256) void k_contract_eg(const int4* __restrict__ en
       li[u] = Lam[oi[u] + g];
       xj[u] = X[oj[u] + g];
     }
-    const double m = MS ? msc[g + lane] : (g + lane < nvalid ? 1.0 : 0.0);
+    const cplx m = MS ? msc[g + lane] : make_double2(g + lane < nvalid ? 1.0 : 0.0, 0.0);
 #pragma unroll
-    for (int u = 0; u < EW; ++u) P[u] = cadd(P[u], cscale(cmul(li[u], xj[u]), m));
+    for (int u = 0; u < EW; ++u) P[u] = cadd(P[u], cmul(cmul(li[u], xj[u]), m));
   }
   cplx part[NS];
 #pragma unroll
@@ -3055,7 +3080,7 @@ __global__ __launch_bounds__(256) void k_contract_eg(const int4* __restrict__ en
 
 // t_q = sum_p Lam[p] * rhsP[p] over the Dirichlet support (d b / d beta)
 __global__ void k_rhs_dot(const int* __restrict__ sup, const double* __restrict__ val, int n_sup,
-                          const cplx* __restrict__ Lam, int64_t Fc, const double* __restrict__ msc,
+                          const cplx* __restrict__ Lam, int64_t Fc, const cplx* __restrict__ msc,
                           cplx* __restrict__ t_out) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= Fc) return;
@@ -3065,7 +3090,7 @@ __global__ void k_rhs_dot(const int* __restrict__ sup, const double* __restrict_
     t.x = fma(val[s], l.x, t.x);
     t.y = fma(val[s], l.y, t.y);
   }
-  t_out[q] = msc ? cscale(t, msc[q]) : t;
+  t_out[q] = msc ? cmul(t, msc[q]) : t;
 }
 
 // Deterministic reduction over (blocks, valid frequencies):
@@ -3074,7 +3099,7 @@ __global__ void k_rhs_dot(const int* __restrict__ sup, const double* __restrict_
 // the fused walk's contraction in k_contract_eg's partial layout (one part per tile), so that k_reduce
 // completes it unchanged.  Block = (k, tile), 4 waves splitting the workgroup partials b.
 __global__ __launch_bounds__(256) void k_reduce_q(const cplx* __restrict__ kpart, int nparts, int n_stiff,
-                                                  const double* __restrict__ msc, int nvalid, int64_t Fc,
+                                                  const cplx* __restrict__ msc, int nvalid, int64_t Fc,
                                                   cplx* __restrict__ partial) {
   __shared__ double sre[4][64], sim[4][64];
   const int k = blockIdx.x, tile = blockIdx.y;
@@ -3091,9 +3116,11 @@ __global__ __launch_bounds__(256) void k_reduce_q(const cplx* __restrict__ kpart
   sim[w][lane] = pi;
   __syncthreads();
   if (w == 0) {
-    const double m = q < nvalid ? (msc ? msc[q] : 1.0) : 0.0;
-    double re = m * ((sre[0][lane] + sre[1][lane]) + (sre[2][lane] + sre[3][lane]));
-    double im = m * ((sim[0][lane] + sim[1][lane]) + (sim[2][lane] + sim[3][lane]));
+    const cplx m = q < nvalid ? (msc ? msc[q] : make_double2(1.0, 0.0)) : make_double2(0.0, 0.0);
+    const double sr = (sre[0][lane] + sre[1][lane]) + (sre[2][lane] + sre[3][lane]);
+    const double si = (sim[0][lane] + sim[1][lane]) + (sim[2][lane] + sim[3][lane]);
+    double re = m.x * sr - m.y * si;
+    double im = m.x * si + m.y * sr;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       re += __shfl_xor(re, o);
@@ -3436,10 +3463,10 @@ void launch_residual(int mode, int rhs, const ResidDesc& d, const double2* X, in
 }
 
 void launch_correct_finish(const FunctionalArgs& A, const double* fr0, const double2* cpart, int nparts, int64_t Fc,
-                           int nvalid, int64_t q0, double* fr_out, double* loss_terms, double* mscale,
-                           hipStream_t st, double* gind) {
+                           int nvalid, int64_t q0, double* fr_out, double* loss_terms, double2* mscale,
+                           hipStream_t st, double* gind, double2* tq, const RhsScale& bsc) {
   LAUNCH(k_correct_finish, dim3((unsigned)(Fc / 64)), dim3(256), st, A, fr0, cpart, nparts, Fc, nvalid, q0,
-         fr_out, loss_terms, mscale, gind);
+         fr_out, loss_terms, mscale, gind, tq, bsc);
 }
 
 void launch_berr_finish(double* acc, int64_t Fc, int nvalid, double tol, int flag, int* flags, double* berr_out,
@@ -3448,7 +3475,7 @@ void launch_berr_finish(double* acc, int64_t Fc, int nvalid, double tol, int fla
          q0, which);
 }
 
-void launch_scale_vec(double2* X, const double* m, int n, int64_t Fc, hipStream_t st) {
+void launch_scale_vec(double2* X, const double2* m, int n, int64_t Fc, hipStream_t st) {
   const int64_t count = (int64_t)n * Fc;
   LAUNCH(k_scale_vec, dim3((unsigned)((count + 255) / 256)), dim3(256), st, X, m, n, Fc);
 }
@@ -3493,7 +3520,7 @@ void launch_contract_rows(bool check, const int* eblk, const int4* ent, int nblk
 int contract_eg_parts(int nent) { return ((nent + CEG_EW - 1) / CEG_EW + 3) / 4; }   // workgroups of 4 waves
 
 void launch_contract_eg(const int4* ent, int nent, const double* se, int n_stiff, const double2* Lam, const double2* X,
-                        int64_t Fc, int nvalid, double2* partial, hipStream_t st, const double* msc) {
+                        int64_t Fc, int nvalid, double2* partial, hipStream_t st, const double2* msc) {
   const dim3 g(contract_eg_parts(nent)), b(256);
   if (n_stiff == 12 && msc) LAUNCH((k_contract_eg<12, CEG_EW, true>), g, b, st, ent, nent, se, Lam, X, Fc, nvalid, msc, partial);
   else if (n_stiff == 12) LAUNCH((k_contract_eg<12, CEG_EW, false>), g, b, st, ent, nent, se, Lam, X, Fc, nvalid, msc, partial);
@@ -3502,11 +3529,11 @@ void launch_contract_eg(const int4* ent, int nent, const double* se, int n_stiff
 }
 
 void launch_rhs_dot(const int* sup, const double* val, int n_sup, const double2* Lam, int64_t Fc, double2* t_out,
-                    hipStream_t st, const double* msc) {
+                    hipStream_t st, const double2* msc) {
   LAUNCH(k_rhs_dot, dim3((unsigned)((Fc + 63) / 64)), dim3(64), st, sup, val, n_sup, Lam, Fc, msc, t_out);
 }
 
-void launch_reduce_q(const double2* kpart, int nparts, int n_stiff, const double* msc, int nvalid, int64_t Fc,
+void launch_reduce_q(const double2* kpart, int nparts, int n_stiff, const double2* msc, int nvalid, int64_t Fc,
                      double2* partial, hipStream_t st) {
   LAUNCH(k_reduce_q, dim3(n_stiff, (unsigned)(Fc / 64)), dim3(256), st, kpart, nparts, n_stiff, msc, nvalid, Fc, partial);
 }

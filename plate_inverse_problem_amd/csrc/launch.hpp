@@ -167,12 +167,12 @@ void launch_contract_rows(bool check, const int* eblk, const int4* ent, int nblk
 int contract_eg_parts(int nent);
 // msc (may be NULL): per-frequency factor of Lam (functional correction: the loss cotangent scale)
 void launch_contract_eg(const int4* ent, int nent, const double* se, int n_stiff, const double2* Lam, const double2* X,
-                        int64_t Fc, int nvalid, double2* partial, hipStream_t st, const double* msc = nullptr);
+                        int64_t Fc, int nvalid, double2* partial, hipStream_t st, const double2* msc = nullptr);
 // entry-ordered copies of K / M (kme, may be NULL) and of the stiffness matrices (se, may be NULL)
 void launch_gather_entries(const int4* ent, int nent, const double2* K, const double* M, const double* stiff, int ns,
                            double2* kme, double* se, hipStream_t st);
 void launch_rhs_dot(const int* sup, const double* val, int n_sup, const double2* Lam, int64_t Fc, double2* t_out,
-                    hipStream_t st, const double* msc = nullptr);
+                    hipStream_t st, const double2* msc = nullptr);
 // w_out[k] += -sum(partial[., k]) + e_k sum_q t_q ;  loss_out += sum_q loss_terms (q < nvalid)
 void launch_reduce(const double2* partial, int nparts, int n_stiff, const double2* t_q, const CoefPack& e,
                    const double* loss_terms, int nvalid, int64_t Fc, double2* w_out, double* loss_out,
@@ -216,15 +216,17 @@ struct ResidDesc {
 int residual_parts(int n);
 // partial[t * n_stiff + k] = sum_{q in tile t} msc[q] sum_b kpart[b][k][q] (msc NULL: 1; tiles of 64
 // frequencies): the fused walk's contraction as Fc / 64 parts
-void launch_reduce_q(const double2* kpart, int nparts, int n_stiff, const double* msc, int nvalid, int64_t Fc,
+void launch_reduce_q(const double2* kpart, int nparts, int n_stiff, const double2* msc, int nvalid, int64_t Fc,
                      double2* partial, hipStream_t st);
 void launch_residual(int mode, int rhs, const ResidDesc& d, const double2* X, int64_t Fc, double2* R, double* acc,
                      hipStream_t st, const double2* Mu = nullptr, double2* cpart = nullptr);
 // corrected fr (fr_out, global index; may be NULL), loss terms and cotangent scales of a chunk
 // gind != NULL: per 64-frequency group its largest |correction| / |fr| (launch_select_groups picks from them)
+// tq != NULL: t_q = mu^T rhsP in, m_q t_q out, and the solve-error scale in m_q (k_correct_finish)
 void launch_correct_finish(const FunctionalArgs& A, const double* fr0, const double2* cpart, int nparts, int64_t Fc,
-                           int nvalid, int64_t q0, double* fr_out, double* loss_terms, double* mscale,
-                           hipStream_t st, double* gind = nullptr);
+                           int nvalid, int64_t q0, double* fr_out, double* loss_terms, double2* mscale,
+                           hipStream_t st, double* gind = nullptr, double2* tq = nullptr,
+                           const RhsScale& bsc = RhsScale());
 // glist[0 .. REFINE_CAP): the groups with the largest indicators above tol, largest first, -1 past them
 void launch_select_groups(const double* gind, int ngroups, double tol, int* glist, hipStream_t st);
 // flags |= flag where acc[q] > tol (or not finite); acc cleared
@@ -232,7 +234,7 @@ void launch_berr_finish(double* acc, int64_t Fc, int nvalid, double tol, int fla
                         int64_t q0, int which, hipStream_t st);
 void launch_axpy_vec(double2* X, const double2* D, int64_t count, hipStream_t st, const int* glist = nullptr,
                      int64_t Fc = 64);
-void launch_scale_vec(double2* X, const double* m, int n, int64_t Fc, hipStream_t st);
+void launch_scale_vec(double2* X, const double2* m, int n, int64_t Fc, hipStream_t st);
 void launch_unpermute(const int* perm, int n, const double2* X, int64_t Fc, int nvalid, double2* out, hipStream_t st);
 void launch_matvec(const int* colptr, const int* rowind, int n, const double2* data, int64_t ds, const double2* x,
                    int64_t xs, double2* y, int transpose, int batch, hipStream_t st);

@@ -5,7 +5,8 @@
   every iteration and by > 10x overall;
 * on the same mesh, a 32-frequency subsample: the L-BFGS iterates driven by the GPU loss + gradient
   and by the oracle's (SuperLU + UMFPACK-default refinement, adjoint gradient; process pool) agree.
-  Tolerance: the GPU gradient matches the oracle's to ~5e-7 at C3 (tests/test_gpu_fullsize.py), and
+  Tolerance: the GPU gradient matches the extended-precision truth to ~2e-8 over the C3 sweep
+  (tests/test_gpu_grad_truth.py; the oracle's own error there is 2.6e-8), and
   the badly identified directions (E2, nu12, b2..b4: docs in DESIGN.md section 7 / profiles/r03
   c5_identifiability.json) carry gradient components of ~1e-6 of the largest, so the quasi-Newton
   steps agree closely (measured 4.3e-9 in x); x within 1e-7.
@@ -17,8 +18,9 @@
   mean_q [2 |d_q| 3e-7 + 9e-14] of the oracle's loss at the same point -- a per-iterate bound that
   tightens as the fit converges, ~4e-5 of the loss at the last iterates here (|d_q| ~ 1e-2), where a
   fixed 1e-6 would be below what the two fp64 solvers determine about a loss that is a small
-  difference; and the two trajectories' loss histories within that bound plus 1e-7 relative (their x
-  differ by ~1e-8).
+  difference; and the two trajectories' loss histories within that bound plus what their x difference
+  (~1e-8) moves the loss, 2 sum_i |g_i| |xg_i - xo_i| with g the GPU gradient at the GPU iterate (the
+  loss falls 200x over three steps, so 2e-8 in x moves the late iterates' loss by ~1e-5 of itself).
 (The reference has no L-BFGS; its optimisers' trajectories are pinned at ny = 3 in
 tests/test_gpu_reference_run.py.)
 """
@@ -70,7 +72,8 @@ def test_c5_full_mesh_iterates_match_oracle_driven(c5):
     th0 = np.asarray(c5.parameters) * (1 + REL0)
     runs = []
     orc_fn = oracle_loss_fn(oracle_for(c5), freqs, ref, "MSE_LOG_AFC", scaling=th0, n_workers=8)
-    for f in (c5.getLossFunction(freqs, ref, "MSE_LOG_AFC", th0), orc_fn):
+    gpu_fn = c5.getLossFunction(freqs, ref, "MSE_LOG_AFC", th0)
+    for f in (gpu_fn, orc_fn):
         res = Optimizers.optimize_lbfgs(f, np.ones(8), N_steps=3)
         runs.append((np.array([np.asarray(v, dtype=np.float64) for v in res.x_history + [res.x]]),
                      np.array([float(v) for v in res.f_history + [res.f]])))
@@ -91,4 +94,13 @@ def test_c5_full_mesh_iterates_match_oracle_driven(c5):
     assert xg.shape == xo.shape and len(xg) >= 3
     assert np.max(np.abs(xg - xo)) < 1e-7
     assert np.all(np.abs(fg - fo_at_xg) <= bound), (np.abs(fg - fo_at_xg), bound)
-    assert np.all(np.abs(fg - fo) <= bound + 1e-7 * fo), (np.abs(fg - fo), bound)
+    # the two trajectories: their losses differ by the loss functions' difference (bound) plus what their
+    # x difference moves the loss, |g . (xg - xo)| to first order (2x for the curvature over ~1e-8 steps)
+    moved = []
+    for x, xo_i in zip(xg, xo):
+        xt = torch.tensor(x, requires_grad=True)
+        gpu_fn(xt).backward()
+        moved.append(2 * float(np.sum(np.abs(xt.grad.numpy()) * np.abs(x - xo_i))))
+    moved = np.array(moved)
+    report("c5_trajectories", f_diff=np.abs(fg - fo).tolist(), moved=moved.tolist(), bound=bound.tolist())
+    assert np.all(np.abs(fg - fo) <= bound + moved), (np.abs(fg - fo), bound, moved)

@@ -10,8 +10,8 @@ is the extended-precision fr at theta_true.
 
 Measure: relative max-norm error of the partials, ``max_k |w_k - w*_k| / max_k |w*_k|`` with
 ``w = sum_S w_f / |S|`` over a frequency set S, and the relative error of the loss and of the theta
-gradient.  Bound: the GPU partials within 2e-7 of the truth, or within twice the oracle's own error
-on the same set.
+gradient.  Bound: the GPU partials within W_RTOL (6e-8) of the truth, or within twice the oracle's own
+error on the same set (asked for 2e-7).
 
 C4 (BASELINE.json configs[3]): a rank of the 8-GPU run sweeps the 512-frequency block
 ``shard_range(4096, r, 8)``; a fresh engine sized for it takes the narrow-sweep path (1 lane, the
@@ -30,7 +30,10 @@ from helpers import make_problem, report
 pytestmark = pytest.mark.gpu
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-W_RTOL = 2e-7              # gradient partials against the extended-precision truth (or 2x the oracle's error)
+# gradient partials against the extended-precision truth (or 2x the oracle's error).  VERDICT round 3 asked for
+# 2e-7; with the solve-error scale of the cotangent (k_correct_finish) the GPU measures 1.2-2.5e-8 on every set
+# (profiles/r04), the oracle 0.9-2.7e-8, so the bound is 6e-8
+W_RTOL = 6e-8
 LOSS_RTOL = 1e-7
 FR_RTOL_C3 = 1e-7          # fr against c3_truth.npz (functional correction on, as in test_gpu_fullsize)
 
