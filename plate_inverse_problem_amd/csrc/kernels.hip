@@ -2535,7 +2535,7 @@ __device__ __forceinline__ void loss_term(int loss_type, double fr, cplx r, doub
 // (1 + dx)(1 + dm), whose imaginary part the real gradient does not forgive (the partials cancel by 1e7-1e9
 // over the sweep); fr = mu*^T A x* = mu*^T b, so mu^T A x = (1 + dx)(1 + dm) fr to first order, and
 // mu^T A x = mu^T b - mu^T r is two dot products the sweep has already formed (k_rhs_dot, the correction's
-// walk): dividing by it removes both factors with no further solve
+// walk): dividing by it removes both factors with no further solve ("Gradient at full size")
 __global__ __launch_bounds__(256) void k_correct_finish(FunctionalArgs A, const double* __restrict__ fr0,
                                                         const cplx* __restrict__ cpart, int nparts, int64_t Fc,
                                                         int nvalid, int64_t q_global0, double* __restrict__ fr_out,

@@ -65,7 +65,30 @@ def main(path, L=None):
 
 
 GAPS = "--gaps" in sys.argv
+SOLVES = "--solves" in sys.argv
+
+
+def solves(path):
+    """The last sweep's solve launches in order: per kernel, (duration us) -- the paired top-down pass
+    runs its levels top first, so its k_usolve2_level launches map to levels L-1 .. 0."""
+    rows = list(csv.DictReader(open(path)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    names = [r["Kernel_Name"].split("(")[0].replace("void ", "").replace("pfr::", "") for r in rows]
+    pads = [i for i, n in enumerate(names) if n.startswith("k_pad_freqs")]
+    a = pads[-1] if pads else 0
+    seq = {}
+    for r, n in zip(rows[a:], names[a:]):
+        if "solve" in n or n.startswith(("k_fn_", "k_residual", "k_dirichlet")):
+            key = n.split("(")[0]
+            seq.setdefault(key, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    for k, v in seq.items():
+        print("%-44s n %3d  total %7.1f us" % (k[:44], len(v), sum(v)))
+        print("    " + " ".join("%.0f" % x for x in v))
+
 
 if __name__ == "__main__":
-    args = [a for a in sys.argv[1:] if a != "--gaps"]
-    main(args[0], int(args[1]) if len(args) > 1 else None)
+    args = [a for a in sys.argv[1:] if a not in ("--gaps", "--solves")]
+    if SOLVES:
+        solves(args[0])
+    else:
+        main(args[0], int(args[1]) if len(args) > 1 else None)
