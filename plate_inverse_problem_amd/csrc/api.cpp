@@ -154,7 +154,8 @@ struct pfr_solver {
   // the residual walk's per-workgroup dot-product partials (residual_parts(n) x Fc)
   double* fr0 = nullptr;
   double2 *mscale = nullptr, *cpart = nullptr;     // mscale complex: the solve-error scale (k_correct_finish)
-  int scale_corr = 1;                   // PFR_SCALE_CORR: the solve-error scale of the loss sweeps' cotangent
+  int scale_corr = 1;
+  int off_rl = 0;                       // PFR_OFF_RL: L21 rows right-looking on levels with pivot blocks <= this (16-32)                   // PFR_SCALE_CORR: the solve-error scale of the loss sweeps' cotangent
   int32_t* flags = nullptr;
   // operator / rhs / functional / stiffness state
   const double2* K = nullptr;
@@ -192,7 +193,7 @@ struct pfr_solver {
   // workgroup, at most), PFR_US2_SMALL (largest front of a level the paired top-down solve treats
   // with its low-register small-front variant)
   int solve_wmax = 8, fac_wmax = 16, us2_small = 110;
-  int us2_cfg = 0;                      // PFR_US2_CFG: register shape of the small-front paired top-down pass
+  int us2_cfg = 2;                      // PFR_US2_CFG: register shape of the small-front paired top-down pass
   int off_small = 1;                    // PFR_OFF_SMALL: no-prefix off-diagonal variant on levels of ns <= 8
   int fac_lds_qf = 1;                   // PFR_FAC_LDS_QF: frequencies per k_factor_sym_lds workgroup (1, 2 or 4)
   int fac_lds = -1;                     // PFR_FAC_LDS: which levels factor A11 in LDS (k_factor_sym_lds): n > 0
@@ -396,7 +397,7 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     mark(l, 2);
     pfr::launch_offdiag(mode, s->P, s->d_items + s->item_ptr[l], s->item_ptr[l + 1] - s->item_ptr[l], s->d_orec,
                         s->d_oxp + s->item_ptr[l], s->d_ox, ngroups, s->F, s->Fc, s->freqs, s->K, s->M, data, ds,
-                        nvalid, s->off_small ? s->level_maxns[l] : pfr::MAX_FRONT, st);
+                        nvalid, s->off_small ? s->level_maxns[l] : pfr::MAX_FRONT, st, s->sym ? s->off_rl : 0);
     if (after_panel) after_panel(l);
     mark(l, 3);
     pfr::launch_schur_blk(s->schur_bc, s->P, s->d_blocks + s->blk_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
@@ -922,7 +923,9 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->solve_wmax = knob("PFR_SOLVE_WMAX", 8, 1, 8);
   s->fac_wmax = knob("PFR_FAC_WMAX", 16, 1, 16);
   s->us2_small = knob("PFR_US2_SMALL", 110, 0, pfr::MAX_FRONT);
-  s->us2_cfg = knob("PFR_US2_CFG", 0, 0, 2);
+  // 2 (8 pivot rows x 2 values per pass) reads 18 % less than 0 (2 x 4) at the same time: 2,048-frequency sweep
+  // 92.5 -> 75.7 GB over four sweeps, 21.7 ms both (profiles/r04/solve_traffic/)
+  s->us2_cfg = knob("PFR_US2_CFG", 2, 0, 2);
   s->off_small = knob("PFR_OFF_SMALL", 1, 0, 1);
   s->split_target = knob("PFR_SOLVE_SPLIT", 256, 0, 1 << 20);
   s->fac_lds = knob("PFR_FAC_LDS", -1, -1, 64);   // LDS holds the lower triangle of up to 64 pivots x 4 frequencies
@@ -933,6 +936,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);
   s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);
   s->scale_corr = knob("PFR_SCALE_CORR", 1, 0, 1);
+  s->off_rl = knob("PFR_OFF_RL", 0, 0, 32);
   s->fuse_asm = knob("PFR_FUSE_ASM", 0, 0, 1);   // measured slower (2,048-frequency chunk: A11 classes 4.1 -> 6.6 ms)
   s->flow = knob("PFR_FLOW", 0, 0, 7);   // bit 0: paired top-down pass, bit 1: bottom-up chain, bit 2: factorisation
   s->flow_fwg = knob("PFR_FLOW_FWG", 256, 0, 1 << 20);

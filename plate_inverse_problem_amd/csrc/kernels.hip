@@ -896,6 +896,89 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMALL ? 5 :
   offdiag_item<MODE, SMALL>(P, items, wid, orec, oxp, ox, F, Fc, freqs, K, M, data, data_stride, nvalid, by);
 }
 
+// Right-looking L21 rows for the levels whose pivot blocks are at most NSM (symmetric analyses: kind-0 items
+// only): one wave = ONE row x 64 frequencies (the two rows of an item on two waves), the whole row in
+// registers.  k_offdiag_level is left-looking: every chunk of OB columns re-loads the row's own earlier L21
+// values and the U11 column block, a chain of ~ns^2 / (2 OB) dependent load rounds per wave that the few
+// fronts of the upper levels cannot hide behind other waves; here the row stays in registers and each chunk
+// updates the columns right of it with independent U11 loads: ns / OB rounds.  The operations per column
+// are those of k_offdiag_level in the same order (columns of earlier chunks in ascending pivot order, then
+// the chunk's own triangle), so the results are identical bit for bit.
+template <int MODE, int NSM>
+__global__ __launch_bounds__(256) void k_offdiag_rl(DevPattern P, const int4* __restrict__ items, int nitems,
+                                                    const int2* __restrict__ orec, const int* __restrict__ oxp,
+                                                    const int2* __restrict__ ox, cplx* __restrict__ F, int64_t Fc,
+                                                    const double* __restrict__ freqs, const cplx* __restrict__ K,
+                                                    const double* __restrict__ M, const cplx* __restrict__ data,
+                                                    int64_t data_stride, int nvalid) {
+  static_assert(OFF_G == 1, "one lane = one frequency");
+  static_assert(NSM % 8 == 0 && OB == 8, "chunks of 8 pivots, as k_offdiag_level");
+  const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
+  const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
+  const int wv = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
+  const int wid = wv / OFF_RPL, h = wv % OFF_RPL;
+  if (wid >= nitems) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)by * 64 + lane;
+  const int4 it = items[wid];
+  const Front fr = P.fronts[it.x];
+  const int f = fr.f, ns = fr.ns;
+  const int row = it.y + h;
+  if (row >= f) return;
+  cplx* __restrict__ base = F + fr.off * Fc + q;
+  const int64_t so = (int64_t)row * f;
+  OffSrc S;
+  S.rec[0] = orec + it.w + (int64_t)h * ns;
+  S.om2 = 0.0;
+  if (MODE == 0) {
+    const double om = 6.283185307179586 * freqs[q];
+    S.om2 = om * om;
+  }
+  S.K = K;
+  S.M = M;
+  S.dq = data + min(q, (int64_t)nvalid - 1) * data_stride;
+  cplx x[NSM];
+#pragma unroll
+  for (int c = 0; c < NSM; ++c) x[c] = c < ns ? off_source<MODE>(S, F, Fc, q, 0, c) : make_double2(0.0, 0.0);
+  for (int e = oxp[wid]; e < oxp[wid + 1]; ++e) {      // rare: several children cover one entry
+    const int2 g = ox[e];
+    if (g.x % OFF_RPL != h) continue;
+    const int c = g.x / OFF_RPL;
+    const cplx v = F[(int64_t)g.y * Fc + q];
+#pragma unroll
+    for (int j = 0; j < NSM; ++j)
+      if (j == c) x[j] = cadd(x[j], v);
+  }
+#define U(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+#pragma unroll
+  for (int c0 = 0; c0 < NSM; c0 += 8) {
+    if (c0 < ns) {
+      // the chunk's own triangle, column by column
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (c0 + j < ns) {
+#pragma unroll
+          for (int a = 0; a < j; ++a) x[c0 + j] = cfms(x[c0 + j], x[c0 + a], U(c0 + a, c0 + j));
+          x[c0 + j] = cmul(x[c0 + j], crecip(U(c0 + j, c0 + j)));
+        }
+      // the columns right of the chunk
+#pragma unroll
+      for (int j = c0 + 8; j < NSM; ++j)
+        if (j < ns) {
+          cplx u[8];
+#pragma unroll
+          for (int a = 0; a < 8; ++a) u[a] = U(c0 + a, j);
+#pragma unroll
+          for (int a = 0; a < 8; ++a) x[j] = cfms(x[j], x[c0 + a], u[a]);
+        }
+    }
+  }
+#undef U
+#pragma unroll
+  for (int c = 0; c < NSM; ++c)
+    if (c < ns) base[(so + c) * Fc] = x[c];
+}
+
 // ------------------------------------------------------------------ K2b: Schur complement
 // A22 -= L21 U12 over all ns pivots of the front: one wavefront per TM x TN tile
 // of A22 (64 lanes = 64 frequencies), accumulators in registers, no stores in
@@ -3283,10 +3366,23 @@ void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, i
 
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
                     const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,
-                    const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st) {
+                    const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st, int rl) {
   if (nitems <= 0) return;
-  dim3 g((nitems + 3) / 4, ngroups * OFF_G), b(256);
   const bool small = maxns <= 8;
+  if (rl > 0 && !small && maxns <= rl) {
+    // right-looking rows (symmetric analyses): OFF_RPL waves per item
+    dim3 g((unsigned)(((int64_t)nitems * OFF_RPL + 3) / 4), ngroups), b(256);
+#define RL(MD, N) LAUNCH((k_offdiag_rl<MD, N>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid)
+    if (mode == 0 && maxns <= 16) RL(0, 16);
+    else if (mode == 0 && maxns <= 24) RL(0, 24);
+    else if (mode == 0) RL(0, 32);
+    else if (maxns <= 16) RL(1, 16);
+    else if (maxns <= 24) RL(1, 24);
+    else RL(1, 32);
+#undef RL
+    return;
+  }
+  dim3 g((nitems + 3) / 4, ngroups * OFF_G), b(256);
   static_assert(OB >= 8, "the SMALL variant covers pivot blocks of up to 8");
 #define OL(MD, SM) LAUNCH((k_offdiag_level<MD, SM>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid)
   if (mode == 0 && small) OL(0, true);

@@ -26,11 +26,13 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
-def _run(monkeypatch, flow, lo, hi, fac_lds="0"):
+def _run(monkeypatch, flow, lo, hi, fac_lds="0", env=None):
     from plate_inverse_problem_amd import _native
     from plate_inverse_problem_amd.Problem import _coeffs18
     monkeypatch.setenv("PFR_FLOW", str(flow))
     monkeypatch.setenv("PFR_FAC_LDS", fac_lds)
+    for k, v in (env or {}).items():
+        monkeypatch.setenv(k, v)
     T = np.load(os.path.join(GOLDEN, "c3_grad_truth.npz"))
     p = make_problem("orthotropic", ny=25, device="cuda:0")
     try:
@@ -85,3 +87,19 @@ def test_factor_flow_default_lds_accuracy(monkeypatch):
     report("flow7_default_lds", fr_vs_truth_level=e0, fr_vs_truth_flow=e1, loss_rel=dl, w_rel=dw)
     assert got[4] == 0 and e0 < 2e-7 and e1 < 2e-7
     assert dl < 1e-7 and dw < 4e-7
+
+
+@pytest.mark.parametrize("lo,hi", [(1024, 1536), (0, 2048)])
+def test_offdiag_right_looking_bitwise(monkeypatch, lo, hi):
+    """k_offdiag_rl (PFR_OFF_RL: the L21 rows right-looking, the row in registers) performs k_offdiag_level's
+    operations per entry in the same order: loss, partials and fr identical, on the narrow (512) and the
+    bench's (2,048) engine."""
+    base = _run(monkeypatch, 0, lo, hi, fac_lds="-1", env={"PFR_OFF_RL": "0"})
+    for rl in ("16", "32"):
+        got = _run(monkeypatch, 0, lo, hi, fac_lds="-1", env={"PFR_OFF_RL": rl})
+        dl = abs(got[0] / base[0] - 1)
+        dw = float(np.max(np.abs(got[1] - base[1])) / np.max(np.abs(base[1])))
+        dfr = float(np.max(np.abs(got[2] / base[2] - 1)))
+        report(f"offdiag_rl{rl}_{lo}_{hi}", loss_rel=dl, w_rel=dw, fr_rel=dfr, flagged=got[4])
+        assert got[4] == 0
+        assert dl == 0 and dw == 0 and dfr == 0, (rl, dl, dw, dfr)

@@ -173,7 +173,7 @@ def test_c2_forward_sweep_matches_truth():
     {"PFR_ORDERING": "2", "PFR_LEAF_SIZE": "96", "PFR_MD_DELTA": "0"},   # the rounds 1-3 ordering
     {"PFR_FUSE_ASM": "1"},             # A11 gathered by the A11 LU kernel itself (no k_assemble_level launches)
     {"PFR_US2_CFG": "1", "PFR_US2_SMALL": "1024"},   # small-front paired top-down pass, 4 rows x 4 values
-    {"PFR_US2_CFG": "2", "PFR_US2_SMALL": "1024"},   # ... 8 rows x 2 values
+    {"PFR_US2_CFG": "0", "PFR_US2_SMALL": "1024"},   # ... 2 rows x 4 values (the default is 8 x 2)
     {"PFR_FLOW": "3"},                 # both solve passes dependency-driven (every level narrow at this size)
     {"PFR_FLOW": "3", "PFR_FLOW_WG": "16"},   # ... only the top levels, the rest level by level
     {"PFR_FLOW": "2"},                 # the bottom-up chain only
@@ -182,6 +182,8 @@ def test_c2_forward_sweep_matches_truth():
     {"PFR_CHECK": "27"},               # + the selective adjoint refinement (opt-in)
     {"PFR_CHECK": "27", "PFR_REFINE_TOL": "0"},   # ... every group listed (the first REFINE_CAP of each chunk)
     {"PFR_SCALE_CORR": "0"},           # the cotangent without the solve-error scale
+    {"PFR_OFF_RL": "32"},              # L21 rows right-looking on the levels with pivot blocks of 9-32
+    {"PFR_OFF_RL": "16"},
 ])
 def test_kernel_variants_match_oracle(env, monkeypatch):
     from oracle.plate_oracle import loss_and_grad
