@@ -2078,8 +2078,15 @@ int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int
       pfr::launch_functional(fs, s->X, Fc, nv, q0, nullptr, nullptr, s->G, st);
       if ((rc = adjoint_solve(s, rg, s->XA, st, 1))) return rc;
       check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st, s->XA, false);
+      // the loss sweep's cotangent, solve-error scale included (k_correct_finish): its gradient is the loss sweep's
+      pfr::RhsScale bsc;
+      bsc.freqs = s->freqs;
+      bsc.mass_sum = s->mass_sum;
+      bsc.beta_re = s->beta_re;
+      bsc.beta_im = s->beta_im;
+      if (s->scale_corr) pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st);
       pfr::launch_correct_finish(fa, s->fr0, s->cpart, pfr::residual_parts(s->n), Fc, nv, q0, nullptr, s->loss_terms,
-                                 s->mscale, st);
+                                 s->mscale, st, nullptr, s->scale_corr ? s->tq : nullptr, bsc);
       pfr::launch_scale_vec(s->XA, s->mscale, s->n, Fc, st);
       // the second-order seeds G (k_functional_tangent) are formed from fa, not the seed mode
     } else {
