@@ -936,7 +936,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);
   s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);
   s->scale_corr = knob("PFR_SCALE_CORR", 1, 0, 1);
-  s->off_rl = knob("PFR_OFF_RL", 0, 0, 32);
+  s->off_rl = knob("PFR_OFF_RL", 0, 0, 124);   // n: one row per wave (n = 16, 24, 32); 100 + n: two rows (n = 16, 24)
+  if (s->off_rl > 100 && s->off_rl % 100 > 24) s->off_rl = 124;
   s->fuse_asm = knob("PFR_FUSE_ASM", 0, 0, 1);   // measured slower (2,048-frequency chunk: A11 classes 4.1 -> 6.6 ms)
   s->flow = knob("PFR_FLOW", 0, 0, 7);   // bit 0: paired top-down pass, bit 1: bottom-up chain, bit 2: factorisation
   s->flow_fwg = knob("PFR_FLOW_FWG", 256, 0, 1 << 20);

@@ -904,7 +904,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMALL ? 5 :
 // updates the columns right of it with independent U11 loads: ns / OB rounds.  The operations per column
 // are those of k_offdiag_level in the same order (columns of earlier chunks in ascending pivot order, then
 // the chunk's own triangle), so the results are identical bit for bit.
-template <int MODE, int NSM>
+template <int MODE, int NSM, int R>
 __global__ __launch_bounds__(256) void k_offdiag_rl(DevPattern P, const int4* __restrict__ items, int nitems,
                                                     const int2* __restrict__ orec, const int* __restrict__ oxp,
                                                     const int2* __restrict__ ox, cplx* __restrict__ F, int64_t Fc,
@@ -913,22 +913,23 @@ __global__ __launch_bounds__(256) void k_offdiag_rl(DevPattern P, const int4* __
                                                     int64_t data_stride, int nvalid) {
   static_assert(OFF_G == 1, "one lane = one frequency");
   static_assert(NSM % 8 == 0 && OB == 8, "chunks of 8 pivots, as k_offdiag_level");
+  static_assert(R == 1 || R == OFF_RPL, "one row per wave, or an item's rows per wave");
+  constexpr int WPI = OFF_RPL / R;            // waves per item
   const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
   const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
   const int wv = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
-  const int wid = wv / OFF_RPL, h = wv % OFF_RPL;
+  const int wid = wv / WPI, h0 = (wv % WPI) * R;
   if (wid >= nitems) return;
   const int lane = threadIdx.x & 63;
   const int64_t q = (int64_t)by * 64 + lane;
   const int4 it = items[wid];
   const Front fr = P.fronts[it.x];
   const int f = fr.f, ns = fr.ns;
-  const int row = it.y + h;
-  if (row >= f) return;
+  if (it.y + h0 >= f) return;
   cplx* __restrict__ base = F + fr.off * Fc + q;
-  const int64_t so = (int64_t)row * f;
   OffSrc S;
-  S.rec[0] = orec + it.w + (int64_t)h * ns;
+#pragma unroll
+  for (int r = 0; r < R; ++r) S.rec[r] = orec + it.w + (int64_t)(h0 + r) * ns;
   S.om2 = 0.0;
   if (MODE == 0) {
     const double om = 6.283185307179586 * freqs[q];
@@ -937,17 +938,22 @@ __global__ __launch_bounds__(256) void k_offdiag_rl(DevPattern P, const int4* __
   S.K = K;
   S.M = M;
   S.dq = data + min(q, (int64_t)nvalid - 1) * data_stride;
-  cplx x[NSM];
+  cplx x[R][NSM];
 #pragma unroll
-  for (int c = 0; c < NSM; ++c) x[c] = c < ns ? off_source<MODE>(S, F, Fc, q, 0, c) : make_double2(0.0, 0.0);
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int c = 0; c < NSM; ++c) x[r][c] = c < ns ? off_source<MODE>(S, F, Fc, q, r, c) : make_double2(0.0, 0.0);
   for (int e = oxp[wid]; e < oxp[wid + 1]; ++e) {      // rare: several children cover one entry
     const int2 g = ox[e];
-    if (g.x % OFF_RPL != h) continue;
+    const int r = g.x % OFF_RPL - h0;
+    if (r < 0 || r >= R) continue;
     const int c = g.x / OFF_RPL;
     const cplx v = F[(int64_t)g.y * Fc + q];
 #pragma unroll
-    for (int j = 0; j < NSM; ++j)
-      if (j == c) x[j] = cadd(x[j], v);
+    for (int rr = 0; rr < R; ++rr)
+#pragma unroll
+      for (int j = 0; j < NSM; ++j)
+        if (rr == r && j == c) x[rr][j] = cadd(x[rr][j], v);
   }
 #define U(a, b) base[((int64_t)(a) * f + (b)) * Fc]
 #pragma unroll
@@ -958,8 +964,14 @@ __global__ __launch_bounds__(256) void k_offdiag_rl(DevPattern P, const int4* __
       for (int j = 0; j < 8; ++j)
         if (c0 + j < ns) {
 #pragma unroll
-          for (int a = 0; a < j; ++a) x[c0 + j] = cfms(x[c0 + j], x[c0 + a], U(c0 + a, c0 + j));
-          x[c0 + j] = cmul(x[c0 + j], crecip(U(c0 + j, c0 + j)));
+          for (int a = 0; a < j; ++a) {
+            const cplx u = U(c0 + a, c0 + j);
+#pragma unroll
+            for (int r = 0; r < R; ++r) x[r][c0 + j] = cfms(x[r][c0 + j], x[r][c0 + a], u);
+          }
+          const cplx d = crecip(U(c0 + j, c0 + j));
+#pragma unroll
+          for (int r = 0; r < R; ++r) x[r][c0 + j] = cmul(x[r][c0 + j], d);
         }
       // the columns right of the chunk
 #pragma unroll
@@ -969,14 +981,21 @@ __global__ __launch_bounds__(256) void k_offdiag_rl(DevPattern P, const int4* __
 #pragma unroll
           for (int a = 0; a < 8; ++a) u[a] = U(c0 + a, j);
 #pragma unroll
-          for (int a = 0; a < 8; ++a) x[j] = cfms(x[j], x[c0 + a], u[a]);
+          for (int a = 0; a < 8; ++a)
+#pragma unroll
+            for (int r = 0; r < R; ++r) x[r][j] = cfms(x[r][j], x[r][c0 + a], u[a]);
         }
     }
   }
 #undef U
 #pragma unroll
-  for (int c = 0; c < NSM; ++c)
-    if (c < ns) base[(so + c) * Fc] = x[c];
+  for (int r = 0; r < R; ++r)
+    if (it.y + h0 + r < f) {
+      const int64_t so = (int64_t)(it.y + h0 + r) * f;
+#pragma unroll
+      for (int c = 0; c < NSM; ++c)
+        if (c < ns) base[(so + c) * Fc] = x[r][c];
+    }
 }
 
 // ------------------------------------------------------------------ K2b: Schur complement
@@ -3369,16 +3388,24 @@ void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems
                     const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st, int rl) {
   if (nitems <= 0) return;
   const bool small = maxns <= 8;
-  if (rl > 0 && !small && maxns <= rl) {
-    // right-looking rows (symmetric analyses): OFF_RPL waves per item
-    dim3 g((unsigned)(((int64_t)nitems * OFF_RPL + 3) / 4), ngroups), b(256);
-#define RL(MD, N) LAUNCH((k_offdiag_rl<MD, N>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid)
-    if (mode == 0 && maxns <= 16) RL(0, 16);
-    else if (mode == 0 && maxns <= 24) RL(0, 24);
-    else if (mode == 0) RL(0, 32);
-    else if (maxns <= 16) RL(1, 16);
-    else if (maxns <= 24) RL(1, 24);
-    else RL(1, 32);
+  const int rlim = rl % 100, rrows = rl >= 100 ? OFF_RPL : 1;
+  if (rlim > 0 && !small && maxns <= rlim) {
+    // right-looking rows (symmetric analyses): rl = n (one row per wave) or 100 + n (an item's rows per wave)
+    dim3 g((unsigned)(((int64_t)nitems * (OFF_RPL / rrows) + 3) / 4), ngroups), b(256);
+#define RL(MD, N, RR) LAUNCH((k_offdiag_rl<MD, N, RR>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid)
+    if (rrows == 1) {
+      if (mode == 0 && maxns <= 16) RL(0, 16, 1);
+      else if (mode == 0 && maxns <= 24) RL(0, 24, 1);
+      else if (mode == 0) RL(0, 32, 1);
+      else if (maxns <= 16) RL(1, 16, 1);
+      else if (maxns <= 24) RL(1, 24, 1);
+      else RL(1, 32, 1);
+    } else {
+      if (mode == 0 && maxns <= 16) RL(0, 16, OFF_RPL);
+      else if (mode == 0) RL(0, 24, OFF_RPL);
+      else if (maxns <= 16) RL(1, 16, OFF_RPL);
+      else RL(1, 24, OFF_RPL);
+    }
 #undef RL
     return;
   }

@@ -95,7 +95,7 @@ def test_offdiag_right_looking_bitwise(monkeypatch, lo, hi):
     operations per entry in the same order: loss, partials and fr identical, on the narrow (512) and the
     bench's (2,048) engine."""
     base = _run(monkeypatch, 0, lo, hi, fac_lds="-1", env={"PFR_OFF_RL": "0"})
-    for rl in ("16", "32"):
+    for rl in ("16", "32", "116", "124"):       # one row per wave; 100 + n: an item's two rows per wave
         got = _run(monkeypatch, 0, lo, hi, fac_lds="-1", env={"PFR_OFF_RL": rl})
         dl = abs(got[0] / base[0] - 1)
         dw = float(np.max(np.abs(got[1] - base[1])) / np.max(np.abs(base[1])))

@@ -184,6 +184,7 @@ def test_c2_forward_sweep_matches_truth():
     {"PFR_SCALE_CORR": "0"},           # the cotangent without the solve-error scale
     {"PFR_OFF_RL": "32"},              # L21 rows right-looking on the levels with pivot blocks of 9-32
     {"PFR_OFF_RL": "16"},
+    {"PFR_OFF_RL": "124"},             # ... two rows per wave
 ])
 def test_kernel_variants_match_oracle(env, monkeypatch):
     from oracle.plate_oracle import loss_and_grad
