@@ -10,3 +10,4 @@ FREQS=2048 STEPS=3 bash tools/gpu.sh env r4h_rl2048 "PFR_OFF_RL=0" "PFR_OFF_RL=1
 FREQS=512 STEPS=6 bash tools/gpu.sh env r4h_rl512 "PFR_OFF_RL=0" "PFR_OFF_RL=116" "PFR_OFF_RL=124" "PFR_OFF_RL=0" "PFR_OFF_RL=116" > $O/rl512.txt 2>&1 || exit $?
 bash tools/gpu.sh trace r4h_t2048 2048 PFR_OFF_RL=116 > $O/t2048rl116.txt 2>&1 || exit $?
 rm -f gpurun_out/r4h_t2048/run_kernel_trace.csv
+FREQS=4096 STEPS=4 bash tools/gpu.sh env r4h_lanes "PFR_LANES=2" "PFR_LANES=1" "PFR_LANES=2" "PFR_LANES=1" > $O/lanes4096.txt 2>&1 || exit $?
