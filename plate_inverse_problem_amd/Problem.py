@@ -154,11 +154,14 @@ class _Engine:
         and dominate the sparse solve passes of narrow sweeps; those get the shallower trees of more
         dissection levels.  C3, freq-solves/s at leaf 96 / 500 / 3,000 / 10,000 (late round 3, with the
         functional from the bottom-up passes): 512 frequencies 32.7k / 33.0k / 31.3k / 30.5k, 1,024
-        41.1k / 42.8k / 43.5k / 44.0k, 2,048 - / 49.8k / 51.4k / 52.7k."""
+        41.1k / 42.8k / 43.5k / 44.0k, 2,048 - / 49.8k / 51.4k / 52.7k.  Round 4 (current kernels, alternated
+        runs, profiles/r04/experiments/leaf*.txt): 512 frequencies leaf 96 / 150 / 200 / 250 / 300: 32.2-33.4k /
+        34.2k / 34.9-35.1k / 33.4k / 33.3-33.9k; 1,024 leaf 600 / 1,000 / 2,000 / 10,000: 43.2k / 45.8-46.1k / 46.7k /
+        44.5-44.9k; 2,048 leaf 1,000 / 2,000 / 10,000: 53.0k / 55.2k / 55.4-55.8k; 4,096: 10,000 best."""
         if self._leaf_env is not None:
             return self._leaf_env
         n_freqs = max(1, n_freqs)
-        return 96 if n_freqs <= 512 else 10000
+        return 200 if n_freqs <= 512 else 2000 if n_freqs <= 1024 else 10000
 
     def _use_symbolic(self, n_freqs: int) -> bool:
         """Select (building once) the symbolic analysis for a sweep width; True if it changed."""

@@ -60,7 +60,9 @@ def _fnv(perm):
 # (leaf, ordering, symmetric, max_ns, md_delta, use_last)
 OPTION_SETS = [
     (10000, 0, 1, 256, 4, 0),   # the engine above 512 frequencies (deep MMD tree)
-    (96, 0, 1, 256, 4, 0),      # the engine up to 512 frequencies (C4's per-rank share)
+    (200, 0, 1, 256, 4, 0),     # the engine up to 512 frequencies (C4's per-rank share)
+    (2000, 0, 1, 256, 4, 0),    # the engine at 513-1,024 frequencies
+    (96, 0, 1, 256, 4, 0),      # the width rule of round 3 at <= 512
     (16, 0, 1, 256, 4, 0),
     (10000, 0, 0, 256, 4, 0),   # general analysis (explicit-matrix solves)
     (96, 2, 1, 256, 0, 0),      # exact minimum degree leaves (rounds 1-3)

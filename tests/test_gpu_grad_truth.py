@@ -15,7 +15,7 @@ error on the same set (asked for 2e-7).
 
 C4 (BASELINE.json configs[3]): a rank of the 8-GPU run sweeps the 512-frequency block
 ``shard_range(4096, r, 8)``; a fresh engine sized for it takes the narrow-sweep path (1 lane, the
-leaf-96 ordering, one 512-frequency chunk, the A11 LU in LDS on its few-workgroup levels).  Block 2
+leaf-200 ordering, one 512-frequency chunk, the A11 LU in LDS on its few-workgroup levels).  Block 2
 holds the resonance (sample 1179).
 """
 import gc
@@ -136,7 +136,7 @@ def test_c4_rank_block_at_c3_size():
         e = _check_set("c4_rank2_grad_truth", p, T, sel, theta)
         eng = p.engine()
         assert eng.n_lanes == 1 and eng.max_batch == 512
-        assert eng.leaf_size_for(512) == 96 and eng.sym is eng._syms[96]
+        assert eng.leaf_size_for(512) == 200 and eng.sym is eng._syms[200]
         assert eng.stats["n_levels"] < 38          # the shallow tree, not the deep one
         # fr at the fixture frequencies inside the block (forward sweep on the same engine)
         inside = (F["index"] >= lo) & (F["index"] < hi)
