@@ -155,6 +155,8 @@ struct pfr_solver {
   double* fr0 = nullptr;
   double2 *mscale = nullptr, *cpart = nullptr;     // mscale complex: the solve-error scale (k_correct_finish)
   int scale_corr = 1;
+  int us2_tiny = 8;                     // PFR_US2_TINY (4 / 8): levels whose pivot blocks are <= this, one wave per front
+  int off_swz_min = 0;                  // PFR_OFF_SWZ_MIN: L21 launches with fewer (item, group) waves keep the hardware order
   int off_rl = 0;                       // PFR_OFF_RL: L21 rows right-looking on levels with pivot blocks <= this (16-32)                   // PFR_SCALE_CORR: the solve-error scale of the loss sweeps' cotangent
   int32_t* flags = nullptr;
   // operator / rhs / functional / stiffness state
@@ -397,7 +399,8 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     mark(l, 2);
     pfr::launch_offdiag(mode, s->P, s->d_items + s->item_ptr[l], s->item_ptr[l + 1] - s->item_ptr[l], s->d_orec,
                         s->d_oxp + s->item_ptr[l], s->d_ox, ngroups, s->F, s->Fc, s->freqs, s->K, s->M, data, ds,
-                        nvalid, s->off_small ? s->level_maxns[l] : pfr::MAX_FRONT, st, s->sym ? s->off_rl : 0);
+                        nvalid, s->off_small ? s->level_maxns[l] : pfr::MAX_FRONT, st, s->sym ? s->off_rl : 0,
+                        (int64_t)(s->item_ptr[l + 1] - s->item_ptr[l]) * ngroups >= s->off_swz_min);
     if (after_panel) after_panel(l);
     mark(l, 3);
     pfr::launch_schur_blk(s->schur_bc, s->P, s->d_blocks + s->blk_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
@@ -689,7 +692,8 @@ int sym_top_down_pair(pfr_solver* s, hipStream_t st, bool fwd_all = false) {
                         small, ngroups,
                         s->F, s->Fc, s->Y,
                         s->X, s->d_reach[0], fwd_all ? nullptr : s->d_reach[1], s->Y2, s->XA, s->d_reach[1], st,
-                        solve_split(s, nf), s->us2_cfg);
+                        solve_split(s, nf), s->us2_cfg,
+                        s->us2_tiny > 0 && s->level_maxns[l] <= s->us2_tiny ? (s->level_maxns[l] <= 4 ? 4 : 8) : 0);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -936,6 +940,9 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);
   s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);
   s->scale_corr = knob("PFR_SCALE_CORR", 1, 0, 1);
+  s->off_swz_min = knob("PFR_OFF_SWZ_MIN", 0, 0, 1 << 30);
+  // 8: the bottom two levels at 2,048 frequencies 685 / 612 -> 509 / 489 us (profiles/r04/experiments/us2_tiny_*)
+  s->us2_tiny = knob("PFR_US2_TINY", 8, 0, 8);
   s->off_rl = knob("PFR_OFF_RL", 0, 0, 124);   // n: one row per wave (n = 16, 24, 32); 100 + n: two rows (n = 16, 24)
   if (s->off_rl > 100 && s->off_rl % 100 > 24) s->off_rl = 124;
   s->fuse_asm = knob("PFR_FUSE_ASM", 0, 0, 1);   // measured slower (2,048-frequency chunk: A11 classes 4.1 -> 6.6 ms)

@@ -888,8 +888,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMALL ? 5 :
                                                         const int2* __restrict__ ox, cplx* __restrict__ F, int64_t Fc,
                                                         const double* __restrict__ freqs, const cplx* __restrict__ K,
                                                         const double* __restrict__ M, const cplx* __restrict__ data,
-                                                        int64_t data_stride, int nvalid) {
-  const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
+                                                        int64_t data_stride, int nvalid, int swz) {
+  // swz: XCD-aware order (a frequency group's items on one XCD, sharing its L2); 0: the hardware's round-robin
+  const int64_t o = blockIdx.x + (int64_t)gridDim.x * blockIdx.y;
+  const int64_t lid = swz ? xcd_swizzle(o, (int64_t)gridDim.x * gridDim.y) : o;
   const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
   const int wid = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (wid >= nitems) return;
@@ -1935,6 +1937,82 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
   __syncthreads();
   usolve2_tri(fr, base, Fc, c, act, Xs);
+}
+
+// The paired top-down pass on levels of tiny fronts (every pivot block <= NSM): ONE WAVE per (front, frequency
+// group), four fronts per workgroup, no LDS and no barrier -- the pivot rows' update sums and the U11 backward
+// solve in registers.  k_usolve2_level gives each of the bottom levels' ~3,000 fronts x 32 groups a workgroup
+// whose waves meet at two barriers and pass the pivot values through global memory; here a front is one
+// wave's independent task (more of them resident per CU, each a shorter dependent chain).  Operations per
+// value and their order are k_usolve2_level's (update columns ascending, then the pivot block bottom-up), so
+// the results are identical bit for bit.
+template <int NSM>   // NSM <= KBS: the level kernel's pivot block is one KBS block, solved in the order below
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSM <= 4 ? 6 : 3))) void k_usolve2_tiny(
+    DevPattern P, const int* __restrict__ lvl, int nfronts, const cplx* __restrict__ F, int64_t Fc, UPair A, UPair B) {
+  static_assert(NSM <= KBS, "one pivot block of the level kernel's triangular solve");
+  int bx;
+  const Ctx c = ctx_xcd(bx);
+  const int slot = bx * 4 + c.w;
+  if (slot >= nfronts) return;
+  const int ft = lvl[slot];
+  const bool act[2] = {!A.skip || !A.skip[ft], !B.skip || !B.skip[ft]};
+  const bool live[2] = {!A.reach || A.reach[ft], !B.reach || B.reach[ft]};
+  const cplx* const Ys[2] = {A.Y, B.Y};
+  cplx* const Xs[2] = {A.X, B.X};
+  const Front fr = P.fronts[ft];
+  const int f = fr.f, ns = fr.ns;
+  const cplx* __restrict__ base = F + fr.off * Fc + c.q;
+  const int* __restrict__ ix = P.idx + fr.row0;
+#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+  cplx acc[2][NSM];
+#pragma unroll
+  for (int a = 0; a < NSM; ++a) acc[0][a] = acc[1][a] = make_double2(0.0, 0.0);
+  for (int b = ns; b < f; ++b) {
+    const int iv = __builtin_amdgcn_readfirstlane(ix[b]);
+    const cplx x0 = Xs[0][(int64_t)iv * Fc + c.q], x1 = Xs[1][(int64_t)iv * Fc + c.q];
+    cplx e[NSM];
+#pragma unroll
+    for (int a = 0; a < NSM; ++a) e[a] = E(b, min(a, ns - 1));
+#pragma unroll
+    for (int a = 0; a < NSM; ++a) {
+      acc[0][a] = cfms(acc[0][a], e[a], x0);
+      acc[1][a] = cfms(acc[1][a], e[a], x1);
+    }
+  }
+  // z_a = y_a + U(a, a) acc_a, then U11 z = ... bottom-up (k_usolve2_level's pivot block, ns <= KBS)
+  cplx z[2][NSM];
+#pragma unroll
+  for (int a = 0; a < NSM; ++a) {
+    const int ra = min(a, ns - 1);
+    const cplx urr = E(ra, ra);
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const cplx y = live[v] ? Ys[v][(int64_t)(fr.col0 + ra) * Fc + c.q] : make_double2(0.0, 0.0);
+      z[v][a] = cadd(y, cmul(urr, acc[v][a]));
+    }
+  }
+#pragma unroll
+  for (int i = NSM - 1; i >= 0; --i)
+    if (i < ns) {
+#pragma unroll
+      for (int k = i + 1; k < NSM; ++k)
+        if (k < ns) {
+          const cplx u = E(i, k);
+#pragma unroll
+          for (int v = 0; v < 2; ++v) z[v][i] = cfms(z[v][i], u, z[v][k]);
+        }
+      const cplx d = crecip(E(i, i));
+#pragma unroll
+      for (int v = 0; v < 2; ++v) z[v][i] = cmul(z[v][i], d);
+    }
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+    if (act[v]) {
+#pragma unroll
+      for (int a = 0; a < NSM; ++a)
+        if (a < ns) Xs[v][(int64_t)(fr.col0 + a) * Fc + c.q] = z[v][a];
+    }
+#undef E
 }
 
 // the pivot rows' update part of k_usolve2_level split over S workgroups per (front, frequency group)
@@ -3385,7 +3463,8 @@ void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, i
 
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
                     const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,
-                    const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st, int rl) {
+                    const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st, int rl,
+                    int swz) {
   if (nitems <= 0) return;
   const bool small = maxns <= 8;
   const int rlim = rl % 100, rrows = rl >= 100 ? OFF_RPL : 1;
@@ -3411,7 +3490,7 @@ void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems
   }
   dim3 g((nitems + 3) / 4, ngroups * OFF_G), b(256);
   static_assert(OB >= 8, "the SMALL variant covers pivot blocks of up to 8");
-#define OL(MD, SM) LAUNCH((k_offdiag_level<MD, SM>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid)
+#define OL(MD, SM) LAUNCH((k_offdiag_level<MD, SM>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid, swz)
   if (mode == 0 && small) OL(0, true);
   else if (mode == 0) OL(0, false);
   else if (small) OL(1, true);
@@ -3501,9 +3580,17 @@ void launch_fn_combine(const int* rows, int nrows, const double2* fcoef, double2
 
 void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, bool small, int ngroups,
                     const double2* F, int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0,
-                    const double2* Y1, double2* X1, const int* reach1, hipStream_t st, int split, int small_cfg) {
+                    const double2* Y1, double2* X1, const int* reach1, hipStream_t st, int split, int small_cfg,
+                    int tiny) {
   if (nfronts <= 0) return;
   UPair a{Y0, X0, reach0, skip0}, b{Y1, X1, reach1, nullptr};
+  if (tiny > 0 && split <= 1) {
+    // every pivot block of the level <= tiny (4 or 8): one wave per (front, group)
+    dim3 gt((unsigned)((nfronts + 3) / 4), ngroups), bt(256);
+    if (tiny <= 4) LAUNCH((k_usolve2_tiny<4>), gt, bt, st, P, lvl, nfronts, F, Fc, a, b);
+    else LAUNCH((k_usolve2_tiny<8>), gt, bt, st, P, lvl, nfronts, F, Fc, a, b);
+    return;
+  }
   dim3 g(nfronts, ngroups), bl(64 * W);
   const int rs = split > 1;
   // split > 1: the pivot rows' update part over `split` workgroups per front first (the small-front

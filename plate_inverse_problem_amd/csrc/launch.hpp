@@ -49,7 +49,8 @@ void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int max
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
                     const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,
                     const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st,
-                    int rl = 0);   // rl > 0 (symmetric analyses): levels with 8 < maxns <= rl right-looking (k_offdiag_rl)
+                    int rl = 0,    // rl > 0 (symmetric analyses): levels with 8 < maxns <= rl right-looking (k_offdiag_rl)
+                    int swz = 1);  // 0: no XCD-aware workgroup order
 void launch_schur(bool sym, const DevPattern& P, const int4* tiles, int ntiles, const int* g1, const int* gxp,
                   const int2* gx, int ngroups, double2* F, int64_t Fc, hipStream_t st);
 // symmetric mode, large update blocks: 16 x 16 blocks, operands staged in LDS per workgroup
@@ -83,7 +84,7 @@ void launch_fn_combine(const int* rows, int nrows, const double2* fcoef, double2
 void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, bool small, int ngroups,
                     const double2* F, int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0,
                     const double2* Y1, double2* X1, const int* reach1, hipStream_t st, int split = 1,
-                    int small_cfg = 0);
+                    int small_cfg = 0, int tiny = 0);   // tiny 4 / 8: the level's pivot blocks all <= tiny (k_usolve2_tiny)
 // dependency-driven pass over the narrow top of the elimination tree (one launch, task tickets, per-front
 // completion words): the task list and its words (ticket, done, cnt: 1 + 2 nslots ngroups unsigned,
 // zeroed by the launcher), flags per frequency (a spin timeout sets PFR_FLAG_BAD_PIVOT)

@@ -103,3 +103,18 @@ def test_offdiag_right_looking_bitwise(monkeypatch, lo, hi):
         report(f"offdiag_rl{rl}_{lo}_{hi}", loss_rel=dl, w_rel=dw, fr_rel=dfr, flagged=got[4])
         assert got[4] == 0
         assert dl == 0 and dw == 0 and dfr == 0, (rl, dl, dw, dfr)
+
+
+@pytest.mark.parametrize("lo,hi", [(1024, 1536), (0, 2048)])
+def test_tiny_front_top_down_bitwise(monkeypatch, lo, hi):
+    """k_usolve2_tiny (PFR_US2_TINY: the paired top-down pass one wave per front on the levels whose pivot blocks
+    are at most 4 / 8) performs k_usolve2_level's operations in the same order: identical results."""
+    base = _run(monkeypatch, 0, lo, hi, fac_lds="-1", env={"PFR_US2_TINY": "0"})
+    for tiny in ("4", "8"):
+        got = _run(monkeypatch, 0, lo, hi, fac_lds="-1", env={"PFR_US2_TINY": tiny})
+        dl = abs(got[0] / base[0] - 1)
+        dw = float(np.max(np.abs(got[1] - base[1])) / np.max(np.abs(base[1])))
+        dfr = float(np.max(np.abs(got[2] / base[2] - 1)))
+        report(f"us2_tiny{tiny}_{lo}_{hi}", loss_rel=dl, w_rel=dw, fr_rel=dfr, flagged=got[4])
+        assert got[4] == 0
+        assert dl == 0 and dw == 0 and dfr == 0, (tiny, dl, dw, dfr)

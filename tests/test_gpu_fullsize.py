@@ -185,6 +185,8 @@ def test_c2_forward_sweep_matches_truth():
     {"PFR_OFF_RL": "32"},              # L21 rows right-looking on the levels with pivot blocks of 9-32
     {"PFR_OFF_RL": "16"},
     {"PFR_OFF_RL": "124"},             # ... two rows per wave
+    {"PFR_US2_TINY": "8"},             # paired top-down pass one wave per front where pivot blocks are <= 8
+    {"PFR_US2_TINY": "0"},
 ])
 def test_kernel_variants_match_oracle(env, monkeypatch):
     from oracle.plate_oracle import loss_and_grad
