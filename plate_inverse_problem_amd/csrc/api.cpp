@@ -693,7 +693,8 @@ int sym_top_down_pair(pfr_solver* s, hipStream_t st, bool fwd_all = false) {
                         s->F, s->Fc, s->Y,
                         s->X, s->d_reach[0], fwd_all ? nullptr : s->d_reach[1], s->Y2, s->XA, s->d_reach[1], st,
                         solve_split(s, nf), s->us2_cfg,
-                        s->us2_tiny > 0 && s->level_maxns[l] <= s->us2_tiny ? (s->level_maxns[l] <= 4 ? 4 : 8) : 0);
+                        s->us2_tiny > 0 && s->level_maxns[l] <= s->us2_tiny
+                            ? (s->level_maxns[l] <= 4 ? 4 : s->level_maxns[l] <= 8 ? 8 : s->us2_tiny) : 0);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -942,7 +943,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->scale_corr = knob("PFR_SCALE_CORR", 1, 0, 1);
   s->off_swz_min = knob("PFR_OFF_SWZ_MIN", 0, 0, 1 << 30);
   // 8: the bottom two levels at 2,048 frequencies 685 / 612 -> 509 / 489 us (profiles/r04/experiments/us2_tiny_*)
-  s->us2_tiny = knob("PFR_US2_TINY", 8, 0, 8);
+  s->us2_tiny = knob("PFR_US2_TINY", 8, 0, 64);   // > 8: k_usolve2_wave on the levels with blocks of 9 .. this
   s->off_rl = knob("PFR_OFF_RL", 0, 0, 124);   // n: one row per wave (n = 16, 24, 32); 100 + n: two rows (n = 16, 24)
   if (s->off_rl > 100 && s->off_rl % 100 > 24) s->off_rl = 124;
   s->fuse_asm = knob("PFR_FUSE_ASM", 0, 0, 1);   // measured slower (2,048-frequency chunk: A11 classes 4.1 -> 6.6 ms)

@@ -2015,6 +2015,90 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSM <= 4 ? 
 #undef E
 }
 
+// k_usolve2_tiny for levels whose pivot blocks reach 16: the pivot rows in blocks of KBS (the update-row solution
+// gathered once per block), the sums written to the pivot values in global memory and the U11 backward solve
+// by the same wave from there in KBS blocks -- usolve2_upd's and usolve2_tri's order, so again identical results.
+// One wave per (front, frequency group): the wave's lanes re-read only their own stores (no barrier needed).
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_usolve2_wave(
+    DevPattern P, const int* __restrict__ lvl, int nfronts, const cplx* __restrict__ F, int64_t Fc, UPair A, UPair B) {
+  int bx;
+  const Ctx c = ctx_xcd(bx);
+  const int slot = bx * 4 + c.w;
+  if (slot >= nfronts) return;
+  const int ft = lvl[slot];
+  const bool act[2] = {!A.skip || !A.skip[ft], !B.skip || !B.skip[ft]};
+  const bool live[2] = {!A.reach || A.reach[ft], !B.reach || B.reach[ft]};
+  const cplx* const Ys[2] = {A.Y, B.Y};
+  cplx* const Xs[2] = {A.X, B.X};
+  const Front fr = P.fronts[ft];
+  const int f = fr.f, ns = fr.ns;
+  const cplx* __restrict__ base = F + fr.off * Fc + c.q;
+  const int* __restrict__ ix = P.idx + fr.row0;
+#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+#define XV(v, a) Xs[v][(int64_t)(fr.col0 + (a)) * Fc + c.q]
+  for (int a0 = 0; a0 < ns; a0 += KBS) {
+    cplx acc[2][KBS];
+#pragma unroll
+    for (int a = 0; a < KBS; ++a) acc[0][a] = acc[1][a] = make_double2(0.0, 0.0);
+    for (int b = ns; b < f; ++b) {
+      const int iv = __builtin_amdgcn_readfirstlane(ix[b]);
+      const cplx x0 = Xs[0][(int64_t)iv * Fc + c.q], x1 = Xs[1][(int64_t)iv * Fc + c.q];
+      cplx e[KBS];
+#pragma unroll
+      for (int a = 0; a < KBS; ++a) e[a] = E(b, min(a0 + a, ns - 1));
+#pragma unroll
+      for (int a = 0; a < KBS; ++a) {
+        acc[0][a] = cfms(acc[0][a], e[a], x0);
+        acc[1][a] = cfms(acc[1][a], e[a], x1);
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < KBS; ++a)
+      if (a0 + a < ns) {
+        const cplx urr = E(a0 + a, a0 + a);
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+          if (act[v]) {
+            const cplx y = live[v] ? Ys[v][(int64_t)(fr.col0 + a0 + a) * Fc + c.q] : make_double2(0.0, 0.0);
+            XV(v, a0 + a) = cadd(y, cmul(urr, acc[v][a]));
+          }
+      }
+  }
+  // U11 backward, KBS blocks from the bottom (usolve2_tri with one wave)
+  for (int k1 = ns; k1 > 0; k1 -= KBS) {
+    const int k0 = max(0, k1 - KBS), kb = k1 - k0;
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+      if (act[v]) {
+        cplx x[KBS];
+#pragma unroll
+        for (int t = 0; t < KBS; ++t) x[t] = XV(v, k0 + min(t, kb - 1));
+#pragma unroll
+        for (int i = KBS - 1; i >= 0; --i) {
+          const int ri = k0 + min(i, kb - 1);
+#pragma unroll
+          for (int k = i + 1; k < KBS; ++k) x[i] = cfms(x[i], E(ri, k0 + min(k, kb - 1)), x[k]);
+          x[i] = cscale(cmul(x[i], crecip(E(ri, ri))), i < kb ? 1.0 : 0.0);
+        }
+#pragma unroll
+        for (int t = 0; t < KBS; ++t)
+          if (t < kb) XV(v, k0 + t) = x[t];
+        if (k0 > 0) {
+#pragma unroll
+          for (int t = 0; t < KBS; ++t) x[t] = cscale(x[t], t < kb ? 1.0 : 0.0);
+          for (int i = 0; i < k0; ++i) {
+            cplx y = XV(v, i);
+#pragma unroll
+            for (int t = 0; t < KBS; ++t) y = cfms(y, E(i, k0 + min(t, kb - 1)), x[t]);
+            XV(v, i) = y;
+          }
+        }
+      }
+  }
+#undef E
+#undef XV
+}
+
 // the pivot rows' update part of k_usolve2_level split over S workgroups per (front, frequency group)
 template <bool SYM, int SR, int SK>
 __global__ __launch_bounds__(256) void k_usolve2_upd(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F,
@@ -3588,7 +3672,8 @@ void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, boo
     // every pivot block of the level <= tiny (4 or 8): one wave per (front, group)
     dim3 gt((unsigned)((nfronts + 3) / 4), ngroups), bt(256);
     if (tiny <= 4) LAUNCH((k_usolve2_tiny<4>), gt, bt, st, P, lvl, nfronts, F, Fc, a, b);
-    else LAUNCH((k_usolve2_tiny<8>), gt, bt, st, P, lvl, nfronts, F, Fc, a, b);
+    else if (tiny <= 8) LAUNCH((k_usolve2_tiny<8>), gt, bt, st, P, lvl, nfronts, F, Fc, a, b);
+    else LAUNCH(k_usolve2_wave, gt, bt, st, P, lvl, nfronts, F, Fc, a, b);
     return;
   }
   dim3 g(nfronts, ngroups), bl(64 * W);

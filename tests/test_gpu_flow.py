@@ -110,7 +110,7 @@ def test_tiny_front_top_down_bitwise(monkeypatch, lo, hi):
     """k_usolve2_tiny (PFR_US2_TINY: the paired top-down pass one wave per front on the levels whose pivot blocks
     are at most 4 / 8) performs k_usolve2_level's operations in the same order: identical results."""
     base = _run(monkeypatch, 0, lo, hi, fac_lds="-1", env={"PFR_US2_TINY": "0"})
-    for tiny in ("4", "8"):
+    for tiny in ("4", "8", "16", "32"):   # > 8: k_usolve2_wave
         got = _run(monkeypatch, 0, lo, hi, fac_lds="-1", env={"PFR_US2_TINY": tiny})
         dl = abs(got[0] / base[0] - 1)
         dw = float(np.max(np.abs(got[1] - base[1])) / np.max(np.abs(base[1])))
