@@ -355,8 +355,8 @@ def main():
                             "concurrent_ms_per_step": kms.tolist()},
         "sptrsv_roofline": {"bound": "hbm",
                             "kernel": "k_lsolve_level_z / k_lsolve_rows_z (one bottom-up chain: forward rhs + "
-                                      "the functional's three vectors) + k_usolve2_level / k_usolve2_upd (paired "
-                                      "top-down) + k_fn_combine",
+                                      "the functional's three vectors) + k_usolve2_level / k_usolve2_upd / "
+                                      "k_usolve2_tiny (paired top-down) + k_fn_combine",
                             "achieved": trsv_gbs, "alg_bytes": trsv_bytes, "alg_bytes_per_freq": sb.tolist(),
                             "ms": trsv_ms, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": trsv_gbs / HBM_PEAK_GBS,
                             "traffic": None if trsv_traffic is None else trsv_traffic * n_iso,
