@@ -3551,8 +3551,8 @@ void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems
                     int swz) {
   if (nitems <= 0) return;
   const bool small = maxns <= 8;
-  const int rlim = rl % 100, rrows = rl >= 100 ? OFF_RPL : 1;
-  if (rlim > 0 && !small && maxns <= rlim) {
+  const int rlim = OFF_G == 1 ? rl % 100 : 0, rrows = rl >= 100 ? OFF_RPL : 1;
+  if constexpr (OFF_G == 1) if (rlim > 0 && !small && maxns <= rlim) {
     // right-looking rows (symmetric analyses): rl = n (one row per wave) or 100 + n (an item's rows per wave)
     dim3 g((unsigned)(((int64_t)nitems * (OFF_RPL / rrows) + 3) / 4), ngroups), b(256);
 #define RL(MD, N, RR) LAUNCH((k_offdiag_rl<MD, N, RR>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid)
