@@ -60,6 +60,8 @@ struct pfr_solver {
   int32_t* d_level_fronts = nullptr;
   int4* d_tiles = nullptr;              // Schur tiles (front, i0, j0, 0), grouped by level
   int4* d_items = nullptr;              // off-diagonal panel items (front, first row/col, kind, record offset)
+  int4* d_shu = nullptr;                // k_offdiag_shu tasks (first item in the level, count <= 4, front, -)
+  std::vector<int32_t> shu_ptr;         // per level: first task
   int2* d_orec = nullptr;               // per item x lane group x pivot: (nz, first child source) of the entry
   int32_t* d_oxp = nullptr;             // per item: range of further child sources in d_ox
   int2* d_ox = nullptr;                 // (pivot * OFF_G OFF_RPL + row slot, element id)
@@ -156,6 +158,7 @@ struct pfr_solver {
   double2 *mscale = nullptr, *cpart = nullptr;     // mscale complex: the solve-error scale (k_correct_finish)
   int scale_corr = 1;
   int us2_tiny = 8;                     // PFR_US2_TINY (4 / 8): levels whose pivot blocks are <= this, one wave per front
+  int off_shu = 0;                      // PFR_OFF_SHU: L21 launches with fewer (item, group) waves share U11 via LDS
   int off_swz_min = 0;                  // PFR_OFF_SWZ_MIN: L21 launches with fewer (item, group) waves keep the hardware order
   int off_rl = 0;                       // PFR_OFF_RL: L21 rows right-looking on levels with pivot blocks <= this (16-32)                   // PFR_SCALE_CORR: the solve-error scale of the loss sweeps' cotangent
   int32_t* flags = nullptr;
@@ -400,7 +403,11 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     pfr::launch_offdiag(mode, s->P, s->d_items + s->item_ptr[l], s->item_ptr[l + 1] - s->item_ptr[l], s->d_orec,
                         s->d_oxp + s->item_ptr[l], s->d_ox, ngroups, s->F, s->Fc, s->freqs, s->K, s->M, data, ds,
                         nvalid, s->off_small ? s->level_maxns[l] : pfr::MAX_FRONT, st, s->sym ? s->off_rl : 0,
-                        (int64_t)(s->item_ptr[l + 1] - s->item_ptr[l]) * ngroups >= s->off_swz_min);
+                        (int64_t)(s->item_ptr[l + 1] - s->item_ptr[l]) * ngroups >= s->off_swz_min,
+                        s->sym && s->off_shu > 0 && !s->shu_ptr.empty() &&
+                                (int64_t)(s->item_ptr[l + 1] - s->item_ptr[l]) * ngroups < s->off_shu
+                            ? s->d_shu + s->shu_ptr[l] : nullptr,
+                        s->shu_ptr.empty() ? 0 : s->shu_ptr[l + 1] - s->shu_ptr[l]);
     if (after_panel) after_panel(l);
     mark(l, 3);
     pfr::launch_schur_blk(s->schur_bc, s->P, s->d_blocks + s->blk_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
@@ -942,6 +949,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);
   s->scale_corr = knob("PFR_SCALE_CORR", 1, 0, 1);
   s->off_swz_min = knob("PFR_OFF_SWZ_MIN", 0, 0, 1 << 30);
+  s->off_shu = knob("PFR_OFF_SHU", 0, 0, 1 << 30);
   // 8: the bottom two levels at 2,048 frequencies 685 / 612 -> 509 / 489 us (profiles/r04/experiments/us2_tiny_*)
   s->us2_tiny = knob("PFR_US2_TINY", 8, 0, 64);   // > 8: k_usolve2_wave on the levels with blocks of 9 .. this
   s->off_rl = knob("PFR_OFF_RL", 0, 0, 124);   // n: one row per wave (n = 16, 24, 32); 100 + n: two rows (n = 16, 24)
@@ -1244,6 +1252,22 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
         (rc = s->up(&s->d_items, iv)) || (rc = s->up(&s->d_orec, orec)) || (rc = s->up(&s->d_oxp, oxp)) ||
         (rc = s->up(&s->d_ox, ox)) || (rc = s->up(&s->d_rec0, rec0)))
       return bail(rc);
+    if (sym) {
+      // k_offdiag_shu workgroup tasks per level: (first item relative to the level, items <= 4), one front each
+      std::vector<int4> sh;
+      s->shu_ptr.assign(1, 0);
+      for (int l = 0; l < L; ++l) {
+        for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
+          const int t = S.level_fronts[e];
+          const int end = e + 1 < S.level_ptr[l + 1] ? item_begin[S.level_fronts[e + 1]] : s->item_ptr[l + 1];
+          for (int i = item_begin[t]; i < end; i += 4)
+            sh.push_back(make_int4(i - s->item_ptr[l], std::min(4, end - i), t, 0));
+        }
+        s->shu_ptr.push_back((int32_t)sh.size());
+      }
+      if (sh.empty()) sh.push_back(make_int4(0, 0, 0, 0));
+      if ((rc = s->up(&s->d_shu, sh))) return bail(rc);
+    }
     if (s->fflow_lcut < L) {
       // task list of the factorisation flow, levels upwards: per level the A11 tasks, then 16-item L21 tasks,
       // then one task per update block

@@ -898,6 +898,144 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMALL ? 5 :
   offdiag_item<MODE, SMALL>(P, items, wid, orec, oxp, ox, F, Fc, freqs, K, M, data, data_stride, nvalid, by);
 }
 
+// L21 rows with U11 shared through LDS (symmetric analyses, the narrow levels; PFR_OFF_SHU): a workgroup = four
+// waves on up to four consecutive items (two rows each) of ONE front, same frequency group.  k_offdiag_level's
+// waves each load the front's U11 for their own two rows; on the top levels, where a front's items are few and
+// their U11 reads are served by L2, that makes the per-CU L2 load rate the bound.  Here every U11 value of the
+// left-looking prefix is loaded once per workgroup -- in stages of SHU_ST pivot rows x 8 columns, wave w staging
+// row w of the stage through registers into a double-buffered LDS image one stage ahead -- and read by the four
+// waves from LDS.  Sources, prefix order (ascending pivot), chunk triangle and stores are k_offdiag_level's: the
+// results are identical bit for bit.
+constexpr int SHU_ST = 4;   // pivot rows per stage (= waves per workgroup)
+template <int MODE>
+__global__ __launch_bounds__(256) void k_offdiag_shu(DevPattern P, const int4* __restrict__ items,
+                                                     const int4* __restrict__ tasks, int ntasks,
+                                                     const int2* __restrict__ orec, const int* __restrict__ oxp,
+                                                     const int2* __restrict__ ox, cplx* __restrict__ F, int64_t Fc,
+                                                     const double* __restrict__ freqs, const cplx* __restrict__ K,
+                                                     const double* __restrict__ M, const cplx* __restrict__ data,
+                                                     int64_t data_stride, int nvalid) {
+  static_assert(OFF_G == 1 && OB == 8, "one lane = one frequency, chunks of 8 pivots");
+  __shared__ cplx Ub[2][SHU_ST][8][64];       // 64 KiB: two stages of 4 pivot rows x 8 columns x 64 frequencies
+  const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
+  const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int4 task = tasks[bx];
+  const bool active = w < task.y;
+  const int wid = task.x + min(w, task.y - 1);
+  const int64_t q = (int64_t)by * 64 + lane;
+  const int4 it = items[wid];
+  const Front fr = P.fronts[it.x];
+  const int f = fr.f, ns = fr.ns;
+  cplx* __restrict__ base = F + fr.off * Fc + q;
+  OffSrc S;
+  int64_t so[OFF_RPL];
+  bool valid[OFF_RPL];
+#pragma unroll
+  for (int h = 0; h < OFF_RPL; ++h) {
+    const int idx = it.y + h;
+    valid[h] = active && idx < f;
+    so[h] = (int64_t)min(idx, f - 1) * f;
+    S.rec[h] = orec + it.w + (int64_t)h * ns;
+  }
+  S.ox = ox;
+  S.ox0 = oxp[wid];
+  S.ox1 = oxp[wid + 1];
+  S.slot0 = 0;
+  S.om2 = 0.0;
+  if (MODE == 0) {
+    const double om = 6.283185307179586 * freqs[q];
+    S.om2 = om * om;
+  }
+  S.K = K;
+  S.M = M;
+  S.dq = data + min(q, (int64_t)nvalid - 1) * data_stride;
+#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+  for (int c0 = 0; c0 < ns; c0 += 8) {
+    const int nb = min(8, ns - c0);
+    cplx x[OFF_RPL][8];
+#pragma unroll
+    for (int h = 0; h < OFF_RPL; ++h)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[h][j] = off_source<MODE>(S, F, Fc, q, h, c0 + min(j, nb - 1));
+    for (int e = S.ox0; e < S.ox1; ++e) {
+      const int2 g = S.ox[e];
+      const int c = g.x / OFF_RPL - c0, slot = g.x % OFF_RPL;
+      if (c >= 0 && c < nb) {
+        const cplx v = F[(int64_t)g.y * Fc + q];
+#pragma unroll
+        for (int h = 0; h < OFF_RPL; ++h)
+          if (slot == h) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              if (j == c) x[h][j] = cadd(x[h][j], v);
+          }
+      }
+    }
+    // prefix: x -= own(0:c0) * U(0:c0, c0:c0+8), U staged SHU_ST pivot rows at a time
+    const int nst = (c0 + SHU_ST - 1) / SHU_ST;
+    cplx st[8];
+    if (nst > 0) {
+      const int t = min(w, c0 - 1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) st[j] = E(t, c0 + min(j, nb - 1));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Ub[0][w][j][lane] = st[j];
+      __syncthreads();
+    }
+    for (int s = 0; s < nst; ++s) {
+      const bool more = s + 1 < nst;
+      if (more) {
+        const int t = min((s + 1) * SHU_ST + w, c0 - 1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) st[j] = E(t, c0 + min(j, nb - 1));
+      }
+#pragma unroll
+      for (int tt = 0; tt < SHU_ST; ++tt) {
+        const int t = s * SHU_ST + tt;
+        if (t < c0) {
+          cplx l[OFF_RPL], u[8];
+#pragma unroll
+          for (int h = 0; h < OFF_RPL; ++h) l[h] = base[(so[h] + t) * Fc];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) u[j] = Ub[s & 1][tt][j][lane];
+#pragma unroll
+          for (int h = 0; h < OFF_RPL; ++h)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) x[h][j] = cfms(x[h][j], l[h], u[j]);
+        }
+      }
+      if (more) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) Ub[(s + 1) & 1][w][j][lane] = st[j];
+      }
+      __syncthreads();
+    }
+    // the chunk's own triangle, column by column
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (j < nb) {
+#pragma unroll
+        for (int a = 0; a < j; ++a) {
+          const cplx t = E(c0 + a, c0 + j);
+#pragma unroll
+          for (int h = 0; h < OFF_RPL; ++h) x[h][j] = cfms(x[h][j], x[h][a], t);
+        }
+        const cplx d = crecip(E(c0 + j, c0 + j));
+#pragma unroll
+        for (int h = 0; h < OFF_RPL; ++h) x[h][j] = cmul(x[h][j], d);
+      }
+#pragma unroll
+    for (int h = 0; h < OFF_RPL; ++h)
+      if (valid[h]) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (j < nb) base[(so[h] + c0 + j) * Fc] = x[h][j];
+      }
+  }
+#undef E
+}
+
 // Right-looking L21 rows for the levels whose pivot blocks are at most NSM (symmetric analyses: kind-0 items
 // only): one wave = ONE row x 64 frequencies (the two rows of an item on two waves), the whole row in
 // registers.  k_offdiag_level is left-looking: every chunk of OB columns re-loads the row's own earlier L21
@@ -3548,9 +3686,15 @@ void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, i
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
                     const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,
                     const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st, int rl,
-                    int swz) {
+                    int swz, const int4* shu, int nshu) {
   if (nitems <= 0) return;
   const bool small = maxns <= 8;
+  if constexpr (OFF_G == 1 && OB == 8) if (shu && nshu > 0 && !small) {
+    dim3 gs((unsigned)nshu, ngroups), bs(256);
+    if (mode == 0) LAUNCH((k_offdiag_shu<0>), gs, bs, st, P, items, shu, nshu, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid);
+    else LAUNCH((k_offdiag_shu<1>), gs, bs, st, P, items, shu, nshu, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid);
+    return;
+  }
   const int rlim = OFF_G == 1 ? rl % 100 : 0, rrows = rl >= 100 ? OFF_RPL : 1;
   if constexpr (OFF_G == 1) if (rlim > 0 && !small && maxns <= rlim) {
     // right-looking rows (symmetric analyses): rl = n (one row per wave) or 100 + n (an item's rows per wave)

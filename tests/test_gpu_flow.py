@@ -118,3 +118,18 @@ def test_tiny_front_top_down_bitwise(monkeypatch, lo, hi):
         report(f"us2_tiny{tiny}_{lo}_{hi}", loss_rel=dl, w_rel=dw, fr_rel=dfr, flagged=got[4])
         assert got[4] == 0
         assert dl == 0 and dw == 0 and dfr == 0, (tiny, dl, dw, dfr)
+
+
+@pytest.mark.parametrize("lo,hi", [(1024, 1536), (0, 2048)])
+def test_offdiag_shared_u11_bitwise(monkeypatch, lo, hi):
+    """k_offdiag_shu (PFR_OFF_SHU: L21 rows with U11 staged once per workgroup in LDS, on the levels with fewer
+    (item, group) waves than the knob) performs k_offdiag_level's operations in the same order: identical."""
+    base = _run(monkeypatch, 0, lo, hi, fac_lds="-1", env={"PFR_OFF_SHU": "0"})
+    for shu in ("4096", "1000000000"):
+        got = _run(monkeypatch, 0, lo, hi, fac_lds="-1", env={"PFR_OFF_SHU": shu})
+        dl = abs(got[0] / base[0] - 1)
+        dw = float(np.max(np.abs(got[1] - base[1])) / np.max(np.abs(base[1])))
+        dfr = float(np.max(np.abs(got[2] / base[2] - 1)))
+        report(f"offdiag_shu{shu}_{lo}_{hi}", loss_rel=dl, w_rel=dw, fr_rel=dfr, flagged=got[4])
+        assert got[4] == 0
+        assert dl == 0 and dw == 0 and dfr == 0, (shu, dl, dw, dfr)
