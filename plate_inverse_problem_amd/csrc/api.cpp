@@ -232,6 +232,8 @@ struct pfr_solver {
   double* gind = nullptr;               // per 64-frequency group: largest |correction| / |fr| of the chunk
   int32_t* glist = nullptr;             // the groups whose adjoint is refined (REFINE_CAP, -1: none)
   double2* Gx = nullptr;                // the fr seed of the forward solution (support rows; zero elsewhere)
+  unsigned long long* wtrace = nullptr;   // pfr_debug_wave_trace buffer (4 x u64 per wave)
+  int64_t wtrace_cap = 0;
   double* berr_out = nullptr;
   double* d_berr_acc = nullptr;
 
@@ -1557,6 +1559,28 @@ int pfr_debug_solution(pfr_solver* s, int32_t which, int32_t q, double* out) {
     out[2 * (int64_t)s->perm[p]] = col[p].x;
     out[2 * (int64_t)s->perm[p] + 1] = col[p].y;
   }
+  return PFR_OK;
+}
+
+int pfr_debug_wave_trace(pfr_solver* s, int64_t cap, uint64_t* out_host, int64_t* count) {
+  if (!s || cap < 0 || (cap > 0 && !out_host) || !count) return fail(PFR_ERR_ARG, "bad wave-trace arguments");
+  HIP_TRY(hipSetDevice(s->device));
+  HIP_TRY(hipDeviceSynchronize());
+  if (cap == 0) {             // start: a device buffer of *count records for the following launches
+    if (s->wtrace) HIP_TRY(hipFree(s->wtrace));
+    s->wtrace = nullptr;
+    s->wtrace_cap = *count;
+    if (s->wtrace_cap > 0) {
+      HIP_TRY(hipMalloc(&s->wtrace, (size_t)s->wtrace_cap * 32));
+      HIP_TRY(hipMemset(s->wtrace, 0, (size_t)s->wtrace_cap * 32));
+    }
+    if (pfr::set_wave_trace(s->wtrace, s->wtrace_cap)) return fail(PFR_ERR_HIP, "wave trace symbols");
+    return PFR_OK;
+  }
+  const int64_t n = std::min<int64_t>(std::min<int64_t>(pfr::wave_trace_count(), s->wtrace_cap), cap);
+  if (n > 0) HIP_TRY(hipMemcpy(out_host, s->wtrace, (size_t)n * 32, hipMemcpyDeviceToHost));
+  *count = n;
+  pfr::set_wave_trace(nullptr, 0);
   return PFR_OK;
 }
 

@@ -57,6 +57,31 @@ constexpr int KBS = PFR_KBS;   // triangular-solve block (its lower triangle: 28
 // the 8 XCDs (each with its own L2), so workgroup `orig` is renumbered such that
 // every XCD receives one contiguous range of logical ids (bijective for any
 // count; MI355X_MICROARCH.md, workgroup dispatch / T1 swizzle).  Speed only.
+#ifndef PFR_WTRACE
+#define PFR_WTRACE 0   // build-time: make EXTRA=-DPFR_WTRACE=1 (the timestamps cost the L21 kernel registers)
+#endif
+// Wave trace (diagnostic, pfr_debug_wave_trace): per wave of the traced launches (start, end) of the 100 MHz
+// real-time counter and the hardware id.  The host sets the buffer and, before each traced launch, the index of
+// its first record (record = base + linear workgroup x 4 + wave: no atomics); lane 0 stores.
+__device__ unsigned long long* g_wtrace = nullptr;
+__device__ long long g_wtrace_base = 0;
+__device__ long long g_wtrace_cap = 0;
+__device__ long long g_wtrace_launch = 0;
+__device__ __forceinline__ void wtrace_end(unsigned long long t0, int tag) {
+  unsigned long long* b = g_wtrace;
+  if (!b) return;
+  const long long i = g_wtrace_base + ((long long)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) +
+                      (threadIdx.x >> 6);
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_REG_HW_ID
+  if ((threadIdx.x & 63) == 0 && i < g_wtrace_cap) {
+    b[4 * i] = t0;
+    b[4 * i + 1] = t1;
+    b[4 * i + 2] = hw;
+    b[4 * i + 3] = (unsigned long long)tag | ((unsigned long long)g_wtrace_launch << 40);
+  }
+}
+
 __device__ __forceinline__ int64_t xcd_swizzle(int64_t orig, int64_t nwg) {
   const int64_t q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
@@ -889,13 +914,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMALL ? 5 :
                                                         const double* __restrict__ freqs, const cplx* __restrict__ K,
                                                         const double* __restrict__ M, const cplx* __restrict__ data,
                                                         int64_t data_stride, int nvalid, int swz) {
+#if PFR_WTRACE
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+#endif
   // swz: XCD-aware order (a frequency group's items on one XCD, sharing its L2); 0: the hardware's round-robin
   const int64_t o = blockIdx.x + (int64_t)gridDim.x * blockIdx.y;
   const int64_t lid = swz ? xcd_swizzle(o, (int64_t)gridDim.x * gridDim.y) : o;
   const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
   const int wid = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
-  if (wid >= nitems) return;
-  offdiag_item<MODE, SMALL>(P, items, wid, orec, oxp, ox, F, Fc, freqs, K, M, data, data_stride, nvalid, by);
+  if (wid < nitems)
+    offdiag_item<MODE, SMALL>(P, items, wid, orec, oxp, ox, F, Fc, freqs, K, M, data, data_stride, nvalid, by);
+#if PFR_WTRACE
+  wtrace_end(t0, wid < nitems ? 1 + (wid << 4) : 0);
+#endif
 }
 
 // L21 rows with U11 shared through LDS (symmetric analyses, the narrow levels; PFR_OFF_SHU): a workgroup = four
@@ -3683,6 +3714,28 @@ void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, i
   else LAUNCH(k_factor_level<true>, dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
 }
 
+static long long h_wtrace_base = 0, h_wtrace_cap = 0, h_wtrace_launch = 0;
+int set_wave_trace(unsigned long long* buf, long long cap) {
+  h_wtrace_base = 0;
+  h_wtrace_launch = 0;
+  h_wtrace_cap = buf ? cap : 0;
+  long long zero = 0;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_wtrace), &buf, sizeof(buf)) != hipSuccess) return -1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_wtrace_cap), &h_wtrace_cap, sizeof(long long)) != hipSuccess) return -1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_wtrace_base), &zero, sizeof(long long)) != hipSuccess) return -1;
+  return 0;
+}
+long long wave_trace_count() { return h_wtrace_base; }
+// before a traced launch of `waves` waves: its records start at the running base
+static void wtrace_launch(long long waves, hipStream_t st) {
+  if (!h_wtrace_cap) return;
+  (void)hipStreamSynchronize(st);     // diagnostic runs only: the previous traced launch has read the old base
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wtrace_base), &h_wtrace_base, sizeof(long long));
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wtrace_launch), &h_wtrace_launch, sizeof(long long));
+  h_wtrace_base += waves;
+  ++h_wtrace_launch;
+}
+
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
                     const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,
                     const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st, int rl,
@@ -3717,6 +3770,7 @@ void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems
     return;
   }
   dim3 g((nitems + 3) / 4, ngroups * OFF_G), b(256);
+  wtrace_launch((long long)g.x * g.y * 4, st);
   static_assert(OB >= 8, "the SMALL variant covers pivot blocks of up to 8");
 #define OL(MD, SM) LAUNCH((k_offdiag_level<MD, SM>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid, swz)
   if (mode == 0 && small) OL(0, true);

@@ -46,6 +46,9 @@ void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, i
 void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int maxns, int qf, double2* F, int64_t Fc,
                        int* flags, hipStream_t st);
 // Schur complement A22 -= L21 U12 for a level's tile list (TM x TN = 4 x 4 tiles)
+// wave trace of the L21 launches (diagnostic): 4 x u64 per wave (start, end, HW_ID, tag = 1 + 16 item | 0 idle)
+int set_wave_trace(unsigned long long* buf, long long cap);
+long long wave_trace_count();
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
                     const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,
                     const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st,
