@@ -768,7 +768,7 @@ __device__ __forceinline__ cplx off_source(const OffSrc& S, const cplx* __restri
 // One chunk of NB consecutive columns (kind 0) / rows (kind 1) c0 .. c0+NB-1 of
 // this lane's OFF_RPL rows (columns); the shared L11 / U11 values each step loads
 // serve all of them.
-template <int MODE, int NB, bool PRE = true>
+template <int MODE, int NB, bool PRE = true, int PU = 2>
 __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int64_t (&so)[OFF_RPL], int64_t sc,
                                               int64_t sa, int64_t sb, bool unit, const bool (&valid)[OFF_RPL],
                                               int c0, const OffSrc& S, const cplx* __restrict__ F, int64_t Fc,
@@ -792,9 +792,30 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
         }
     }
   }
-  // x -= own(0:c0) * shared(0:c0, c0:c0+NB)   (PRE = false: c0 = 0, no prefix)
+  // x -= own(0:c0) * shared(0:c0, c0:c0+NB)   (PRE = false: c0 = 0, no prefix); PU > 2: batches of PU pivots
+  // whose loads are all issued before their products (the same products in the same order)
+  int t0 = 0;
+  if (PU > 2 && PRE) {
+    for (; t0 + PU <= c0; t0 += PU) {
+      cplx l[PU][OFF_RPL], u[PU][NB];
+#pragma unroll
+      for (int k = 0; k < PU; ++k) {
+#pragma unroll
+        for (int h = 0; h < OFF_RPL; ++h) l[k][h] = base[(so[h] + (int64_t)(t0 + k) * sc) * Fc];
+#pragma unroll
+        for (int j = 0; j < NB; ++j) u[k][j] = base[((int64_t)(t0 + k) * sa + (int64_t)(c0 + j) * sb) * Fc];
+      }
+      __builtin_amdgcn_sched_group_barrier(0x020, PU * (OFF_RPL + NB), 0);   // every load of the batch first
+#pragma unroll
+      for (int k = 0; k < PU; ++k)
+#pragma unroll
+        for (int h = 0; h < OFF_RPL; ++h)
+#pragma unroll
+          for (int j = 0; j < NB; ++j) x[h][j] = cfms(x[h][j], l[k][h], u[k][j]);
+    }
+  }
 #pragma unroll 2
-  for (int t = 0; t < (PRE ? c0 : 0); ++t) {
+  for (int t = t0; t < (PRE ? c0 : 0); ++t) {
     cplx l[OFF_RPL], u[NB];
 #pragma unroll
     for (int h = 0; h < OFF_RPL; ++h) l[h] = base[(so[h] + (int64_t)t * sc) * Fc];
@@ -840,7 +861,7 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
 // load chain, which more resident waves overlap.
 // One item (OFF_G OFF_RPL rows / columns of a front) of the panel for the frequency group `by`: the wave's
 // own work, no barrier
-template <int MODE, bool SMALL>
+template <int MODE, bool SMALL, int PU = 2>
 __device__ __forceinline__ void offdiag_item(const DevPattern& P, const int4* __restrict__ items, int wid,
                                              const int2* __restrict__ orec, const int* __restrict__ oxp,
                                              const int2* __restrict__ ox, cplx* __restrict__ F, int64_t Fc,
@@ -894,10 +915,10 @@ __device__ __forceinline__ void offdiag_item(const DevPattern& P, const int4* __
     return;
   }
   int c0 = 0;
-  for (; c0 + OB <= ns; c0 += OB) offdiag_chunk<MODE, OB>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q);
+  for (; c0 + OB <= ns; c0 += OB) offdiag_chunk<MODE, OB, true, PU>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q);
   switch (ns - c0) {     // wave-uniform tail width
 #define TAIL(n) \
-  case n: offdiag_chunk<MODE, n>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q); break;
+  case n: offdiag_chunk<MODE, n, true, PU>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q); break;
     TAIL(1) TAIL(2) TAIL(3) TAIL(4) TAIL(5) TAIL(6) TAIL(7)
 #if PFR_OB > 8
     TAIL(8) TAIL(9) TAIL(10) TAIL(11) TAIL(12) TAIL(13) TAIL(14) TAIL(15)
@@ -907,7 +928,7 @@ __device__ __forceinline__ void offdiag_item(const DevPattern& P, const int4* __
   }
 }
 
-template <int MODE, bool SMALL>
+template <int MODE, bool SMALL, int PU = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMALL ? 5 : 1))) void k_offdiag_level(DevPattern P, const int4* __restrict__ items, int nitems,
                                                         const int2* __restrict__ orec, const int* __restrict__ oxp,
                                                         const int2* __restrict__ ox, cplx* __restrict__ F, int64_t Fc,
@@ -923,7 +944,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMALL ? 5 :
   const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
   const int wid = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (wid < nitems)
-    offdiag_item<MODE, SMALL>(P, items, wid, orec, oxp, ox, F, Fc, freqs, K, M, data, data_stride, nvalid, by);
+    offdiag_item<MODE, SMALL, PU>(P, items, wid, orec, oxp, ox, F, Fc, freqs, K, M, data, data_stride, nvalid, by);
 #if PFR_WTRACE
   wtrace_end(t0, wid < nitems ? 1 + (wid << 4) : 0);
 #endif
@@ -3739,7 +3760,7 @@ static void wtrace_launch(long long waves, hipStream_t st) {
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
                     const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,
                     const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st, int rl,
-                    int swz, const int4* shu, int nshu) {
+                    int swz, const int4* shu, int nshu, int pu) {
   if (nitems <= 0) return;
   const bool small = maxns <= 8;
   if constexpr (OFF_G == 1 && OB == 8) if (shu && nshu > 0 && !small) {
@@ -3773,6 +3794,15 @@ void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems
   wtrace_launch((long long)g.x * g.y * 4, st);
   static_assert(OB >= 8, "the SMALL variant covers pivot blocks of up to 8");
 #define OL(MD, SM) LAUNCH((k_offdiag_level<MD, SM>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid, swz)
+  // pu > 2: the prefix loop with pu pivots' loads in flight (narrow levels, where few waves are resident)
+  if (!small && mode == 0 && pu >= 8) {
+    LAUNCH((k_offdiag_level<0, false, 8>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid, swz);
+    return;
+  }
+  if (!small && mode == 0 && pu >= 4) {
+    LAUNCH((k_offdiag_level<0, false, 4>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid, swz);
+    return;
+  }
   if (mode == 0 && small) OL(0, true);
   else if (mode == 0) OL(0, false);
   else if (small) OL(1, true);

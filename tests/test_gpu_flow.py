@@ -133,3 +133,18 @@ def test_offdiag_shared_u11_bitwise(monkeypatch, lo, hi):
         report(f"offdiag_shu{shu}_{lo}_{hi}", loss_rel=dl, w_rel=dw, fr_rel=dfr, flagged=got[4])
         assert got[4] == 0
         assert dl == 0 and dw == 0 and dfr == 0, (shu, dl, dw, dfr)
+
+
+@pytest.mark.parametrize("lo,hi", [(1024, 1536), (0, 2048)])
+def test_offdiag_prefix_batches_bitwise(monkeypatch, lo, hi):
+    """PFR_OFF_PU: the L21 prefix loop in batches of 4 / 8 pivots whose loads are issued first (on the launches
+    with fewer waves than PFR_OFF_PU_WAVES) -- the same products in the same order: identical results."""
+    base = _run(monkeypatch, 0, lo, hi, fac_lds="-1", env={"PFR_OFF_PU_WAVES": "0"})
+    for pu in ("4", "8"):
+        got = _run(monkeypatch, 0, lo, hi, fac_lds="-1", env={"PFR_OFF_PU": pu, "PFR_OFF_PU_WAVES": "1000000000"})
+        dl = abs(got[0] / base[0] - 1)
+        dw = float(np.max(np.abs(got[1] - base[1])) / np.max(np.abs(base[1])))
+        dfr = float(np.max(np.abs(got[2] / base[2] - 1)))
+        report(f"offdiag_pu{pu}_{lo}_{hi}", loss_rel=dl, w_rel=dw, fr_rel=dfr, flagged=got[4])
+        assert got[4] == 0
+        assert dl == 0 and dw == 0 and dfr == 0, (pu, dl, dw, dfr)
