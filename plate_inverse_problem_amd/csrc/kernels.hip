@@ -67,7 +67,21 @@ __device__ unsigned long long* g_wtrace = nullptr;
 __device__ long long g_wtrace_base = 0;
 __device__ long long g_wtrace_cap = 0;
 __device__ long long g_wtrace_launch = 0;
-__device__ __forceinline__ void wtrace_end(unsigned long long t0, int tag) {
+// phase clocks of the traced L21 waves (PFR_WTRACE builds): sources, prefix, triangle + stores, each closed by a
+// wait for the wave's outstanding memory operations (the waits serialise what the kernel otherwise overlaps)
+struct WPhase {
+  unsigned long long t, src, pre, tri;
+};
+__device__ __forceinline__ void wphase(WPhase* w, unsigned long long WPhase::*acc) {
+#if PFR_WTRACE
+  if (!w) return;
+  __builtin_amdgcn_s_waitcnt(0);
+  const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+  w->*acc += now - w->t;
+  w->t = now;
+#endif
+}
+__device__ __forceinline__ void wtrace_end(unsigned long long t0, int tag, const WPhase* ph = nullptr) {
   unsigned long long* b = g_wtrace;
   if (!b) return;
   const long long i = g_wtrace_base + ((long long)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) +
@@ -77,7 +91,7 @@ __device__ __forceinline__ void wtrace_end(unsigned long long t0, int tag) {
   if ((threadIdx.x & 63) == 0 && i < g_wtrace_cap) {
     b[4 * i] = t0;
     b[4 * i + 1] = t1;
-    b[4 * i + 2] = hw;
+    b[4 * i + 2] = ph ? ((ph->src & 0xFFFFFFFFull) << 32) | (ph->pre & 0xFFFFFFFFull) : (unsigned long long)hw;
     b[4 * i + 3] = (unsigned long long)tag | ((unsigned long long)g_wtrace_launch << 40);
   }
 }
@@ -772,7 +786,7 @@ template <int MODE, int NB, bool PRE = true, int PU = 2>
 __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int64_t (&so)[OFF_RPL], int64_t sc,
                                               int64_t sa, int64_t sb, bool unit, const bool (&valid)[OFF_RPL],
                                               int c0, const OffSrc& S, const cplx* __restrict__ F, int64_t Fc,
-                                              int64_t q) {
+                                              int64_t q, WPhase* wp = nullptr) {
   cplx x[OFF_RPL][NB];
 #pragma unroll
   for (int h = 0; h < OFF_RPL; ++h)
@@ -792,6 +806,7 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
         }
     }
   }
+  wphase(wp, &WPhase::src);
   // x -= own(0:c0) * shared(0:c0, c0:c0+NB)   (PRE = false: c0 = 0, no prefix); PU > 2: batches of PU pivots
   // whose loads are all issued before their products (the same products in the same order)
   int t0 = 0;
@@ -826,6 +841,7 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
 #pragma unroll
       for (int j = 0; j < NB; ++j) x[h][j] = cfms(x[h][j], l[h], u[j]);
   }
+  wphase(wp, &WPhase::pre);
   // triangular block shared(c0:c0+NB, c0:c0+NB), column by column
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
@@ -848,6 +864,7 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
 #pragma unroll
       for (int j = 0; j < NB; ++j) base[(so[h] + (int64_t)(c0 + j) * sc) * Fc] = x[h][j];
     }
+  wphase(wp, &WPhase::tri);
 }
 
 // Item = (front, first row / column, kind, record offset): one wave = 64 / OFF_G
@@ -862,7 +879,7 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
 // One item (OFF_G OFF_RPL rows / columns of a front) of the panel for the frequency group `by`: the wave's
 // own work, no barrier
 template <int MODE, bool SMALL, int PU = 2>
-__device__ __forceinline__ void offdiag_item(const DevPattern& P, const int4* __restrict__ items, int wid,
+__device__ __forceinline__ void offdiag_item(WPhase* wp, const DevPattern& P, const int4* __restrict__ items, int wid,
                                              const int2* __restrict__ orec, const int* __restrict__ oxp,
                                              const int2* __restrict__ ox, cplx* __restrict__ F, int64_t Fc,
                                              const double* __restrict__ freqs, const cplx* __restrict__ K,
@@ -915,10 +932,10 @@ __device__ __forceinline__ void offdiag_item(const DevPattern& P, const int4* __
     return;
   }
   int c0 = 0;
-  for (; c0 + OB <= ns; c0 += OB) offdiag_chunk<MODE, OB, true, PU>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q);
+  for (; c0 + OB <= ns; c0 += OB) offdiag_chunk<MODE, OB, true, PU>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q, wp);
   switch (ns - c0) {     // wave-uniform tail width
 #define TAIL(n) \
-  case n: offdiag_chunk<MODE, n, true, PU>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q); break;
+  case n: offdiag_chunk<MODE, n, true, PU>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q, wp); break;
     TAIL(1) TAIL(2) TAIL(3) TAIL(4) TAIL(5) TAIL(6) TAIL(7)
 #if PFR_OB > 8
     TAIL(8) TAIL(9) TAIL(10) TAIL(11) TAIL(12) TAIL(13) TAIL(14) TAIL(15)
@@ -943,10 +960,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMALL ? 5 :
   const int64_t lid = swz ? xcd_swizzle(o, (int64_t)gridDim.x * gridDim.y) : o;
   const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
   const int wid = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
-  if (wid < nitems)
-    offdiag_item<MODE, SMALL, PU>(P, items, wid, orec, oxp, ox, F, Fc, freqs, K, M, data, data_stride, nvalid, by);
 #if PFR_WTRACE
-  wtrace_end(t0, wid < nitems ? 1 + (wid << 4) : 0);
+  WPhase ph{t0, 0, 0, 0};
+  WPhase* wp = &ph;
+#else
+  WPhase* wp = nullptr;
+#endif
+  if (wid < nitems)
+    offdiag_item<MODE, SMALL, PU>(wp, P, items, wid, orec, oxp, ox, F, Fc, freqs, K, M, data, data_stride, nvalid, by);
+#if PFR_WTRACE
+  wtrace_end(t0, wid < nitems ? 1 + (wid << 4) : 0, &ph);
 #endif
 }
 
@@ -2521,7 +2544,7 @@ static __device__ __noinline__ void fflow_a(DevPattern P, int front, cplx* F, in
 static __device__ __noinline__ void fflow_b(DevPattern P, const int4* items, const int2* orec, const int* oxp,
                                             const int2* ox, int wid, cplx* F, int64_t Fc, const double* freqs,
                                             const cplx* K, const double* M, int g) {
-  offdiag_item<0, false>(P, items, wid, orec, oxp, ox, F, Fc, freqs, K, M, nullptr, 0, 1, g);
+  offdiag_item<0, false>(nullptr, P, items, wid, orec, oxp, ox, F, Fc, freqs, K, M, nullptr, 0, 1, g);
 }
 
 __global__ __launch_bounds__(1024) void k_factor_flow(DevPattern P, cplx* __restrict__ F, int64_t Fc, FFlowArgs G,

@@ -6,7 +6,9 @@
 (libpfr_wt.so: make -C plate_inverse_problem_amd/csrc OUT=../_lib/libpfr_wt.so OBJDIR=../_lib/obj_wt
 EXTRA=-DPFR_WTRACE=1.)  Per launch (= level): waves with work, the launch's span, the waves' lifetimes
 (median / 90th percentile / max), how late the last wave started, waves resident at once (mean over the span)
-and the CUs used -- whether a level is bound by the length of each wave's work or by waiting for a slot.
+-- whether a level is bound by the length of each wave's work or by waiting for a slot -- and, for the slowest
+10 % of its waves, the time in the source gathers, the left-looking prefix and the rest (each phase closed by a
+wait for the wave's memory operations, which the production kernel overlaps).
 """
 from __future__ import annotations
 
@@ -63,20 +65,22 @@ def main():
         life = (t1 - t0) * 10e-3                       # us (100 MHz)
         span = (t1.max() - t0.min()) * 10e-3
         late = (t0.max() - t0.min()) * 10e-3
-        hw = rec[m, 2]
-        cu = (hw >> 8) & 0xF
-        sh = (hw >> 12) & 0x1
-        se = (hw >> 13) & 0x7
-        ncu = len(set(zip(se.tolist(), sh.tolist(), cu.tolist())))
+        # phase clocks (sources / prefix; the rest = triangle + stores + setup), 10 ns units
+        src = (rec[m, 2] >> 32) * 10e-3
+        pre = (rec[m, 2] & 0xFFFFFFFF) * 10e-3
+        slow = life >= np.percentile(life, 90)
         resident = life.sum() / span if span > 0 else 0.0
         rows.append(dict(launch=int(k), waves=int(m.sum()), span_us=float(span), life_med_us=float(np.median(life)),
                          life_p90_us=float(np.percentile(life, 90)), life_max_us=float(life.max()),
-                         last_start_us=float(late), resident_mean=float(resident), cu_ids=int(ncu)))
+                         last_start_us=float(late), resident_mean=float(resident),
+                         slow_src_us=float(src[slow].mean()), slow_pre_us=float(pre[slow].mean()),
+                         slow_rest_us=float((life - src - pre)[slow].mean())))
     print(f"{'launch':>6} {'waves':>7} {'span':>8} {'life med':>9} {'p90':>8} {'max':>8} {'last start':>10} "
-          f"{'resident':>9} {'CU ids':>6}")
+          f"{'resident':>9} | slowest 10 %: {'sources':>8} {'prefix':>8} {'rest':>8}")
     for r in rows:
         print(f"{r['launch']:6d} {r['waves']:7d} {r['span_us']:8.1f} {r['life_med_us']:9.1f} {r['life_p90_us']:8.1f} "
-              f"{r['life_max_us']:8.1f} {r['last_start_us']:10.1f} {r['resident_mean']:9.1f} {r['cu_ids']:6d}")
+              f"{r['life_max_us']:8.1f} {r['last_start_us']:10.1f} {r['resident_mean']:9.1f} |               "
+              f"{r['slow_src_us']:8.1f} {r['slow_pre_us']:8.1f} {r['slow_rest_us']:8.1f}")
     if args.out:
         with open(args.out, "w") as f:
             json.dump(rows, f, indent=1)
