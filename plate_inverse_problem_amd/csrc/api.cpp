@@ -159,6 +159,7 @@ struct pfr_solver {
   int scale_corr = 1;
   int us2_tiny = 8;                     // PFR_US2_TINY (4 / 8): levels whose pivot blocks are <= this, one wave per front
   int off_pu = 2, off_pu_waves = 0;     // PFR_OFF_PU / PFR_OFF_PU_WAVES: prefix unroll on launches with fewer waves
+  int off_shu_st = 2;                   // PFR_OFF_SHU_ST: its stage, 2 or 4 pivot rows
   int off_shu = 0;                      // PFR_OFF_SHU: L21 launches with fewer (item, group) waves share U11 via LDS
   int off_swz_min = 0;                  // PFR_OFF_SWZ_MIN: L21 launches with fewer (item, group) waves keep the hardware order
   int off_rl = 0;                       // PFR_OFF_RL: L21 rows right-looking on levels with pivot blocks <= this (16-32)                   // PFR_SCALE_CORR: the solve-error scale of the loss sweeps' cotangent
@@ -411,7 +412,8 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
                                 (int64_t)(s->item_ptr[l + 1] - s->item_ptr[l]) * ngroups < s->off_shu
                             ? s->d_shu + s->shu_ptr[l] : nullptr,
                         s->shu_ptr.empty() ? 0 : s->shu_ptr[l + 1] - s->shu_ptr[l],
-                        (int64_t)(s->item_ptr[l + 1] - s->item_ptr[l]) * ngroups < s->off_pu_waves ? s->off_pu : 2);
+                        (int64_t)(s->item_ptr[l + 1] - s->item_ptr[l]) * ngroups < s->off_pu_waves ? s->off_pu : 2,
+                        s->off_shu_st);
     if (after_panel) after_panel(l);
     mark(l, 3);
     pfr::launch_schur_blk(s->schur_bc, s->P, s->d_blocks + s->blk_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
@@ -954,6 +956,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->scale_corr = knob("PFR_SCALE_CORR", 1, 0, 1);
   s->off_swz_min = knob("PFR_OFF_SWZ_MIN", 0, 0, 1 << 30);
   s->off_shu = knob("PFR_OFF_SHU", 0, 0, 1 << 30);
+  s->off_shu_st = knob("PFR_OFF_SHU_ST", 2, 2, 4) >= 4 ? 4 : 2;
   s->off_pu = knob("PFR_OFF_PU", 4, 2, 8);
   s->off_pu_waves = knob("PFR_OFF_PU_WAVES", 0, 0, 1 << 30);
   // 8: the bottom two levels at 2,048 frequencies 685 / 612 -> 509 / 489 us (profiles/r04/experiments/us2_tiny_*)

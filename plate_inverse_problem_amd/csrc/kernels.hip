@@ -981,8 +981,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMALL ? 5 :
 // row w of the stage through registers into a double-buffered LDS image one stage ahead -- and read by the four
 // waves from LDS.  Sources, prefix order (ascending pivot), chunk triangle and stores are k_offdiag_level's: the
 // results are identical bit for bit.
-constexpr int SHU_ST = 4;   // pivot rows per stage (= waves per workgroup)
-template <int MODE>
+template <int MODE, int SHU_ST>   // SHU_ST pivot rows per stage (4: 64 KiB of LDS, 2: 32 KiB)
 __global__ __launch_bounds__(256) void k_offdiag_shu(DevPattern P, const int4* __restrict__ items,
                                                      const int4* __restrict__ tasks, int ntasks,
                                                      const int2* __restrict__ orec, const int* __restrict__ oxp,
@@ -991,7 +990,9 @@ __global__ __launch_bounds__(256) void k_offdiag_shu(DevPattern P, const int4* _
                                                      const double* __restrict__ M, const cplx* __restrict__ data,
                                                      int64_t data_stride, int nvalid) {
   static_assert(OFF_G == 1 && OB == 8, "one lane = one frequency, chunks of 8 pivots");
-  __shared__ cplx Ub[2][SHU_ST][8][64];       // 64 KiB: two stages of 4 pivot rows x 8 columns x 64 frequencies
+  static_assert(SHU_ST == 2 || SHU_ST == 4, "stage of 2 or 4 pivot rows");
+  constexpr int PW = SHU_ST * 8 / 4;          // staged entries per wave
+  __shared__ cplx Ub[2][SHU_ST][8][64];       // two stages of SHU_ST pivot rows x 8 columns x 64 frequencies
   const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
   const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -1049,21 +1050,26 @@ __global__ __launch_bounds__(256) void k_offdiag_shu(DevPattern P, const int4* _
     }
     // prefix: x -= own(0:c0) * U(0:c0, c0:c0+8), U staged SHU_ST pivot rows at a time
     const int nst = (c0 + SHU_ST - 1) / SHU_ST;
-    cplx st[8];
+    // wave w stages entries e = w PW + k of the stage: pivot row e / 8, column e % 8
+    cplx st[PW];
     if (nst > 0) {
-      const int t = min(w, c0 - 1);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) st[j] = E(t, c0 + min(j, nb - 1));
+      for (int k = 0; k < PW; ++k) {
+        const int e = w * PW + k;
+        st[k] = E(min(e / 8, c0 - 1), c0 + min(e % 8, nb - 1));
+      }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) Ub[0][w][j][lane] = st[j];
+      for (int k = 0; k < PW; ++k) Ub[0][(w * PW + k) / 8][(w * PW + k) % 8][lane] = st[k];
       __syncthreads();
     }
     for (int s = 0; s < nst; ++s) {
       const bool more = s + 1 < nst;
       if (more) {
-        const int t = min((s + 1) * SHU_ST + w, c0 - 1);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) st[j] = E(t, c0 + min(j, nb - 1));
+        for (int k = 0; k < PW; ++k) {
+          const int e = w * PW + k;
+          st[k] = E(min((s + 1) * SHU_ST + e / 8, c0 - 1), c0 + min(e % 8, nb - 1));
+        }
       }
 #pragma unroll
       for (int tt = 0; tt < SHU_ST; ++tt) {
@@ -1082,7 +1088,7 @@ __global__ __launch_bounds__(256) void k_offdiag_shu(DevPattern P, const int4* _
       }
       if (more) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) Ub[(s + 1) & 1][w][j][lane] = st[j];
+        for (int k = 0; k < PW; ++k) Ub[(s + 1) & 1][(w * PW + k) / 8][(w * PW + k) % 8][lane] = st[k];
       }
       __syncthreads();
     }
@@ -3783,13 +3789,17 @@ static void wtrace_launch(long long waves, hipStream_t st) {
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
                     const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,
                     const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st, int rl,
-                    int swz, const int4* shu, int nshu, int pu) {
+                    int swz, const int4* shu, int nshu, int pu, int shu_st) {
   if (nitems <= 0) return;
   const bool small = maxns <= 8;
   if constexpr (OFF_G == 1 && OB == 8) if (shu && nshu > 0 && !small) {
     dim3 gs((unsigned)nshu, ngroups), bs(256);
-    if (mode == 0) LAUNCH((k_offdiag_shu<0>), gs, bs, st, P, items, shu, nshu, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid);
-    else LAUNCH((k_offdiag_shu<1>), gs, bs, st, P, items, shu, nshu, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid);
+#define SHU(MD, T) LAUNCH((k_offdiag_shu<MD, T>), gs, bs, st, P, items, shu, nshu, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid)
+    if (mode == 0 && shu_st == 4) SHU(0, 4);
+    else if (mode == 0) SHU(0, 2);
+    else if (shu_st == 4) SHU(1, 4);
+    else SHU(1, 2);
+#undef SHU
     return;
   }
   const int rlim = OFF_G == 1 ? rl % 100 : 0, rrows = rl >= 100 ? OFF_RPL : 1;

@@ -55,7 +55,8 @@ void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems
                     int rl = 0,    // rl > 0 (symmetric analyses): levels with 8 < maxns <= rl right-looking (k_offdiag_rl)
                     int swz = 1,   // 0: no XCD-aware workgroup order
                     const int4* shu = nullptr, int nshu = 0,    // != NULL: k_offdiag_shu over these tasks
-                    int pu = 2);   // prefix loads in flight, in pivots (2, 4 or 8)
+                    int pu = 2,    // prefix loads in flight, in pivots (2, 4 or 8)
+                    int shu_st = 2);   // k_offdiag_shu stage: pivot rows (2 or 4)
 void launch_schur(bool sym, const DevPattern& P, const int4* tiles, int ntiles, const int* g1, const int* gxp,
                   const int2* gx, int ngroups, double2* F, int64_t Fc, hipStream_t st);
 // symmetric mode, large update blocks: 16 x 16 blocks, operands staged in LDS per workgroup
