@@ -253,8 +253,10 @@ PFR_API int pfr_debug_solution(pfr_solver* s, int32_t which, int32_t q, double* 
 
 /* Diagnostic: wave trace of the L21 row launches (k_offdiag_level).  cap == 0: start tracing into a device buffer
  * of *count records; cap > 0: copy up to cap records (4 x uint64: start, end of the 100 MHz real-time counter,
- * HW_ID, tag = 1 + 16 item, 0 for idle waves) into out_host, set *count, stop tracing.  Synchronises.  Records
- * are written only by a library built with -DPFR_WTRACE=1 (zeros otherwise). */
+ * HW_ID or the phase clocks, tag = launch << 40 | 1 + 16 item, 0 for idle waves) into out_host, set *count, stop
+ * tracing.  Synchronises.  Records are written only by a library built with -DPFR_WTRACE=1 (zeros otherwise);
+ * the trace state is process-wide: one solver (one lane) at a time, and each traced launch synchronises its
+ * stream. */
 PFR_API int pfr_debug_wave_trace(pfr_solver* s, int64_t cap, uint64_t* out_host, int64_t* count);
 
 /* Per-phase device times [ms] of the last pfr_sweep/pfr_solve call on this solver, measured with HIP
