@@ -957,8 +957,11 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->off_swz_min = knob("PFR_OFF_SWZ_MIN", 0, 0, 1 << 30);
   s->off_shu = knob("PFR_OFF_SHU", 0, 0, 1 << 30);
   s->off_shu_st = knob("PFR_OFF_SHU_ST", 2, 2, 4) >= 4 ? 4 : 2;
-  s->off_pu = knob("PFR_OFF_PU", 4, 2, 8);
-  s->off_pu_waves = knob("PFR_OFF_PU_WAVES", 0, 0, 1 << 30);
+  // 3 = the software-pipelined prefix; on by default for chunks of <= 1,024 frequencies on the launches with fewer
+  // than 8,000 waves (the narrow levels of C4's per-rank sweeps: 512 frequencies 35.3-35.7k -> 36.2-36.6k
+  // freq-solves/s; 2,048-frequency chunks unchanged, profiles/r04/offdiag_layout/pu3_*)
+  s->off_pu = knob("PFR_OFF_PU", 3, 2, 8);
+  s->off_pu_waves = -1;         // after Fc is known (below)
   // 8: the bottom two levels at 2,048 frequencies 685 / 612 -> 509 / 489 us (profiles/r04/experiments/us2_tiny_*)
   s->us2_tiny = knob("PFR_US2_TINY", 8, 0, 64);   // > 8: k_usolve2_wave on the levels with blocks of 9 .. this
   s->off_rl = knob("PFR_OFF_RL", 0, 0, 124);   // n: one row per wave (n = 16, 24, 32); 100 + n: two rows (n = 16, 24)
@@ -970,6 +973,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->n = S.n;
   s->nnz = S.nnz;
   s->Fc = round64(max_batch);
+  if (s->off_pu_waves < 0) s->off_pu_waves = knob("PFR_OFF_PU_WAVES", s->Fc <= 1024 ? 8000 : 0, 0, 1 << 30);
   s->level_ptr = S.level_ptr;
   s->level_maxf = S.level_maxf;
   s->perm = S.perm;

@@ -810,7 +810,35 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
   // x -= own(0:c0) * shared(0:c0, c0:c0+NB)   (PRE = false: c0 = 0, no prefix); PU > 2: batches of PU pivots
   // whose loads are all issued before their products (the same products in the same order)
   int t0 = 0;
-  if (PU > 2 && PRE) {
+  if (PU == 3 && PRE && c0 > 0) {
+    // software-pipelined prefix: pivot t + 1's loads are issued before pivot t's products, so the products wait
+    // only for the older loads (the compiler's s_waitcnt then counts the younger ones) -- two pivots' loads in
+    // flight instead of the plain loop's drain at every iteration; same products, same order
+    cplx la[OFF_RPL], ua[NB], lb[OFF_RPL], ub[NB];
+    auto ld = [&](cplx (&l)[OFF_RPL], cplx (&u)[NB], int t) {
+#pragma unroll
+      for (int h = 0; h < OFF_RPL; ++h) l[h] = base[(so[h] + (int64_t)t * sc) * Fc];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) u[j] = base[((int64_t)t * sa + (int64_t)(c0 + j) * sb) * Fc];
+    };
+    auto fm = [&](const cplx (&l)[OFF_RPL], const cplx (&u)[NB]) {
+#pragma unroll
+      for (int h = 0; h < OFF_RPL; ++h)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) x[h][j] = cfms(x[h][j], l[h], u[j]);
+    };
+    ld(la, ua, 0);
+    int t = 0;
+    for (; t + 2 <= c0; t += 2) {
+      ld(lb, ub, t + 1);
+      fm(la, ua);
+      if (t + 2 < c0) ld(la, ua, t + 2);
+      fm(lb, ub);
+    }
+    if (t < c0) fm(la, ua);
+    t0 = c0;
+  }
+  if (PU > 3 && PRE) {
     for (; t0 + PU <= c0; t0 += PU) {
       cplx l[PU][OFF_RPL], u[PU][NB];
 #pragma unroll
@@ -3834,6 +3862,10 @@ void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems
   }
   if (!small && mode == 0 && pu >= 4) {
     LAUNCH((k_offdiag_level<0, false, 4>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid, swz);
+    return;
+  }
+  if (!small && mode == 0 && pu == 3) {
+    LAUNCH((k_offdiag_level<0, false, 3>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid, swz);
     return;
   }
   if (mode == 0 && small) OL(0, true);

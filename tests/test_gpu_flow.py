@@ -140,7 +140,7 @@ def test_offdiag_prefix_batches_bitwise(monkeypatch, lo, hi):
     """PFR_OFF_PU: the L21 prefix loop in batches of 4 / 8 pivots whose loads are issued first (on the launches
     with fewer waves than PFR_OFF_PU_WAVES) -- the same products in the same order: identical results."""
     base = _run(monkeypatch, 0, lo, hi, fac_lds="-1", env={"PFR_OFF_PU_WAVES": "0"})
-    for pu in ("4", "8"):
+    for pu in ("3", "4", "8"):   # 3: software-pipelined
         got = _run(monkeypatch, 0, lo, hi, fac_lds="-1", env={"PFR_OFF_PU": pu, "PFR_OFF_PU_WAVES": "1000000000"})
         dl = abs(got[0] / base[0] - 1)
         dw = float(np.max(np.abs(got[1] - base[1])) / np.max(np.abs(base[1])))
