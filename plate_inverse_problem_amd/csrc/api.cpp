@@ -157,6 +157,7 @@ struct pfr_solver {
   double* fr0 = nullptr;
   double2 *mscale = nullptr, *cpart = nullptr;     // mscale complex: the solve-error scale (k_correct_finish)
   int scale_corr = 1;
+  int us2_pp = 0;                       // PFR_US2_PP: the paired pass's split update parts software-pipelined
   int us2_tiny = 8;                     // PFR_US2_TINY (4 / 8): levels whose pivot blocks are <= this, one wave per front
   int off_pu = 2, off_pu_waves = 0;     // PFR_OFF_PU / PFR_OFF_PU_WAVES: prefix unroll on launches with fewer waves
   int off_shu_st = 2;                   // PFR_OFF_SHU_ST: its stage, 2 or 4 pivot rows
@@ -707,7 +708,8 @@ int sym_top_down_pair(pfr_solver* s, hipStream_t st, bool fwd_all = false) {
                         s->X, s->d_reach[0], fwd_all ? nullptr : s->d_reach[1], s->Y2, s->XA, s->d_reach[1], st,
                         solve_split(s, nf), s->us2_cfg,
                         s->us2_tiny > 0 && s->level_maxns[l] <= s->us2_tiny
-                            ? (s->level_maxns[l] <= 4 ? 4 : s->level_maxns[l] <= 8 ? 8 : s->us2_tiny) : 0);
+                            ? (s->level_maxns[l] <= 4 ? 4 : s->level_maxns[l] <= 8 ? 8 : s->us2_tiny) : 0,
+                        s->us2_pp);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -963,7 +965,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->off_pu = knob("PFR_OFF_PU", 3, 2, 8);
   s->off_pu_waves = -1;         // after Fc is known (below)
   // 8: the bottom two levels at 2,048 frequencies 685 / 612 -> 509 / 489 us (profiles/r04/experiments/us2_tiny_*)
-  s->us2_tiny = knob("PFR_US2_TINY", 8, 0, 64);   // > 8: k_usolve2_wave on the levels with blocks of 9 .. this
+  s->us2_tiny = knob("PFR_US2_TINY", 8, 0, 64);
+  s->us2_pp = knob("PFR_US2_PP", 0, 0, 1);   // > 8: k_usolve2_wave on the levels with blocks of 9 .. this
   s->off_rl = knob("PFR_OFF_RL", 0, 0, 124);   // n: one row per wave (n = 16, 24, 32); 100 + n: two rows (n = 16, 24)
   if (s->off_rl > 100 && s->off_rl % 100 > 24) s->off_rl = 124;
   s->fuse_asm = knob("PFR_FUSE_ASM", 0, 0, 1);   // measured slower (2,048-frequency chunk: A11 classes 4.1 -> 6.6 ms)

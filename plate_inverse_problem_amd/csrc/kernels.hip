@@ -2109,6 +2109,79 @@ __device__ __forceinline__ void usolve2_upd(const Front& fr, const int* six, con
 #undef XV
 }
 
+// usolve2_upd software-pipelined: chunk k + 1's index reads and loads issued before chunk k's products (the products
+// then wait only for the older loads; the plain loop drains at every chunk).  Same products in the same order.
+template <bool SYM, int SR, int SK>
+__device__ __forceinline__ void usolve2_upd_pp(const Front& fr, const int* six, const cplx* __restrict__ base,
+                                               int64_t Fc, int64_t q, const bool (&act)[2], const bool (&live)[2],
+                                               const cplx* const (&Ys)[2], cplx* const (&Xs)[2], int a_begin, int a_step) {
+  const int f = fr.f, ns = fr.ns;
+#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+#define XV(v, a) Xs[v][(int64_t)(fr.col0 + (a)) * Fc + q]
+  for (int a0 = a_begin; a0 < ns; a0 += a_step) {
+    int ra[SR];
+    cplx acc[2][SR];
+#pragma unroll
+    for (int r = 0; r < SR; ++r) {
+      ra[r] = min(a0 + r, ns - 1);
+      acc[0][r] = acc[1][r] = make_double2(0.0, 0.0);
+    }
+    const cplx* pu[SR];
+#pragma unroll
+    for (int r = 0; r < SR; ++r) pu[r] = base + (SYM ? (int64_t)ra[r] : (int64_t)ra[r] * f) * Fc;
+    const int64_t su = SYM ? (int64_t)f * Fc : Fc;
+    cplx xa[2][SK], ea[SR][SK], xb[2][SK], eb[SR][SK];
+    auto ld = [&](cplx (&xv)[2][SK], cplx (&ev)[SR][SK], int b0) {
+      int iv[SK];
+#pragma unroll
+      for (int u = 0; u < SK; ++u) iv[u] = __builtin_amdgcn_readfirstlane(six[min(b0 + u, f - 1)]);
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int u = 0; u < SK; ++u) xv[v][u] = Xs[v][(int64_t)iv[u] * Fc + q];
+#pragma unroll
+      for (int r = 0; r < SR; ++r)
+#pragma unroll
+        for (int u = 0; u < SK; ++u) ev[r][u] = pu[r][min(b0 + u, f - 1) * su];
+    };
+    auto fm = [&](cplx (&xv)[2][SK], const cplx (&ev)[SR][SK], int b0) {
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int u = 0; u < SK; ++u)
+          if (b0 + u >= f) xv[v][u] = make_double2(0.0, 0.0);
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int r = 0; r < SR; ++r)
+#pragma unroll
+          for (int u = 0; u < SK; ++u) acc[v][r] = cfms(acc[v][r], ev[r][u], xv[v][u]);
+    };
+    int b0 = ns;
+    if (b0 < f) ld(xa, ea, b0);
+    for (; b0 + SK < f; b0 += 2 * SK) {
+      ld(xb, eb, b0 + SK);
+      fm(xa, ea, b0);
+      if (b0 + 2 * SK < f) ld(xa, ea, b0 + 2 * SK);
+      fm(xb, eb, b0 + SK);
+    }
+    if (b0 < f) fm(xa, ea, b0);
+#pragma unroll
+    for (int r = 0; r < SR; ++r)
+      if (a0 + r < ns) {
+        const cplx urr = SYM ? E(ra[r], ra[r]) : make_double2(1.0, 0.0);
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+          if (act[v]) {
+            const cplx y = live[v] ? Ys[v][(int64_t)(fr.col0 + a0 + r) * Fc + q] : make_double2(0.0, 0.0);
+            XV(v, a0 + r) = SYM ? cadd(y, cmul(urr, acc[v][r])) : cadd(y, acc[v][r]);
+          }
+      }
+  }
+#undef E
+#undef XV
+}
+
 // U11 backward for the pivot values XV(v, 0 .. ns) the update part left there: KBS blocks, the diagonal
 // block by wave 0 in registers, the rows above updated by all waves
 __device__ __forceinline__ void usolve2_tri(const Front& fr, const cplx* __restrict__ base, int64_t Fc, const Ctx& c,
@@ -2347,7 +2420,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 }
 
 // the pivot rows' update part of k_usolve2_level split over S workgroups per (front, frequency group)
-template <bool SYM, int SR, int SK>
+template <bool SYM, int SR, int SK, bool PP = false>
 __global__ __launch_bounds__(256) void k_usolve2_upd(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F,
                                                      int64_t Fc, UPair A, UPair B, int S) {
   int bx;
@@ -2362,8 +2435,12 @@ __global__ __launch_bounds__(256) void k_usolve2_upd(DevPattern P, const int* __
   __shared__ int six[MAX_FRONT];
   for (int a = threadIdx.x; a < fr.f; a += blockDim.x) six[a] = P.idx[fr.row0 + a];
   __syncthreads();
-  usolve2_upd<SYM, SR, SK>(fr, six, F + fr.off * Fc + c.q, Fc, c.q, act, live, Ys, Xs, SR * (split * c.W + c.w),
-                           SR * c.W * S);
+  if (PP)
+    usolve2_upd_pp<SYM, SR, SK>(fr, six, F + fr.off * Fc + c.q, Fc, c.q, act, live, Ys, Xs, SR * (split * c.W + c.w),
+                                SR * c.W * S);
+  else
+    usolve2_upd<SYM, SR, SK>(fr, six, F + fr.off * Fc + c.q, Fc, c.q, act, live, Ys, Xs, SR * (split * c.W + c.w),
+                             SR * c.W * S);
 }
 
 // ------------------------------------------------------------------ dependency-driven passes (narrow top)
@@ -3958,7 +4035,7 @@ void launch_fn_combine(const int* rows, int nrows, const double2* fcoef, double2
 void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, bool small, int ngroups,
                     const double2* F, int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0,
                     const double2* Y1, double2* X1, const int* reach1, hipStream_t st, int split, int small_cfg,
-                    int tiny) {
+                    int tiny, int pp) {
   if (nfronts <= 0) return;
   UPair a{Y0, X0, reach0, skip0}, b{Y1, X1, reach1, nullptr};
   if (tiny > 0 && split <= 1) {
@@ -3973,8 +4050,10 @@ void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, boo
   const int rs = split > 1;
   // split > 1: the pivot rows' update part over `split` workgroups per front first (the small-front
   // register shape: many short waves)
-  if (rs) LAUNCH((k_usolve2_upd<true, 2, 4>), dim3(nfronts * split, ngroups), dim3(64 * SPLIT_W), st, P, lvl, F, Fc, a, b,
-                 split);
+  if (rs && pp) LAUNCH((k_usolve2_upd<true, 2, 4, true>), dim3(nfronts * split, ngroups), dim3(64 * SPLIT_W), st, P, lvl, F,
+                       Fc, a, b, split);
+  else if (rs) LAUNCH((k_usolve2_upd<true, 2, 4>), dim3(nfronts * split, ngroups), dim3(64 * SPLIT_W), st, P, lvl, F, Fc, a,
+                      b, split);
   // symmetric mode only (the paired top-down pass serves the symmetric loss + gradient sweep).  Small-front levels:
   // SR pivot rows per pass share each gathered update-row value (small_cfg 0: 2 rows x 4 values at 4 waves/SIMD;
   // 1: 4 x 4 at 3; 2: 8 x 2 at 3 -- more rows per pass, fewer re-gathers of the update-row solution)

@@ -90,7 +90,8 @@ void launch_fn_combine(const int* rows, int nrows, const double2* fcoef, double2
 void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, bool small, int ngroups,
                     const double2* F, int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0,
                     const double2* Y1, double2* X1, const int* reach1, hipStream_t st, int split = 1,
-                    int small_cfg = 0, int tiny = 0);   // tiny 4 / 8: the level's pivot blocks all <= tiny (k_usolve2_tiny)
+                    int small_cfg = 0, int tiny = 0,    // tiny 4 / 8: the level's pivot blocks all <= tiny (k_usolve2_tiny)
+                    int pp = 0);   // split update parts software-pipelined (usolve2_upd_pp)
 // dependency-driven pass over the narrow top of the elimination tree (one launch, task tickets, per-front
 // completion words): the task list and its words (ticket, done, cnt: 1 + 2 nslots ngroups unsigned,
 // zeroed by the launcher), flags per frequency (a spin timeout sets PFR_FLAG_BAD_PIVOT)

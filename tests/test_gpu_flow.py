@@ -148,3 +148,17 @@ def test_offdiag_prefix_batches_bitwise(monkeypatch, lo, hi):
         report(f"offdiag_pu{pu}_{lo}_{hi}", loss_rel=dl, w_rel=dw, fr_rel=dfr, flagged=got[4])
         assert got[4] == 0
         assert dl == 0 and dw == 0 and dfr == 0, (pu, dl, dw, dfr)
+
+
+@pytest.mark.parametrize("lo,hi", [(1024, 1536), (0, 2048)])
+def test_paired_update_pipelined_bitwise(monkeypatch, lo, hi):
+    """PFR_US2_PP: the paired top-down pass's split update parts software-pipelined (the next chunk's loads before
+    the current chunk's products): identical results."""
+    base = _run(monkeypatch, 0, lo, hi, fac_lds="-1", env={"PFR_US2_PP": "0"})
+    got = _run(monkeypatch, 0, lo, hi, fac_lds="-1", env={"PFR_US2_PP": "1"})
+    dl = abs(got[0] / base[0] - 1)
+    dw = float(np.max(np.abs(got[1] - base[1])) / np.max(np.abs(base[1])))
+    dfr = float(np.max(np.abs(got[2] / base[2] - 1)))
+    report(f"us2_pp_{lo}_{hi}", loss_rel=dl, w_rel=dw, fr_rel=dfr, flagged=got[4])
+    assert got[4] == 0
+    assert dl == 0 and dw == 0 and dfr == 0, (dl, dw, dfr)
