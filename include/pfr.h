@@ -251,14 +251,6 @@ PFR_API int pfr_set_refine_tol(pfr_solver* s, double tol);
  * into out_host.  Synchronises the device. */
 PFR_API int pfr_debug_solution(pfr_solver* s, int32_t which, int32_t q, double* out_host);
 
-/* Diagnostic: wave trace of the L21 row launches (k_offdiag_level).  cap == 0: start tracing into a device buffer
- * of *count records; cap > 0: copy up to cap records (4 x uint64: start, end of the 100 MHz real-time counter,
- * HW_ID or the phase clocks, tag = launch << 40 | 1 + 16 item, 0 for idle waves) into out_host, set *count, stop
- * tracing.  Synchronises.  Records are written only by a library built with -DPFR_WTRACE=1 (zeros otherwise);
- * the trace state is process-wide: one solver (one lane) at a time, and each traced launch synchronises its
- * stream. */
-PFR_API int pfr_debug_wave_trace(pfr_solver* s, int64_t cap, uint64_t* out_host, int64_t* count);
-
 /* Per-phase device times [ms] of the last pfr_sweep/pfr_solve call on this solver, measured with HIP
  * events on the call's stream (0 = factor, 1 = forward solves, 2 = functional, 3 = adjoint solves,
  * 4 = contraction).  Timing is enabled by pfr_set_timing(s, 1). */

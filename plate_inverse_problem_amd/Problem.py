@@ -224,10 +224,7 @@ class _Engine:
             self._pool = None
         self.n_lanes = lanes
         self.solvers = [_native.Solver(self.sym, self.device.index, batch) for _ in range(lanes)]
-        # PFR_LANE_PRIO=1: lane 0's stream at high priority, so that the other lanes fill the gaps of its
-        # latency-bound phases instead of running in lockstep with it
-        prio = os.environ.get("PFR_LANE_PRIO", "0") != "0"
-        self.streams = [torch.cuda.Stream(self.device, priority=-1 if (prio and i == 0) else 0) for i in range(lanes)]
+        self.streams = [torch.cuda.Stream(self.device) for i in range(lanes)]
         if lanes > 1 and os.environ.get("PFR_PAR_LAUNCH", "1") != "0":
             from concurrent.futures import ThreadPoolExecutor
             self._pool = ThreadPoolExecutor(max_workers=lanes, thread_name_prefix="pfr-lane")

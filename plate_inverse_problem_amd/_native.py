@@ -81,7 +81,6 @@ _PROTOS = {
     "pfr_set_check": (C.c_int, [_P, C.c_int32, C.c_double, _P]),
     "pfr_set_refine_tol": (C.c_int, [_P, C.c_double]),
     "pfr_debug_solution": (C.c_int, [_P, C.c_int32, C.c_int32, _DP]),
-    "pfr_debug_wave_trace": (C.c_int, [_P, C.c_int64, C.c_void_p, C.POINTER(C.c_int64)]),
     "pfr_set_timing": (C.c_int, [_P, C.c_int32]),
     "pfr_last_timings": (C.c_int, [_P, _DP]),
     "pfr_last_kernel_timings": (C.c_int, [_P, _DP, _P]),
@@ -305,19 +304,6 @@ class Solver:
         out = np.zeros(2 * self.sym.stats()["n"], dtype=np.float64)
         check(lib().pfr_debug_solution(self._h, int(which), int(q), out.ctypes.data_as(_DP)), "pfr_debug_solution")
         return out[0::2] + 1j * out[1::2]
-
-    def wave_trace_start(self, cap: int):
-        """Start the L21 launches' wave trace (diagnostic) into a device buffer of ``cap`` records."""
-        n = C.c_int64(int(cap))
-        check(lib().pfr_debug_wave_trace(self._h, 0, None, C.byref(n)), "pfr_debug_wave_trace")
-
-    def wave_trace_fetch(self, cap: int) -> np.ndarray:
-        """Stop the wave trace; records (n, 4) uint64: start, end (100 MHz), HW_ID, tag (launch << 40 | 1 + 16 item)."""
-        out = np.zeros((int(cap), 4), dtype=np.uint64)
-        n = C.c_int64(0)
-        check(lib().pfr_debug_wave_trace(self._h, int(cap), out.ctypes.data_as(C.c_void_p), C.byref(n)),
-              "pfr_debug_wave_trace")
-        return out[:n.value]
 
     def set_refine_tol(self, tol: float):
         """Threshold of the selective adjoint refinement (PFR_CHECK_REFINE_ADJ): groups where the functional

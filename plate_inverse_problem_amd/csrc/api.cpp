@@ -45,7 +45,6 @@ int upload(T** dst, const std::vector<T>& src) {
 
 int64_t round64(int64_t x) { return (x + 63) / 64 * 64; }
 
-constexpr int kContractBlocks = 2048;   // row ranges per frequency group of the row kernels (at most)
 }  // namespace
 
 struct pfr_solver {
@@ -60,8 +59,6 @@ struct pfr_solver {
   int32_t* d_level_fronts = nullptr;
   int4* d_tiles = nullptr;              // Schur tiles (front, i0, j0, 0), grouped by level
   int4* d_items = nullptr;              // off-diagonal panel items (front, first row/col, kind, record offset)
-  int4* d_shu = nullptr;                // k_offdiag_shu tasks (first item in the level, count <= 4, front, -)
-  std::vector<int32_t> shu_ptr;         // per level: first task
   int2* d_orec = nullptr;               // per item x lane group x pivot: (nz, first child source) of the entry
   int32_t* d_oxp = nullptr;             // per item: range of further child sources in d_ox
   int2* d_ox = nullptr;                 // (pivot * OFF_G OFF_RPL + row slot, element id)
@@ -76,14 +73,10 @@ struct pfr_solver {
   int32_t* d_bgxp = nullptr;            // per block: range of further sources in d_bgx
   int2* d_bgx = nullptr;                // (wave * 16 + position, element id)
   std::vector<int32_t> blk_ptr;
-  int schur_bc = 16;                    // block columns (16: 16 waves per block, 8: 8 waves)
   int4* d_asm = nullptr;                // panel-entry assembly records (dst, nz, first child source, 0), by level
   int32_t* d_asm_xp = nullptr;          // per 8-record chunk: range of further child sources in d_asm_x
   int2* d_asm_x = nullptr;              // (record within chunk, child element id)
   std::vector<int32_t> asm_ptr;         // record offset of each level (multiple of 8)
-  int32_t* d_rec0 = nullptr;            // per front: its first A11 assembly record (fused assembly)
-  int fuse_asm = 0;                     // PFR_FUSE_ASM: A11 gathered by k_factor_sym itself (symmetric mode,
-                                        // levels on the global-memory A11 LU)
   int32_t* d_colptr = nullptr;
   int32_t* d_rowind = nullptr;
   // symmetric mode (options.symmetric): U never formed; Dirichlet nodes decoupled
@@ -124,11 +117,6 @@ struct pfr_solver {
   // the functional correction's walk): per (workgroup, k, frequency) sums, reduced with m_q by k_reduce_q
   int contract_walk = 1;
   double2* kpart = nullptr;
-  // side stream for the forward bottom-up solve over the rhs reach, overlapped with the
-  // factorisation level by level (symmetric loss + gradient sweeps)
-  hipStream_t aux = nullptr;
-  std::vector<hipEvent_t> lev_ev;
-  hipEvent_t aux_start = nullptr, aux_done = nullptr;
   int32_t* d_reach[2] = {nullptr, nullptr};
   int32_t* d_reach_fronts[2] = {nullptr, nullptr};
   std::vector<int32_t> reach_ptr[2];
@@ -141,13 +129,10 @@ struct pfr_solver {
                                         // walks' order (mesh-local gathers, whatever the ordering)
   int32_t *d_cptr = nullptr, *d_cidx = nullptr, *d_cnz = nullptr;
   double2 *DX = nullptr, *DL = nullptr, *Kdir = nullptr;
-  // fused contraction + checks (k_contract_rows): per permuted row a pseudo-entry (-1, -1, -1, i),
-  // then (column, nz of (i, j) or -1, nz of (j, i) or -1, i) over the union of the row's and the
-  // column's patterns; entry ranges of whole rows, about equal size (kContractBlocks of them)
-  int32_t* d_ublk = nullptr;
+  // gradient contraction entries (k_contract_eg): per permuted row a pseudo-entry (-1, -1, -1, i), then
+  // (column, nz of (i, j) or -1, nz of (j, i) or -1, i) over the union of the row's and the column's patterns
   int4* d_uent = nullptr;
-  int n_uent = 0, n_ublk = 0;           // entries; row ranges (one single-wave workgroup each per 64 frequencies)
-  double2* d_kme = nullptr;             // entry-ordered K(i, j), K(j, i), (M(i, j), M(j, i)) (refreshed per sweep)
+  int n_uent = 0;
   double* d_se = nullptr;               // entry-ordered S_k(i, j) (pfr_set_stiffness)
   int n_kdir = 0;
   double2 *partial = nullptr, *tq = nullptr;
@@ -156,14 +141,9 @@ struct pfr_solver {
   // the residual walk's per-workgroup dot-product partials (residual_parts(n) x Fc)
   double* fr0 = nullptr;
   double2 *mscale = nullptr, *cpart = nullptr;     // mscale complex: the solve-error scale (k_correct_finish)
-  int scale_corr = 1;
-  int us2_pp = 0;                       // PFR_US2_PP: the paired pass's split update parts software-pipelined
-  int us2_tiny = 8;                     // PFR_US2_TINY (4 / 8): levels whose pivot blocks are <= this, one wave per front
-  int off_pu = 2, off_pu_waves = 0;     // PFR_OFF_PU / PFR_OFF_PU_WAVES: prefix unroll on launches with fewer waves
-  int off_shu_st = 2;                   // PFR_OFF_SHU_ST: its stage, 2 or 4 pivot rows
-  int off_shu = 0;                      // PFR_OFF_SHU: L21 launches with fewer (item, group) waves share U11 via LDS
-  int off_swz_min = 0;                  // PFR_OFF_SWZ_MIN: L21 launches with fewer (item, group) waves keep the hardware order
-  int off_rl = 0;                       // PFR_OFF_RL: L21 rows right-looking on levels with pivot blocks <= this (16-32)                   // PFR_SCALE_CORR: the solve-error scale of the loss sweeps' cotangent
+  int scale_corr = 1;                   // PFR_SCALE_CORR: the solve-error scale of the loss sweeps' cotangent
+  int us2_tiny = 8;                     // PFR_US2_TINY (0 / 4 / 8): levels whose pivot blocks are <= this, one wave per front
+  int off_pu_waves = 0;                 // PFR_OFF_PU_WAVES: L21 launches with fewer waves run the pipelined prefix
   int32_t* flags = nullptr;
   // operator / rhs / functional / stiffness state
   const double2* K = nullptr;
@@ -193,17 +173,14 @@ struct pfr_solver {
   std::vector<ChunkEvents> tev;
   int n_tev = 0;                        // chunks recorded by the last call
   int64_t alg_bytes[5]{};               // algorithmic HBM bytes per frequency of each class (one sweep)
-  // per level: A11 assembly, A11 LU, and the fused class (children's entries gathered + L11 / U11 written)
-  std::vector<int64_t> lev_asm_bytes, lev_lu_bytes, lev_fused_bytes;
+  // per level: A11 assembly, A11 LU
+  std::vector<int64_t> lev_asm_bytes, lev_lu_bytes;
   // launch-shape tuning knobs, read from the environment when the solver is created (so that a
   // process can build solvers with different settings, e.g. tests forcing each kernel variant):
   // PFR_SOLVE_WMAX (waves per solve workgroup, at most), PFR_FAC_WMAX (waves per A11 LU
   // workgroup, at most), PFR_US2_SMALL (largest front of a level the paired top-down solve treats
   // with its low-register small-front variant)
   int solve_wmax = 8, fac_wmax = 16, us2_small = 110;
-  int us2_cfg = 2;                      // PFR_US2_CFG: register shape of the small-front paired top-down pass
-  int off_small = 1;                    // PFR_OFF_SMALL: no-prefix off-diagonal variant on levels of ns <= 8
-  int fac_lds_qf = 1;                   // PFR_FAC_LDS_QF: frequencies per k_factor_sym_lds workgroup (1, 2 or 4)
   int fac_lds = -1;                     // PFR_FAC_LDS: which levels factor A11 in LDS (k_factor_sym_lds): n > 0
                                         // those whose largest pivot block has at least n pivots, 0 none, -1 auto
                                         // (default since round 3: 512-frequency sweeps +2.6 %, 4,096 unchanged)
@@ -211,22 +188,6 @@ struct pfr_solver {
   int split_target = 256;               // PFR_SOLVE_SPLIT: solve launches with fewer (front, group) workgroups
                                         // than this (one per CU) split their update parts up to about this
                                         // many workgroups (0: off)
-  int check_fused = 0;                  // PFR_CHECK_FUSED=1: loss sweeps check both solutions in one entry walk
-  // dependency-driven passes over the narrow top of the tree (PFR_FLOW bits: 1 the paired top-down pass,
-  // k_usolve2_flow; 2 the sliced bottom-up chain, k_lsolve_flow): the levels from the root down while a level
-  // has fewer than PFR_FLOW_WG (front, frequency group) workgroups
-  int flow = 0, flow_wg = 1024, flow_lcut = 0;
-  pfr::FlowDesc fd{};
-  // ... and the sliced bottom-up chain over the same levels (task list rebuilt whenever a reach changes)
-  std::vector<int32_t> flow_slot;       // per front: region slot or -1
-  pfr::LFlowDesc lfd{};
-  // the factorisation's narrow top in one dependency-driven launch (PFR_FLOW bit 2, k_factor_flow): levels
-  // [fflow_lcut, L) -- from the root down while a level has fewer than PFR_FLOW_FWG (front, group) A11 tasks
-  int fflow_lcut = 0, flow_fwg = 256;
-  int timed_levels = 0;                 // levels the last factorisation launched level by level (class timings)
-  pfr::FactorFlowDesc ffd{};
-  int4* d_lf_tasks = nullptr;
-  int32_t *d_lf_cptr = nullptr, *d_lf_cslot = nullptr, *d_lf_parts = nullptr;
   // backward-error checks (pfr_set_check): PFR_CHECK_* bits, tolerance, optional per-item output;
   // per-frequency maxima scratch, forward and adjoint (kept zero between checks)
   int check_mode = 0;
@@ -235,16 +196,10 @@ struct pfr_solver {
   double* gind = nullptr;               // per 64-frequency group: largest |correction| / |fr| of the chunk
   int32_t* glist = nullptr;             // the groups whose adjoint is refined (REFINE_CAP, -1: none)
   double2* Gx = nullptr;                // the fr seed of the forward solution (support rows; zero elsewhere)
-  unsigned long long* wtrace = nullptr;   // pfr_debug_wave_trace buffer (4 x u64 per wave)
-  int64_t wtrace_cap = 0;
   double* berr_out = nullptr;
   double* d_berr_acc = nullptr;
 
   ~pfr_solver() {
-    for (auto e : lev_ev) (void)hipEventDestroy(e);
-    if (aux_start) (void)hipEventDestroy(aux_start);
-    if (aux_done) (void)hipEventDestroy(aux_done);
-    if (aux) (void)hipStreamDestroy(aux);
     for (void* p : owned) (void)hipFree(p);
     for (auto& c : tev) {
       for (auto& x : c.ev)
@@ -275,7 +230,7 @@ int64_t workspace_bytes(const Symbolic& S, int64_t Fc) {
   int64_t b = 0;
   b += S.factor_entries * Fc * 16;   // F
   b += S.total_rows * Fc * 16;       // WV
-  b += 6 * (int64_t)S.n * Fc * 16;   // X, Y, XA, G, Y2, XR
+  b += 7 * (int64_t)S.n * Fc * 16;   // X, Y, XA, G, Y2, XR, Gx (the selective adjoint refinement's seed)
   b += Fc * (8 + 8 + 4 + 16);        // freqs, loss terms, flags, tq
   b += Fc * (8 + 16) + (int64_t)pfr::residual_parts(S.n) * Fc * 16;   // fr0, mscale, cpart
   if (S.symmetric)   // functional from the bottom-up passes: WVk, YVk, fn_parts, fcoef
@@ -347,12 +302,7 @@ bool level_lds(const pfr_solver* s, int l) {
                          : s->fac_lds < 0 && s->level_maxns[l] >= 16 && wgs < s->fac_lds_wg);
 }
 
-// A11 of level l gathered by k_factor_sym itself (PFR_FUSE_ASM; operator-form sweeps of a symmetric analysis)
-bool level_fused(const pfr_solver* s, int l, int mode) { return s->sym && s->fuse_asm && mode == 0 && !level_lds(s, l); }
-
-// after_panel(l): called once level l's L21 panel is launched (its L factor complete in stream order)
-int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nvalid, hipStream_t st,
-               const std::function<void(int)>& after_panel = nullptr) {
+int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nvalid, hipStream_t st) {
   const int L = (int)s->level_ptr.size() - 1;
   const int ngroups = (int)(s->Fc / 64);
   const bool kt = (s->timing & 2) && s->n_tev < (int)s->tev.size() && !s->tev[s->n_tev].kev.empty();
@@ -360,11 +310,7 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
   auto mark = [&](int l, int c) {
     if (kt) (void)hipEventRecord(kev[6 * l + c], st);
   };
-  // the narrow top as one dependency-driven launch (PFR_FLOW bit 2; operator-form sweeps of a symmetric analysis)
-  const bool fflow = (s->flow & 4) && s->ffd.ntasks > 0 && mode == 0 && s->sym && s->schur_bc == 16 && !after_panel;
-  const int l_end = fflow ? s->fflow_lcut : L;
-  s->timed_levels = l_end;
-  for (int l = 0; l < l_end; ++l) {
+  for (int l = 0; l < L; ++l) {
     int nf = s->level_ptr[l + 1] - s->level_ptr[l];
     mark(l, 0);
     // panel: enough workgroups (front x 16 frequencies) to fill the chip -> one wave
@@ -376,70 +322,29 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     const int64_t wfill = (4096 + wgs - 1) / wgs;
     const int Wp = (int)std::max<int64_t>(
         1, s->sym ? std::min<int64_t>(fac_wmax, wfill) : std::min<int64_t>(s->level_W[l], wfill));
-    // A11 in LDS: PFR_FAC_LDS = n > 0: levels whose largest pivot block has >= n pivots; -1: levels on which the
-    // global-memory kernel would get fewer than PFR_FAC_LDS_WG workgroups (the top of the tree in small chunks:
-    // 512 frequencies levels 10-16, 2,048 level 16 -- faster per level there, slower elsewhere; the default
-    // since the MMD ordering: 512-frequency sweeps 31.8k -> 32.6k freq-solves/s, 4,096 unchanged)
-    const bool lds = level_lds(s, l);
-    // the A11 assembly fused into the global-memory LU (k_factor_sym gathers its own pivot block)
-    const bool fused = level_fused(s, l, mode);
-    if (!fused)
-      pfr::launch_assemble(mode, s->d_asm + s->asm_ptr[l], s->asm_ptr[l + 1] - s->asm_ptr[l],
-                           s->d_asm_xp + s->asm_ptr[l] / 8, s->d_asm_x, ngroups, s->F, s->Fc, s->freqs, s->K, s->M,
-                           data, ds, nvalid, st);
+    pfr::launch_assemble(mode, s->d_asm + s->asm_ptr[l], s->asm_ptr[l + 1] - s->asm_ptr[l],
+                         s->d_asm_xp + s->asm_ptr[l] / 8, s->d_asm_x, ngroups, s->F, s->Fc, s->freqs, s->K, s->M,
+                         data, ds, nvalid, st);
     mark(l, 1);
-    pfr::AsmArgs asmb;
-    if (fused) {
-      asmb.recs = s->d_asm;
-      asmb.rec0 = s->d_rec0;
-      asmb.xptr = s->d_asm_xp;
-      asmb.xl = s->d_asm_x;
-      asmb.freqs = s->freqs;
-      asmb.K = s->K;
-      asmb.M = s->M;
-    }
-    if (lds)
-      pfr::launch_factor_lds(s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_maxns[l], s->fac_lds_qf, s->F, s->Fc,
-                             s->flags, st);
+    if (level_lds(s, l))
+      pfr::launch_factor_lds(s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_maxns[l], s->F, s->Fc, s->flags, st);
     else
-      pfr::launch_factor(s->sym, s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st,
-                         asmb);
+      pfr::launch_factor(s->sym, s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st);
     mark(l, 2);
+    // the software-pipelined L21 prefix on the launches with few waves (symmetric analyses, operator form)
+    const int64_t owaves = (int64_t)(s->item_ptr[l + 1] - s->item_ptr[l]) * ngroups;
     pfr::launch_offdiag(mode, s->P, s->d_items + s->item_ptr[l], s->item_ptr[l + 1] - s->item_ptr[l], s->d_orec,
                         s->d_oxp + s->item_ptr[l], s->d_ox, ngroups, s->F, s->Fc, s->freqs, s->K, s->M, data, ds,
-                        nvalid, s->off_small ? s->level_maxns[l] : pfr::MAX_FRONT, st, s->sym ? s->off_rl : 0,
-                        (int64_t)(s->item_ptr[l + 1] - s->item_ptr[l]) * ngroups >= s->off_swz_min,
-                        s->sym && s->off_shu > 0 && !s->shu_ptr.empty() &&
-                                (int64_t)(s->item_ptr[l + 1] - s->item_ptr[l]) * ngroups < s->off_shu
-                            ? s->d_shu + s->shu_ptr[l] : nullptr,
-                        s->shu_ptr.empty() ? 0 : s->shu_ptr[l + 1] - s->shu_ptr[l],
-                        (int64_t)(s->item_ptr[l + 1] - s->item_ptr[l]) * ngroups < s->off_pu_waves ? s->off_pu : 2,
-                        s->off_shu_st);
-    if (after_panel) after_panel(l);
+                        nvalid, s->level_maxns[l], st, s->sym && owaves < s->off_pu_waves);
     mark(l, 3);
-    pfr::launch_schur_blk(s->schur_bc, s->P, s->d_blocks + s->blk_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
-                          s->d_bg1 + (int64_t)s->blk_ptr[l] * 16 * s->schur_bc, s->d_bgxp + s->blk_ptr[l], s->d_bgx, ngroups, s->F,
+    pfr::launch_schur_blk(s->P, s->d_blocks + s->blk_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
+                          s->d_bg1 + (int64_t)s->blk_ptr[l] * 16 * 16, s->d_bgxp + s->blk_ptr[l], s->d_bgx, ngroups, s->F,
                           s->Fc, st);
     mark(l, 4);
     pfr::launch_schur(s->sym, s->P, s->d_tiles + s->tile_ptr[l], s->tile_ptr[l + 1] - s->tile_ptr[l],
                       s->d_g1 + (int64_t)s->tile_ptr[l] * pfr::SCHUR_TM * pfr::SCHUR_TN * pfr::SCHUR_SR * pfr::SCHUR_SC,
-                      s->d_gxp + s->tile_ptr[l],
-                      s->d_gx, ngroups, s->F,
-                      s->Fc, st);
+                      s->d_gxp + s->tile_ptr[l], s->d_gx, ngroups, s->F, s->Fc, st);
     mark(l, 5);
-  }
-  if (fflow) {
-    pfr::FactorFlowDesc d = s->ffd;
-    d.flags = s->flags;
-    pfr::AsmArgs asmb;
-    asmb.recs = s->d_asm;
-    asmb.rec0 = s->d_rec0;
-    asmb.xptr = s->d_asm_xp;
-    asmb.xl = s->d_asm_x;
-    asmb.freqs = s->freqs;
-    asmb.K = s->K;
-    asmb.M = s->M;
-    pfr::launch_factor_flow(s->P, d, ngroups, s->F, s->Fc, asmb, st);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -521,75 +426,6 @@ int adjoint_solve(pfr_solver* s, const pfr::RhsDesc& rg, double2* Out, hipStream
   return solve_all(s, 3, 0, rg, s->Y, Out, st, subset);
 }
 
-// Task list of the dependency-driven bottom-up chain (k_lsolve_flow) for the current reaches: levels from
-// flow_lcut up; per level the pivot tasks of every (front, slice) reached (slice 0: the forward rhs reach, slices
-// 1-3: the functional support's reach), then their update-row tasks
-int lflow_build(pfr_solver* s) {
-  constexpr int SRB = 4, W = 4, NZ = 4;
-  const int L = (int)s->level_ptr.size() - 1, ng = (int)(s->Fc / 64);
-  const int nslots = s->fd.nslots;
-  s->lfd.ntasks = 0;
-  if (!(s->flow & 2) || nslots == 0) return PFR_OK;
-  int rc;
-  if (!s->d_lf_tasks) {
-    const int64_t nw = (1 + 2 * (int64_t)nslots * NZ * ng + 3) / 4 * 4;
-    unsigned* dw;
-    if ((rc = s->alloc(&s->d_lf_tasks, (int64_t)nslots * NZ * 17)) || (rc = s->alloc(&s->d_lf_cptr, (int64_t)nslots * NZ + 1)) ||
-        (rc = s->alloc(&s->d_lf_cslot, (int64_t)nslots * NZ + 1)) || (rc = s->alloc(&s->d_lf_parts, nslots)) ||
-        (rc = s->alloc(&dw, nw)))
-      return rc;
-    s->lfd.words = dw;
-    s->lfd.words_bytes = (size_t)nw * sizeof(unsigned);
-  }
-  auto reached = [&](int t, int z) { return s->reach_host[z == 0 ? 0 : 1][t] != 0; };
-  std::vector<int32_t> parts(nslots, 0), cptr(1, 0), cslot;
-  std::vector<std::vector<int>> kids(nslots);
-  for (size_t t = 0; t < s->flow_slot.size(); ++t) {
-    const int sl = s->flow_slot[t];
-    if (sl < 0) continue;
-    const int r = s->front_f[t] - s->front_ns[t];
-    parts[sl] = r == 0 ? 0 : std::max(1, std::min(16, (r + SRB * W - 1) / (SRB * W)));
-    const int p = s->front_parent[t];
-    if (p >= 0 && s->flow_slot[p] >= 0) kids[s->flow_slot[p]].push_back((int)t);
-  }
-  std::vector<int> slot_front(nslots);
-  for (size_t t = 0; t < s->flow_slot.size(); ++t)
-    if (s->flow_slot[t] >= 0) slot_front[s->flow_slot[t]] = (int)t;
-  for (int sl = 0; sl < nslots; ++sl)
-    for (int z = 0; z < NZ; ++z) {
-      for (int c : kids[sl])
-        if (reached(c, z) && parts[s->flow_slot[c]] > 0) cslot.push_back(s->flow_slot[c]);
-      cptr.push_back((int32_t)cslot.size());
-    }
-  std::vector<int4> tasks;
-  for (int l = s->flow_lcut; l < L; ++l) {
-    for (int e = s->level_ptr[l]; e < s->level_ptr[l + 1]; ++e) {
-      const int t = s->level_fronts_host[e];
-      for (int z = 0; z < NZ; ++z)
-        if (reached(t, z)) tasks.push_back(make_int4(t, z, -1, s->flow_slot[t]));
-    }
-    for (int e = s->level_ptr[l]; e < s->level_ptr[l + 1]; ++e) {
-      const int t = s->level_fronts_host[e];
-      for (int z = 0; z < NZ; ++z)
-        if (reached(t, z))
-          for (int p = 0; p < parts[s->flow_slot[t]]; ++p) tasks.push_back(make_int4(t, z, p, s->flow_slot[t]));
-    }
-  }
-  if (cslot.empty()) cslot.push_back(0);
-  HIP_TRY(hipMemcpy(s->d_lf_cptr, cptr.data(), cptr.size() * 4, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(s->d_lf_cslot, cslot.data(), cslot.size() * 4, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(s->d_lf_parts, parts.data(), parts.size() * 4, hipMemcpyHostToDevice));
-  if (!tasks.empty()) HIP_TRY(hipMemcpy(s->d_lf_tasks, tasks.data(), tasks.size() * sizeof(int4), hipMemcpyHostToDevice));
-  s->lfd.tasks = s->d_lf_tasks;
-  s->lfd.ntasks = (int)tasks.size();
-  s->lfd.cptr = s->d_lf_cptr;
-  s->lfd.cslot = s->d_lf_cslot;
-  s->lfd.parts = s->d_lf_parts;
-  s->lfd.nslots = nslots;
-  (void)ng;
-  return PFR_OK;
-}
-
 // Row lists and buffers of the functional-from-bottom-up path (allocated on first use, lists rebuilt
 // whenever a reach changed)
 int fn_setup(pfr_solver* s) {
@@ -622,7 +458,6 @@ int fn_setup(pfr_solver* s) {
   // at most n rows each (pivot rows are distinct): into the buffers allocated for n
   if (!both.empty()) HIP_TRY(hipMemcpy(s->d_fn_rows, both.data(), both.size() * sizeof(int2), hipMemcpyHostToDevice));
   if (!sup.empty()) HIP_TRY(hipMemcpy(s->d_sup_rows, sup.data(), sup.size() * 4, hipMemcpyHostToDevice));
-  if ((rc = lflow_build(s))) return rc;
   s->fn_ready = true;
   return PFR_OK;
 }
@@ -645,10 +480,7 @@ int fn_bottom_up(pfr_solver* s, int rhs_mode, const pfr::RhsDesc& rf, hipStream_
     rd[k].beta_im = 0.0;
     rd[k].cslot = s->d_noslot;
   }
-  // the narrow top in one dependency-driven launch after the wide levels (PFR_FLOW)
-  const bool flow = (s->flow & 2) && s->lfd.ntasks > 0;
-  const int l_end = flow ? s->flow_lcut : L;
-  for (int l = 0; l < l_end; ++l) {
+  for (int l = 0; l < L; ++l) {
     const int* lvl[4];
     int nf[4];
     lvl[0] = s->d_reach_fronts[0] + s->reach_ptr[0][l];
@@ -661,11 +493,6 @@ int fn_bottom_up(pfr_solver* s, int rhs_mode, const pfr::RhsDesc& rf, hipStream_
     if (nmax == 0) continue;
     pfr::launch_lsolve_multi(rhs_mode, s->P, 4, lvl, nf, solve_W(s, l, nmax), ngroups, s->F, s->Fc, WV, rd, Y, reach,
                              st, solve_split(s, nf[0] + 3 * nf[1]));
-  }
-  if (flow) {
-    pfr::LFlowDesc d = s->lfd;
-    d.flags = s->flags;
-    pfr::launch_lsolve_flow(rhs_mode, s->P, d, ngroups, s->F, s->Fc, WV, rd, Y, reach, st);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -690,26 +517,13 @@ int sym_top_down_support(pfr_solver* s, const pfr::RhsDesc& rd, hipStream_t st) 
 int sym_top_down_pair(pfr_solver* s, hipStream_t st, bool fwd_all = false) {
   const int L = (int)s->level_ptr.size() - 1;
   const int ngroups = (int)(s->Fc / 64);
-  int l_hi = L - 1;
-  if ((s->flow & 1) && s->fd.ntasks > 0) {
-    // the narrow top in one dependency-driven launch, the wide levels below it level by level
-    pfr::FlowDesc d = s->fd;
-    d.flags = s->flags;
-    pfr::launch_usolve2_flow(s->P, d, ngroups, s->F, s->Fc, s->Y, s->X, s->d_reach[0], fwd_all ? nullptr : s->d_reach[1],
-                             s->Y2, s->XA, s->d_reach[1], st);
-    l_hi = s->flow_lcut - 1;
-  }
-  for (int l = l_hi; l >= 0; --l) {
+  for (int l = L - 1; l >= 0; --l) {
     const int nf = s->level_ptr[l + 1] - s->level_ptr[l];
     const bool small = s->level_maxf[l] <= s->us2_small;
-    pfr::launch_usolve2(s->P, s->d_level_fronts + s->level_ptr[l], nf, solve_W(s, l, nf),
-                        small, ngroups,
-                        s->F, s->Fc, s->Y,
-                        s->X, s->d_reach[0], fwd_all ? nullptr : s->d_reach[1], s->Y2, s->XA, s->d_reach[1], st,
-                        solve_split(s, nf), s->us2_cfg,
-                        s->us2_tiny > 0 && s->level_maxns[l] <= s->us2_tiny
-                            ? (s->level_maxns[l] <= 4 ? 4 : s->level_maxns[l] <= 8 ? 8 : s->us2_tiny) : 0,
-                        s->us2_pp);
+    const int tiny = s->us2_tiny > 0 && s->level_maxns[l] <= s->us2_tiny ? (s->level_maxns[l] <= 4 ? 4 : 8) : 0;
+    pfr::launch_usolve2(s->P, s->d_level_fronts + s->level_ptr[l], nf, solve_W(s, l, nf), small, ngroups, s->F, s->Fc,
+                        s->Y, s->X, s->d_reach[0], fwd_all ? nullptr : s->d_reach[1], s->Y2, s->XA, s->d_reach[1], st,
+                        solve_split(s, nf), tiny);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -940,43 +754,30 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     const char* e = getenv(name);
     return e ? std::max(lo, std::min(hi, atoi(e))) : def;
   };
+  // launch-shape and path knobs (the measured-slower variants of rounds 1-4 are in git history, DESIGN.md
+  // section 8): waves per solve / A11 LU workgroup, the small-front paired top-down variant's front limit,
+  // the solve update-part split target, the A11 LU in LDS, the functional from the bottom-up passes, the
+  // contraction in the forward walk, the cotangent's solve-error scale, the one-wave top-down pass, the
+  // Schur block-kernel threshold and the pipelined L21 prefix
   s->solve_wmax = knob("PFR_SOLVE_WMAX", 8, 1, 8);
   s->fac_wmax = knob("PFR_FAC_WMAX", 16, 1, 16);
   s->us2_small = knob("PFR_US2_SMALL", 110, 0, pfr::MAX_FRONT);
-  // 2 (8 pivot rows x 2 values per pass) reads 18 % less than 0 (2 x 4) at the same time: 2,048-frequency sweep
-  // 92.5 -> 75.7 GB over four sweeps, 21.7 ms both (profiles/r04/solve_traffic/)
-  s->us2_cfg = knob("PFR_US2_CFG", 2, 0, 2);
-  s->off_small = knob("PFR_OFF_SMALL", 1, 0, 1);
   s->split_target = knob("PFR_SOLVE_SPLIT", 256, 0, 1 << 20);
-  s->fac_lds = knob("PFR_FAC_LDS", -1, -1, 64);   // LDS holds the lower triangle of up to 64 pivots x 4 frequencies
-  s->fac_lds_wg = knob("PFR_FAC_LDS_WG", 160, 0, 1 << 20);
-  s->fac_lds_qf = knob("PFR_FAC_LDS_QF", 1, 1, 4);
-  if (s->fac_lds_qf == 3) s->fac_lds_qf = 4;
-  s->check_fused = knob("PFR_CHECK_FUSED", 0, 0, 1);   // measured 2.3 ms against 2 x 0.87 ms per 2,048-frequency chunk
+  s->fac_lds = knob("PFR_FAC_LDS", -1, -1, 64);   // LDS holds the lower triangle of up to 64 pivots
   s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);
   s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);
   s->scale_corr = knob("PFR_SCALE_CORR", 1, 0, 1);
-  s->off_swz_min = knob("PFR_OFF_SWZ_MIN", 0, 0, 1 << 30);
-  s->off_shu = knob("PFR_OFF_SHU", 0, 0, 1 << 30);
-  s->off_shu_st = knob("PFR_OFF_SHU_ST", 2, 2, 4) >= 4 ? 4 : 2;
-  // 3 = the software-pipelined prefix; on by default for chunks of <= 1,024 frequencies on the launches with fewer
-  // than 8,000 waves (the narrow levels of C4's per-rank sweeps: 512 frequencies 35.3-35.7k -> 36.2-36.6k
-  // freq-solves/s; 2,048-frequency chunks unchanged, profiles/r04/offdiag_layout/pu3_*)
-  s->off_pu = knob("PFR_OFF_PU", 3, 2, 8);
-  s->off_pu_waves = -1;         // after Fc is known (below)
   // 8: the bottom two levels at 2,048 frequencies 685 / 612 -> 509 / 489 us (profiles/r04/experiments/us2_tiny_*)
-  s->us2_tiny = knob("PFR_US2_TINY", 8, 0, 64);
-  s->us2_pp = knob("PFR_US2_PP", 0, 0, 1);   // > 8: k_usolve2_wave on the levels with blocks of 9 .. this
-  s->off_rl = knob("PFR_OFF_RL", 0, 0, 124);   // n: one row per wave (n = 16, 24, 32); 100 + n: two rows (n = 16, 24)
-  if (s->off_rl > 100 && s->off_rl % 100 > 24) s->off_rl = 124;
-  s->fuse_asm = knob("PFR_FUSE_ASM", 0, 0, 1);   // measured slower (2,048-frequency chunk: A11 classes 4.1 -> 6.6 ms)
-  s->flow = knob("PFR_FLOW", 0, 0, 7);   // bit 0: paired top-down pass, bit 1: bottom-up chain, bit 2: factorisation
-  s->flow_fwg = knob("PFR_FLOW_FWG", 256, 0, 1 << 20);
-  s->flow_wg = knob("PFR_FLOW_WG", 1024, 0, 1 << 20);   // functional from the bottom-up passes (symmetric paired sweeps)
+  s->us2_tiny = knob("PFR_US2_TINY", 8, 0, 8);
+  const int blk_min = knob("PFR_SCHUR_BLK_MIN", 24, 0, pfr::MAX_FRONT);   // update blocks of >= this many rows: block kernel
   s->n = S.n;
+  s->nnz = S.nnz;  s->n = S.n;
   s->nnz = S.nnz;
   s->Fc = round64(max_batch);
-  if (s->off_pu_waves < 0) s->off_pu_waves = knob("PFR_OFF_PU_WAVES", s->Fc <= 1024 ? 8000 : 0, 0, 1 << 30);
+  // the pipelined L21 prefix on launches of fewer than 8,000 waves in chunks of <= 1,024 frequencies (the narrow
+  // levels of C4's per-rank sweeps: 512 frequencies 35.3-35.7k -> 36.2-36.6k freq-solves/s; 2,048-frequency
+  // chunks unchanged, profiles/r04/offdiag_layout/pu3_*)
+  s->off_pu_waves = knob("PFR_OFF_PU_WAVES", s->Fc <= 1024 ? 8000 : 0, 0, 1 << 30);
   s->level_ptr = S.level_ptr;
   s->level_maxf = S.level_maxf;
   s->perm = S.perm;
@@ -1014,20 +815,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     std::vector<int32_t> bg1, bgxp(1, 0);
     std::vector<int2> bgx;
     s->blk_ptr.assign(1, 0);
-    // update blocks of at least this many rows go to the 16 x 16 block kernel (symmetric mode)
-    const char* bce = getenv("PFR_SCHUR_BC");   // tuning knob: Schur block columns (16 or 8)
-    s->schur_bc = bce && atoi(bce) == 8 ? 8 : 16;
-    const char* be = getenv("PFR_SCHUR_BLK_MIN");
-    const int blk_min = be ? atoi(be) : 24;
     const int L = (int)S.level_ptr.size() - 1;
-    // the factorisation flow's region: every update block there goes through the block kernel (its Schur tasks)
-    s->fflow_lcut = L;
-    if (sym && (s->flow & 4)) {
-      const int64_t ng = s->Fc / 64;
-      while (s->fflow_lcut > 0 && (int64_t)(S.level_ptr[s->fflow_lcut] - S.level_ptr[s->fflow_lcut - 1]) * ng < s->flow_fwg)
-        --s->fflow_lcut;
-    }
-    std::vector<int32_t> blk_begin(S.fronts.size(), 0), blk_end(S.fronts.size(), 0);
     for (int l = 0; l < L; ++l) {
       for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
         const int t = S.level_fronts[e];
@@ -1056,11 +844,9 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
           }
         }
         std::sort(more.begin(), more.end());
-        blk_begin[t] = blk_end[t] = (int32_t)bv.size();
-        if (sym && ((blk_min > 0 && r >= blk_min) || (F.level >= s->fflow_lcut && r > 0))) {
-          // 16 x BC blocks touching the lower triangle; wave w owns the 4 x 4 tile (w / tcw, w % tcw)
-          constexpr int B = pfr::SCHUR_BLK;
-          const int BC = s->schur_bc, tcw = BC / 4;
+        if (sym && blk_min > 0 && r >= blk_min) {
+          // 16 x 16 blocks touching the lower triangle; wave w owns the 4 x 4 tile (w / 4, w % 4)
+          constexpr int B = pfr::SCHUR_BLK, BC = pfr::SCHUR_BLK, tcw = BC / 4;
           for (int i0 = 0; i0 < r; i0 += B)
             for (int j0 = 0; j0 < i0 + B; j0 += BC) {
               bv.push_back(make_int4(t, i0, j0, 0));
@@ -1079,7 +865,6 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
               bgxp.push_back((int32_t)bgx.size());
             }
           blk_front[t] = 1;
-          blk_end[t] = (int32_t)bv.size();
           continue;
         }
         // super-tiles of (SCHUR_TM SCHUR_SR) x (SCHUR_TN SCHUR_SC): lane group `sub` owns the
@@ -1138,7 +923,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     std::vector<int2> ax, orec, ox;
     s->asm_ptr.assign(1, 0);
     s->item_ptr.assign(1, 0);
-    std::vector<int32_t> nzm, s1m, rec0(S.fronts.size(), 0), item_begin(S.fronts.size(), 0);
+    std::vector<int32_t> nzm, s1m;
     std::vector<std::pair<int32_t, int32_t>> morem;   // (a * f + b, id)
     for (int l = 0; l < L; ++l) {
       for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
@@ -1178,7 +963,6 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
           for (; lo != morem.end() && lo->first == a * f + b; ++lo) out.push_back(lo->second);
           return out;
         };
-        rec0[t] = (int32_t)av.size();
         for (int a = 0; a < ns; ++a)
           for (int b = 0; b < (sym ? a + 1 : ns); ++b) {   // symmetric: A11's lower triangle only
             const int k = (int)(av.size() % 8);
@@ -1187,7 +971,6 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
             for (int32_t id : extras(a, b)) ax.push_back(make_int2(k, id));
             if (av.size() % 8 == 0) axp.push_back((int32_t)ax.size());
           }
-        item_begin[t] = (int32_t)iv.size();
         for (int kind = 0; kind < (sym ? 1 : 2); ++kind)   // symmetric: U12 = diag(U11) L21^T implicit
           for (int i0 = ns; i0 < f; i0 += pfr::OFF_G * pfr::OFF_RPL) {
             iv.push_back(make_int4(t, i0, kind, (int32_t)orec.size()));
@@ -1237,23 +1020,19 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       g_s[1] += (int64_t)gxp.back();                       // gx may hold a placeholder
       s->alg_bytes[0] = 16 * (s_a11 + g_a11);             // A11 (symmetric: lower) stores + child entries gathered
       s->alg_bytes[1] = 16 * (s_a11 + s_ns2);             // A11 read + L11/U11 write
-      // the same per level, and the fused form (children's entries gathered + L11/U11 written: A11 itself
-      // never makes a round trip through HBM)
+      // the same per level
       s->lev_asm_bytes.assign(L, 0);
       s->lev_lu_bytes.assign(L, 0);
-      s->lev_fused_bytes.assign(L, 0);
       for (const Front& F : S.fronts) {
         const int64_t a11 = sym ? (int64_t)F.ns * (F.ns + 1) / 2 : (int64_t)F.ns * F.ns;
         s->lev_asm_bytes[F.level] += 16 * a11;
         s->lev_lu_bytes[F.level] += 16 * (a11 + (int64_t)F.ns * F.ns);
-        s->lev_fused_bytes[F.level] += 16 * (int64_t)F.ns * F.ns;
       }
       for (int l = 0; l < L; ++l) {
         int64_t g = 0;
         for (int r = s->asm_ptr[l]; r < s->asm_ptr[l + 1]; ++r) g += av[r].z >= 0;
         g += axp[s->asm_ptr[l + 1] / 8] - axp[s->asm_ptr[l] / 8];
         s->lev_asm_bytes[l] += 16 * g;
-        s->lev_fused_bytes[l] += 16 * g;
       }
       s->alg_bytes[2] = 16 * (s_rns + g_off + s_ns2);     // L21/U12 stores + gathered children + L11/U11 read
       for (int k = 0; k < 2; ++k)                         // A22 stores + gathered children + L21/U12 read
@@ -1266,97 +1045,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     if (ox.empty()) ox.push_back(make_int2(0, 0));
     if ((rc = s->up(&s->d_asm, av)) || (rc = s->up(&s->d_asm_xp, axp)) || (rc = s->up(&s->d_asm_x, ax)) ||
         (rc = s->up(&s->d_items, iv)) || (rc = s->up(&s->d_orec, orec)) || (rc = s->up(&s->d_oxp, oxp)) ||
-        (rc = s->up(&s->d_ox, ox)) || (rc = s->up(&s->d_rec0, rec0)))
+        (rc = s->up(&s->d_ox, ox)))
       return bail(rc);
-    if (sym) {
-      // k_offdiag_shu workgroup tasks per level: (first item relative to the level, items <= 4), one front each
-      std::vector<int4> sh;
-      s->shu_ptr.assign(1, 0);
-      for (int l = 0; l < L; ++l) {
-        for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
-          const int t = S.level_fronts[e];
-          const int end = e + 1 < S.level_ptr[l + 1] ? item_begin[S.level_fronts[e + 1]] : s->item_ptr[l + 1];
-          for (int i = item_begin[t]; i < end; i += 4)
-            sh.push_back(make_int4(i - s->item_ptr[l], std::min(4, end - i), t, 0));
-        }
-        s->shu_ptr.push_back((int32_t)sh.size());
-      }
-      if (sh.empty()) sh.push_back(make_int4(0, 0, 0, 0));
-      if ((rc = s->up(&s->d_shu, sh))) return bail(rc);
-    }
-    if (s->fflow_lcut < L) {
-      // task list of the factorisation flow, levels upwards: per level the A11 tasks, then 16-item L21 tasks,
-      // then one task per update block
-      std::vector<int32_t> slot(S.fronts.size(), -1), item_end, nb, nc, cptr(1, 0), cslot;
-      std::vector<int4> tasks;
-      int nslots = 0;
-      for (int l = s->fflow_lcut; l < L; ++l)
-        for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) slot[S.level_fronts[e]] = nslots++;
-      item_end.resize(nslots);
-      nb.resize(nslots);
-      nc.resize(nslots);
-      std::vector<std::vector<int>> kids(nslots);
-      for (size_t t = 0; t < S.fronts.size(); ++t) {
-        if (slot[t] < 0) continue;
-        const int sl = slot[t];
-        nc[sl] = blk_end[t] - blk_begin[t];
-        if (S.fronts[t].parent >= 0 && slot[S.fronts[t].parent] >= 0) kids[slot[S.fronts[t].parent]].push_back((int)t);
-      }
-      // item ranges: a front's items are consecutive, the next front's (in level order) start where it ends
-      for (int l = s->fflow_lcut; l < L; ++l)
-        for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
-          const int t = S.level_fronts[e];
-          const int end = e + 1 < S.level_ptr[l + 1] ? item_begin[S.level_fronts[e + 1]] : s->item_ptr[l + 1];
-          item_end[slot[t]] = end;
-          nb[slot[t]] = (end - item_begin[t] + 15) / 16;
-        }
-      for (int sl = 0; sl < nslots; ++sl) {
-        for (int c : kids[sl])
-          if (nc[slot[c]] > 0) cslot.push_back(slot[c]);
-        cptr.push_back((int32_t)cslot.size());
-      }
-      for (int l = s->fflow_lcut; l < L; ++l) {
-        for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
-          const int t = S.level_fronts[e];
-          tasks.push_back(make_int4(0, t, 0, slot[t]));
-        }
-        for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
-          const int t = S.level_fronts[e];
-          for (int it = item_begin[t]; it < item_end[slot[t]]; it += 16) tasks.push_back(make_int4(1, t, it, slot[t]));
-        }
-        for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
-          const int t = S.level_fronts[e];
-          for (int b = blk_begin[t]; b < blk_end[t]; ++b) tasks.push_back(make_int4(2, t, b, slot[t]));
-        }
-      }
-      if (cslot.empty()) cslot.push_back(0);
-      int4* dt;
-      int32_t *dcp, *dcs, *die, *dnb, *dnc;
-      unsigned* dw;
-      const int64_t nw = (1 + 3 * (int64_t)nslots * (s->Fc / 64) + 3) / 4 * 4;
-      if ((rc = s->up(&dt, tasks)) || (rc = s->up(&dcp, cptr)) || (rc = s->up(&dcs, cslot)) || (rc = s->up(&die, item_end)) ||
-          (rc = s->up(&dnb, nb)) || (rc = s->up(&dnc, nc)) || (rc = s->alloc(&dw, nw)))
-        return bail(rc);
-      pfr::FactorFlowDesc& d = s->ffd;
-      d.tasks = dt;
-      d.ntasks = (int)tasks.size();
-      d.cptr = dcp;
-      d.cslot = dcs;
-      d.item_end = die;
-      d.nb = dnb;
-      d.nc = dnc;
-      d.nslots = nslots;
-      d.words = dw;
-      d.words_bytes = (size_t)nw * sizeof(unsigned);
-      d.items = s->d_items;
-      d.orec = s->d_orec;
-      d.oxp = s->d_oxp;
-      d.ox = s->d_ox;
-      d.blocks = s->d_blocks;
-      d.bg1 = s->d_bg1;
-      d.bgxp = s->d_bgxp;
-      d.bgx = s->d_bgx;
-    }
   }
   std::vector<int32_t> cp(colptr, colptr + S.n + 1), ri(rowind, rowind + S.nnz);
   if ((rc = s->up(&s->d_colptr, cp)) || (rc = s->up(&s->d_rowind, ri))) return bail(rc);
@@ -1410,7 +1100,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     if ((rc = compress(S.prow, S.pcol, &s->d_rptr, &s->d_ridx, &s->d_rnz)) ||
         (rc = compress(S.pcol, S.prow, &s->d_cptr, &s->d_cidx, &s->d_cnz)) || (rc = s->up(&s->d_walk, S.iperm)))
       return bail(rc);
-    // union row structure of the fused contraction + checks
+    // union row structure of the gradient contraction (k_contract_eg)
     std::vector<int64_t> key(S.nnz);
     std::vector<int32_t> ord(S.nnz);
     for (int64_t e = 0; e < S.nnz; ++e) {
@@ -1442,19 +1132,9 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       for (const int4& v : rows[i]) uent.push_back(make_int4(v.x, v.y, v.z, i));
       uptr[t + 1] = (int32_t)uent.size();
     }
-    std::vector<int32_t> ublk(1, 0);   // entry offsets at row starts
-    // enough single-wave workgroups to fill the chip (many short walks: the walk is latency-bound)
-    s->n_ublk = std::max(1, std::min(kContractBlocks, S.n));
-    for (int b = 1; b < s->n_ublk; ++b) {
-      const int64_t target = (int64_t)uent.size() * b / s->n_ublk;
-      const int32_t at = *std::lower_bound(uptr.begin(), uptr.end(), (int32_t)target);
-      ublk.push_back(std::max(ublk.back(), at));
-    }
-    ublk.push_back((int32_t)uent.size());
     s->n_uent = (int)uent.size();
     for (int pad = 0; pad < 4; ++pad) uent.push_back(make_int4(-1, -1, -1, -1));   // a step reads 4 entries at once
-    if ((rc = s->up(&s->d_uent, uent)) || (rc = s->up(&s->d_ublk, ublk)) || (rc = s->alloc(&s->d_kme, 3 * ((int64_t)s->n_uent + 4))))
-      return bail(rc);
+    if ((rc = s->up(&s->d_uent, uent))) return bail(rc);
   }
   s->P = DevPattern{d_fronts, idx, relpos, rowf, ap, ac, an, ep, es, pm, pr, pc, S.n};
   {
@@ -1487,61 +1167,6 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       (rc = s->alloc(&s->gind, Fc / 64)) || (rc = s->alloc(&s->glist, pfr::REFINE_CAP)))
     return bail(rc);
   HIP_TRY(hipMemset(s->d_berr_acc, 0, 2 * Fc * sizeof(double)));
-  if (s->sym && s->flow) {
-    // task list of the dependency-driven top-down pass: levels from the root down while narrow; per level its
-    // fronts' update parts (S per front: every wave of a part at least one SR-row group), then their
-    // triangular parts -- a topological order (a front after its parent's triangular part, its triangular
-    // part after its own update parts)
-    const int L = (int)S.level_ptr.size() - 1, ng = (int)(Fc / 64);
-    constexpr int SR = 4, W = 4;
-    int lcut = L;
-    while (lcut > 0 && (int64_t)(S.level_ptr[lcut] - S.level_ptr[lcut - 1]) * ng < s->flow_wg) --lcut;
-    std::vector<int32_t> slot(S.fronts.size(), -1), pslot(S.fronts.size(), -1);
-    std::vector<int4> tasks;
-    int nslots = 0;
-    for (int l = L - 1; l >= lcut; --l) {
-      for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
-        const int t = S.level_fronts[e];
-        const Front& F = S.fronts[t];
-        slot[t] = nslots++;
-        const int parts = std::max(1, std::min(16, (F.ns + SR * W - 1) / (SR * W)));
-        for (int p = 0; p < parts; ++p) tasks.push_back(make_int4(t, p, parts, slot[t]));
-      }
-      for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
-        const int t = S.level_fronts[e];
-        const Front& F = S.fronts[t];
-        const int parts = std::max(1, std::min(16, (F.ns + SR * W - 1) / (SR * W)));
-        tasks.push_back(make_int4(t, -1, parts, slot[t]));
-      }
-    }
-    for (size_t t = 0; t < S.fronts.size(); ++t)
-      if (slot[t] >= 0 && S.fronts[t].parent >= 0) pslot[t] = slot[S.fronts[t].parent];
-    s->flow_lcut = lcut;
-    s->flow_slot = slot;
-    if (!tasks.empty()) {
-      int4* dt;
-      int32_t* dp;
-      unsigned* dw;
-      const int64_t nw = (1 + 2 * (int64_t)nslots * ng + 3) / 4 * 4;   // memset block: a multiple of 16 B
-      if ((rc = s->up(&dt, tasks)) || (rc = s->up(&dp, pslot)) || (rc = s->alloc(&dw, nw))) return bail(rc);
-      s->fd.tasks = dt;
-      s->fd.ntasks = (int)tasks.size();
-      s->fd.pslot = dp;
-      s->fd.nslots = nslots;
-      s->fd.words = dw;
-      s->fd.words_bytes = (size_t)nw * sizeof(unsigned);
-    }
-  }
-  // PFR_AUX=1: run the forward sparse L-solve on a side stream, level by level behind the
-  // factorisation (+2% with one solver lane; with two lanes the extra queues cost more than it saves)
-  const char* aux_env = getenv("PFR_AUX");
-  if (s->sym && aux_env && atoi(aux_env) == 1) {
-    HIP_TRY(hipStreamCreateWithFlags(&s->aux, hipStreamNonBlocking));
-    HIP_TRY(hipEventCreateWithFlags(&s->aux_start, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&s->aux_done, hipEventDisableTiming));
-    s->lev_ev.resize(s->level_ptr.size() - 1);
-    for (auto& e : s->lev_ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  }
   *out = s;
   return PFR_OK;
 }
@@ -1573,28 +1198,6 @@ int pfr_debug_solution(pfr_solver* s, int32_t which, int32_t q, double* out) {
     out[2 * (int64_t)s->perm[p]] = col[p].x;
     out[2 * (int64_t)s->perm[p] + 1] = col[p].y;
   }
-  return PFR_OK;
-}
-
-int pfr_debug_wave_trace(pfr_solver* s, int64_t cap, uint64_t* out_host, int64_t* count) {
-  if (!s || cap < 0 || (cap > 0 && !out_host) || !count) return fail(PFR_ERR_ARG, "bad wave-trace arguments");
-  HIP_TRY(hipSetDevice(s->device));
-  HIP_TRY(hipDeviceSynchronize());
-  if (cap == 0) {             // start: a device buffer of *count records for the following launches
-    if (s->wtrace) HIP_TRY(hipFree(s->wtrace));
-    s->wtrace = nullptr;
-    s->wtrace_cap = *count;
-    if (s->wtrace_cap > 0) {
-      HIP_TRY(hipMalloc(&s->wtrace, (size_t)s->wtrace_cap * 32));
-      HIP_TRY(hipMemset(s->wtrace, 0, (size_t)s->wtrace_cap * 32));
-    }
-    if (pfr::set_wave_trace(s->wtrace, s->wtrace_cap)) return fail(PFR_ERR_HIP, "wave trace symbols");
-    return PFR_OK;
-  }
-  const int64_t n = std::min<int64_t>(std::min<int64_t>(pfr::wave_trace_count(), s->wtrace_cap), cap);
-  if (n > 0) HIP_TRY(hipMemcpy(out_host, s->wtrace, (size_t)n * 32, hipMemcpyDeviceToHost));
-  *count = n;
-  pfr::set_wave_trace(nullptr, 0);
   return PFR_OK;
 }
 
@@ -1634,11 +1237,11 @@ int pfr_last_kernel_timings(const pfr_solver* s, double* ms, int64_t* launches) 
   }
   if (!(s->timing & 2) || s->n_tev == 0) return PFR_OK;
   HIP_TRY(hipEventSynchronize(s->tev[s->n_tev - 1].ev[5]));
-  const int L = std::min((int)s->level_ptr.size() - 1, s->timed_levels);   // the flow region has no level events
+  const int L = (int)s->level_ptr.size() - 1;
   for (int c = 0; c < s->n_tev; ++c) {
     if (!s->tev[c].used[0]) continue;
     for (int l = 0; l < L; ++l) {
-      const int work[5] = {level_fused(s, l, 0) ? 0 : s->asm_ptr[l + 1] - s->asm_ptr[l], s->level_ptr[l + 1] - s->level_ptr[l],
+      const int work[5] = {s->asm_ptr[l + 1] - s->asm_ptr[l], s->level_ptr[l + 1] - s->level_ptr[l],
                            s->item_ptr[l + 1] - s->item_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
                            s->tile_ptr[l + 1] - s->tile_ptr[l]};
       for (int k = 0; k < 5; ++k) {
@@ -1655,16 +1258,10 @@ int pfr_last_kernel_timings(const pfr_solver* s, double* ms, int64_t* launches) 
 int pfr_solver_alg_bytes(const pfr_solver* s, int64_t* bytes) {
   if (!s || !bytes) return fail(PFR_ERR_ARG, "null argument");
   for (int i = 0; i < 5; ++i) bytes[i] = s->alg_bytes[i];
-  // levels whose A11 assembly is fused into the LU (operator-form sweeps): class 0 empty there, class 1 the
-  // fused form
   bytes[0] = bytes[1] = 0;
   for (int l = 0; l + 1 < (int)s->level_ptr.size(); ++l) {
-    if (level_fused(s, l, 0)) {
-      bytes[1] += s->lev_fused_bytes[l];
-    } else {
-      bytes[0] += s->lev_asm_bytes[l];
-      bytes[1] += s->lev_lu_bytes[l];
-    }
+    bytes[0] += s->lev_asm_bytes[l];
+    bytes[1] += s->lev_lu_bytes[l];
   }
   return PFR_OK;
 }
@@ -1732,7 +1329,7 @@ int pfr_set_stiffness(pfr_solver* s, int32_t n_stiff, const double* stiff_dev, c
   }
   // the entry-ordered copy of S the gradient contraction reads (taken now: a later change of the
   // registered buffer needs another pfr_set_stiffness, include/pfr.h)
-  pfr::launch_gather_entries(s->d_uent, s->n_uent + 4, nullptr, nullptr, stiff_dev, n_stiff, nullptr, s->d_se, nullptr);
+  pfr::launch_gather_entries(s->d_uent, s->n_uent + 4, stiff_dev, n_stiff, s->d_se, nullptr);
   HIP_TRY(hipStreamSynchronize(nullptr));
   return PFR_OK;
 }
@@ -1843,7 +1440,6 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
   hipStream_t st = (hipStream_t)stream;
   reset_timing(s);
   const int64_t Fc = s->Fc;
-  const int ngroups = (int)(Fc / 64);
   const bool refine = (s->check_mode & PFR_CHECK_REFINE) != 0;
   // functional correction: the adjoint of fr is solved in every sweep (in a loss sweep it IS the loss
   // adjoint up to one scalar per frequency) and the forward residual walk adds Re(mu^T r) to fr
@@ -1851,16 +1447,10 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
   const bool adj = reverse || correct;                 // an adjoint solve runs
   const bool paired = s->sym && adj && !refine;        // one top-down pass for both solutions
   const bool fwd_late = paired || correct;             // forward residual walk after the adjoint
-  const bool fn_fast = paired && !s->aux && s->fn_dot; // functional from the bottom-up passes
+  const bool fn_fast = paired && s->fn_dot;            // functional from the bottom-up passes
   if (fn_fast)
     if (int rc0 = fn_setup(s)) return rc0;
   bool used[5] = {true, true, true, adj, adj};
-  // K may have been recombined since the last sweep (pfr_combine, any solver): refresh the entry-ordered
-  // copy the fused contraction + checks read (2.6 % of one chunk's traffic at C3, once per call) -- only
-  // when that fused check path will run
-  const bool fused_checks = reverse && !correct && s->check_fused && (s->check_mode & (PFR_CHECK_FORWARD | PFR_CHECK_ADJOINT));
-  if (fused_checks)
-    pfr::launch_gather_entries(s->d_uent, s->n_uent + 4, s->K, s->M, nullptr, 0, s->d_kme, nullptr, st);
   for (int64_t q0 = 0; q0 < nfreq; q0 += Fc) {
     const int nv = (int)std::min<int64_t>(Fc, nfreq - q0);
     HIP_TRY(hipMemcpyAsync(s->freqs, freqs_dev + q0, nv * sizeof(double), hipMemcpyDeviceToDevice, st));
@@ -1876,7 +1466,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
     rd.freqs = s->freqs;
     pfr::RhsDesc rf = rd;
     int rc;
-    if (paired && !s->aux) {
+    if (paired) {
       pfr::launch_dirichlet_rhs(0, dir_desc(s), s->n_crow, rd, nullptr, s->Bc, s->Fc, st);
       rf.cslot = s->d_cslot;
       rf.Bc = s->Bc;
@@ -1887,28 +1477,6 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
       } else if ((rc = solve_all(s, 0, s->n_crow > 0 ? 3 : 0, rf, nullptr, s->Y, st, 0))) {
         return rc;
       }
-    } else if (paired) {
-      // forward bottom-up solve over the rhs reach on the side stream, level l as soon as level
-      // l's L factor is formed (it needs nothing else), overlapping the factorisation
-      const int ngroups_ = ngroups;
-      HIP_TRY(hipEventRecord(s->aux_start, st));
-      HIP_TRY(hipStreamWaitEvent(s->aux, s->aux_start, 0));
-      pfr::launch_dirichlet_rhs(0, dir_desc(s), s->n_crow, rd, nullptr, s->Bc, s->Fc, s->aux);
-      rf.cslot = s->d_cslot;
-      rf.Bc = s->Bc;
-      const int rmode = s->n_crow > 0 ? 3 : 0;
-      auto hook = [&](int l) {
-        (void)hipEventRecord(s->lev_ev[l], st);
-        (void)hipStreamWaitEvent(s->aux, s->lev_ev[l], 0);
-        const int nf = s->reach_ptr[0][l + 1] - s->reach_ptr[0][l];
-        pfr::launch_solve(0, rmode, true, s->P, s->d_reach_fronts[0] + s->reach_ptr[0][l], nf, solve_W(s, l, nf), ngroups_,
-                          s->F, s->Fc, s->WV, rf, nullptr, s->Y, s->d_reach[0], s->aux, solve_split(s, nf));
-      };
-      rc = factor_all(s, 0, nullptr, 0, nv, st, hook);
-      if (rc) return rc;
-      HIP_TRY(hipEventRecord(s->aux_done, s->aux));
-      HIP_TRY(hipStreamWaitEvent(st, s->aux_done, 0));
-      record(s, 1, st);
     } else {
       rc = factor_all(s, 0, nullptr, 0, nv, st);
       if (rc) return rc;
@@ -1985,7 +1553,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
       bool want_f = fwd_late && (s->check_mode & PFR_CHECK_FORWARD);
       bool want_a = (s->check_mode & PFR_CHECK_ADJOINT) != 0;
       // the gradient contraction rides on the forward residual walk (loss sweeps with the correction)
-      const bool cwalk = reverse && correct && s->contract_walk && !fused_checks &&
+      const bool cwalk = reverse && correct && s->contract_walk &&
                          (s->n_stiff == 12 || s->n_stiff == 18);
       if (cwalk && !s->kpart) {
         if ((rc = s->alloc(&s->kpart, (int64_t)pfr::residual_parts(s->n) * 18 * Fc))) return rc;
@@ -2039,32 +1607,9 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
         pfr::launch_reduce_q(s->kpart, pfr::residual_parts(s->n), s->n_stiff, msc, nv, Fc, s->partial, st);
       else if (reverse)
         pfr::launch_contract_eg(s->d_uent, s->n_uent, s->d_se, s->n_stiff, s->XA, s->X, Fc, nv, s->partial, st, msc);
-      if (fused_checks && (want_f || want_a)) {
-        // gradient contraction's row walk fused with both checks (PFR_CHECK_FUSED=1)
-        pfr::RowCheckDesc cd;
-        cd.K = s->K;
-        cd.M = s->M;
-        cd.freqs = s->freqs;
-        cd.rhsP = s->rhsP;
-        cd.beta_re = s->beta_re;
-        cd.beta_im = s->beta_im;
-        cd.mass_sum = s->mass_sum;
-        cd.G = s->G;
-        pfr::launch_contract_rows(true, s->d_ublk, s->d_uent, s->n_ublk, ngroups, s->d_se, s->n_stiff, s->d_kme, cd,
-                                  s->XA, s->X, Fc, nv, nullptr, s->d_berr_acc, s->d_berr_acc + Fc, st);
-        for (int w = 0; w < 2; ++w) {
-          double* acc = s->d_berr_acc + w * Fc;
-          if (w == 0 ? want_f : want_a)
-            pfr::launch_berr_finish(acc, Fc, nv, s->check_tol, w == 0 ? PFR_FLAG_BACKWARD_ERROR : PFR_FLAG_BACKWARD_ERROR_ADJ,
-                                    s->flags, s->berr_out, q0, w, st);
-          else
-            HIP_TRY(hipMemsetAsync(acc, 0, Fc * sizeof(double), st));   // computed, not requested: keep zero
-        }
-      } else {
-        // the checks as row / column walks of the original pattern (k_residual)
-        if (want_f) check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st);
-        if (want_a) check_solution(s, 1, 0, 2, rg, nullptr, 0, nv, s->XA, nullptr, q0, st);
-      }
+      // the checks as row / column walks of the original pattern (k_residual)
+      if (want_f) check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st);
+      if (want_a) check_solution(s, 1, 0, 2, rg, nullptr, 0, nv, s->XA, nullptr, q0, st);
       if (reverse) {
         if (!scorr) pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st, msc);
         pfr::launch_reduce(s->partial, cwalk ? (int)(Fc / 64) : pfr::contract_eg_parts(s->n_uent), s->n_stiff, s->tq, s->e,

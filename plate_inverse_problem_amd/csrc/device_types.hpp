@@ -29,35 +29,19 @@ struct DevPattern {
 
 // Schur super-tile: a wavefront = SCHUR_QG frequencies x (SCHUR_SR x SCHUR_SC) lane groups,
 // each lane group one SCHUR_TM x SCHUR_TN register tile -> (SCHUR_TM SCHUR_SR) x
-// (SCHUR_TN SCHUR_SC) entries per wave.
-#ifndef PFR_SCHUR_SR
-#define PFR_SCHUR_SR 1
-#endif
-#ifndef PFR_SCHUR_TM
-#define PFR_SCHUR_TM 4
-#endif
-constexpr int SCHUR_SR = PFR_SCHUR_SR, SCHUR_SC = PFR_SCHUR_SR, SCHUR_QG = 64 / (SCHUR_SR * SCHUR_SC);
-#ifndef PFR_SCHUR_TN
-#define PFR_SCHUR_TN PFR_SCHUR_TM
-#endif
-constexpr int SCHUR_TM = PFR_SCHUR_TM, SCHUR_TN = PFR_SCHUR_TN;
+// (SCHUR_TN SCHUR_SC) entries per wave.  Lane = frequency, one 4 x 4 tile per wave (measured 10 %
+// faster than 16 frequencies x a 2 x 2 arrangement of 4 x 4 tiles).
+constexpr int SCHUR_SR = 1, SCHUR_SC = 1, SCHUR_QG = 64 / (SCHUR_SR * SCHUR_SC);
+constexpr int SCHUR_TM = 4, SCHUR_TN = 4;
 static_assert(SCHUR_SR * SCHUR_SC * SCHUR_QG == 64, "one wavefront per super-tile");
 
 // Off-diagonal panel kernel: a wave = OFF_G lane groups of 64 / OFF_G frequencies, OFF_RPL rows
-// (columns) per lane: OFF_G OFF_RPL rows per wave.
-#ifndef PFR_OFF_G
-#define PFR_OFF_G 1
-#endif
-#ifndef PFR_OFF_RPL
-#define PFR_OFF_RPL 2
-#endif
-constexpr int OFF_G = PFR_OFF_G;
+// (columns) per lane: OFF_G OFF_RPL rows per wave.  Lane = frequency, two rows per lane (measured best of
+// 1 / 2 lane groups and 1 / 2 / 4 rows per lane; the other shapes are in git history).
+constexpr int OFF_G = 1;
+constexpr int OFF_RPL = 2;
 // A11 factorisation kernel: lane groups per wave (64 / FAC_G frequencies each, one front row each)
-#ifndef PFR_FAC_G
-#define PFR_FAC_G 2
-#endif
-constexpr int FAC_G = PFR_FAC_G;
-constexpr int OFF_RPL = PFR_OFF_RPL;
+constexpr int FAC_G = 2;
 
 // Largest front the solve kernels stage index lists for in LDS (checked at solver creation)
 constexpr int MAX_FRONT = 1024;
@@ -67,21 +51,6 @@ constexpr int COEF_MAX = 32;
 struct CoefPack {
   double re[COEF_MAX];
   double im[COEF_MAX];
-};
-
-// The A11 assembly fused into the symmetric A11 LU (k_factor_sym prologue, PFR_FUSE_ASM): the
-// assembly records of the level (dst, nz, first child source, -) with each front's first record at
-// rec0[front] (its ns (ns + 1) / 2 records, lower triangle row by row), the overflow lists of further
-// child sources per 8-record chunk (xptr / xl, global chunk numbering), and the operator K - omega^2 M.
-// recs == NULL: A11 was assembled by k_assemble_level.
-struct AsmArgs {
-  const int4* recs = nullptr;
-  const int32_t* rec0 = nullptr;
-  const int32_t* xptr = nullptr;
-  const int2* xl = nullptr;
-  const double* freqs = nullptr;
-  const double2* K = nullptr;
-  const double* M = nullptr;
 };
 
 // b = rhsP * (beta_re - omega^2 mass_sum + i beta_im) per frequency (the rhs of a sweep's solves)

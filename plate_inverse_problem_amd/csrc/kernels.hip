@@ -47,55 +47,13 @@ __device__ __forceinline__ void pivot_check(cplx p, int* flags, int64_t q) {
 }
 
 constexpr int KB = 4;    // factorisation pivot block
-#ifndef PFR_KBS
-#define PFR_KBS 8
-#endif
-constexpr int KBS = PFR_KBS;   // triangular-solve block (its lower triangle: 28 loads, all in flight)
+constexpr int KBS = 8;   // triangular-solve block (its lower triangle: 28 loads, all in flight)
 
 // ------------------------------------------------------------------ helpers
 // XCD-aware workgroup order: the dispatcher deals workgroups round-robin over
 // the 8 XCDs (each with its own L2), so workgroup `orig` is renumbered such that
 // every XCD receives one contiguous range of logical ids (bijective for any
 // count; MI355X_MICROARCH.md, workgroup dispatch / T1 swizzle).  Speed only.
-#ifndef PFR_WTRACE
-#define PFR_WTRACE 0   // build-time: make EXTRA=-DPFR_WTRACE=1 (the timestamps cost the L21 kernel registers)
-#endif
-// Wave trace (diagnostic, pfr_debug_wave_trace): per wave of the traced launches (start, end) of the 100 MHz
-// real-time counter and the hardware id.  The host sets the buffer and, before each traced launch, the index of
-// its first record (record = base + linear workgroup x 4 + wave: no atomics); lane 0 stores.
-__device__ unsigned long long* g_wtrace = nullptr;
-__device__ long long g_wtrace_base = 0;
-__device__ long long g_wtrace_cap = 0;
-__device__ long long g_wtrace_launch = 0;
-// phase clocks of the traced L21 waves (PFR_WTRACE builds): sources, prefix, triangle + stores, each closed by a
-// wait for the wave's outstanding memory operations (the waits serialise what the kernel otherwise overlaps)
-struct WPhase {
-  unsigned long long t, src, pre, tri;
-};
-__device__ __forceinline__ void wphase(WPhase* w, unsigned long long WPhase::*acc) {
-#if PFR_WTRACE
-  if (!w) return;
-  __builtin_amdgcn_s_waitcnt(0);
-  const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-  w->*acc += now - w->t;
-  w->t = now;
-#endif
-}
-__device__ __forceinline__ void wtrace_end(unsigned long long t0, int tag, const WPhase* ph = nullptr) {
-  unsigned long long* b = g_wtrace;
-  if (!b) return;
-  const long long i = g_wtrace_base + ((long long)blockIdx.y * gridDim.x + blockIdx.x) * (blockDim.x >> 6) +
-                      (threadIdx.x >> 6);
-  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-  const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);     // HW_REG_HW_ID
-  if ((threadIdx.x & 63) == 0 && i < g_wtrace_cap) {
-    b[4 * i] = t0;
-    b[4 * i + 1] = t1;
-    b[4 * i + 2] = ph ? ((ph->src & 0xFFFFFFFFull) << 32) | (ph->pre & 0xFFFFFFFFull) : (unsigned long long)hw;
-    b[4 * i + 3] = (unsigned long long)tag | ((unsigned long long)g_wtrace_launch << 40);
-  }
-}
-
 __device__ __forceinline__ int64_t xcd_swizzle(int64_t orig, int64_t nwg) {
   const int64_t q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
@@ -430,74 +388,17 @@ __device__ __forceinline__ void row_updateR(const cplx* __restrict__ rd, cplx* _
   }
 }
 
-#ifndef PFR_FAC_JBU
-#define PFR_FAC_JBU 2
-#endif
-#ifndef PFR_FAC_LB
-#define PFR_FAC_LB 1024
-#endif
-#ifndef PFR_FAC_SB
-#define PFR_FAC_SB 2          // 4-pivot blocks per super-block (rank of the trailing update / 4)
-#endif
-
-// A11's lower triangle gathered by the LU workgroup itself (PFR_FUSE_ASM): per entry the original
-// K - omega^2 M value plus the first child update-matrix entry, one store each (the (row, lane group)
-// slots of the workgroup take the front's records in turn, 4 in flight); then the rare further child
-// entries (overflow lists of the records' 8-record chunks) added by one lane group in list order.  The
-// workgroup's own later loads of these entries are served by its XCD's L2 (written moments before), so
-// A11 no longer makes a store -> HBM -> reload trip between two launches, and the level's
-// k_assemble_level launch is gone.  Loads unconditional from clamped indices, masked arithmetically.
-__device__ __forceinline__ void factor_gather_a11(const AsmArgs& A, int front, int ns, cplx* __restrict__ F, int64_t Fc,
-                                                  int64_t q, int e0, int es, bool lead) {
-  const int R0 = A.rec0[front], nr = ns * (ns + 1) / 2;
-  const double om = 6.283185307179586 * A.freqs[q];
-  const double om2 = om * om;
-  constexpr int U = 4;
-  for (int e = e0; e < nr; e += U * es) {
-    int4 r[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) r[u] = A.recs[R0 + min(e + u * es, nr - 1)];
-    cplx o[U], ch[U];
-    double mm[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      o[u] = A.K[max(r[u].y, 0)];
-      mm[u] = A.M[max(r[u].y, 0)];
-      ch[u] = F[(int64_t)max(r[u].z, 0) * Fc + q];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const double so = r[u].y >= 0 ? 1.0 : 0.0, sc = r[u].z >= 0 ? 1.0 : 0.0;
-      const cplx v = make_double2(fma(so, fma(-om2, mm[u], o[u].x), sc * ch[u].x), fma(so, o[u].y, sc * ch[u].y));
-      if (e + u * es < nr) F[(int64_t)r[u].x * Fc + q] = v;
-    }
-  }
-  __syncthreads();
-  if (lead) {
-    const int c0 = R0 >> 3, c1 = (R0 + nr - 1) >> 3;
-    for (int ck = c0; ck <= c1; ++ck) {
-      const int x1 = A.xptr[ck + 1];
-      for (int x = A.xptr[ck]; x < x1; ++x) {
-        const int2 g = A.xl[x];
-        const int rec = ck * 8 + g.x;
-        if (rec < R0 || rec >= R0 + nr) continue;
-        cplx* d = F + (int64_t)A.recs[rec].x * Fc + q;
-        *d = cadd(*d, F[(int64_t)g.y * Fc + q]);
-      }
-    }
-  }
-  __syncthreads();
-}
+constexpr int FAC_JBU = 2;   // trailing-update columns per read-modify-write step
+constexpr int FAC_SB = 2;    // 4-pivot blocks per super-block (rank of the trailing update / 4)
 
 // One front's A11 LU for the 64 / FAC_G frequencies of c.q's lane group: c.w / c.W the wave's index and count
 // among the waves working on these frequencies (every wave of the workgroup reaches the same barriers)
 __device__ __forceinline__ void factor_sym_front(const DevPattern& P, int front, cplx* __restrict__ F, int64_t Fc,
-                                                 int* __restrict__ flags, const AsmArgs& asmb, const Ctx& c, int sub) {
+                                                 int* __restrict__ flags, const Ctx& c, int sub) {
   const Front fr = P.fronts[front];
   const int f = fr.f, ns = fr.ns;
   cplx* __restrict__ base = F + fr.off * Fc + c.q;
   const int r0 = FAC_G * c.w + sub, rs = FAC_G * c.W;   // this lane's first row offset, row stride
-  if (asmb.recs) factor_gather_a11(asmb, front, ns, F, Fc, c.q, r0, rs, c.w == 0 && sub == 0);
 #define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
   // 4-pivot diagonal block at k0 (kb pivots): one load burst from the lower triangle, LU in
   // registers (U = diag(U) L^T up to rounding), one store burst
@@ -562,7 +463,7 @@ __device__ __forceinline__ void factor_sym_front(const DevPattern& P, int front,
         }
     }
   };
-  constexpr int SB = PFR_FAC_SB, R = SB * KB;
+  constexpr int SB = FAC_SB, R = SB * KB;
   for (int k0 = 0; k0 < ns; k0 += R) {
     const int kr = min(R, ns - k0);
 #pragma unroll 1
@@ -592,7 +493,7 @@ __device__ __forceinline__ void factor_sym_front(const DevPattern& P, int front,
         cplx l[R];
 #pragma unroll
         for (int t = 0; t < R; ++t) l[t] = cscale(E(i, k0 + min(t, kr - 1)), t < kr ? 1.0 : 0.0);
-        row_updateR<R, PFR_FAC_JBU>(base, base, (int64_t)i * f, (int64_t)k0 * f, f, Fc, k1, i + 1, kr, l);
+        row_updateR<R, FAC_JBU>(base, base, (int64_t)i * f, (int64_t)k0 * f, f, Fc, k1, i + 1, kr, l);
       }
       __syncthreads();
     }
@@ -600,15 +501,15 @@ __device__ __forceinline__ void factor_sym_front(const DevPattern& P, int front,
 #undef E
 }
 
-__global__ __launch_bounds__(PFR_FAC_LB) void k_factor_sym(DevPattern P, const int* __restrict__ lvl, cplx* __restrict__ F,
-                                                     int64_t Fc, int* __restrict__ flags, AsmArgs asmb) {
+__global__ __launch_bounds__(1024) void k_factor_sym(DevPattern P, const int* __restrict__ lvl, cplx* __restrict__ F,
+                                               int64_t Fc, int* __restrict__ flags) {
   Ctx c;
   c.lane = threadIdx.x & 63;
   c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   c.W = blockDim.x >> 6;
   constexpr int QG = 64 / FAC_G;     // frequencies per lane group
   c.q = (int64_t)blockIdx.y * QG + c.lane % QG;
-  factor_sym_front(P, lvl[blockIdx.x], F, Fc, flags, asmb, c, c.lane / QG);
+  factor_sym_front(P, lvl[blockIdx.x], F, Fc, flags, c, c.lane / QG);
 }
 
 // Symmetric A11 LU with the pivot block resident in LDS, for the levels of large pivot blocks (the
@@ -743,11 +644,7 @@ __global__ __launch_bounds__(256) void k_factor_sym_lds(DevPattern P, const int*
 // entries each step reads are the same for the four lane groups of a wave.
 // Item = (front, first row / column, kind): one wave = 16 frequencies x 4
 // consecutive rows (columns).
-#ifndef PFR_OB
-#define PFR_OB 8
-#endif
-static_assert(PFR_OB >= 1 && PFR_OB <= 16, "k_offdiag_level tail cases cover chunks of at most 16 columns");
-constexpr int OB = PFR_OB;   // columns per left-looking chunk of k_offdiag_level
+constexpr int OB = 8;   // columns per left-looking chunk of k_offdiag_level (the tail cases cover 1-7)
 
 // Where the off-diagonal entries come from (the panel entries of L21 / U12 are
 // assembled here, at their first load, instead of being stored by the assembly
@@ -786,7 +683,7 @@ template <int MODE, int NB, bool PRE = true, int PU = 2>
 __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int64_t (&so)[OFF_RPL], int64_t sc,
                                               int64_t sa, int64_t sb, bool unit, const bool (&valid)[OFF_RPL],
                                               int c0, const OffSrc& S, const cplx* __restrict__ F, int64_t Fc,
-                                              int64_t q, WPhase* wp = nullptr) {
+                                              int64_t q) {
   cplx x[OFF_RPL][NB];
 #pragma unroll
   for (int h = 0; h < OFF_RPL; ++h)
@@ -806,9 +703,7 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
         }
     }
   }
-  wphase(wp, &WPhase::src);
-  // x -= own(0:c0) * shared(0:c0, c0:c0+NB)   (PRE = false: c0 = 0, no prefix); PU > 2: batches of PU pivots
-  // whose loads are all issued before their products (the same products in the same order)
+  // x -= own(0:c0) * shared(0:c0, c0:c0+NB)   (PRE = false: c0 = 0, no prefix); PU = 3: software-pipelined
   int t0 = 0;
   if (PU == 3 && PRE && c0 > 0) {
     // software-pipelined prefix: pivot t + 1's loads are issued before pivot t's products, so the products wait
@@ -838,25 +733,6 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
     if (t < c0) fm(la, ua);
     t0 = c0;
   }
-  if (PU > 3 && PRE) {
-    for (; t0 + PU <= c0; t0 += PU) {
-      cplx l[PU][OFF_RPL], u[PU][NB];
-#pragma unroll
-      for (int k = 0; k < PU; ++k) {
-#pragma unroll
-        for (int h = 0; h < OFF_RPL; ++h) l[k][h] = base[(so[h] + (int64_t)(t0 + k) * sc) * Fc];
-#pragma unroll
-        for (int j = 0; j < NB; ++j) u[k][j] = base[((int64_t)(t0 + k) * sa + (int64_t)(c0 + j) * sb) * Fc];
-      }
-      __builtin_amdgcn_sched_group_barrier(0x020, PU * (OFF_RPL + NB), 0);   // every load of the batch first
-#pragma unroll
-      for (int k = 0; k < PU; ++k)
-#pragma unroll
-        for (int h = 0; h < OFF_RPL; ++h)
-#pragma unroll
-          for (int j = 0; j < NB; ++j) x[h][j] = cfms(x[h][j], l[k][h], u[k][j]);
-    }
-  }
 #pragma unroll 2
   for (int t = t0; t < (PRE ? c0 : 0); ++t) {
     cplx l[OFF_RPL], u[NB];
@@ -869,7 +745,6 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
 #pragma unroll
       for (int j = 0; j < NB; ++j) x[h][j] = cfms(x[h][j], l[h], u[j]);
   }
-  wphase(wp, &WPhase::pre);
   // triangular block shared(c0:c0+NB, c0:c0+NB), column by column
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
@@ -892,7 +767,6 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
 #pragma unroll
       for (int j = 0; j < NB; ++j) base[(so[h] + (int64_t)(c0 + j) * sc) * Fc] = x[h][j];
     }
-  wphase(wp, &WPhase::tri);
 }
 
 // Item = (front, first row / column, kind, record offset): one wave = 64 / OFF_G
@@ -907,7 +781,7 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
 // One item (OFF_G OFF_RPL rows / columns of a front) of the panel for the frequency group `by`: the wave's
 // own work, no barrier
 template <int MODE, bool SMALL, int PU = 2>
-__device__ __forceinline__ void offdiag_item(WPhase* wp, const DevPattern& P, const int4* __restrict__ items, int wid,
+__device__ __forceinline__ void offdiag_item(const DevPattern& P, const int4* __restrict__ items, int wid,
                                              const int2* __restrict__ orec, const int* __restrict__ oxp,
                                              const int2* __restrict__ ox, cplx* __restrict__ F, int64_t Fc,
                                              const double* __restrict__ freqs, const cplx* __restrict__ K,
@@ -960,291 +834,28 @@ __device__ __forceinline__ void offdiag_item(WPhase* wp, const DevPattern& P, co
     return;
   }
   int c0 = 0;
-  for (; c0 + OB <= ns; c0 += OB) offdiag_chunk<MODE, OB, true, PU>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q, wp);
+  for (; c0 + OB <= ns; c0 += OB) offdiag_chunk<MODE, OB, true, PU>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q);
   switch (ns - c0) {     // wave-uniform tail width
 #define TAIL(n) \
-  case n: offdiag_chunk<MODE, n, true, PU>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q, wp); break;
+  case n: offdiag_chunk<MODE, n, true, PU>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q); break;
     TAIL(1) TAIL(2) TAIL(3) TAIL(4) TAIL(5) TAIL(6) TAIL(7)
-#if PFR_OB > 8
-    TAIL(8) TAIL(9) TAIL(10) TAIL(11) TAIL(12) TAIL(13) TAIL(14) TAIL(15)
-#endif
 #undef TAIL
     default: break;
   }
 }
 
+// XCD-aware order: a frequency group's items on one XCD, sharing its L2
 template <int MODE, bool SMALL, int PU = 2>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMALL ? 5 : 1))) void k_offdiag_level(DevPattern P, const int4* __restrict__ items, int nitems,
-                                                        const int2* __restrict__ orec, const int* __restrict__ oxp,
-                                                        const int2* __restrict__ ox, cplx* __restrict__ F, int64_t Fc,
-                                                        const double* __restrict__ freqs, const cplx* __restrict__ K,
-                                                        const double* __restrict__ M, const cplx* __restrict__ data,
-                                                        int64_t data_stride, int nvalid, int swz) {
-#if PFR_WTRACE
-  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-#endif
-  // swz: XCD-aware order (a frequency group's items on one XCD, sharing its L2); 0: the hardware's round-robin
-  const int64_t o = blockIdx.x + (int64_t)gridDim.x * blockIdx.y;
-  const int64_t lid = swz ? xcd_swizzle(o, (int64_t)gridDim.x * gridDim.y) : o;
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMALL ? 5 : 1))) void k_offdiag_level(
+    DevPattern P, const int4* __restrict__ items, int nitems, const int2* __restrict__ orec, const int* __restrict__ oxp,
+    const int2* __restrict__ ox, cplx* __restrict__ F, int64_t Fc, const double* __restrict__ freqs,
+    const cplx* __restrict__ K, const double* __restrict__ M, const cplx* __restrict__ data, int64_t data_stride,
+    int nvalid) {
+  const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
   const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
   const int wid = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
-#if PFR_WTRACE
-  WPhase ph{t0, 0, 0, 0};
-  WPhase* wp = &ph;
-#else
-  WPhase* wp = nullptr;
-#endif
   if (wid < nitems)
-    offdiag_item<MODE, SMALL, PU>(wp, P, items, wid, orec, oxp, ox, F, Fc, freqs, K, M, data, data_stride, nvalid, by);
-#if PFR_WTRACE
-  wtrace_end(t0, wid < nitems ? 1 + (wid << 4) : 0, &ph);
-#endif
-}
-
-// L21 rows with U11 shared through LDS (symmetric analyses, the narrow levels; PFR_OFF_SHU): a workgroup = four
-// waves on up to four consecutive items (two rows each) of ONE front, same frequency group.  k_offdiag_level's
-// waves each load the front's U11 for their own two rows; on the top levels, where a front's items are few and
-// their U11 reads are served by L2, that makes the per-CU L2 load rate the bound.  Here every U11 value of the
-// left-looking prefix is loaded once per workgroup -- in stages of SHU_ST pivot rows x 8 columns, wave w staging
-// row w of the stage through registers into a double-buffered LDS image one stage ahead -- and read by the four
-// waves from LDS.  Sources, prefix order (ascending pivot), chunk triangle and stores are k_offdiag_level's: the
-// results are identical bit for bit.
-template <int MODE, int SHU_ST>   // SHU_ST pivot rows per stage (4: 64 KiB of LDS, 2: 32 KiB)
-__global__ __launch_bounds__(256) void k_offdiag_shu(DevPattern P, const int4* __restrict__ items,
-                                                     const int4* __restrict__ tasks, int ntasks,
-                                                     const int2* __restrict__ orec, const int* __restrict__ oxp,
-                                                     const int2* __restrict__ ox, cplx* __restrict__ F, int64_t Fc,
-                                                     const double* __restrict__ freqs, const cplx* __restrict__ K,
-                                                     const double* __restrict__ M, const cplx* __restrict__ data,
-                                                     int64_t data_stride, int nvalid) {
-  static_assert(OFF_G == 1 && OB == 8, "one lane = one frequency, chunks of 8 pivots");
-  static_assert(SHU_ST == 2 || SHU_ST == 4, "stage of 2 or 4 pivot rows");
-  constexpr int PW = SHU_ST * 8 / 4;          // staged entries per wave
-  __shared__ cplx Ub[2][SHU_ST][8][64];       // two stages of SHU_ST pivot rows x 8 columns x 64 frequencies
-  const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
-  const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int4 task = tasks[bx];
-  const bool active = w < task.y;
-  const int wid = task.x + min(w, task.y - 1);
-  const int64_t q = (int64_t)by * 64 + lane;
-  const int4 it = items[wid];
-  const Front fr = P.fronts[it.x];
-  const int f = fr.f, ns = fr.ns;
-  cplx* __restrict__ base = F + fr.off * Fc + q;
-  OffSrc S;
-  int64_t so[OFF_RPL];
-  bool valid[OFF_RPL];
-#pragma unroll
-  for (int h = 0; h < OFF_RPL; ++h) {
-    const int idx = it.y + h;
-    valid[h] = active && idx < f;
-    so[h] = (int64_t)min(idx, f - 1) * f;
-    S.rec[h] = orec + it.w + (int64_t)h * ns;
-  }
-  S.ox = ox;
-  S.ox0 = oxp[wid];
-  S.ox1 = oxp[wid + 1];
-  S.slot0 = 0;
-  S.om2 = 0.0;
-  if (MODE == 0) {
-    const double om = 6.283185307179586 * freqs[q];
-    S.om2 = om * om;
-  }
-  S.K = K;
-  S.M = M;
-  S.dq = data + min(q, (int64_t)nvalid - 1) * data_stride;
-#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
-  for (int c0 = 0; c0 < ns; c0 += 8) {
-    const int nb = min(8, ns - c0);
-    cplx x[OFF_RPL][8];
-#pragma unroll
-    for (int h = 0; h < OFF_RPL; ++h)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) x[h][j] = off_source<MODE>(S, F, Fc, q, h, c0 + min(j, nb - 1));
-    for (int e = S.ox0; e < S.ox1; ++e) {
-      const int2 g = S.ox[e];
-      const int c = g.x / OFF_RPL - c0, slot = g.x % OFF_RPL;
-      if (c >= 0 && c < nb) {
-        const cplx v = F[(int64_t)g.y * Fc + q];
-#pragma unroll
-        for (int h = 0; h < OFF_RPL; ++h)
-          if (slot == h) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-              if (j == c) x[h][j] = cadd(x[h][j], v);
-          }
-      }
-    }
-    // prefix: x -= own(0:c0) * U(0:c0, c0:c0+8), U staged SHU_ST pivot rows at a time
-    const int nst = (c0 + SHU_ST - 1) / SHU_ST;
-    // wave w stages entries e = w PW + k of the stage: pivot row e / 8, column e % 8
-    cplx st[PW];
-    if (nst > 0) {
-#pragma unroll
-      for (int k = 0; k < PW; ++k) {
-        const int e = w * PW + k;
-        st[k] = E(min(e / 8, c0 - 1), c0 + min(e % 8, nb - 1));
-      }
-#pragma unroll
-      for (int k = 0; k < PW; ++k) Ub[0][(w * PW + k) / 8][(w * PW + k) % 8][lane] = st[k];
-      __syncthreads();
-    }
-    for (int s = 0; s < nst; ++s) {
-      const bool more = s + 1 < nst;
-      if (more) {
-#pragma unroll
-        for (int k = 0; k < PW; ++k) {
-          const int e = w * PW + k;
-          st[k] = E(min((s + 1) * SHU_ST + e / 8, c0 - 1), c0 + min(e % 8, nb - 1));
-        }
-      }
-#pragma unroll
-      for (int tt = 0; tt < SHU_ST; ++tt) {
-        const int t = s * SHU_ST + tt;
-        if (t < c0) {
-          cplx l[OFF_RPL], u[8];
-#pragma unroll
-          for (int h = 0; h < OFF_RPL; ++h) l[h] = base[(so[h] + t) * Fc];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) u[j] = Ub[s & 1][tt][j][lane];
-#pragma unroll
-          for (int h = 0; h < OFF_RPL; ++h)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) x[h][j] = cfms(x[h][j], l[h], u[j]);
-        }
-      }
-      if (more) {
-#pragma unroll
-        for (int k = 0; k < PW; ++k) Ub[(s + 1) & 1][(w * PW + k) / 8][(w * PW + k) % 8][lane] = st[k];
-      }
-      __syncthreads();
-    }
-    // the chunk's own triangle, column by column
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (j < nb) {
-#pragma unroll
-        for (int a = 0; a < j; ++a) {
-          const cplx t = E(c0 + a, c0 + j);
-#pragma unroll
-          for (int h = 0; h < OFF_RPL; ++h) x[h][j] = cfms(x[h][j], x[h][a], t);
-        }
-        const cplx d = crecip(E(c0 + j, c0 + j));
-#pragma unroll
-        for (int h = 0; h < OFF_RPL; ++h) x[h][j] = cmul(x[h][j], d);
-      }
-#pragma unroll
-    for (int h = 0; h < OFF_RPL; ++h)
-      if (valid[h]) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          if (j < nb) base[(so[h] + c0 + j) * Fc] = x[h][j];
-      }
-  }
-#undef E
-}
-
-// Right-looking L21 rows for the levels whose pivot blocks are at most NSM (symmetric analyses: kind-0 items
-// only): one wave = ONE row x 64 frequencies (the two rows of an item on two waves), the whole row in
-// registers.  k_offdiag_level is left-looking: every chunk of OB columns re-loads the row's own earlier L21
-// values and the U11 column block, a chain of ~ns^2 / (2 OB) dependent load rounds per wave that the few
-// fronts of the upper levels cannot hide behind other waves; here the row stays in registers and each chunk
-// updates the columns right of it with independent U11 loads: ns / OB rounds.  The operations per column
-// are those of k_offdiag_level in the same order (columns of earlier chunks in ascending pivot order, then
-// the chunk's own triangle), so the results are identical bit for bit.
-template <int MODE, int NSM, int R>
-__global__ __launch_bounds__(256) void k_offdiag_rl(DevPattern P, const int4* __restrict__ items, int nitems,
-                                                    const int2* __restrict__ orec, const int* __restrict__ oxp,
-                                                    const int2* __restrict__ ox, cplx* __restrict__ F, int64_t Fc,
-                                                    const double* __restrict__ freqs, const cplx* __restrict__ K,
-                                                    const double* __restrict__ M, const cplx* __restrict__ data,
-                                                    int64_t data_stride, int nvalid) {
-  static_assert(OFF_G == 1, "one lane = one frequency");
-  static_assert(NSM % 8 == 0 && OB == 8, "chunks of 8 pivots, as k_offdiag_level");
-  static_assert(R == 1 || R == OFF_RPL, "one row per wave, or an item's rows per wave");
-  constexpr int WPI = OFF_RPL / R;            // waves per item
-  const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
-  const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
-  const int wv = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
-  const int wid = wv / WPI, h0 = (wv % WPI) * R;
-  if (wid >= nitems) return;
-  const int lane = threadIdx.x & 63;
-  const int64_t q = (int64_t)by * 64 + lane;
-  const int4 it = items[wid];
-  const Front fr = P.fronts[it.x];
-  const int f = fr.f, ns = fr.ns;
-  if (it.y + h0 >= f) return;
-  cplx* __restrict__ base = F + fr.off * Fc + q;
-  OffSrc S;
-#pragma unroll
-  for (int r = 0; r < R; ++r) S.rec[r] = orec + it.w + (int64_t)(h0 + r) * ns;
-  S.om2 = 0.0;
-  if (MODE == 0) {
-    const double om = 6.283185307179586 * freqs[q];
-    S.om2 = om * om;
-  }
-  S.K = K;
-  S.M = M;
-  S.dq = data + min(q, (int64_t)nvalid - 1) * data_stride;
-  cplx x[R][NSM];
-#pragma unroll
-  for (int r = 0; r < R; ++r)
-#pragma unroll
-    for (int c = 0; c < NSM; ++c) x[r][c] = c < ns ? off_source<MODE>(S, F, Fc, q, r, c) : make_double2(0.0, 0.0);
-  for (int e = oxp[wid]; e < oxp[wid + 1]; ++e) {      // rare: several children cover one entry
-    const int2 g = ox[e];
-    const int r = g.x % OFF_RPL - h0;
-    if (r < 0 || r >= R) continue;
-    const int c = g.x / OFF_RPL;
-    const cplx v = F[(int64_t)g.y * Fc + q];
-#pragma unroll
-    for (int rr = 0; rr < R; ++rr)
-#pragma unroll
-      for (int j = 0; j < NSM; ++j)
-        if (rr == r && j == c) x[rr][j] = cadd(x[rr][j], v);
-  }
-#define U(a, b) base[((int64_t)(a) * f + (b)) * Fc]
-#pragma unroll
-  for (int c0 = 0; c0 < NSM; c0 += 8) {
-    if (c0 < ns) {
-      // the chunk's own triangle, column by column
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (c0 + j < ns) {
-#pragma unroll
-          for (int a = 0; a < j; ++a) {
-            const cplx u = U(c0 + a, c0 + j);
-#pragma unroll
-            for (int r = 0; r < R; ++r) x[r][c0 + j] = cfms(x[r][c0 + j], x[r][c0 + a], u);
-          }
-          const cplx d = crecip(U(c0 + j, c0 + j));
-#pragma unroll
-          for (int r = 0; r < R; ++r) x[r][c0 + j] = cmul(x[r][c0 + j], d);
-        }
-      // the columns right of the chunk
-#pragma unroll
-      for (int j = c0 + 8; j < NSM; ++j)
-        if (j < ns) {
-          cplx u[8];
-#pragma unroll
-          for (int a = 0; a < 8; ++a) u[a] = U(c0 + a, j);
-#pragma unroll
-          for (int a = 0; a < 8; ++a)
-#pragma unroll
-            for (int r = 0; r < R; ++r) x[r][j] = cfms(x[r][j], x[r][c0 + a], u[a]);
-        }
-    }
-  }
-#undef U
-#pragma unroll
-  for (int r = 0; r < R; ++r)
-    if (it.y + h0 + r < f) {
-      const int64_t so = (int64_t)(it.y + h0 + r) * f;
-#pragma unroll
-      for (int c = 0; c < NSM; ++c)
-        if (c < ns) base[(so + c) * Fc] = x[r][c];
-    }
+    offdiag_item<MODE, SMALL, PU>(P, items, wid, orec, oxp, ox, F, Fc, freqs, K, M, data, data_stride, nvalid, by);
 }
 
 // ------------------------------------------------------------------ K2b: Schur complement
@@ -1394,15 +1005,12 @@ __global__ __launch_bounds__(256) void k_schur_level(DevPattern P, const int4* _
 }
 
 // symmetric mode: explicit register budget (3 waves per SIMD) so that every load of a pivot
-// step (KU steps) is in flight at once (the default budget serialises them)
-template <int KU>
-#ifndef PFR_SCHUR_WPE
-#define PFR_SCHUR_WPE 3
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PFR_SCHUR_WPE, PFR_SCHUR_WPE))) void k_schur_sym_level(
+// step is in flight at once (the default budget serialises them; 1 step at 3 waves/SIMD measured 4 %
+// faster than 2 steps at 2 waves/SIMD)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void k_schur_sym_level(
     DevPattern P, const int4* __restrict__ tiles, int ntiles, const int* __restrict__ g1,
     const int* __restrict__ gxp, const int2* __restrict__ gx, cplx* __restrict__ F, int64_t Fc) {
-  schur_tile<true, true, KU>(P, tiles, ntiles, g1, gxp, gx, F, Fc);
+  schur_tile<true, true, 1>(P, tiles, ntiles, g1, gxp, gx, F, Fc);
 }
 
 // Symmetric mode, large update blocks (r >= PFR_SCHUR_BLK_MIN rows): a workgroup = 16 waves
@@ -2109,79 +1717,6 @@ __device__ __forceinline__ void usolve2_upd(const Front& fr, const int* six, con
 #undef XV
 }
 
-// usolve2_upd software-pipelined: chunk k + 1's index reads and loads issued before chunk k's products (the products
-// then wait only for the older loads; the plain loop drains at every chunk).  Same products in the same order.
-template <bool SYM, int SR, int SK>
-__device__ __forceinline__ void usolve2_upd_pp(const Front& fr, const int* six, const cplx* __restrict__ base,
-                                               int64_t Fc, int64_t q, const bool (&act)[2], const bool (&live)[2],
-                                               const cplx* const (&Ys)[2], cplx* const (&Xs)[2], int a_begin, int a_step) {
-  const int f = fr.f, ns = fr.ns;
-#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
-#define XV(v, a) Xs[v][(int64_t)(fr.col0 + (a)) * Fc + q]
-  for (int a0 = a_begin; a0 < ns; a0 += a_step) {
-    int ra[SR];
-    cplx acc[2][SR];
-#pragma unroll
-    for (int r = 0; r < SR; ++r) {
-      ra[r] = min(a0 + r, ns - 1);
-      acc[0][r] = acc[1][r] = make_double2(0.0, 0.0);
-    }
-    const cplx* pu[SR];
-#pragma unroll
-    for (int r = 0; r < SR; ++r) pu[r] = base + (SYM ? (int64_t)ra[r] : (int64_t)ra[r] * f) * Fc;
-    const int64_t su = SYM ? (int64_t)f * Fc : Fc;
-    cplx xa[2][SK], ea[SR][SK], xb[2][SK], eb[SR][SK];
-    auto ld = [&](cplx (&xv)[2][SK], cplx (&ev)[SR][SK], int b0) {
-      int iv[SK];
-#pragma unroll
-      for (int u = 0; u < SK; ++u) iv[u] = __builtin_amdgcn_readfirstlane(six[min(b0 + u, f - 1)]);
-#pragma unroll
-      for (int v = 0; v < 2; ++v)
-#pragma unroll
-        for (int u = 0; u < SK; ++u) xv[v][u] = Xs[v][(int64_t)iv[u] * Fc + q];
-#pragma unroll
-      for (int r = 0; r < SR; ++r)
-#pragma unroll
-        for (int u = 0; u < SK; ++u) ev[r][u] = pu[r][min(b0 + u, f - 1) * su];
-    };
-    auto fm = [&](cplx (&xv)[2][SK], const cplx (&ev)[SR][SK], int b0) {
-#pragma unroll
-      for (int v = 0; v < 2; ++v)
-#pragma unroll
-        for (int u = 0; u < SK; ++u)
-          if (b0 + u >= f) xv[v][u] = make_double2(0.0, 0.0);
-#pragma unroll
-      for (int v = 0; v < 2; ++v)
-#pragma unroll
-        for (int r = 0; r < SR; ++r)
-#pragma unroll
-          for (int u = 0; u < SK; ++u) acc[v][r] = cfms(acc[v][r], ev[r][u], xv[v][u]);
-    };
-    int b0 = ns;
-    if (b0 < f) ld(xa, ea, b0);
-    for (; b0 + SK < f; b0 += 2 * SK) {
-      ld(xb, eb, b0 + SK);
-      fm(xa, ea, b0);
-      if (b0 + 2 * SK < f) ld(xa, ea, b0 + 2 * SK);
-      fm(xb, eb, b0 + SK);
-    }
-    if (b0 < f) fm(xa, ea, b0);
-#pragma unroll
-    for (int r = 0; r < SR; ++r)
-      if (a0 + r < ns) {
-        const cplx urr = SYM ? E(ra[r], ra[r]) : make_double2(1.0, 0.0);
-#pragma unroll
-        for (int v = 0; v < 2; ++v)
-          if (act[v]) {
-            const cplx y = live[v] ? Ys[v][(int64_t)(fr.col0 + a0 + r) * Fc + q] : make_double2(0.0, 0.0);
-            XV(v, a0 + r) = SYM ? cadd(y, cmul(urr, acc[v][r])) : cadd(y, acc[v][r]);
-          }
-      }
-  }
-#undef E
-#undef XV
-}
-
 // U11 backward for the pivot values XV(v, 0 .. ns) the update part left there: KBS blocks, the diagonal
 // block by wave 0 in registers, the rows above updated by all waves
 __device__ __forceinline__ void usolve2_tri(const Front& fr, const cplx* __restrict__ base, int64_t Fc, const Ctx& c,
@@ -2335,92 +1870,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSM <= 4 ? 
 #undef E
 }
 
-// k_usolve2_tiny for levels whose pivot blocks reach 16: the pivot rows in blocks of KBS (the update-row solution
-// gathered once per block), the sums written to the pivot values in global memory and the U11 backward solve
-// by the same wave from there in KBS blocks -- usolve2_upd's and usolve2_tri's order, so again identical results.
-// One wave per (front, frequency group): the wave's lanes re-read only their own stores (no barrier needed).
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_usolve2_wave(
-    DevPattern P, const int* __restrict__ lvl, int nfronts, const cplx* __restrict__ F, int64_t Fc, UPair A, UPair B) {
-  int bx;
-  const Ctx c = ctx_xcd(bx);
-  const int slot = bx * 4 + c.w;
-  if (slot >= nfronts) return;
-  const int ft = lvl[slot];
-  const bool act[2] = {!A.skip || !A.skip[ft], !B.skip || !B.skip[ft]};
-  const bool live[2] = {!A.reach || A.reach[ft], !B.reach || B.reach[ft]};
-  const cplx* const Ys[2] = {A.Y, B.Y};
-  cplx* const Xs[2] = {A.X, B.X};
-  const Front fr = P.fronts[ft];
-  const int f = fr.f, ns = fr.ns;
-  const cplx* __restrict__ base = F + fr.off * Fc + c.q;
-  const int* __restrict__ ix = P.idx + fr.row0;
-#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
-#define XV(v, a) Xs[v][(int64_t)(fr.col0 + (a)) * Fc + c.q]
-  for (int a0 = 0; a0 < ns; a0 += KBS) {
-    cplx acc[2][KBS];
-#pragma unroll
-    for (int a = 0; a < KBS; ++a) acc[0][a] = acc[1][a] = make_double2(0.0, 0.0);
-    for (int b = ns; b < f; ++b) {
-      const int iv = __builtin_amdgcn_readfirstlane(ix[b]);
-      const cplx x0 = Xs[0][(int64_t)iv * Fc + c.q], x1 = Xs[1][(int64_t)iv * Fc + c.q];
-      cplx e[KBS];
-#pragma unroll
-      for (int a = 0; a < KBS; ++a) e[a] = E(b, min(a0 + a, ns - 1));
-#pragma unroll
-      for (int a = 0; a < KBS; ++a) {
-        acc[0][a] = cfms(acc[0][a], e[a], x0);
-        acc[1][a] = cfms(acc[1][a], e[a], x1);
-      }
-    }
-#pragma unroll
-    for (int a = 0; a < KBS; ++a)
-      if (a0 + a < ns) {
-        const cplx urr = E(a0 + a, a0 + a);
-#pragma unroll
-        for (int v = 0; v < 2; ++v)
-          if (act[v]) {
-            const cplx y = live[v] ? Ys[v][(int64_t)(fr.col0 + a0 + a) * Fc + c.q] : make_double2(0.0, 0.0);
-            XV(v, a0 + a) = cadd(y, cmul(urr, acc[v][a]));
-          }
-      }
-  }
-  // U11 backward, KBS blocks from the bottom (usolve2_tri with one wave)
-  for (int k1 = ns; k1 > 0; k1 -= KBS) {
-    const int k0 = max(0, k1 - KBS), kb = k1 - k0;
-#pragma unroll
-    for (int v = 0; v < 2; ++v)
-      if (act[v]) {
-        cplx x[KBS];
-#pragma unroll
-        for (int t = 0; t < KBS; ++t) x[t] = XV(v, k0 + min(t, kb - 1));
-#pragma unroll
-        for (int i = KBS - 1; i >= 0; --i) {
-          const int ri = k0 + min(i, kb - 1);
-#pragma unroll
-          for (int k = i + 1; k < KBS; ++k) x[i] = cfms(x[i], E(ri, k0 + min(k, kb - 1)), x[k]);
-          x[i] = cscale(cmul(x[i], crecip(E(ri, ri))), i < kb ? 1.0 : 0.0);
-        }
-#pragma unroll
-        for (int t = 0; t < KBS; ++t)
-          if (t < kb) XV(v, k0 + t) = x[t];
-        if (k0 > 0) {
-#pragma unroll
-          for (int t = 0; t < KBS; ++t) x[t] = cscale(x[t], t < kb ? 1.0 : 0.0);
-          for (int i = 0; i < k0; ++i) {
-            cplx y = XV(v, i);
-#pragma unroll
-            for (int t = 0; t < KBS; ++t) y = cfms(y, E(i, k0 + min(t, kb - 1)), x[t]);
-            XV(v, i) = y;
-          }
-        }
-      }
-  }
-#undef E
-#undef XV
-}
-
 // the pivot rows' update part of k_usolve2_level split over S workgroups per (front, frequency group)
-template <bool SYM, int SR, int SK, bool PP = false>
+template <bool SYM, int SR, int SK>
 __global__ __launch_bounds__(256) void k_usolve2_upd(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F,
                                                      int64_t Fc, UPair A, UPair B, int S) {
   int bx;
@@ -2435,262 +1886,8 @@ __global__ __launch_bounds__(256) void k_usolve2_upd(DevPattern P, const int* __
   __shared__ int six[MAX_FRONT];
   for (int a = threadIdx.x; a < fr.f; a += blockDim.x) six[a] = P.idx[fr.row0 + a];
   __syncthreads();
-  if (PP)
-    usolve2_upd_pp<SYM, SR, SK>(fr, six, F + fr.off * Fc + c.q, Fc, c.q, act, live, Ys, Xs, SR * (split * c.W + c.w),
-                                SR * c.W * S);
-  else
-    usolve2_upd<SYM, SR, SK>(fr, six, F + fr.off * Fc + c.q, Fc, c.q, act, live, Ys, Xs, SR * (split * c.W + c.w),
-                             SR * c.W * S);
-}
-
-// ------------------------------------------------------------------ dependency-driven passes (narrow top)
-// The narrow top of the elimination tree -- levels of a few fronts, whose per-level launches give a few
-// workgroups each and drain the chip at every level boundary -- as ONE launch in which every workgroup
-// takes the next task ticket and waits only for the tasks it depends on:
-//  * tickets are issued by an atomic counter in a topological order of the tasks (the host's list), so a
-//    workgroup waits only on tasks with smaller tickets, which running workgroups hold: no dependence on
-//    dispatch order, residency or placement, whatever the grid size;
-//  * hand-off (MI355X_MICROARCH.md, inter-workgroup visibility): the producer's waves retire their
-//    stores, one lane fences release at agent scope (the XCD L2's dirty lines written back) and stores /
-//    adds the flag word by an agent-scope atomic; the consumer's one lane polls the word relaxed (s_sleep
-//    between polls), fences acquire at agent scope (its CU's L1 dropped) and releases the workgroup at a
-//    barrier; every polled word is zeroed by a memset on the stream before the launch;
-//  * spins are bounded (~1 s): a timeout flags the group's frequencies (PFR_FLAG_BAD_PIVOT) and goes on, so
-//    a broken schedule ends in flagged results, never in a hung GPU.
-struct FlowArgs {
-  const int4* tasks;     // (front, part (-1: the triangular part), parts S, region slot of the front)
-  int ntasks;
-  const int* pslot;      // per front: region slot of its parent, -1 when the front has no parent in the region
-  unsigned* ticket;      // the task counter
-  unsigned* done;        // per (slot, group): 1 once the front's pass is complete
-  unsigned* cnt;         // per (slot, group): update parts complete
-  int* flags;            // per frequency of the chunk
-};
-
-__device__ __forceinline__ bool flow_wait(unsigned* w, unsigned want) {
-  int bad = 0;
-  if (threadIdx.x == 0) {
-    unsigned spins = 0;
-    while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 21)) {   // ~2 s of polls: give up (flagged), never hang the GPU
-        bad = 1;
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  return !__syncthreads_or(bad);   // the barrier after the acquire releases the other waves' loads
-}
-
-__device__ __forceinline__ void flow_publish(unsigned* w, bool add) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave: its stores retired
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // keep: the release's own wait can be dropped (ROCm 7.2)
-    if (add)
-      __hip_atomic_fetch_add(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-      __hip_atomic_store(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// the task record, wave-uniform (scalar registers: its indices address whole-workgroup data)
-__device__ __forceinline__ int4 flow_task(const int4* tasks, int task) {
-  const int4 t = tasks[task];
-  return make_int4(__builtin_amdgcn_readfirstlane(t.x), __builtin_amdgcn_readfirstlane(t.y),
-                   __builtin_amdgcn_readfirstlane(t.z), __builtin_amdgcn_readfirstlane(t.w));
-}
-
-__device__ __forceinline__ int flow_ticket(unsigned* ticket) {
-  __shared__ int s_t;
-  if (threadIdx.x == 0) s_t = (int)__hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  return __builtin_amdgcn_readfirstlane(s_t);   // uniform: the task's indices live in scalar registers
-}
-
-// The paired top-down pass (k_usolve2_level + k_usolve2_upd) over the narrow top: per front and
-// 64-frequency group, S update-part tasks (pivot rows a = SR (p W + w) + k SR W S, after the parent's pass)
-// and one triangular task (after the front's S update parts).
-template <int SR, int SK>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_usolve2_flow(
-    DevPattern P, const cplx* __restrict__ F, int64_t Fc, UPair A, UPair B, FlowArgs G, int ngroups) {
-  const int tk = flow_ticket(G.ticket);
-  if (tk >= G.ntasks * ngroups) return;
-  const int task = tk / ngroups, g = tk - task * ngroups;
-  const int4 T = flow_task(G.tasks, task);
-  Ctx c;
-  c.lane = threadIdx.x & 63;
-  c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  c.W = blockDim.x >> 6;
-  c.q = (int64_t)g * 64 + c.lane;
-  const int ft = T.x;
-  const bool act[2] = {!A.skip || !A.skip[ft], !B.skip || !B.skip[ft]};
-  const bool live[2] = {!A.reach || A.reach[ft], !B.reach || B.reach[ft]};
-  const cplx* const Ys[2] = {A.Y, B.Y};
-  cplx* const Xs[2] = {A.X, B.X};
-  const Front fr = P.fronts[ft];
-  const cplx* __restrict__ base = F + fr.off * Fc + c.q;
-  __shared__ int six[MAX_FRONT];
-  bool ok = true;
-  if (T.y >= 0) {
-    for (int a = threadIdx.x; a < fr.f; a += blockDim.x) six[a] = P.idx[fr.row0 + a];
-    const int ps = G.pslot[ft];
-    if (ps >= 0) ok = flow_wait(G.done + (int64_t)ps * ngroups + g, 1u);
-    else __syncthreads();
-    usolve2_upd<true, SR, SK>(fr, six, base, Fc, c.q, act, live, Ys, Xs, SR * (T.y * c.W + c.w), SR * c.W * T.z);
-    if (!ok) atomicOr(G.flags + c.q, PFR_FLAG_BAD_PIVOT);
-    flow_publish(G.cnt + (int64_t)T.w * ngroups + g, true);
-  } else {
-    ok = flow_wait(G.cnt + (int64_t)T.w * ngroups + g, (unsigned)T.z);
-    usolve2_tri(fr, base, Fc, c, act, Xs);
-    if (!ok) atomicOr(G.flags + c.q, PFR_FLAG_BAD_PIVOT);
-    flow_publish(G.done + (int64_t)T.w * ngroups + g, false);
-  }
-}
-
-// The sliced bottom-up chain (k_lsolve_level_z + k_lsolve_rows_z) over the narrow top, level by level
-// upwards: per (front, slice) reached, a pivot task (frontal vector gathered from the rhs and the children's
-// update vectors, pivot blocks, y; after every in-region child's update rows of that slice) and S_t update-row
-// tasks (rows ns + SRB (p W + w) + k SRB W S, after the front's pivot task).
-struct LFlowArgs {
-  const int4* tasks;     // (front, slice, part (-1: the pivot task), region slot of the front)
-  int ntasks;
-  const int* cptr;       // per (slot, slice): its in-region children reached in the slice, cslot[cptr[4 slot + z] ..]
-  const int* cslot;      //   (only children with update rows: the others contribute nothing to the gather)
-  const int* parts;      // per slot: update-row tasks S of the front (0: no update rows)
-  unsigned* ticket;
-  unsigned* pdone;       // per (slot, slice, group): pivot task complete
-  unsigned* rcnt;        // per (slot, slice, group): update-row tasks complete
-  int* flags;
-};
-
-template <int RHS>
-__global__ __launch_bounds__(256) void k_lsolve_flow(DevPattern P, LSlices S, const cplx* __restrict__ F, int64_t Fc,
-                                                     LFlowArgs G, int ngroups) {
-  const int tk = flow_ticket(G.ticket);
-  if (tk >= G.ntasks * ngroups) return;
-  const int task = tk / ngroups, g = tk - task * ngroups;
-  const int4 T = flow_task(G.tasks, task);
-  Ctx c;
-  c.lane = threadIdx.x & 63;
-  c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  c.W = blockDim.x >> 6;
-  c.q = (int64_t)g * 64 + c.lane;
-  const int z = T.y, sl = T.w;
-  const Front fr = P.fronts[T.x];
-  const int64_t wz = ((int64_t)sl * MAX_SLICES + z) * ngroups + g;
-  bool ok = true;
-  if (T.z < 0) {
-    // every in-region child of this slice: its update rows complete (children outside the region were
-    // solved by earlier launches; unreached children are skipped by the gather itself)
-    const int key = sl * MAX_SLICES + z;
-    const int c1 = G.cptr[key + 1];
-    for (int k = G.cptr[key]; k < c1; ++k) {
-      const int cs = G.cslot[k];
-      ok = flow_wait(G.rcnt + ((int64_t)cs * MAX_SLICES + z) * ngroups + g, (unsigned)G.parts[cs]) && ok;
-    }
-    lsolve_front<RHS>(P, fr, F, Fc, S.WV[z], S.R[z], S.Y[z], S.reach[z], 1, c);
-    if (!ok) atomicOr(G.flags + c.q, PFR_FLAG_BAD_PIVOT);
-    flow_publish(G.pdone + wz, false);
-  } else {
-    ok = flow_wait(G.pdone + wz, 1u);
-    const int Sp = G.parts[sl];
-    lsolve_rows(fr, F + fr.off * Fc + c.q, S.WV[z] + (int64_t)fr.row0 * Fc + c.q, Fc, fr.ns + SRB * (T.z * c.W + c.w),
-                SRB * c.W * Sp);
-    if (!ok) atomicOr(G.flags + c.q, PFR_FLAG_BAD_PIVOT);
-    flow_publish(G.rcnt + wz, true);
-  }
-}
-
-// The factorisation's narrow top (symmetric mode) as ONE dependency-driven launch of 16-wave workgroups, per
-// front and 64-frequency group three kinds of task (ticket order: per level upwards its A tasks, B tasks,
-// C tasks -- topological):
-//  A  the A11 LU with the assembly gathered in (factor_sym_front; waves 0-7 the first 32 frequencies, 8-15
-//     the second), after every in-region child's C tasks (their update matrices feed the gather);
-//  B  16 consecutive items of the front's L21 rows (offdiag_item, one per wave), after the front's A task;
-//  C  one 16 x 16 block of the update matrix (schur_blk_body; every update block of the region goes through
-//     the block kernel), after all the front's B tasks.
-// Hand-offs as the solve passes' (flow_wait / flow_publish).
-struct FFlowArgs {
-  const int4* tasks;     // (kind, front, first item / block, region slot)
-  int ntasks;
-  const int* cptr;       // per slot: in-region children with update blocks, cslot[cptr[slot] .. cptr[slot + 1])
-  const int* cslot;
-  const int* item_end;   // per slot: end of the front's items (global item index)
-  const int* nb;         // per slot: B tasks of the front
-  const int* nc;         // per slot: C tasks (update blocks) of the front
-  unsigned* ticket;
-  unsigned* a_done;      // per (slot, group)
-  unsigned* b_cnt;
-  unsigned* c_cnt;
-  int* flags;
-  const int4* items;
-  const int2* orec;
-  const int* oxp;
-  const int2* ox;
-  const int4* blocks;
-  const int* bg1;
-  const int* bgxp;
-  const int2* bgx;
-  AsmArgs asmb;
-};
-
-// the A and B task bodies out of line: each gets the register budget to itself (inlined into one kernel the
-// three bodies' live ranges added up and spilled).  Arguments by value: a reference would put the kernel's
-// argument block in per-lane memory, and every index loaded from it would count as divergent.
-static __device__ __noinline__ void fflow_a(DevPattern P, int front, cplx* F, int64_t Fc, int* flags, AsmArgs asmb, int g,
-                                            int lane, int w) {
-  Ctx c;
-  c.lane = lane;
-  c.w = w & 7;
-  c.W = 8;
-  constexpr int QG = 64 / FAC_G;
-  c.q = (int64_t)(FAC_G * g + (w >> 3)) * QG + lane % QG;
-  factor_sym_front(P, front, F, Fc, flags, asmb, c, lane / QG);
-}
-
-static __device__ __noinline__ void fflow_b(DevPattern P, const int4* items, const int2* orec, const int* oxp,
-                                            const int2* ox, int wid, cplx* F, int64_t Fc, const double* freqs,
-                                            const cplx* K, const double* M, int g) {
-  offdiag_item<0, false>(nullptr, P, items, wid, orec, oxp, ox, F, Fc, freqs, K, M, nullptr, 0, 1, g);
-}
-
-__global__ __launch_bounds__(1024) void k_factor_flow(DevPattern P, cplx* __restrict__ F, int64_t Fc, FFlowArgs G,
-                                                      int ngroups) {
-  const int tk = flow_ticket(G.ticket);
-  if (tk >= G.ntasks * ngroups) return;
-  const int task = tk / ngroups, g = tk - task * ngroups;
-  const int4 T = flow_task(G.tasks, task);
-  const int sl = T.w;
-  const int64_t wg = (int64_t)sl * ngroups + g;
-  const int lane = threadIdx.x & 63;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  bool ok = true;
-  if (T.x == 0) {
-    const int c1 = G.cptr[sl + 1];
-    for (int k = G.cptr[sl]; k < c1; ++k) {
-      const int cs = G.cslot[k];
-      ok = flow_wait(G.c_cnt + (int64_t)cs * ngroups + g, (unsigned)G.nc[cs]) && ok;
-    }
-    fflow_a(P, T.y, F, Fc, G.flags, G.asmb, g, lane, w);
-    if (!ok) atomicOr(G.flags + (int64_t)g * 64 + lane, PFR_FLAG_BAD_PIVOT);
-    flow_publish(G.a_done + wg, false);
-  } else if (T.x == 1) {
-    ok = flow_wait(G.a_done + wg, 1u);
-    const int wid = T.z + w;
-    if (wid < G.item_end[sl])
-      fflow_b(P, G.items, G.orec, G.oxp, G.ox, wid, F, Fc, G.asmb.freqs, G.asmb.K, G.asmb.M, g);
-    if (!ok) atomicOr(G.flags + (int64_t)g * 64 + lane, PFR_FLAG_BAD_PIVOT);
-    flow_publish(G.b_cnt + wg, true);
-  } else {
-    ok = flow_wait(G.b_cnt + wg, (unsigned)G.nb[sl]);
-    schur_blk_body<4, 1, 16>(P, T.z, g, G.blocks, G.bg1, G.bgxp, G.bgx, F, Fc);
-    if (!ok) atomicOr(G.flags + (int64_t)g * 64 + lane, PFR_FLAG_BAD_PIVOT);
-    flow_publish(G.c_cnt + wg, true);
-  }
+  usolve2_upd<SYM, SR, SK>(fr, six, F + fr.off * Fc + c.q, Fc, c.q, act, live, Ys, Xs, SR * (split * c.W + c.w),
+                           SR * c.W * S);
 }
 
 // ------------------------------------------------------------------ K3c: U^T y = g (bottom-up)
@@ -2940,16 +2137,14 @@ __device__ __forceinline__ cplx resid_entry(const ResidArgs& A, const cplx* __re
   return dq[nz];
 }
 
-#ifndef PFR_RES_WPE
-#define PFR_RES_WPE 5   // the fused walk at 96 VGPRs (5 waves/SIMD): its phase 9.5 -> 8.0 ms per step, lane-summed
-#endif
+constexpr int RES_WPE = 5;   // the fused walk at 96 VGPRs (5 waves/SIMD): its phase 9.5 -> 8.0 ms per step, lane-summed
 // NSK > 0 (with DOT, the loss sweep's forward walk under the functional correction): the gradient
 // contraction rides on the walk -- every entry (p, j, nz) it visits has x_j gathered and mu_p loaded
 // already, so s_k(q) += S_k(nz) mu_p x_j per lane (frequency), per workgroup; the loss cotangent scale
 // m_q is only known after this walk (k_correct_finish), so the partials stay per frequency and
 // k_reduce_q applies m_q.  Replaces k_contract_eg's separate entry walk.
 template <int MODE, int RHS, bool DOT = false, int NSK = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSK > 0 ? PFR_RES_WPE : 1))) void k_residual(ResidArgs A, const cplx* __restrict__ X, int64_t Fc,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSK > 0 ? RES_WPE : 1))) void k_residual(ResidArgs A, const cplx* __restrict__ X, int64_t Fc,
                                                   cplx* __restrict__ R, double* __restrict__ acc,
                                                   const cplx* __restrict__ Mu, cplx* __restrict__ cpart) {
   // XCD-aware order: the workgroups of one 64-frequency group run together on one XCD, so the
@@ -3425,169 +2620,16 @@ __global__ __launch_bounds__(256) void k_fn_combine(const int* __restrict__ rows
 // ------------------------------------------------------------------ K5: gradient contraction + checks
 // s_{q,k} = sum_nz stiff[nz][k] * Lam[prow] * X[pcol]   (Sparse.py:173-176 matrix cotangent,
 // contracted with the stiffness matrices as JAX's einsum transpose does), fused with the checks.
-// Row-ordered gradient contraction with the backward-error checks of both solutions in the same pass.
-// Entries, rows ascending: each permuted row i starts with a pseudo-entry (-1, -1, -1, i), followed
-// by (column j, nz of A(i, j) or -1, nz of A(j, i) or -1, i) over the union of row i's and column
-// i's patterns.  One walk gathers x_j and lambda_j once per entry for
-//   s_{q,k} += S_k(i, j) lambda_i x_j                        (contraction, as k_contract)
-//   r_i = b_i - sum_j A(i, j) x_j,   s_i = g_i - sum_j A(j, i) lambda_j   (forward / adjoint residuals)
-// and the componentwise backward errors max_i |r_i| / (|A||x| + |b|)_i (resp. |A^T||lambda| + |g|);
-// the pseudo-entry gathers lambda_i and g_i instead (kept in registers for the row), so every entry
-// costs two vector loads whatever its kind (the base pointers are selected per entry, wave-uniform).
-// The walk is flat over the block's entries, 4 per step with all loads of a step independent (a
-// row-by-row loop chains several memory round trips per short row).  Block = a range of whole rows of
-// about equal entry count, one wave of 64 frequencies; partials as k_contract (k_reduce sums them).
-struct RowCheckArgs {
-  const cplx* K;
-  const double* M;
-  const double* freqs;
-  const double* rhsP;
-  double beta_re, beta_im, mass_sum;
-  const cplx* G;
-};
-
-// Per-entry coefficients in entry order (so that a step's scalar loads are addressed by the entry
-// counter alone, not by a loaded index): kme[3 e] = K(i, j), kme[3 e + 1] = K(j, i),
-// kme[3 e + 2] = (M(i, j), M(j, i)) (zeros where the entry is absent), se[NS e + k] = S_k(i, j).
-// Refreshed on the device whenever K may have changed (every sweep) / once for S.
-__global__ void k_gather_entries(const int4* __restrict__ ent, int nent, const cplx* __restrict__ K,
-                                 const double* __restrict__ M, const double* __restrict__ stiff, int ns,
-                                 cplx* __restrict__ kme, double* __restrict__ se) {
+// Entries of the union pattern, rows ascending: each permuted row i starts with a pseudo-entry (-1, -1, -1, i),
+// followed by (column j, nz of A(i, j) or -1, nz of A(j, i) or -1, i) over the union of row i's and column i's
+// patterns.  se[NS e + k] = S_k(i, j) (zeros where the entry is absent), copied once per stiffness upload.
+__global__ void k_gather_entries(const int4* __restrict__ ent, int nent, const double* __restrict__ stiff, int ns,
+                                 double* __restrict__ se) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= nent) return;
   const int4 en = ent[e];
-  const bool ij = en.x >= 0 && en.y >= 0, ji = en.x >= 0 && en.z >= 0;
-  if (kme) {
-    kme[3 * (int64_t)e] = ij ? K[en.y] : make_double2(0, 0);
-    kme[3 * (int64_t)e + 1] = ji ? K[en.z] : make_double2(0, 0);
-    kme[3 * (int64_t)e + 2] = make_double2(ij ? M[en.y] : 0.0, ji ? M[en.z] : 0.0);
-  }
-  if (se)
-    for (int k = 0; k < ns; ++k) se[(int64_t)e * ns + k] = ij ? stiff[(int64_t)en.y * ns + k] : 0.0;
-}
-
-// NS: stiffness matrices contracted (12 when the coupling block B is absent, 18 otherwise; 0 = no
-// contraction, checks only).  The contraction and the checks run as two launches over the same
-// entries (CHECK = false, NS > 0 / CHECK = true, NS = 0): fused, the pair of varying gathers per entry
-// (x_j and lambda_j; the contraction alone gathers only x_j, lambda_i once per row) at the register
-// footprint of the 12-18 accumulators halves the loads in flight per SIMD -- measured 5.1 ms per
-// 2,048-frequency chunk against 0.9 + 1.2 ms for the two launches.
-// Branch-free per entry (pseudo-entry and tail handling by selects), so that the loads of a step stay
-// counted waits instead of the vmcnt(0) a branch between them would force.
-template <bool CHECK, int NS>
-__global__ __launch_bounds__(64) void k_contract_rows(const int* __restrict__ eblk, const int4* __restrict__ ent,
-                                                      const double* __restrict__ se, const cplx* __restrict__ kme,
-                                                      RowCheckArgs A, const cplx* __restrict__ Lam,
-                                                      const cplx* __restrict__ X, int64_t Fc, int nvalid,
-                                                      cplx* __restrict__ partial, double* __restrict__ acc_f,
-                                                      double* __restrict__ acc_a) {
-  // entries per step: every scalar operand of a step (entries, S rows / K, M values) is loaded up front
-  // in SGPRs, then every vector load, then one wait -- S needs 2 NS dwords per entry
-  constexpr int U = NS > 0 ? 2 : 4;
-  const int lane = threadIdx.x & 63;
-  const int64_t q = (int64_t)blockIdx.y * 64 + lane;
-  const int e0 = eblk[blockIdx.x], e1 = eblk[blockIdx.x + 1];
-  cplx acc[NS > 0 ? NS : 1];
-#pragma unroll
-  for (int k = 0; k < NS; ++k) acc[k] = make_double2(0, 0);
-  double om2 = 0.0, bsr = 0.0, bsi = 0.0;
-  if (CHECK) {
-    const double om = 6.283185307179586 * A.freqs[q];
-    om2 = om * om;
-    bsr = fma(-om2, A.mass_sum, A.beta_re);
-    bsi = A.beta_im;
-  }
-  double bf = 0.0, ba = 0.0, open = 0.0;
-  bool bad = false;
-  cplx lam = make_double2(0, 0), r = lam, s = lam;
-  double dr = 0.0, ds = 0.0;
-  const cplx* __restrict__ Xq = X + q;
-  const cplx* __restrict__ Lq = Lam + q;
-  const cplx* __restrict__ Gq = A.G + q;
-  for (int e = e0; e < e1; e += U) {
-    // the entry array is padded by 4 entries: the step's entries load as one block
-    int4 en[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) en[u] = ent[e + u];
-    double sv[U][NS > 0 ? NS : 1];
-    cplx kij[U], kji[U], mm[U];
-    double rv[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-#pragma unroll
-      for (int k = 0; k < NS; ++k) sv[u][k] = se[(int64_t)(e + u) * NS + k];
-      if (CHECK) {
-        kij[u] = kme[3 * (int64_t)(e + u)];
-        kji[u] = kme[3 * (int64_t)(e + u) + 1];
-        mm[u] = kme[3 * (int64_t)(e + u) + 2];
-        rv[u] = A.rhsP[max(en[u].w, 0)];
-      }
-    }
-    cplx v1[U], v2[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const bool pseudo = en[u].x < 0;                           // wave-uniform
-      const int64_t o = (int64_t)(pseudo ? max(en[u].w, 0) : en[u].x) * Fc;
-      v1[u] = (pseudo ? Lq : Xq)[o];                             // lambda_i | x_j
-      if (CHECK) v2[u] = (pseudo ? Gq : Lq)[o];                  // g_i | lambda_j
-    }
-    __builtin_amdgcn_sched_group_barrier(0x020, CHECK ? 2 * U : U, 0);   // the step's vector loads first
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const bool in = e + u < e1;                                // wave-uniform
-      const bool start = in && en[u].x < 0;                      // a row starts here
-      if (NS > 0) {
-        lam = start ? v1[u] : lam;
-        const cplx p = cscale(cmul(lam, v1[u]), in ? 1.0 : 0.0);   // S is zero on pseudo / absent entries
-#pragma unroll
-        for (int k = 0; k < NS; ++k) {
-          acc[k].x = fma(sv[u][k], p.x, acc[k].x);
-          acc[k].y = fma(sv[u][k], p.y, acc[k].y);
-        }
-      }
-      if (CHECK) {
-        // close the previous row where a new one starts
-        const double cr = cabs1(r), cs = cabs1(s);
-        const bool closing = start && open != 0.0;
-        bad = bad || (closing && (!isfinite(cr) || !isfinite(cs) || !isfinite(dr) || !isfinite(ds) ||
-                                  (dr == 0.0 && cr > 0.0) || (ds == 0.0 && cs > 0.0)));
-        bf = closing && dr > 0.0 ? fmax(bf, cr / dr) : bf;
-        ba = closing && ds > 0.0 ? fmax(ba, cs / ds) : ba;
-        open = start ? 1.0 : open;
-        const double m = in ? 1.0 : 0.0;                          // kme is zero on pseudo / absent entries
-        const cplx aij = cscale(make_double2(fma(-om2, mm[u].x, kij[u].x), kij[u].y), m);
-        const cplx aji = cscale(make_double2(fma(-om2, mm[u].y, kji[u].x), kji[u].y), m);
-        const cplx b = make_double2(rv[u] * bsr, rv[u] * bsi);
-        r = start ? b : cfms(r, aij, v1[u]);
-        s = start ? v2[u] : cfms(s, aji, v2[u]);
-        dr = start ? cabs1(b) : fma(cabs1(aij), cabs1(v1[u]), dr);
-        ds = start ? cabs1(v2[u]) : fma(cabs1(aji), cabs1(v2[u]), ds);
-      }
-    }
-  }
-  const bool valid = q < nvalid;
-#pragma unroll
-  for (int k = 0; k < NS; ++k) {
-    double re = valid ? acc[k].x : 0.0, im = valid ? acc[k].y : 0.0;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      re += __shfl_xor(re, o);
-      im += __shfl_xor(im, o);
-    }
-    if (lane == 0) partial[((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * NS + k] = make_double2(re, im);
-  }
-  if (CHECK) {
-    if (open != 0.0) {
-      const double cr = cabs1(r), cs = cabs1(s);
-      bad = bad || !isfinite(cr) || !isfinite(cs) || !isfinite(dr) || !isfinite(ds) || (dr == 0.0 && cr > 0.0) ||
-            (ds == 0.0 && cs > 0.0);
-      if (dr > 0.0) bf = fmax(bf, cr / dr);
-      if (ds > 0.0) ba = fmax(ba, cs / ds);
-    }
-    if (bad) bf = ba = __longlong_as_double(0x7ff0000000000000LL);
-    atomicMax(reinterpret_cast<unsigned long long*>(acc_f + q), (unsigned long long)__double_as_longlong(bf));
-    atomicMax(reinterpret_cast<unsigned long long*>(acc_a + q), (unsigned long long)__double_as_longlong(ba));
-  }
+  const bool ij = en.x >= 0 && en.y >= 0;
+  for (int k = 0; k < ns; ++k) se[(int64_t)e * ns + k] = ij ? stiff[(int64_t)en.y * ns + k] : 0.0;
 }
 
 // Gradient contraction, entry-major: w_k = sum_e S_k(e) P_e with P_e = sum_q lambda_i(q) x_j(q) -- the
@@ -3597,10 +2639,7 @@ __global__ __launch_bounds__(64) void k_contract_rows(const int* __restrict__ eb
 // frequency group: with the sum over frequencies inside, the 12-18 scalar stiffness loads per entry and
 // the per-lane accumulators of all stiffness matrices drop out of the frequency loop).
 // Pseudo entries (row starts) and absent entries carry S = 0.  One partial per wave (k_reduce).
-#ifndef PFR_CEG_EW
-#define PFR_CEG_EW 8
-#endif
-constexpr int CEG_EW = PFR_CEG_EW;   // entries per wave of k_contract_eg
+constexpr int CEG_EW = 8;   // entries per wave of k_contract_eg
 // MS: lambda = m_q Lam per frequency (functional correction: Lam is the adjoint of fr, m_q the loss
 // cotangent scale k_correct_finish formed); m_q = 0 on the padded frequencies.
 template <int NS, int EW, bool MS>
@@ -3806,32 +2845,15 @@ void launch_schur(bool sym, const DevPattern& P, const int4* tiles, int ntiles, 
                   const int2* gx, int ngroups, double2* F, int64_t Fc, hipStream_t st) {
   if (ntiles <= 0) return;
   dim3 g((ntiles + 3) / 4, ngroups * (64 / SCHUR_QG)), b(256);
-  static const int ku = [] {
-    const char* e = getenv("PFR_SCHUR_KU");   // tuning knob: pivot steps per prefetched batch
-    return e ? atoi(e) : 1;   // 1 at 3 waves/SIMD measured 4 % faster than 2 at 2 waves/SIMD
-  }();
-  if (sym && ku == 1) LAUNCH(k_schur_sym_level<1>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
-  else if (sym) LAUNCH(k_schur_sym_level<2>, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
+  if (sym) LAUNCH(k_schur_sym_level, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
   else LAUNCH(k_schur_level, g, b, st, P, tiles, ntiles, g1, gxp, gx, F, Fc);
 }
 
-void launch_schur_blk(int bc, const DevPattern& P, const int4* blocks, int nblocks, const int* bg1, const int* bgxp,
+// 4 LDS buffers of one pivot each, 16 x 16 blocks (measured best of 2-4 buffers, 1-2 pivots per stage, 16 x 8 blocks)
+void launch_schur_blk(const DevPattern& P, const int4* blocks, int nblocks, const int* bg1, const int* bgxp,
                       const int2* bgx, int ngroups, double2* F, int64_t Fc, hipStream_t st) {
   if (nblocks <= 0) return;
-  static const int cfg = [] {
-    const char* e = getenv("PFR_SCHUR_BLK_CFG");   // tuning knob: buffers x 10 + pivots per stage
-    return e ? atoi(e) : 41;
-  }();
-  const dim3 g(nblocks, ngroups), b(64 * bc);
-  if (bc == 8) {
-    if (cfg == 31) LAUNCH((k_schur_sym_blk<3, 1, 8>), g, b, st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
-    else LAUNCH((k_schur_sym_blk<4, 1, 8>), g, b, st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
-  } else {
-    if (cfg == 31) LAUNCH((k_schur_sym_blk<3, 1, 16>), g, b, st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
-    else if (cfg == 21) LAUNCH((k_schur_sym_blk<2, 1, 16>), g, b, st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
-    else if (cfg == 22) LAUNCH((k_schur_sym_blk<2, 2, 16>), g, b, st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
-    else LAUNCH((k_schur_sym_blk<4, 1, 16>), g, b, st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
-  }
+  LAUNCH((k_schur_sym_blk<4, 1, 16>), dim3(nblocks, ngroups), dim3(64 * 16), st, P, blocks, nblocks, bg1, bgxp, bgx, F, Fc);
 }
 
 void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, const int2* xl, int ngroups, double2* F,
@@ -3843,112 +2865,38 @@ void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, cons
   else LAUNCH(k_assemble_level<1>, g, b, st, recs, nrec, xptr, xl, F, Fc, freqs, K, M, data, ds, nvalid);
 }
 
-template <int QF>
-static void launch_factor_lds_q(const DevPattern& P, const int* lvl, int nfronts, int maxns, double2* F, int64_t Fc,
-                                int* flags, hipStream_t st) {
-  const size_t lds = ((size_t)maxns * (maxns + 1) / 2 + (size_t)maxns * KB) * QF * sizeof(double2);
-  static const bool attr = [] {   // dynamic LDS beyond the default 64 KiB (up to 64 pivots x 4 frequencies: 146 KiB)
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_factor_sym_lds<QF>),
+void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int maxns, double2* F, int64_t Fc, int* flags,
+                       hipStream_t st) {
+  const size_t lds = ((size_t)maxns * (maxns + 1) / 2 + (size_t)maxns * KB) * sizeof(double2);
+  static const bool attr = [] {   // dynamic LDS beyond the default 64 KiB (up to 64 pivots: 37 KiB; headroom)
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_factor_sym_lds<1>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   }();
   (void)attr;
-  LAUNCH_DYN(k_factor_sym_lds<QF>, dim3((unsigned)(nfronts * (Fc / QF))), dim3(256), lds, st, P, lvl, F, Fc, flags,
-             maxns);
-}
-
-void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int maxns, int qf, double2* F, int64_t Fc,
-                       int* flags, hipStream_t st) {
-  if (qf == 1) launch_factor_lds_q<1>(P, lvl, nfronts, maxns, F, Fc, flags, st);
-  else if (qf == 2) launch_factor_lds_q<2>(P, lvl, nfronts, maxns, F, Fc, flags, st);
-  else launch_factor_lds_q<4>(P, lvl, nfronts, maxns, F, Fc, flags, st);
+  LAUNCH_DYN(k_factor_sym_lds<1>, dim3((unsigned)(nfronts * Fc)), dim3(256), lds, st, P, lvl, F, Fc, flags, maxns);
 }
 
 void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F,
-                   int64_t Fc, int* flags, hipStream_t st, const AsmArgs& asmb) {
-  if (sym) LAUNCH(k_factor_sym, dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags, asmb);
+                   int64_t Fc, int* flags, hipStream_t st) {
+  if (sym) LAUNCH(k_factor_sym, dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
   else LAUNCH(k_factor_level<true>, dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
-}
-
-static long long h_wtrace_base = 0, h_wtrace_cap = 0, h_wtrace_launch = 0;
-int set_wave_trace(unsigned long long* buf, long long cap) {
-  h_wtrace_base = 0;
-  h_wtrace_launch = 0;
-  h_wtrace_cap = buf ? cap : 0;
-  long long zero = 0;
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_wtrace), &buf, sizeof(buf)) != hipSuccess) return -1;
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_wtrace_cap), &h_wtrace_cap, sizeof(long long)) != hipSuccess) return -1;
-  if (hipMemcpyToSymbol(HIP_SYMBOL(g_wtrace_base), &zero, sizeof(long long)) != hipSuccess) return -1;
-  return 0;
-}
-long long wave_trace_count() { return h_wtrace_base; }
-// before a traced launch of `waves` waves: its records start at the running base
-static void wtrace_launch(long long waves, hipStream_t st) {
-  if (!h_wtrace_cap) return;
-  (void)hipStreamSynchronize(st);     // diagnostic runs only: the previous traced launch has read the old base
-  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wtrace_base), &h_wtrace_base, sizeof(long long));
-  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wtrace_launch), &h_wtrace_launch, sizeof(long long));
-  h_wtrace_base += waves;
-  ++h_wtrace_launch;
 }
 
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
                     const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,
-                    const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st, int rl,
-                    int swz, const int4* shu, int nshu, int pu, int shu_st) {
+                    const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st, bool pipelined) {
   if (nitems <= 0) return;
   const bool small = maxns <= 8;
-  if constexpr (OFF_G == 1 && OB == 8) if (shu && nshu > 0 && !small) {
-    dim3 gs((unsigned)nshu, ngroups), bs(256);
-#define SHU(MD, T) LAUNCH((k_offdiag_shu<MD, T>), gs, bs, st, P, items, shu, nshu, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid)
-    if (mode == 0 && shu_st == 4) SHU(0, 4);
-    else if (mode == 0) SHU(0, 2);
-    else if (shu_st == 4) SHU(1, 4);
-    else SHU(1, 2);
-#undef SHU
-    return;
-  }
-  const int rlim = OFF_G == 1 ? rl % 100 : 0, rrows = rl >= 100 ? OFF_RPL : 1;
-  if constexpr (OFF_G == 1) if (rlim > 0 && !small && maxns <= rlim) {
-    // right-looking rows (symmetric analyses): rl = n (one row per wave) or 100 + n (an item's rows per wave)
-    dim3 g((unsigned)(((int64_t)nitems * (OFF_RPL / rrows) + 3) / 4), ngroups), b(256);
-#define RL(MD, N, RR) LAUNCH((k_offdiag_rl<MD, N, RR>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid)
-    if (rrows == 1) {
-      if (mode == 0 && maxns <= 16) RL(0, 16, 1);
-      else if (mode == 0 && maxns <= 24) RL(0, 24, 1);
-      else if (mode == 0) RL(0, 32, 1);
-      else if (maxns <= 16) RL(1, 16, 1);
-      else if (maxns <= 24) RL(1, 24, 1);
-      else RL(1, 32, 1);
-    } else {
-      if (mode == 0 && maxns <= 16) RL(0, 16, OFF_RPL);
-      else if (mode == 0) RL(0, 24, OFF_RPL);
-      else if (maxns <= 16) RL(1, 16, OFF_RPL);
-      else RL(1, 24, OFF_RPL);
-    }
-#undef RL
-    return;
-  }
   dim3 g((nitems + 3) / 4, ngroups * OFF_G), b(256);
-  wtrace_launch((long long)g.x * g.y * 4, st);
   static_assert(OB >= 8, "the SMALL variant covers pivot blocks of up to 8");
-#define OL(MD, SM) LAUNCH((k_offdiag_level<MD, SM>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid, swz)
-  // pu > 2: the prefix loop with pu pivots' loads in flight (narrow levels, where few waves are resident)
-  if (!small && mode == 0 && pu >= 8) {
-    LAUNCH((k_offdiag_level<0, false, 8>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid, swz);
-    return;
-  }
-  if (!small && mode == 0 && pu >= 4) {
-    LAUNCH((k_offdiag_level<0, false, 4>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid, swz);
-    return;
-  }
-  if (!small && mode == 0 && pu == 3) {
-    LAUNCH((k_offdiag_level<0, false, 3>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid, swz);
-    return;
-  }
-  if (mode == 0 && small) OL(0, true);
-  else if (mode == 0) OL(0, false);
-  else if (small) OL(1, true);
-  else OL(1, false);
+#define OL(MD, SM, PU) LAUNCH((k_offdiag_level<MD, SM, PU>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid)
+  // pipelined: the prefix loop with the next pivot's loads issued before the current pivot's products (the
+  // narrow levels, where few waves are resident)
+  if (mode == 0 && small) OL(0, true, 2);
+  else if (mode == 0 && pipelined) OL(0, false, 3);
+  else if (mode == 0) OL(0, false, 2);
+  else if (small) OL(1, true, 2);
+  else OL(1, false, 2);
 #undef OL
 }
 
@@ -4034,70 +2982,26 @@ void launch_fn_combine(const int* rows, int nrows, const double2* fcoef, double2
 
 void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, bool small, int ngroups,
                     const double2* F, int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0,
-                    const double2* Y1, double2* X1, const int* reach1, hipStream_t st, int split, int small_cfg,
-                    int tiny, int pp) {
+                    const double2* Y1, double2* X1, const int* reach1, hipStream_t st, int split, int tiny) {
   if (nfronts <= 0) return;
   UPair a{Y0, X0, reach0, skip0}, b{Y1, X1, reach1, nullptr};
   if (tiny > 0 && split <= 1) {
     // every pivot block of the level <= tiny (4 or 8): one wave per (front, group)
     dim3 gt((unsigned)((nfronts + 3) / 4), ngroups), bt(256);
     if (tiny <= 4) LAUNCH((k_usolve2_tiny<4>), gt, bt, st, P, lvl, nfronts, F, Fc, a, b);
-    else if (tiny <= 8) LAUNCH((k_usolve2_tiny<8>), gt, bt, st, P, lvl, nfronts, F, Fc, a, b);
-    else LAUNCH(k_usolve2_wave, gt, bt, st, P, lvl, nfronts, F, Fc, a, b);
+    else LAUNCH((k_usolve2_tiny<8>), gt, bt, st, P, lvl, nfronts, F, Fc, a, b);
     return;
   }
   dim3 g(nfronts, ngroups), bl(64 * W);
   const int rs = split > 1;
   // split > 1: the pivot rows' update part over `split` workgroups per front first (the small-front
   // register shape: many short waves)
-  if (rs && pp) LAUNCH((k_usolve2_upd<true, 2, 4, true>), dim3(nfronts * split, ngroups), dim3(64 * SPLIT_W), st, P, lvl, F,
-                       Fc, a, b, split);
-  else if (rs) LAUNCH((k_usolve2_upd<true, 2, 4>), dim3(nfronts * split, ngroups), dim3(64 * SPLIT_W), st, P, lvl, F, Fc, a,
-                      b, split);
+  if (rs) LAUNCH((k_usolve2_upd<true, 2, 4>), dim3(nfronts * split, ngroups), dim3(64 * SPLIT_W), st, P, lvl, F, Fc, a, b, split);
   // symmetric mode only (the paired top-down pass serves the symmetric loss + gradient sweep).  Small-front levels:
-  // SR pivot rows per pass share each gathered update-row value (small_cfg 0: 2 rows x 4 values at 4 waves/SIMD;
-  // 1: 4 x 4 at 3; 2: 8 x 2 at 3 -- more rows per pass, fewer re-gathers of the update-row solution)
-  if (small && small_cfg == 1) LAUNCH((k_usolve2_level<true, 4, 4, 3>), g, bl, st, P, lvl, F, Fc, a, b, rs);
-  else if (small && small_cfg == 2) LAUNCH((k_usolve2_level<true, 8, 2, 3>), g, bl, st, P, lvl, F, Fc, a, b, rs);
-  else if (small) LAUNCH((k_usolve2_level<true, 2, 4, 4>), g, bl, st, P, lvl, F, Fc, a, b, rs);
+  // 8 pivot rows per pass share each gathered update-row value, 2 values per chunk, 3 waves/SIMD (18 % less traffic
+  // than 2 rows x 4 values at 4 waves/SIMD, the same time: profiles/r04/solve_traffic/)
+  if (small) LAUNCH((k_usolve2_level<true, 8, 2, 3>), g, bl, st, P, lvl, F, Fc, a, b, rs);
   else LAUNCH((k_usolve2_level<true, 4, 8, 2>), g, bl, st, P, lvl, F, Fc, a, b, rs);
-}
-
-void launch_usolve2_flow(const DevPattern& P, const FlowDesc& d, int ngroups, const double2* F, int64_t Fc,
-                         const double2* Y0, double2* X0, const int* reach0, const int* skip0, const double2* Y1,
-                         double2* X1, const int* reach1, hipStream_t st) {
-  if (d.ntasks <= 0) return;
-  UPair a{Y0, X0, reach0, skip0}, b{Y1, X1, reach1, nullptr};
-  FlowArgs G{d.tasks, d.ntasks, d.pslot, d.words, d.words + 1, d.words + 1 + (int64_t)d.nslots * ngroups, d.flags};
-  (void)hipMemsetAsync(d.words, 0, d.words_bytes, st);
-  LAUNCH((k_usolve2_flow<4, 8>), dim3((unsigned)(d.ntasks * ngroups)), dim3(256), st, P, F, Fc, a, b, G, ngroups);
-}
-
-void launch_lsolve_flow(int rhs_mode, const DevPattern& P, const LFlowDesc& d, int ngroups, const double2* F, int64_t Fc,
-                        double2* const* WV, const RhsDesc* rd, double2* const* Y, const int* const* reach, hipStream_t st) {
-  if (d.ntasks <= 0) return;
-  LSlices S{};
-  for (int z = 0; z < MAX_SLICES; ++z) {
-    S.WV[z] = WV[z];
-    S.Y[z] = Y[z];
-    S.reach[z] = reach[z];
-    S.R[z] = make_rhs(rd[z]);
-  }
-  const int64_t per = (int64_t)d.nslots * MAX_SLICES * ngroups;
-  LFlowArgs G{d.tasks, d.ntasks, d.cptr, d.cslot, d.parts, d.words, d.words + 1, d.words + 1 + per, d.flags};
-  (void)hipMemsetAsync(d.words, 0, d.words_bytes, st);
-  if (rhs_mode == 0) LAUNCH(k_lsolve_flow<0>, dim3((unsigned)(d.ntasks * ngroups)), dim3(256), st, P, S, F, Fc, G, ngroups);
-  else LAUNCH(k_lsolve_flow<3>, dim3((unsigned)(d.ntasks * ngroups)), dim3(256), st, P, S, F, Fc, G, ngroups);
-}
-
-void launch_factor_flow(const DevPattern& P, const FactorFlowDesc& d, int ngroups, double2* F, int64_t Fc,
-                        const AsmArgs& asmb, hipStream_t st) {
-  if (d.ntasks <= 0) return;
-  const int64_t per = (int64_t)d.nslots * ngroups;
-  FFlowArgs G{d.tasks, d.ntasks, d.cptr, d.cslot, d.item_end, d.nb, d.nc, d.words, d.words + 1, d.words + 1 + per,
-              d.words + 1 + 2 * per, d.flags, d.items, d.orec, d.oxp, d.ox, d.blocks, d.bg1, d.bgxp, d.bgx, asmb};
-  (void)hipMemsetAsync(d.words, 0, d.words_bytes, st);
-  LAUNCH(k_factor_flow, dim3((unsigned)(d.ntasks * ngroups)), dim3(1024), st, P, F, Fc, G, ngroups);
 }
 
 void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nrows, const double2* Kd,
@@ -4166,22 +3070,9 @@ void launch_functional(const FunctionalArgs& A, const double2* X, int64_t Fc, in
   LAUNCH(k_functional, dim3((unsigned)((Fc + 63) / 64)), dim3(64), st, A, X, Fc, nvalid, q0, fr_out, loss_terms, G);
 }
 
-void launch_gather_entries(const int4* ent, int nent, const double2* K, const double* M, const double* stiff, int ns,
-                           double2* kme, double* se, hipStream_t st) {
+void launch_gather_entries(const int4* ent, int nent, const double* stiff, int ns, double* se, hipStream_t st) {
   if (nent <= 0) return;
-  LAUNCH(k_gather_entries, dim3((nent + 255) / 256), dim3(256), st, ent, nent, K, M, stiff, ns, kme, se);
-}
-
-void launch_contract_rows(bool check, const int* eblk, const int4* ent, int nblk, int ngroups, const double* se,
-                          int n_stiff, const double2* kme, const RowCheckDesc& d, const double2* Lam, const double2* X,
-                          int64_t Fc, int nvalid, double2* partial, double* acc_f, double* acc_a, hipStream_t st) {
-  RowCheckArgs a;
-  a.K = d.K; a.M = d.M; a.freqs = d.freqs; a.rhsP = d.rhsP; a.beta_re = d.beta_re; a.beta_im = d.beta_im;
-  a.mass_sum = d.mass_sum; a.G = d.G;
-  const dim3 g(nblk, ngroups), b(64);
-#define CR(C, N) LAUNCH((k_contract_rows<C, N>), g, b, st, eblk, ent, se, kme, a, Lam, X, Fc, nvalid, partial, acc_f, acc_a)
-  if (check) CR(true, 0);
-#undef CR
+  LAUNCH(k_gather_entries, dim3((nent + 255) / 256), dim3(256), st, ent, nent, stiff, ns, se);
 }
 
 int contract_eg_parts(int nent) { return ((nent + CEG_EW - 1) / CEG_EW + 3) / 4; }   // workgroups of 4 waves

@@ -38,29 +38,23 @@ void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPac
 void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, const int2* xl, int ngroups, double2* F,
                      int64_t Fc, const double* freqs, const double2* K, const double* M, const double2* data,
                      int64_t ds, int nvalid, hipStream_t st);
-// asmb.recs != NULL (symmetric mode): A11 gathered by the LU kernel itself (no k_assemble_level launch)
 void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F, int64_t Fc,
-                   int* flags, hipStream_t st, const AsmArgs& asmb = AsmArgs());
-// symmetric A11 LU with the pivot block in LDS (one front x qf = 2 or 4 frequencies per workgroup); maxns =
-// the level's largest pivot block (sizes the dynamic LDS: (maxns (maxns + 1) / 2 + 4 maxns) x 16 qf B)
-void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int maxns, int qf, double2* F, int64_t Fc,
-                       int* flags, hipStream_t st);
-// Schur complement A22 -= L21 U12 for a level's tile list (TM x TN = 4 x 4 tiles)
-// wave trace of the L21 launches (diagnostic): 4 x u64 per wave (start, end, HW_ID, tag = 1 + 16 item | 0 idle)
-int set_wave_trace(unsigned long long* buf, long long cap);
-long long wave_trace_count();
+                   int* flags, hipStream_t st);
+// symmetric A11 LU with the pivot block in LDS (one front x one frequency per workgroup); maxns = the level's
+// largest pivot block (sizes the dynamic LDS: (maxns (maxns + 1) / 2 + 4 maxns) x 16 B)
+void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int maxns, double2* F, int64_t Fc, int* flags,
+                       hipStream_t st);
+// L21 rows (and U12 columns in general mode) of a level's items; pipelined: the software-pipelined prefix
+// (symmetric, operator-form launches with few waves)
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
                     const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,
                     const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st,
-                    int rl = 0,    // rl > 0 (symmetric analyses): levels with 8 < maxns <= rl right-looking (k_offdiag_rl)
-                    int swz = 1,   // 0: no XCD-aware workgroup order
-                    const int4* shu = nullptr, int nshu = 0,    // != NULL: k_offdiag_shu over these tasks
-                    int pu = 2,    // prefix loads in flight, in pivots (2, 4 or 8)
-                    int shu_st = 2);   // k_offdiag_shu stage: pivot rows (2 or 4)
+                    bool pipelined = false);
+// Schur complement A22 -= L21 U12 for a level's tile list (TM x TN = 4 x 4 tiles)
 void launch_schur(bool sym, const DevPattern& P, const int4* tiles, int ntiles, const int* g1, const int* gxp,
                   const int2* gx, int ngroups, double2* F, int64_t Fc, hipStream_t st);
 // symmetric mode, large update blocks: 16 x 16 blocks, operands staged in LDS per workgroup
-void launch_schur_blk(int bc, const DevPattern& P, const int4* blocks, int nblocks, const int* bg1, const int* bgxp,
+void launch_schur_blk(const DevPattern& P, const int4* blocks, int nblocks, const int* bg1, const int* bgxp,
                       const int2* bgx, int ngroups, double2* F, int64_t Fc, hipStream_t st);
 // which: 0 = L (bottom-up), 1 = U (top-down), 2 = U^T (bottom-up), 3 = L^T (top-down)
 // split > 1 (L and U solves): the update part of every front (L: the update rows; U: the pivot rows'
@@ -90,65 +84,7 @@ void launch_fn_combine(const int* rows, int nrows, const double2* fcoef, double2
 void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, bool small, int ngroups,
                     const double2* F, int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0,
                     const double2* Y1, double2* X1, const int* reach1, hipStream_t st, int split = 1,
-                    int small_cfg = 0, int tiny = 0,    // tiny 4 / 8: the level's pivot blocks all <= tiny (k_usolve2_tiny)
-                    int pp = 0);   // split update parts software-pipelined (usolve2_upd_pp)
-// dependency-driven pass over the narrow top of the elimination tree (one launch, task tickets, per-front
-// completion words): the task list and its words (ticket, done, cnt: 1 + 2 nslots ngroups unsigned,
-// zeroed by the launcher), flags per frequency (a spin timeout sets PFR_FLAG_BAD_PIVOT)
-struct FlowDesc {
-  const int4* tasks = nullptr;
-  int ntasks = 0;
-  const int* pslot = nullptr;
-  int nslots = 0;
-  unsigned* words = nullptr;
-  size_t words_bytes = 0;
-  int* flags = nullptr;
-};
-void launch_usolve2_flow(const DevPattern& P, const FlowDesc& d, int ngroups, const double2* F, int64_t Fc,
-                         const double2* Y0, double2* X0, const int* reach0, const int* skip0, const double2* Y1,
-                         double2* X1, const int* reach1, hipStream_t st);
-// the sliced bottom-up chain over the narrow top (4 slices as launch_lsolve_multi; words: ticket, pdone, rcnt:
-// 1 + 2 nslots 4 ngroups unsigned).  cptr / cslot: per slot its in-region children REACHED in each slice
-// are waited for -- the host lists, per (slot, slice), the children of that slice (cptr indexed slot * 4 + z)
-struct LFlowDesc {
-  const int4* tasks = nullptr;
-  int ntasks = 0;
-  const int* cptr = nullptr;
-  const int* cslot = nullptr;
-  const int* parts = nullptr;
-  int nslots = 0;
-  unsigned* words = nullptr;
-  size_t words_bytes = 0;
-  int* flags = nullptr;
-};
-void launch_lsolve_flow(int rhs_mode, const DevPattern& P, const LFlowDesc& d, int ngroups, const double2* F, int64_t Fc,
-                        double2* const* WV, const RhsDesc* rd, double2* const* Y, const int* const* reach, hipStream_t st);
-// the factorisation's narrow top (symmetric mode, operator form) in one launch: tasks (kind 0 A11 LU, 1 L21
-// items, 2 Schur blocks; front; first item / block; slot), words ticket, a_done, b_cnt, c_cnt (1 + 3 nslots
-// ngroups unsigned, zeroed by the launcher)
-struct FactorFlowDesc {
-  const int4* tasks = nullptr;
-  int ntasks = 0;
-  const int* cptr = nullptr;
-  const int* cslot = nullptr;
-  const int* item_end = nullptr;
-  const int* nb = nullptr;
-  const int* nc = nullptr;
-  int nslots = 0;
-  unsigned* words = nullptr;
-  size_t words_bytes = 0;
-  int* flags = nullptr;
-  const int4* items = nullptr;
-  const int2* orec = nullptr;
-  const int* oxp = nullptr;
-  const int2* ox = nullptr;
-  const int4* blocks = nullptr;
-  const int* bg1 = nullptr;
-  const int* bgxp = nullptr;
-  const int2* bgx = nullptr;
-};
-void launch_factor_flow(const DevPattern& P, const FactorFlowDesc& d, int ngroups, double2* F, int64_t Fc,
-                        const AsmArgs& asmb, hipStream_t st);
+                    int tiny = 0);    // tiny 4 / 8: the level's pivot blocks all <= tiny (k_usolve2_tiny)
 // Hessian sweep: tangent right-hand sides (rows of the permuted matrix, or of its
 // transpose with accumulate = 1) and the directional derivative of the loss cotangent
 void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nrows, const double2* Kd,
@@ -158,28 +94,13 @@ void launch_functional_tangent(const FunctionalArgs& A, const double2* X, const 
                                int64_t q0, double2* G, hipStream_t st);
 void launch_functional(const FunctionalArgs& A, const double2* X, int64_t Fc, int nvalid, int64_t q0, double* fr_out,
                        double* loss_terms, double2* G, hipStream_t st);
-// Row-ordered gradient contraction fused with the forward / adjoint backward-error checks
-// (check = false: contraction only); partials as launch_contract; acc_f / acc_a: per-frequency
-// maxima (zero on entry), finished by launch_berr_finish
-struct RowCheckDesc {
-  const double2* K = nullptr;
-  const double* M = nullptr;
-  const double* freqs = nullptr;
-  const double* rhsP = nullptr;
-  double beta_re = 0, beta_im = 0, mass_sum = 0;
-  const double2* G = nullptr;
-};
-void launch_contract_rows(bool check, const int* eblk, const int4* ent, int nblk, int ngroups, const double* se,
-                          int n_stiff, const double2* kme, const RowCheckDesc& d, const double2* Lam, const double2* X,
-                          int64_t Fc, int nvalid, double2* partial, double* acc_f, double* acc_a, hipStream_t st);
 // gradient contraction with the frequency sum first (one partial per wave: contract_eg_parts of them)
 int contract_eg_parts(int nent);
 // msc (may be NULL): per-frequency factor of Lam (functional correction: the loss cotangent scale)
 void launch_contract_eg(const int4* ent, int nent, const double* se, int n_stiff, const double2* Lam, const double2* X,
                         int64_t Fc, int nvalid, double2* partial, hipStream_t st, const double2* msc = nullptr);
-// entry-ordered copies of K / M (kme, may be NULL) and of the stiffness matrices (se, may be NULL)
-void launch_gather_entries(const int4* ent, int nent, const double2* K, const double* M, const double* stiff, int ns,
-                           double2* kme, double* se, hipStream_t st);
+// entry-ordered copy of the stiffness matrices (se)
+void launch_gather_entries(const int4* ent, int nent, const double* stiff, int ns, double* se, hipStream_t st);
 void launch_rhs_dot(const int* sup, const double* val, int n_sup, const double2* Lam, int64_t Fc, double2* t_out,
                     hipStream_t st, const double2* msc = nullptr);
 // w_out[k] += -sum(partial[., k]) + e_k sum_q t_q ;  loss_out += sum_q loss_terms (q < nvalid)

@@ -10,8 +10,7 @@
 * kernel variants forced on small meshes through the per-solver launch knobs (read when a solver
   is created): PFR_US2_SMALL=0 (every level through the large-front paired top-down solve),
   PFR_US2_SMALL=1024 (every level through the small-front variant), PFR_FAC_WMAX=1 / 16 and
-  PFR_SOLVE_WMAX=1 (one-wave and widest LU / solve workgroups), PFR_OFF_SMALL=0 (the bottom
-  levels' off-diagonal rows through the general kernel instead of the no-prefix variant),
+  PFR_SOLVE_WMAX=1 (one-wave and widest LU / solve workgroups),
   PFR_SOLVE_SPLIT=0 / 1000000 (the solves' update parts never / always split over workgroups).
 
 Tolerances.  These systems are badly scaled (membrane, bending and unit Dirichlet rows) and their
@@ -158,12 +157,9 @@ def test_c2_forward_sweep_matches_truth():
     {"PFR_US2_SMALL": "1024"},
     {"PFR_FAC_WMAX": "1", "PFR_SOLVE_WMAX": "1"},
     {"PFR_FAC_WMAX": "16", "PFR_SOLVE_WMAX": "8"},
-    {"PFR_CHECK_FUSED": "1", "PFR_CHECK": "3"},    # the fused walk replaces the checks without the correction
-    {"PFR_OFF_SMALL": "0"},
     {"PFR_SOLVE_SPLIT": "0"},          # every solve launch unsplit (the small meshes split by default)
     {"PFR_SOLVE_SPLIT": "1000000"},    # every solve launch split 16 ways
     {"PFR_FAC_LDS": "1"},              # every level's A11 LU through the LDS-resident kernel (1 frequency / workgroup)
-    {"PFR_FAC_LDS": "1", "PFR_FAC_LDS_QF": "4"},   # ... 4 frequencies per workgroup
     {"PFR_FAC_LDS": "-1"},             # auto: the levels where k_factor_sym would get few workgroups
     {"PFR_FAC_LDS": "0"},              # never (the global-memory A11 LU on every level)
     {"PFR_FN_DOT": "0"},               # fr from the top-down pass over the support's fronts
@@ -171,21 +167,11 @@ def test_c2_forward_sweep_matches_truth():
     {"PFR_FN_DOT": "0", "PFR_CONTRACT_WALK": "0"},
     {"PFR_LEAF_SIZE": "10000"},        # the deep MMD tree on a narrow sweep
     {"PFR_ORDERING": "2", "PFR_LEAF_SIZE": "96", "PFR_MD_DELTA": "0"},   # the rounds 1-3 ordering
-    {"PFR_FUSE_ASM": "1"},             # A11 gathered by the A11 LU kernel itself (no k_assemble_level launches)
-    {"PFR_US2_CFG": "1", "PFR_US2_SMALL": "1024"},   # small-front paired top-down pass, 4 rows x 4 values
-    {"PFR_US2_CFG": "0", "PFR_US2_SMALL": "1024"},   # ... 2 rows x 4 values (the default is 8 x 2)
-    {"PFR_FLOW": "3"},                 # both solve passes dependency-driven (every level narrow at this size)
-    {"PFR_FLOW": "3", "PFR_FLOW_WG": "16"},   # ... only the top levels, the rest level by level
-    {"PFR_FLOW": "2"},                 # the bottom-up chain only
-    {"PFR_FLOW": "7"},                 # the factorisation's narrow top too (every level at this size)
-    {"PFR_FLOW": "7", "PFR_FLOW_FWG": "8", "PFR_FLOW_WG": "8"},   # ... only the topmost levels
     {"PFR_CHECK": "27"},               # + the selective adjoint refinement (opt-in)
     {"PFR_CHECK": "27", "PFR_REFINE_TOL": "0"},   # ... every group listed (the first REFINE_CAP of each chunk)
     {"PFR_SCALE_CORR": "0"},           # the cotangent without the solve-error scale
-    {"PFR_OFF_RL": "32"},              # L21 rows right-looking on the levels with pivot blocks of 9-32
-    {"PFR_OFF_RL": "16"},
-    {"PFR_OFF_RL": "124"},             # ... two rows per wave
     {"PFR_US2_TINY": "8"},             # paired top-down pass one wave per front where pivot blocks are <= 8
+    {"PFR_OFF_PU_WAVES": "1000000000"},   # the pipelined L21 prefix on every launch
     {"PFR_US2_TINY": "0"},
 ])
 def test_kernel_variants_match_oracle(env, monkeypatch):
@@ -207,24 +193,6 @@ def test_kernel_variants_match_oracle(env, monkeypatch):
             grad_rel=_rel(x.grad.numpy(), go))
     assert abs(val.item() - lo) / abs(lo) < FR_RTOL
     assert _rel(x.grad.numpy(), go) < GRAD_RTOL
-    if env.get("PFR_CHECK_FUSED") == "1":
-        # the fused contraction + checks walk (k_contract_rows) must report the backward errors the
-        # separate k_residual walks report: same solutions, same per-frequency maxima (to rounding)
-        eng = p.engine()
-        fused_berr, fused_flags = eng.last_berr.cpu().numpy(), eng.last_flags
-        monkeypatch.setenv("PFR_CHECK_FUSED", "0")
-        q = make_problem("orthotropic", ny=6, device="cuda:0")
-        y = torch.tensor(theta, requires_grad=True)
-        q.getLossFunction(freqs, ref, "MSE_LOG_AFC")(y).backward()
-        plain_berr = q.engine().last_berr.cpu().numpy()
-        assert not fused_flags.any() and not q.engine().last_flags.any()
-        assert np.all(np.isfinite(fused_berr)) and np.all(fused_berr <= BERR_MAX)
-        # the residuals are rounding-level (~1e-16 .. 1e-15) and the two walks sum them in different
-        # orders: per frequency within a factor 4, the sweep's maximum of each column within 2
-        ratio = (fused_berr + 1e-18) / (plain_berr + 1e-18)
-        assert np.all(ratio < 4.0) and np.all(ratio > 0.25), (ratio.min(), ratio.max())
-        mr = fused_berr.max(axis=0) / plain_berr.max(axis=0)
-        assert np.all(mr < 2.0) and np.all(mr > 0.5), mr
 
 
 def test_engine_grows_after_small_first_call():
