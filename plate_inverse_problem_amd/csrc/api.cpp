@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <functional>
 #include <cstring>
 #include <string>
@@ -53,6 +54,7 @@ struct pfr_solver {
   int64_t nnz = 0;
   int64_t Fc = 0;  // frequencies per chunk (multiple of 64)
   std::vector<int32_t> level_ptr, level_maxf, level_maxns, level_W, perm, iperm;
+  std::vector<int32_t> tile_ptr, blk_ptr, asm_ptr, item_ptr;   // per level: first Schur tile / block, A11 record, L21 item
   DevPattern P{};
   // owned device arrays
   std::vector<void*> owned;
@@ -62,21 +64,17 @@ struct pfr_solver {
   int2* d_orec = nullptr;               // per item x lane group x pivot: (nz, first child source) of the entry
   int32_t* d_oxp = nullptr;             // per item: range of further child sources in d_ox
   int2* d_ox = nullptr;                 // (pivot * OFF_G OFF_RPL + row slot, element id)
-  std::vector<int32_t> item_ptr;
   int32_t* d_g1 = nullptr;              // per super-tile, lane group, position: first child source (or -1)
   int32_t* d_gxp = nullptr;             // per super-tile: range of further sources in d_gx
   int2* d_gx = nullptr;                 // (lane group * 16 + position, element id) of the rare extra sources
-  std::vector<int32_t> tile_ptr;
   // symmetric mode, fronts with large update blocks: 16 x 16 Schur blocks (k_schur_sym_blk)
   int4* d_blocks = nullptr;             // (front, i0, j0, 0), grouped by level
   int32_t* d_bg1 = nullptr;             // per block, wave, position: first child source (or -1)
   int32_t* d_bgxp = nullptr;            // per block: range of further sources in d_bgx
   int2* d_bgx = nullptr;                // (wave * 16 + position, element id)
-  std::vector<int32_t> blk_ptr;
   int4* d_asm = nullptr;                // panel-entry assembly records (dst, nz, first child source, 0), by level
   int32_t* d_asm_xp = nullptr;          // per 8-record chunk: range of further child sources in d_asm_x
   int2* d_asm_x = nullptr;              // (record within chunk, child element id)
-  std::vector<int32_t> asm_ptr;         // record offset of each level (multiple of 8)
   int32_t* d_colptr = nullptr;
   int32_t* d_rowind = nullptr;
   // symmetric mode (options.symmetric): U never formed; Dirichlet nodes decoupled
@@ -166,15 +164,22 @@ struct pfr_solver {
   // different streams overlap.
   struct ChunkEvents {
     hipEvent_t ev[6]{};
-    std::vector<hipEvent_t> kev;
+    std::vector<hipEvent_t> kev;        // factorisation kernel classes: NKC + 1 events per level
     bool used[5]{};
   };
   int timing = 0;
   std::vector<ChunkEvents> tev;
   int n_tev = 0;                        // chunks recorded by the last call
-  int64_t alg_bytes[5]{};               // algorithmic HBM bytes per frequency of each class (one sweep)
-  // per level: A11 assembly, A11 LU
-  std::vector<int64_t> lev_asm_bytes, lev_lu_bytes;
+  // algorithmic HBM bytes per frequency of each factorisation kernel class, per level (16 B per complex entry
+  // loaded or stored; index data is shared by all frequencies and not counted)
+  std::vector<std::array<int64_t, pfr::NKC>> lev_bytes;
+  // frequency-major fronts (k_front_fm) on the narrow levels (symmetric analyses, operator-form sweeps):
+  // PFR_FM_FRONTS = levels of at most this many fronts (0: off); per front its first gather record
+  std::vector<char> fm_level;
+  pfr::Workspace ws;                    // element counts of the chunk buffers (plan.cpp; what is allocated)
+  int32_t* d_fm_off = nullptr;
+  int4* d_fm_rec = nullptr;             // per lower-triangle entry: (nz, child source, child source, extras or -1)
+  int32_t* d_fm_x = nullptr;            // extra child sources, each list ended by -1
   // launch-shape tuning knobs, read from the environment when the solver is created (so that a
   // process can build solvers with different settings, e.g. tests forcing each kernel variant):
   // PFR_SOLVE_WMAX (waves per solve workgroup, at most), PFR_FAC_WMAX (waves per A11 LU
@@ -222,25 +227,27 @@ struct pfr_solver {
     if (rc == PFR_OK && *p) owned.push_back(*p);
     return rc;
   }
+  // a plan record array (pfr::I2 / I4) as its HIP vector type (same layout), never empty on the device
+  template <class D, class H>
+  int up_rec(D** p, const std::vector<H>& v, H pad) {
+    static_assert(sizeof(D) == sizeof(H), "record layout");
+    std::vector<H> w(v);
+    if (w.empty()) w.push_back(pad);
+    *p = nullptr;
+    HIP_TRY(hipMalloc(p, w.size() * sizeof(H)));
+    owned.push_back(*p);
+    HIP_TRY(hipMemcpy(*p, w.data(), w.size() * sizeof(H), hipMemcpyHostToDevice));
+    return PFR_OK;
+  }
 };
 
 namespace {
 
 int64_t workspace_bytes(const Symbolic& S, int64_t Fc) {
-  int64_t b = 0;
-  b += S.factor_entries * Fc * 16;   // F
-  b += S.total_rows * Fc * 16;       // WV
-  b += 7 * (int64_t)S.n * Fc * 16;   // X, Y, XA, G, Y2, XR, Gx (the selective adjoint refinement's seed)
-  b += Fc * (8 + 8 + 4 + 16);        // freqs, loss terms, flags, tq
-  b += Fc * (8 + 16) + (int64_t)pfr::residual_parts(S.n) * Fc * 16;   // fr0, mscale, cpart
-  if (S.symmetric)   // functional from the bottom-up passes: WVk, YVk, fn_parts, fcoef
-    b += (3 * S.total_rows + 2 * (int64_t)S.n + 3 * pfr::FN_PARTS_HOST + 3) * Fc * 16;
-  b += (int64_t)pfr::residual_parts(S.n) * 18 * Fc * 16;   // kpart (contraction in the forward walk)
-  return b;
+  int n_crow = 0;                     // coupled rows (Dirichlet decoupling): count as in build_plan
+  for (size_t c = 0; c < S.cpl_p.size(); ++c) n_crow += c == 0 || S.cpl_p[c] != S.cpl_p[c - 1];
+  return pfr::workspace(S, Fc, S.symmetric ? n_crow : 0).bytes;
 }
-
-// waves per workgroup for a level whose largest front is maxf
-int waves_for(int maxf) { return std::max(1, std::min(8, (maxf + 23) / 24)); }
 
 // start the timing record of a new chunk (events created once per chunk slot)
 int begin_chunk(pfr_solver* s) {
@@ -250,7 +257,7 @@ int begin_chunk(pfr_solver* s) {
     for (auto& e : s->tev.back().ev) HIP_TRY(hipEventCreate(&e));
   }
   auto& c = s->tev[s->n_tev];
-  const size_t nk = 6 * (s->level_ptr.size() - 1);
+  const size_t nk = (pfr::NKC + 1) * (s->level_ptr.size() - 1);
   while ((s->timing & 2) && c.kev.size() < nk) {
     hipEvent_t e;
     HIP_TRY(hipEventCreate(&e));
@@ -275,20 +282,11 @@ void reset_timing(pfr_solver* s) { s->n_tev = 0; }
 // Waves per workgroup of a solve launch over nf fronts of level l: the level's size-based count,
 // raised (up to 8) when the launch has too few workgroups to fill the chip -- the sparse passes
 // and the top levels, which are latency-bound: every wave more takes rows off each wave's chain.
-int solve_W(const pfr_solver* s, int l, int nf) {
-  const int wmax = s->solve_wmax;
-  const int64_t wgs = std::max<int64_t>(1, (int64_t)nf * (s->Fc / 64));
-  const int64_t fill = (4096 + wgs - 1) / wgs;
-  return (int)std::max<int64_t>(s->level_W[l], std::min<int64_t>(wmax, fill));
-}
+int solve_W(const pfr_solver* s, int l, int nf) { return pfr::solve_waves(s->level_W[l], nf, s->Fc, s->solve_wmax); }
 
 // Workgroups per (front, frequency group) for the update part of a solve launch over nf fronts: 1 when the
 // launch already has split_target workgroups, else enough to reach it (at most 16).
-int solve_split(const pfr_solver* s, int nf) {
-  const int64_t wgs = (int64_t)nf * (s->Fc / 64);
-  if (s->split_target <= 0 || wgs <= 0 || wgs >= s->split_target) return 1;
-  return (int)std::min<int64_t>(16, (s->split_target + wgs - 1) / wgs);
-}
+int solve_split(const pfr_solver* s, int nf) { return pfr::solve_split(nf, s->Fc, s->split_target); }
 
 // A11 of level l factored in LDS (k_factor_sym_lds): PFR_FAC_LDS = n > 0: levels whose largest pivot block has
 // >= n pivots; -1: levels on which the global-memory kernel would get fewer than PFR_FAC_LDS_WG workgroups (the
@@ -308,10 +306,18 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
   const bool kt = (s->timing & 2) && s->n_tev < (int)s->tev.size() && !s->tev[s->n_tev].kev.empty();
   hipEvent_t* kev = kt ? s->tev[s->n_tev].kev.data() : nullptr;
   auto mark = [&](int l, int c) {
-    if (kt) (void)hipEventRecord(kev[6 * l + c], st);
+    if (kt) (void)hipEventRecord(kev[(pfr::NKC + 1) * l + c], st);
   };
   for (int l = 0; l < L; ++l) {
     int nf = s->level_ptr[l + 1] - s->level_ptr[l];
+    if (mode == 0 && s->fm_level[l]) {
+      // the whole level frequency-major: one launch (classes 0-4 empty)
+      for (int c = 0; c <= pfr::NKC - 1; ++c) mark(l, c);
+      pfr::launch_front_fm(s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_maxf[l], s->d_fm_off, s->d_fm_rec,
+                           s->d_fm_x, s->F, s->Fc, s->freqs, s->K, s->M, s->flags, st);
+      mark(l, pfr::NKC);
+      continue;
+    }
     mark(l, 0);
     // panel: enough workgroups (front x 16 frequencies) to fill the chip -> one wave
     // each (no idle waves at the block barriers); few large fronts -> more waves
@@ -345,6 +351,7 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
                       s->d_g1 + (int64_t)s->tile_ptr[l] * pfr::SCHUR_TM * pfr::SCHUR_TN * pfr::SCHUR_SR * pfr::SCHUR_SC,
                       s->d_gxp + s->tile_ptr[l], s->d_gx, ngroups, s->F, s->Fc, st);
     mark(l, 5);
+    mark(l, 6);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -430,12 +437,10 @@ int adjoint_solve(pfr_solver* s, const pfr::RhsDesc& rg, double2* Out, hipStream
 // whenever a reach changed)
 int fn_setup(pfr_solver* s) {
   int rc;
-  const int64_t Fc = s->Fc, n = s->n;
+  const int64_t n = s->n;
   if (!s->WVk) {
-    int64_t rows = 0;
-    for (size_t t = 0; t < s->front_f.size(); ++t) rows += s->front_f[t];
-    if ((rc = s->alloc(&s->WVk, 3 * rows * Fc)) || (rc = s->alloc(&s->YVk, 2 * n * Fc)) ||
-        (rc = s->alloc(&s->fn_parts, 3 * (int64_t)pfr::FN_PARTS_HOST * Fc)) || (rc = s->alloc(&s->fcoef, 3 * Fc)) ||
+    if ((rc = s->alloc(&s->WVk, s->ws.WVk)) || (rc = s->alloc(&s->YVk, s->ws.YVk)) ||
+        (rc = s->alloc(&s->fn_parts, s->ws.fn_parts)) || (rc = s->alloc(&s->fcoef, s->ws.fcoef)) ||
         (rc = s->up(&s->d_noslot, std::vector<int32_t>(n, -1))) || (rc = s->alloc(&s->d_aP, 3 * n)) ||
         (rc = s->alloc(&s->d_fn_rows, n)) || (rc = s->alloc(&s->d_sup_rows, n)))
       return rc;
@@ -532,22 +537,12 @@ int sym_top_down_pair(pfr_solver* s, hipStream_t st, bool fwd_all = false) {
 // Mark the fronts holding the given permuted rows and all their ancestors; upload the flags and
 // the marked fronts level by level (level_fronts order kept).
 int set_reach(pfr_solver* s, int which, const std::vector<int32_t>& prows) {
-  const int nf = (int)s->front_parent.size();
-  std::vector<int32_t> mark(nf, 0);
-  for (int32_t p : prows)
-    for (int t = s->front_of_col[p]; t >= 0 && !mark[t]; t = s->front_parent[t]) mark[t] = 1;
-  const int L = (int)s->level_ptr.size() - 1;
-  std::vector<int32_t> lf(s->level_fronts_host.size());
-  std::vector<int32_t> list;
-  s->reach_ptr[which].assign(1, 0);
-  for (int l = 0; l < L; ++l) {
-    for (int e = s->level_ptr[l]; e < s->level_ptr[l + 1]; ++e)
-      if (mark[s->level_fronts_host[e]]) list.push_back(s->level_fronts_host[e]);
-    s->reach_ptr[which].push_back((int32_t)list.size());
-  }
+  std::vector<int32_t> mark, list;
+  pfr::reach_lists(s->front_of_col, s->front_parent, s->level_ptr, s->level_fronts_host, prows, mark, list,
+                   s->reach_ptr[which]);
   s->reach_host[which].assign(mark.begin(), mark.end());
   s->fn_ready = false;
-  HIP_TRY(hipMemcpy(s->d_reach[which], mark.data(), nf * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(s->d_reach[which], mark.data(), mark.size() * 4, hipMemcpyHostToDevice));
   if (!list.empty()) HIP_TRY(hipMemcpy(s->d_reach_fronts[which], list.data(), list.size() * 4, hipMemcpyHostToDevice));
   return PFR_OK;
 }
@@ -745,10 +740,6 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     delete s;
     return rc;
   };
-  if (S.max_front > pfr::MAX_FRONT) {
-    delete s;
-    return fail(PFR_ERR_ARG, "front larger than MAX_FRONT (device_types.hpp)");
-  }
   s->device = device;
   auto knob = [](const char* name, int def, int lo, int hi) {
     const char* e = getenv(name);
@@ -770,8 +761,10 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   // 8: the bottom two levels at 2,048 frequencies 685 / 612 -> 509 / 489 us (profiles/r04/experiments/us2_tiny_*)
   s->us2_tiny = knob("PFR_US2_TINY", 8, 0, 8);
   const int blk_min = knob("PFR_SCHUR_BLK_MIN", 24, 0, pfr::MAX_FRONT);   // update blocks of >= this many rows: block kernel
+  pfr::PlanOptions po;
+  po.blk_min = blk_min;
+  po.fm_fronts = knob("PFR_FM_FRONTS", 4, 0, 1 << 30);
   s->n = S.n;
-  s->nnz = S.nnz;  s->n = S.n;
   s->nnz = S.nnz;
   s->Fc = round64(max_batch);
   // the pipelined L21 prefix on launches of fewer than 8,000 waves in chunks of <= 1,024 frequencies (the narrow
@@ -782,9 +775,19 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->level_maxf = S.level_maxf;
   s->perm = S.perm;
   s->iperm = S.iperm;
-  for (int m : S.level_maxf) s->level_W.push_back(waves_for(m));
-  s->level_maxns.assign(S.level_maxf.size(), 0);   // largest pivot block of each level
-  for (const Front& F : S.fronts) s->level_maxns[F.level] = std::max(s->level_maxns[F.level], F.ns);
+  for (int m : S.level_maxf) s->level_W.push_back(pfr::waves_for(m));
+  // the launch plan (host, plan.cpp): every record array the kernels gather through, level by level
+  pfr::Plan pl;
+  std::string perr;
+  if (pfr::build_plan(S, po, pl, perr)) return bail(fail(PFR_ERR_ARG, perr));
+  s->sym = pl.sym;
+  s->level_maxns = pl.level_maxns;
+  s->tile_ptr = pl.tile_ptr;
+  s->blk_ptr = pl.blk_ptr;
+  s->asm_ptr = pl.asm_ptr;
+  s->item_ptr = pl.item_ptr;
+  s->lev_bytes = pl.lev_bytes;
+  s->fm_level = pl.fm_level;
   Front* d_fronts = nullptr;
   int rc = PFR_OK;
   std::vector<Front> fv(S.fronts);
@@ -795,347 +798,33 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       (rc = s->up(&ep, S.ea_ptr)) || (rc = s->up(&es, S.ea_src)) || (rc = s->up(&pm, S.perm)) ||
       (rc = s->up(&pr, S.prow)) || (rc = s->up(&pc, S.pcol)) || (rc = s->up(&s->d_level_fronts, S.level_fronts)))
     return bail(rc);
-  std::vector<char> blk_front(S.fronts.size(), 0);   // front's Schur complement by the block kernel
-  {
-    // Schur-complement tiles (4 x 4) of every front's update block, level by level
-    // plus, per tile and tile position, the children's update-matrix entries that
-    // land there (the extend-add of the Schur block, done as a gather)
-    if (S.factor_entries > INT32_MAX) return bail(fail(PFR_ERR_ARG, "front storage exceeds int32 element ids"));
-    const bool sym = S.symmetric != 0;
-    s->sym = sym;
-    std::vector<std::vector<int>> kids(S.fronts.size());
-    for (size_t t = 0; t < S.fronts.size(); ++t)
-      if (S.fronts[t].parent >= 0) kids[S.fronts[t].parent].push_back((int)t);
-    std::vector<int4> tv, iv;
-    s->item_ptr.assign(1, 0);
-    std::vector<int32_t> g1, gxp(1, 0);
-    std::vector<int2> gx;
-    s->tile_ptr.assign(1, 0);
-    std::vector<int4> bv;
-    std::vector<int32_t> bg1, bgxp(1, 0);
-    std::vector<int2> bgx;
-    s->blk_ptr.assign(1, 0);
-    const int L = (int)S.level_ptr.size() - 1;
-    for (int l = 0; l < L; ++l) {
-      for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
-        const int t = S.level_fronts[e];
-        const Front& F = S.fronts[t];
-        const int r = F.f - F.ns;
-        // children's update-matrix entries per A22 position: the first densely, the
-        // rare further ones (two or more children covering a position) aside
-        std::vector<int32_t> first((size_t)r * r, -1);
-        std::vector<std::pair<int32_t, int32_t>> more;   // (i * r + j, element id)
-        for (int c : kids[t]) {
-          const Front& C = S.fronts[c];
-          const int32_t* rp = S.relpos.data() + C.row0;
-          for (int a = C.ns; a < C.f; ++a) {
-            const int i = rp[a] - F.ns;
-            if (i < 0) continue;
-            for (int b = C.ns; b < C.f; ++b) {
-              const int j = rp[b] - F.ns;
-              if (j < 0 || (sym && j > i)) continue;   // symmetric: lower triangle only
-              const int32_t id = (int32_t)(C.off + (int64_t)a * C.f + b);
-              int32_t& f1 = first[(size_t)i * r + j];
-              if (f1 < 0)
-                f1 = id;
-              else
-                more.emplace_back(i * r + j, id);
-            }
-          }
-        }
-        std::sort(more.begin(), more.end());
-        if (sym && blk_min > 0 && r >= blk_min) {
-          // 16 x 16 blocks touching the lower triangle; wave w owns the 4 x 4 tile (w / 4, w % 4)
-          constexpr int B = pfr::SCHUR_BLK, BC = pfr::SCHUR_BLK, tcw = BC / 4;
-          for (int i0 = 0; i0 < r; i0 += B)
-            for (int j0 = 0; j0 < i0 + B; j0 += BC) {
-              bv.push_back(make_int4(t, i0, j0, 0));
-              for (int w = 0; w < BC; ++w)
-                for (int pos = 0; pos < 16; ++pos) {
-                  const int i = i0 + 4 * (w / tcw) + pos / 4, j = j0 + 4 * (w % tcw) + pos % 4;
-                  if (i >= r || j > i) {
-                    bg1.push_back(-1);
-                    continue;
-                  }
-                  bg1.push_back(first[(size_t)i * r + j]);
-                  auto lo = std::lower_bound(more.begin(), more.end(), std::make_pair(i * r + j, INT32_MIN));
-                  for (; lo != more.end() && lo->first == i * r + j; ++lo)
-                    bgx.push_back(make_int2(w * 16 + pos, lo->second));
-                }
-              bgxp.push_back((int32_t)bgx.size());
-            }
-          blk_front[t] = 1;
-          continue;
-        }
-        // super-tiles of (SCHUR_TM SCHUR_SR) x (SCHUR_TN SCHUR_SC): lane group `sub` owns the
-        // SCHUR_TM x SCHUR_TN tile at (TM (sub / SC), TN (sub % SC)); per super-tile the dense
-        // first-source ids (-1 = none), lane group by lane group, then one overflow range
-        constexpr int TM = pfr::SCHUR_TM, TN = pfr::SCHUR_TN, SR = pfr::SCHUR_SR, SC = pfr::SCHUR_SC;
-        constexpr int STR = TM * SR, STC = TN * SC;
-        std::vector<std::pair<int, int>> order;   // super-tiles (symmetric: those touching the lower triangle)
-        for (int i0 = 0; i0 < r; i0 += STR)
-          for (int j0 = 0; j0 < r && (!sym || j0 <= i0 + STR - 1); j0 += STC) order.emplace_back(i0, j0);
-        for (const auto& ij : order) {
-          const int i0 = ij.first, j0 = ij.second;
-          {
-            tv.push_back(make_int4(t, i0, j0, 0));
-            for (int sub = 0; sub < SR * SC; ++sub)
-              for (int pos = 0; pos < TM * TN; ++pos) {
-                const int i = i0 + TM * (sub / SC) + pos / TN, j = j0 + TN * (sub % SC) + pos % TN;
-                if (i >= r || j >= r || (sym && j > i)) {
-                  g1.push_back(-1);
-                  continue;
-                }
-                g1.push_back(first[(size_t)i * r + j]);
-                auto lo = std::lower_bound(more.begin(), more.end(), std::make_pair(i * r + j, INT32_MIN));
-                for (; lo != more.end() && lo->first == i * r + j; ++lo)
-                  gx.push_back(make_int2(sub * TM * TN + pos, lo->second));
-              }
-            gxp.push_back((int32_t)gx.size());
-          }
-        }
-      }
-      s->tile_ptr.push_back((int32_t)tv.size());
-      s->blk_ptr.push_back((int32_t)bv.size());
-    }
-    if (gx.empty()) gx.push_back(make_int2(0, 0));   // keep the buffers non-null
-    if (bv.empty()) bv.push_back(make_int4(0, 0, 0, 0));
-    if (bg1.empty()) bg1.push_back(-1);
-    if (bgx.empty()) bgx.push_back(make_int2(0, 0));
-    if ((rc = s->up(&s->d_tiles, tv)) || (rc = s->up(&s->d_g1, g1)) || (rc = s->up(&s->d_gxp, gxp)) ||
-        (rc = s->up(&s->d_gx, gx)) || (rc = s->up(&s->d_blocks, bv)) || (rc = s->up(&s->d_bg1, bg1)) ||
-        (rc = s->up(&s->d_bgxp, bgxp)) || (rc = s->up(&s->d_bgx, bgx)))
-      return bail(rc);
-    // assembly of the panel region (pivot rows: all columns; update rows: pivot
-    // columns) as a gather: one record per entry = original matrix entry (or -1)
-    // + the first child update-matrix entry landing there (or -1); rare further
-    // child sources in a per-chunk overflow list.  Levels padded to 8 records.
-    // Panel-region sources of every front, as a gather: per entry the original
-    // matrix entry (or -1) and the first child update-matrix entry landing there
-    // (or -1); rare further child entries in overflow lists.
-    //  * A11 (pivot rows x pivot columns): assembly records (dst, nz, src, -) in
-    //    chunks of 8 (k_assemble_level), levels padded to 8 records;
-    //  * L21 rows / U12 columns: gathered by k_offdiag_level itself when it loads
-    //    them (records (nz, src) per item x lane group x pivot, item.w = offset),
-    //    so those entries are never stored before their final value.
-    std::vector<int4> av;
-    std::vector<int32_t> axp(1, 0), oxp(1, 0);
-    std::vector<int2> ax, orec, ox;
-    s->asm_ptr.assign(1, 0);
-    s->item_ptr.assign(1, 0);
-    std::vector<int32_t> nzm, s1m;
-    std::vector<std::pair<int32_t, int32_t>> morem;   // (a * f + b, id)
-    for (int l = 0; l < L; ++l) {
-      for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
-        const int t = S.level_fronts[e];
-        const Front& F = S.fronts[t];
-        const int f = F.f, ns = F.ns;
-        nzm.assign((size_t)f * f, -1);
-        s1m.assign((size_t)f * f, -1);
-        morem.clear();
-        for (int a = 0; a < f; ++a) {
-          const int r = F.row0 + a;
-          const int width = a < ns ? f : ns;
-          for (int x = S.asm_ptr[r]; x < S.asm_ptr[r + 1]; ++x)
-            if (S.asm_col[x] < width) nzm[(size_t)a * f + S.asm_col[x]] = S.asm_nz[x];
-          for (int x = S.ea_ptr[r]; x < S.ea_ptr[r + 1]; ++x) {
-            const int src = S.ea_src[x];
-            const Front& C = S.fronts[S.row_front[src]];
-            const int32_t* rp = S.relpos.data() + C.row0;
-            for (int b = C.ns; b < C.f; ++b) {
-              const int pb = rp[b];
-              if (pb >= width) continue;
-              // symmetric: the child's update matrix holds its lower triangle only
-              const int ca = src - C.row0;
-              const int32_t id = (int32_t)(C.off + (sym && ca < b ? (int64_t)b * C.f + ca : (int64_t)ca * C.f + b));
-              int32_t& s1 = s1m[(size_t)a * f + pb];
-              if (s1 < 0)
-                s1 = id;
-              else
-                morem.emplace_back(a * f + pb, id);
-            }
-          }
-        }
-        std::sort(morem.begin(), morem.end());
-        auto extras = [&](int a, int b) {
-          auto lo = std::lower_bound(morem.begin(), morem.end(), std::make_pair(a * f + b, INT32_MIN));
-          std::vector<int32_t> out;
-          for (; lo != morem.end() && lo->first == a * f + b; ++lo) out.push_back(lo->second);
-          return out;
-        };
-        for (int a = 0; a < ns; ++a)
-          for (int b = 0; b < (sym ? a + 1 : ns); ++b) {   // symmetric: A11's lower triangle only
-            const int k = (int)(av.size() % 8);
-            av.push_back(make_int4((int32_t)(F.off + (int64_t)a * f + b), nzm[(size_t)a * f + b],
-                                   s1m[(size_t)a * f + b], 0));
-            for (int32_t id : extras(a, b)) ax.push_back(make_int2(k, id));
-            if (av.size() % 8 == 0) axp.push_back((int32_t)ax.size());
-          }
-        for (int kind = 0; kind < (sym ? 1 : 2); ++kind)   // symmetric: U12 = diag(U11) L21^T implicit
-          for (int i0 = ns; i0 < f; i0 += pfr::OFF_G * pfr::OFF_RPL) {
-            iv.push_back(make_int4(t, i0, kind, (int32_t)orec.size()));
-            for (int slot = 0; slot < pfr::OFF_G * pfr::OFF_RPL; ++slot)   // row i0 + slot = i0 + OFF_G h + lane group
-              for (int c = 0; c < ns; ++c) {
-                const int idx = i0 + slot;
-                if (idx >= f) {
-                  orec.push_back(make_int2(-1, -1));
-                  continue;
-                }
-                const int a = kind == 0 ? idx : c, b = kind == 0 ? c : idx;
-                orec.push_back(make_int2(nzm[(size_t)a * f + b], s1m[(size_t)a * f + b]));
-                for (int32_t id : extras(a, b)) ox.push_back(make_int2(c * pfr::OFF_G * pfr::OFF_RPL + slot, id));
-              }
-            oxp.push_back((int32_t)ox.size());
-          }
-      }
-      while (av.size() % 8) {        // pad: no-op records (dst = -1)
-        av.push_back(make_int4(-1, -1, -1, 0));
-        if (av.size() % 8 == 0) axp.push_back((int32_t)ax.size());
-      }
-      s->asm_ptr.push_back((int32_t)av.size());
-      s->item_ptr.push_back((int32_t)iv.size());
-    }
-    {
-      // algorithmic bytes per frequency (16 B per complex entry; index data is
-      // shared by all frequencies and not counted)
-      int64_t s_ns2 = 0, s_a11 = 0, s_r2[2] = {0, 0}, s_rns = 0, s_rns2[2] = {0, 0}, g_a11 = 0, g_off = 0;
-      int64_t g_s[2] = {0, 0};   // [0] block kernel, [1] tile kernel
-      for (size_t t = 0; t < S.fronts.size(); ++t) {
-        const Front& F = S.fronts[t];
-        const int64_t r = F.f - F.ns;
-        const int k = blk_front[t] ? 0 : 1;
-        s_ns2 += (int64_t)F.ns * F.ns;
-        s_a11 += sym ? (int64_t)F.ns * (F.ns + 1) / 2 : (int64_t)F.ns * F.ns;
-        s_r2[k] += sym ? r * (r + 1) / 2 : r * r;
-        s_rns += (sym ? 1 : 2) * r * F.ns;
-        s_rns2[k] += (sym ? 1 : 2) * r * F.ns;
-      }
-      for (const int4& a : av) g_a11 += a.z >= 0;
-      for (const int2& o : orec) g_off += o.y >= 0;
-      for (int32_t g : g1) g_s[1] += g >= 0;
-      for (int32_t g : bg1) g_s[0] += g >= 0;
-      g_s[0] += (int64_t)bgxp.back();
-      g_a11 += (int64_t)ax.size();
-      g_off += (int64_t)ox.size();
-      g_s[1] += (int64_t)gxp.back();                       // gx may hold a placeholder
-      s->alg_bytes[0] = 16 * (s_a11 + g_a11);             // A11 (symmetric: lower) stores + child entries gathered
-      s->alg_bytes[1] = 16 * (s_a11 + s_ns2);             // A11 read + L11/U11 write
-      // the same per level
-      s->lev_asm_bytes.assign(L, 0);
-      s->lev_lu_bytes.assign(L, 0);
-      for (const Front& F : S.fronts) {
-        const int64_t a11 = sym ? (int64_t)F.ns * (F.ns + 1) / 2 : (int64_t)F.ns * F.ns;
-        s->lev_asm_bytes[F.level] += 16 * a11;
-        s->lev_lu_bytes[F.level] += 16 * (a11 + (int64_t)F.ns * F.ns);
-      }
-      for (int l = 0; l < L; ++l) {
-        int64_t g = 0;
-        for (int r = s->asm_ptr[l]; r < s->asm_ptr[l + 1]; ++r) g += av[r].z >= 0;
-        g += axp[s->asm_ptr[l + 1] / 8] - axp[s->asm_ptr[l] / 8];
-        s->lev_asm_bytes[l] += 16 * g;
-      }
-      s->alg_bytes[2] = 16 * (s_rns + g_off + s_ns2);     // L21/U12 stores + gathered children + L11/U11 read
-      for (int k = 0; k < 2; ++k)                         // A22 stores + gathered children + L21/U12 read
-        s->alg_bytes[3 + k] = 16 * (s_r2[k] + g_s[k] + s_rns2[k]);
-    }
-    if (av.empty()) av.assign(8, make_int4(-1, -1, -1, 0));
-    if (ax.empty()) ax.push_back(make_int2(0, 0));
-    if (iv.empty()) iv.push_back(make_int4(0, 0, 0, 0));
-    if (orec.empty()) orec.push_back(make_int2(-1, -1));
-    if (ox.empty()) ox.push_back(make_int2(0, 0));
-    if ((rc = s->up(&s->d_asm, av)) || (rc = s->up(&s->d_asm_xp, axp)) || (rc = s->up(&s->d_asm_x, ax)) ||
-        (rc = s->up(&s->d_items, iv)) || (rc = s->up(&s->d_orec, orec)) || (rc = s->up(&s->d_oxp, oxp)) ||
-        (rc = s->up(&s->d_ox, ox)))
-      return bail(rc);
-  }
+  const pfr::I2 z2{0, 0}, n2{-1, -1};
+  const pfr::I4 z4{0, 0, 0, 0}, n4{-1, -1, -1, -1};
+  if ((rc = s->up_rec(&s->d_tiles, pl.tiles, z4)) || (rc = s->up(&s->d_g1, pl.g1)) || (rc = s->up(&s->d_gxp, pl.gxp)) ||
+      (rc = s->up_rec(&s->d_gx, pl.gx, z2)) || (rc = s->up_rec(&s->d_blocks, pl.blocks, z4)) ||
+      (rc = s->up_rec(&s->d_bg1, pl.bg1, -1)) || (rc = s->up(&s->d_bgxp, pl.bgxp)) || (rc = s->up_rec(&s->d_bgx, pl.bgx, z2)) ||
+      (rc = s->up_rec(&s->d_asm, pl.asm_rec, n4)) || (rc = s->up(&s->d_asm_xp, pl.asm_xp)) ||
+      (rc = s->up_rec(&s->d_asm_x, pl.asm_x, z2)) || (rc = s->up_rec(&s->d_items, pl.items, z4)) ||
+      (rc = s->up_rec(&s->d_orec, pl.orec, n2)) || (rc = s->up(&s->d_oxp, pl.oxp)) || (rc = s->up_rec(&s->d_ox, pl.ox, z2)) ||
+      (rc = s->up_rec(&s->d_fm_off, pl.fm_off, -1)) || (rc = s->up_rec(&s->d_fm_rec, pl.fm_rec, n4)) ||
+      (rc = s->up_rec(&s->d_fm_x, pl.fm_x, -1)))
+    return bail(rc);
   std::vector<int32_t> cp(colptr, colptr + S.n + 1), ri(rowind, rowind + S.nnz);
   if ((rc = s->up(&s->d_colptr, cp)) || (rc = s->up(&s->d_rowind, ri))) return bail(rc);
   if (s->sym && !S.dir_p.empty()) {
-    // Dirichlet decoupling lists: coupled rows (with their entries), and per Dirichlet node
-    // the entries of its column (adjoint correction); slot of every permuted row
-    std::vector<int2> dir, ce, de;
-    std::vector<int32_t> crow, cptr(1, 0), dptr(1, 0), cslot(S.n, -1);
-    for (size_t d = 0; d < S.dir_p.size(); ++d) dir.push_back(make_int2(S.dir_p[d], S.dir_nz[d]));
-    for (size_t c = 0; c < S.cpl_p.size(); ++c) {
-      if (crow.empty() || crow.back() != S.cpl_p[c]) {
-        if (!crow.empty()) cptr.push_back((int32_t)ce.size());
-        cslot[S.cpl_p[c]] = (int32_t)crow.size();
-        crow.push_back(S.cpl_p[c]);
-      }
-      ce.push_back(make_int2(S.cpl_dir[c], S.cpl_nz[c]));
-    }
-    cptr.push_back((int32_t)ce.size());
-    for (size_t d = 0; d < S.dir_p.size(); ++d) {
-      for (size_t c = 0; c < S.cpl_p.size(); ++c)
-        if (S.cpl_dir[c] == (int32_t)d) de.push_back(make_int2(S.cpl_p[c], S.cpl_nz[c]));
-      dptr.push_back((int32_t)de.size());
-    }
-    if (ce.empty()) ce.push_back(make_int2(0, 0));
-    if (de.empty()) de.push_back(make_int2(0, 0));
-    if (crow.empty()) crow.push_back(0);
-    s->n_dir = (int)S.dir_p.size();
-    s->n_crow = (int)(cptr.size() - 1);
-    if ((rc = s->up(&s->d_dir, dir)) || (rc = s->up(&s->d_crow, crow)) || (rc = s->up(&s->d_cptr_dir, cptr)) ||
-        (rc = s->up(&s->d_ce, ce)) || (rc = s->up(&s->d_dptr, dptr)) || (rc = s->up(&s->d_de, de)) ||
-        (rc = s->up(&s->d_cslot, cslot)) || (rc = s->alloc(&s->Bc, (int64_t)std::max(1, s->n_crow) * s->Fc)))
+    s->n_dir = pl.n_dir;
+    s->n_crow = pl.n_crow;
+    if ((rc = s->up_rec(&s->d_dir, pl.dir, z2)) || (rc = s->up_rec(&s->d_crow, pl.crow, 0)) ||
+        (rc = s->up(&s->d_cptr_dir, pl.cptr_dir)) || (rc = s->up_rec(&s->d_ce, pl.ce, z2)) ||
+        (rc = s->up(&s->d_dptr, pl.dptr)) || (rc = s->up_rec(&s->d_de, pl.de, z2)) || (rc = s->up(&s->d_cslot, pl.cslot)) ||
+        (rc = s->alloc(&s->Bc, pfr::workspace(S, s->Fc, s->n_crow).Bc)))
       return bail(rc);
   }
-  {
-    // permuted matrix compressed by rows and by columns (Hessian tangent operators)
-    auto compress = [&](const std::vector<int32_t>& key, const std::vector<int32_t>& other, int32_t** dptr,
-                        int32_t** didx, int32_t** dnz) {
-      std::vector<int32_t> ptr(S.n + 1, 0), idx(S.nnz), nz(S.nnz);
-      for (int64_t e = 0; e < S.nnz; ++e) ++ptr[key[e] + 1];
-      for (int i = 0; i < S.n; ++i) ptr[i + 1] += ptr[i];
-      std::vector<int32_t> fill(ptr.begin(), ptr.end() - 1);
-      for (int64_t e = 0; e < S.nnz; ++e) {
-        const int32_t at = fill[key[e]]++;
-        idx[at] = other[e];
-        nz[at] = (int32_t)e;
-      }
-      int r;
-      if ((r = s->up(dptr, ptr)) || (r = s->up(didx, idx)) || (r = s->up(dnz, nz))) return r;
-      return (int)PFR_OK;
-    };
-    if ((rc = compress(S.prow, S.pcol, &s->d_rptr, &s->d_ridx, &s->d_rnz)) ||
-        (rc = compress(S.pcol, S.prow, &s->d_cptr, &s->d_cidx, &s->d_cnz)) || (rc = s->up(&s->d_walk, S.iperm)))
-      return bail(rc);
-    // union row structure of the gradient contraction (k_contract_eg)
-    std::vector<int64_t> key(S.nnz);
-    std::vector<int32_t> ord(S.nnz);
-    for (int64_t e = 0; e < S.nnz; ++e) {
-      key[e] = (int64_t)S.prow[e] * S.n + S.pcol[e];
-      ord[e] = (int32_t)e;
-    }
-    std::sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return key[a] < key[b]; });
-    auto find = [&](int64_t k) -> int32_t {
-      auto it = std::lower_bound(ord.begin(), ord.end(), k, [&](int32_t a, int64_t v) { return key[a] < v; });
-      return (it != ord.end() && key[*it] == k) ? *it : -1;
-    };
-    std::vector<std::vector<int4>> rows(S.n);
-    for (int32_t e : ord) {   // row-major, columns ascending
-      const int32_t i = S.prow[e], j = S.pcol[e];
-      rows[i].push_back(make_int4(j, e, find((int64_t)j * S.n + i), 0));
-    }
-    for (int32_t e : ord) {   // (i, j) whose mirror (j, i) is not in the pattern: column-only entry of row j
-      const int32_t i = S.prow[e], j = S.pcol[e];
-      if (find((int64_t)j * S.n + i) < 0) rows[j].push_back(make_int4(i, -1, e, 0));
-    }
-    // rows in original order (mesh-local: neighbouring walks gather the same solution rows
-    // whatever the fill-reducing ordering), entries of a row by permuted column
-    std::vector<int32_t> uptr(S.n + 1, 0);
-    std::vector<int4> uent;
-    for (int t = 0; t < S.n; ++t) {
-      const int i = S.iperm[t];
-      std::sort(rows[i].begin(), rows[i].end(), [](const int4& a, const int4& b) { return a.x < b.x; });
-      uent.push_back(make_int4(-1, -1, -1, i));
-      for (const int4& v : rows[i]) uent.push_back(make_int4(v.x, v.y, v.z, i));
-      uptr[t + 1] = (int32_t)uent.size();
-    }
-    s->n_uent = (int)uent.size();
-    for (int pad = 0; pad < 4; ++pad) uent.push_back(make_int4(-1, -1, -1, -1));   // a step reads 4 entries at once
-    if ((rc = s->up(&s->d_uent, uent))) return bail(rc);
-  }
+  if ((rc = s->up(&s->d_rptr, pl.rptr)) || (rc = s->up(&s->d_ridx, pl.ridx)) || (rc = s->up(&s->d_rnz, pl.rnz)) ||
+      (rc = s->up(&s->d_cptr, pl.cptr)) || (rc = s->up(&s->d_cidx, pl.cidx)) || (rc = s->up(&s->d_cnz, pl.cnz)) ||
+      (rc = s->up(&s->d_walk, S.iperm)) || (rc = s->up_rec(&s->d_uent, pl.uent, n4)))
+    return bail(rc);
+  s->n_uent = pl.n_uent;
   s->P = DevPattern{d_fronts, idx, relpos, rowf, ap, ac, an, ep, es, pm, pr, pc, S.n};
   {
     const int nf = (int)S.fronts.size();
@@ -1157,13 +846,14 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
     }
   }
   const int64_t Fc = s->Fc;
-  if ((rc = s->alloc(&s->F, S.factor_entries * Fc)) || (rc = s->alloc(&s->WV, S.total_rows * Fc)) ||
+  s->ws = pfr::workspace(S, Fc, s->n_crow);
+  if ((rc = s->alloc(&s->F, s->ws.F)) || (rc = s->alloc(&s->WV, s->ws.WV)) ||
       (rc = s->alloc(&s->X, (int64_t)S.n * Fc)) || (rc = s->alloc(&s->Y, (int64_t)S.n * Fc)) ||
       (rc = s->alloc(&s->XA, (int64_t)S.n * Fc)) || (rc = s->alloc(&s->G, (int64_t)S.n * Fc)) ||
       (rc = s->alloc(&s->Y2, (int64_t)S.n * Fc)) || (rc = s->alloc(&s->XR, (int64_t)S.n * Fc)) ||
       (rc = s->alloc(&s->freqs, Fc)) || (rc = s->alloc(&s->loss_terms, Fc)) || (rc = s->alloc(&s->flags, Fc)) ||
       (rc = s->alloc(&s->tq, Fc)) || (rc = s->alloc(&s->d_berr_acc, 2 * Fc)) || (rc = s->alloc(&s->fr0, Fc)) ||
-      (rc = s->alloc(&s->mscale, Fc)) || (rc = s->alloc(&s->cpart, (int64_t)pfr::residual_parts(S.n) * Fc)) ||
+      (rc = s->alloc(&s->mscale, Fc)) || (rc = s->alloc(&s->cpart, s->ws.cpart)) ||
       (rc = s->alloc(&s->gind, Fc / 64)) || (rc = s->alloc(&s->glist, pfr::REFINE_CAP)))
     return bail(rc);
   HIP_TRY(hipMemset(s->d_berr_acc, 0, 2 * Fc * sizeof(double)));
@@ -1231,7 +921,7 @@ int pfr_last_timings(const pfr_solver* s, double* ms) {
 
 int pfr_last_kernel_timings(const pfr_solver* s, double* ms, int64_t* launches) {
   if (!s || !ms) return fail(PFR_ERR_ARG, "null argument");
-  for (int i = 0; i < 5; ++i) {
+  for (int i = 0; i < pfr::NKC; ++i) {
     ms[i] = 0.0;
     if (launches) launches[i] = 0;
   }
@@ -1241,12 +931,13 @@ int pfr_last_kernel_timings(const pfr_solver* s, double* ms, int64_t* launches) 
   for (int c = 0; c < s->n_tev; ++c) {
     if (!s->tev[c].used[0]) continue;
     for (int l = 0; l < L; ++l) {
-      const int work[5] = {s->asm_ptr[l + 1] - s->asm_ptr[l], s->level_ptr[l + 1] - s->level_ptr[l],
-                           s->item_ptr[l + 1] - s->item_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
-                           s->tile_ptr[l + 1] - s->tile_ptr[l]};
-      for (int k = 0; k < 5; ++k) {
+      const bool fm = s->fm_level[l];
+      const int work[pfr::NKC] = {fm ? 0 : s->asm_ptr[l + 1] - s->asm_ptr[l], fm ? 0 : s->level_ptr[l + 1] - s->level_ptr[l],
+                                  fm ? 0 : s->item_ptr[l + 1] - s->item_ptr[l], fm ? 0 : s->blk_ptr[l + 1] - s->blk_ptr[l],
+                                  fm ? 0 : s->tile_ptr[l + 1] - s->tile_ptr[l], fm ? s->level_ptr[l + 1] - s->level_ptr[l] : 0};
+      for (int k = 0; k < pfr::NKC; ++k) {
         float m = 0;
-        HIP_TRY(hipEventElapsedTime(&m, s->tev[c].kev[6 * l + k], s->tev[c].kev[6 * l + k + 1]));
+        HIP_TRY(hipEventElapsedTime(&m, s->tev[c].kev[(pfr::NKC + 1) * l + k], s->tev[c].kev[(pfr::NKC + 1) * l + k + 1]));
         ms[k] += m;
         if (launches) launches[k] += work[k] > 0;    // empty classes launch nothing
       }
@@ -1257,12 +948,11 @@ int pfr_last_kernel_timings(const pfr_solver* s, double* ms, int64_t* launches) 
 
 int pfr_solver_alg_bytes(const pfr_solver* s, int64_t* bytes) {
   if (!s || !bytes) return fail(PFR_ERR_ARG, "null argument");
-  for (int i = 0; i < 5; ++i) bytes[i] = s->alg_bytes[i];
-  bytes[0] = bytes[1] = 0;
-  for (int l = 0; l + 1 < (int)s->level_ptr.size(); ++l) {
-    bytes[0] += s->lev_asm_bytes[l];
-    bytes[1] += s->lev_lu_bytes[l];
-  }
+  // operator-form sweeps: a frequency-major level counts in class 5 alone
+  for (int i = 0; i < pfr::NKC; ++i) bytes[i] = 0;
+  for (int l = 0; l + 1 < (int)s->level_ptr.size(); ++l)
+    for (int i = 0; i < pfr::NKC; ++i)
+      if ((i == pfr::NKC - 1) == (s->fm_level[l] != 0)) bytes[i] += s->lev_bytes[l][i];
   return PFR_OK;
 }
 
@@ -1556,7 +1246,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
       const bool cwalk = reverse && correct && s->contract_walk &&
                          (s->n_stiff == 12 || s->n_stiff == 18);
       if (cwalk && !s->kpart) {
-        if ((rc = s->alloc(&s->kpart, (int64_t)pfr::residual_parts(s->n) * 18 * Fc))) return rc;
+        if ((rc = s->alloc(&s->kpart, s->ws.kpart))) return rc;
       }
       // selective adjoint refinement (PFR_CHECK_REFINE_ADJ): the groups next to a resonance, where the unrefined
       // solves' first-order error dominates the gradient, get one refinement step of mu
@@ -1584,7 +1274,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
         // dot products and gradient contraction again with the refined mu, and their fr / m_q
         pfr::launch_select_groups(s->gind, (int)(Fc / 64), s->refine_tol, s->glist, st);
         if (!s->Gx) {
-          if ((rc = s->alloc(&s->Gx, (int64_t)s->n * Fc))) return rc;
+          if ((rc = s->alloc(&s->Gx, s->ws.nvec))) return rc;
           HIP_TRY(hipMemsetAsync(s->Gx, 0, (size_t)s->n * Fc * 16, st));   // only the support rows are ever written
         }
         pfr::FunctionalArgs fs = fa;

@@ -6,6 +6,7 @@
 #include <cstdint>
 
 #include "../../include/pfr.h"
+#include "plan.hpp"
 #include "symbolic.hpp"
 
 namespace pfr {
@@ -26,26 +27,6 @@ struct DevPattern {
   const int32_t* pcol;
   int32_t n;
 };
-
-// Schur super-tile: a wavefront = SCHUR_QG frequencies x (SCHUR_SR x SCHUR_SC) lane groups,
-// each lane group one SCHUR_TM x SCHUR_TN register tile -> (SCHUR_TM SCHUR_SR) x
-// (SCHUR_TN SCHUR_SC) entries per wave.  Lane = frequency, one 4 x 4 tile per wave (measured 10 %
-// faster than 16 frequencies x a 2 x 2 arrangement of 4 x 4 tiles).
-constexpr int SCHUR_SR = 1, SCHUR_SC = 1, SCHUR_QG = 64 / (SCHUR_SR * SCHUR_SC);
-constexpr int SCHUR_TM = 4, SCHUR_TN = 4;
-static_assert(SCHUR_SR * SCHUR_SC * SCHUR_QG == 64, "one wavefront per super-tile");
-
-// Off-diagonal panel kernel: a wave = OFF_G lane groups of 64 / OFF_G frequencies, OFF_RPL rows
-// (columns) per lane: OFF_G OFF_RPL rows per wave.  Lane = frequency, two rows per lane (measured best of
-// 1 / 2 lane groups and 1 / 2 / 4 rows per lane; the other shapes are in git history).
-constexpr int OFF_G = 1;
-constexpr int OFF_RPL = 2;
-// A11 factorisation kernel: lane groups per wave (64 / FAC_G frequencies each, one front row each)
-constexpr int FAC_G = 2;
-
-// Largest front the solve kernels stage index lists for in LDS (checked at solver creation)
-constexpr int MAX_FRONT = 1024;
-constexpr int SCHUR_BLK = 16;   // k_schur_sym_blk block edge (16 waves x 4 x 4 tiles)
 
 constexpr int COEF_MAX = 32;
 struct CoefPack {

@@ -636,6 +636,176 @@ __global__ __launch_bounds__(256) void k_factor_sym_lds(DevPattern P, const int*
 #undef E
 }
 
+// ------------------------------------------------------------------ K2c: frequency-major fronts (narrow top)
+// The narrow top of the elimination tree -- levels of a few large fronts, which the frequency-minor kernels run
+// as five dependent launches of a few workgroups each (assembly, A11 LU, L21 rows, two Schur classes) -- as ONE
+// launch in which a workgroup is one front x ONE frequency.  The front's whole lower triangle (A11, L21, A22) is
+// gathered into LDS -- original entries K - omega^2 M plus every child's update-matrix entries, one record per
+// entry -- partially factorised there (LDL^T of the ns pivots in blocks of FM_KB, the update matrix formed in
+// place by rank-FM_KB updates of the trailing triangle) and written back once, in the frequency-minor layout
+// every other kernel reads: L11 below the diagonal, U(k, k) on it, U11 = diag(U) L11^T above it, L21, and the
+// update matrix (A22 lower).  Fc workgroups per front fill the chip on levels of one to a few fronts, and the
+// O(ns f^2) arithmetic runs out of LDS instead of global-memory round trips per pivot block.
+//  * global accesses are 16 B per lane at a stride of Fc entries; consecutive frequencies are consecutive
+//    logical workgroups on one XCD (xcd_swizzle), so each 128 B line is fetched into / written back from that
+//    XCD's L2 once for its 8 frequencies;
+//  * panel of a pivot block: every wave holds the block's FM_KB rows in lanes 0 .. FM_KB-1 (redundantly) and
+//    FM_PR panel rows in the other lanes, each lane its row's FM_KB entries in registers; the block's LDL^T and
+//    the panel solve run wave-synchronously, the pivot row values broadcast by v_readlane (no barrier per pivot);
+//  * trailing update: 4 x 4 tiles of the lower triangle per thread, A(i, j) -= sum_t L(i, t) W(j, t) with
+//    W(j, t) = U(t, t) L(j, t) kept beside the triangle (zero past a short last block).
+// Results equal the frequency-minor kernels' up to rounding (same pivots, same static order).
+constexpr int FM_T = 256;             // threads per workgroup
+constexpr int FM_PR = 64 - FM_KB;     // panel rows per wave
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+__device__ __forceinline__ cplx readlane_c(cplx v, int l) { return make_double2(readlane_d(v.x, l), readlane_d(v.y, l)); }
+
+__global__ __launch_bounds__(FM_T, 2) void k_front_fm(DevPattern P, const int* __restrict__ lvl,
+                                                  const int* __restrict__ fm_off, const int4* __restrict__ recs,
+                                                  const int* __restrict__ xl, cplx* __restrict__ F, int64_t Fc,
+                                                  const double* __restrict__ freqs, const cplx* __restrict__ K,
+                                                  const double* __restrict__ M, int* __restrict__ flags, int maxf) {
+  extern __shared__ cplx sA[];        // packed lower triangle of the front, then W (FM_KB per row)
+  cplx* __restrict__ sW = sA + (maxf * (maxf + 1)) / 2;
+  const int64_t lid = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int slot = (int)(lid / Fc);
+  const int64_t q = lid - (int64_t)slot * Fc;
+  const int front = lvl[slot];
+  const Front fr = P.fronts[front];
+  const int f = fr.f, ns = fr.ns, nlow = f * (f + 1) / 2;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  cplx* __restrict__ base = F + fr.off * Fc + q;
+#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+#define A(i, j) sA[((i) * ((i) + 1)) / 2 + (j)]
+  // 1. gather: per entry (nz of the original entry, two child sources, extra-source list or -1), 4 entries'
+  //    loads in flight per thread, masks as multipliers (loads unconditional from clamped addresses)
+  {
+    const int4* __restrict__ R = recs + fm_off[front];
+    const double om = 6.283185307179586 * freqs[q];
+    const double om2 = om * om;
+    constexpr int U = 4;
+    for (int e0 = tid; e0 < nlow; e0 += U * FM_T) {
+      int4 r[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) r[u] = R[min(e0 + u * FM_T, nlow - 1)];
+      cplx kk[U], c0[U], c1[U];
+      double mm[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        kk[u] = K[max(r[u].x, 0)];
+        mm[u] = M[max(r[u].x, 0)];
+        c0[u] = F[(int64_t)max(r[u].y, 0) * Fc + q];
+        c1[u] = F[(int64_t)max(r[u].z, 0) * Fc + q];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const double so = r[u].x >= 0 ? 1.0 : 0.0, s0 = r[u].y >= 0 ? 1.0 : 0.0, s1 = r[u].z >= 0 ? 1.0 : 0.0;
+        cplx v = make_double2(fma(so, fma(-om2, mm[u], kk[u].x), fma(s0, c0[u].x, s1 * c1[u].x)),
+                              fma(so, kk[u].y, fma(s0, c0[u].y, s1 * c1[u].y)));
+        if (r[u].w >= 0)     // rare: three or more children cover the entry
+          for (int x = r[u].w; xl[x] >= 0; ++x) v = cadd(v, F[(int64_t)xl[x] * Fc + q]);
+        if (e0 + u * FM_T < nlow) sA[e0 + u * FM_T] = v;
+      }
+    }
+  }
+  __syncthreads();
+  // 2. partial LDL^T of the ns pivots
+  for (int k0 = 0; k0 < ns; k0 += FM_KB) {
+    const int kb = min(FM_KB, ns - k0), k1 = k0 + kb;
+    // panel: lane t < FM_KB the block row k0 + t, the others the rows k1 + FM_PR w + (lane - FM_KB)
+    const bool brow = lane < FM_KB;
+    const int prow = k1 + FM_PR * w + lane - FM_KB;
+    const int row = brow ? k0 + min(lane, kb - 1) : min(prow, f - 1);
+    cplx a[FM_KB], wv[FM_KB];
+#pragma unroll
+    for (int u = 0; u < FM_KB; ++u) a[u] = A(row, min(k0 + min(u, kb - 1), row));   // block rows: right of the
+                                                                                     // diagonal unused
+#pragma unroll
+    for (int t = 0; t < FM_KB; ++t) {
+      if (t < kb) {                   // wave-uniform
+        const cplx d = readlane_c(a[t], t);        // U(k0 + t, k0 + t), updated by the earlier pivots
+        if (tid == 0) pivot_check(d, flags, q);
+        const cplx inv = crecip(d);
+        wv[t] = a[t];                              // U(t, t) L(row, t)
+        const cplx l = cmul(a[t], inv);
+#pragma unroll
+        for (int u = t + 1; u < FM_KB; ++u)
+          if (u < kb) a[u] = cfms(a[u], l, readlane_c(a[t], u));   // lane u: A(k0 + u, k0 + t) before its division
+        a[t] = l;
+      } else {
+        a[t] = make_double2(0.0, 0.0);
+        wv[t] = make_double2(0.0, 0.0);
+      }
+    }
+    __syncthreads();                  // every wave has read the block rows before wave 0 overwrites them
+    if (brow) {
+      if (w == 0 && lane < kb) {
+#pragma unroll
+        for (int u = 0; u < FM_KB; ++u) {
+          if (u < lane) A(k0 + lane, k0 + u) = a[u];
+          else if (u == lane) A(k0 + lane, k0 + lane) = wv[u];
+        }
+      }
+    } else if (prow < f) {
+#pragma unroll
+      for (int u = 0; u < FM_KB; ++u) {
+        if (u < kb) A(prow, k0 + u) = a[u];
+        sW[prow * FM_KB + u] = wv[u];
+      }
+    }
+    __syncthreads();
+    // trailing lower triangle [k1, f): 4 x 4 tiles
+    const int m = f - k1, nb = (m + 3) >> 2, nt = nb * (nb + 1) / 2;
+    for (int tau = tid; tau < nt; tau += FM_T) {
+      const int bi = tri_row(tau), bj = tau - bi * (bi + 1) / 2;
+      const int i0 = k1 + 4 * bi, j0 = k1 + 4 * bj;
+      int ri[4], cj[4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        ri[x] = min(i0 + x, f - 1);
+        cj[x] = min(j0 + x, f - 1);
+      }
+      cplx acc[4][4];
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] = A(ri[x], min(cj[y], ri[x]));
+#pragma unroll
+      for (int t = 0; t < FM_KB; ++t) {
+        cplx li[4], wj[4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) li[x] = A(ri[x], k0 + min(t, kb - 1));   // W = 0 past kb
+#pragma unroll
+        for (int y = 0; y < 4; ++y) wj[y] = sW[cj[y] * FM_KB + t];
+#pragma unroll
+        for (int x = 0; x < 4; ++x)
+#pragma unroll
+          for (int y = 0; y < 4; ++y) acc[x][y] = cfms(acc[x][y], li[x], wj[y]);
+      }
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y)
+          if (i0 + x < f && j0 + y <= i0 + x) A(i0 + x, j0 + y) = acc[x][y];
+    }
+    __syncthreads();
+  }
+  // 3. write back: L11 / U(k, k) / L21 / update matrix (lower triangle), U11 = diag(U) L11^T above the diagonal
+  for (int e = tid; e < nlow; e += FM_T) {
+    const int i = tri_row(e), j = e - i * (i + 1) / 2;
+    const cplx v = sA[e];
+    E(i, j) = v;
+    if (j < i && i < ns) E(j, i) = cmul(A(j, j), v);
+  }
+#undef A
+#undef E
+}
+
 // Off-diagonal panel blocks once A11 = L11 U11 is factored, every row of L21 and
 // every column of U12 independently (read once, written once):
 //   kind 0, row i >= ns:     L(i, :ns) = A(i, :ns) U11^{-1}
@@ -2128,6 +2298,31 @@ struct ResidArgs {
 
 __device__ __forceinline__ double cabs1(cplx z) { return fabs(z.x) + fabs(z.y); }
 
+// Compensated residual (the functional correction's walk): r = b - sum A x accumulated as an unevaluated sum
+// rh + rl (Ogita-Rump-Oishi Dot2: every product split exactly by an fma, every addition by TwoSum), i.e. as if
+// in twice the working precision and rounded once.  Next to a resonance the static-pivot solves are backward
+// stable to ~1e-15, so b - A x is as small as the rounding of the plain fp64 accumulation itself and the
+// correction mu^T r read mostly that rounding; with the compensated sum it reads the solve's error, and the
+// corrected fr no longer depends on the rounding order of the factorisation.  Contraction off: an fma fused
+// into TwoSum would break its exactness.
+__device__ __forceinline__ void dd_sub_prod(double& h, double& l, double a, double b) {
+#pragma clang fp contract(off)
+  const double p = a * b;
+  const double pe = fma(a, b, -p);        // a b - p exactly
+  const double s = h - p;
+  const double bb = s - h;
+  const double se = (h - (s - bb)) + (-p - bb);
+  h = s;
+  l -= pe;
+  l += se;
+}
+__device__ __forceinline__ void cfms_dd(cplx& rh, cplx& rl, cplx a, cplx x) {
+  dd_sub_prod(rh.x, rl.x, a.x, x.x);
+  dd_sub_prod(rh.x, rl.x, -a.y, x.y);
+  dd_sub_prod(rh.y, rl.y, a.x, x.y);
+  dd_sub_prod(rh.y, rl.y, a.y, x.x);
+}
+
 template <int MODE>
 __device__ __forceinline__ cplx resid_entry(const ResidArgs& A, const cplx* __restrict__ dq, int nz, double om2) {
   if (MODE == 0) {
@@ -2182,7 +2377,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSK > 0 ? R
     } else {
       b = A.G[(int64_t)p * Fc + q];
     }
-    cplx r = b;
+    cplx r = b, rl = make_double2(0.0, 0.0);    // DOT: r + rl compensated
     double den = cabs1(b);
     const int e1 = A.ptr[p + 1];
     int e = A.ptr[p];
@@ -2195,7 +2390,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSK > 0 ? R
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        r = cfms(r, a[u], x[u]);
+        if (DOT)
+          cfms_dd(r, rl, a[u], x[u]);
+        else
+          r = cfms(r, a[u], x[u]);
         den = fma(cabs1(a[u]), cabs1(x[u]), den);
       }
       if (NSK > 0) {
@@ -2214,7 +2412,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSK > 0 ? R
     for (; e < e1; ++e) {
       const cplx a = resid_entry<MODE>(A, dq, A.nzs[e], om2);
       const cplx x = X[(int64_t)A.idx[e] * Fc + q];
-      r = cfms(r, a, x);
+      if (DOT)
+        cfms_dd(r, rl, a, x);
+      else
+        r = cfms(r, a, x);
       den = fma(cabs1(a), cabs1(x), den);
       if (NSK > 0) {
         const cplx mx = cmul(mup, x);
@@ -2226,6 +2427,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSK > 0 ? R
         }
       }
     }
+    if (DOT) r = cadd(r, rl);
     if (R) R[(int64_t)p * Fc + q] = r;
     if (DOT) {
       const cplx m = NSK > 0 ? mup : Mu[(int64_t)p * Fc + q];
@@ -2533,7 +2735,7 @@ __global__ void k_functional(FunctionalArgs A, const cplx* __restrict__ X, int64
 // F_k = a_k^T x = sum_i (L^-1 a_k)_i (L^-1 b)_i / U(i, i) over the pivot rows i reached by both the rhs
 // and the support (rows: (permuted row, factor element of U(i, i))).  Per frequency group FN_PARTS
 // workgroups, each one partial per frequency (deterministic; k_functional_fn sums them in order).
-constexpr int FN_PARTS = 16;
+constexpr int FN_PARTS = FN_PARTS_HOST;
 __global__ __launch_bounds__(256) void k_fn_dot(const int2* __restrict__ rows, int nrows, const cplx* __restrict__ F,
                                                 const cplx* __restrict__ Yb, const cplx* __restrict__ Y0,
                                                 const cplx* __restrict__ Y1, const cplx* __restrict__ Y2, int64_t Fc,
@@ -2639,7 +2841,6 @@ __global__ void k_gather_entries(const int4* __restrict__ ent, int nent, const d
 // frequency group: with the sum over frequencies inside, the 12-18 scalar stiffness loads per entry and
 // the per-lane accumulators of all stiffness matrices drop out of the frequency loop).
 // Pseudo entries (row starts) and absent entries carry S = 0.  One partial per wave (k_reduce).
-constexpr int CEG_EW = 8;   // entries per wave of k_contract_eg
 // MS: lambda = m_q Lam per frequency (functional correction: Lam is the adjoint of fr, m_q the loss
 // cotangent scale k_correct_finish formed); m_q = 0 on the padded frequencies.
 template <int NS, int EW, bool MS>
@@ -2867,13 +3068,28 @@ void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, cons
 
 void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int maxns, double2* F, int64_t Fc, int* flags,
                        hipStream_t st) {
-  const size_t lds = ((size_t)maxns * (maxns + 1) / 2 + (size_t)maxns * KB) * sizeof(double2);
+  const size_t lds = (size_t)fac_lds_bytes(maxns);
+  static_assert(KB == 4, "fac_lds_bytes: 4 W columns per row");
   static const bool attr = [] {   // dynamic LDS beyond the default 64 KiB (up to 64 pivots: 37 KiB; headroom)
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_factor_sym_lds<1>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   }();
   (void)attr;
   LAUNCH_DYN(k_factor_sym_lds<1>, dim3((unsigned)(nfronts * Fc)), dim3(256), lds, st, P, lvl, F, Fc, flags, maxns);
+}
+
+void launch_front_fm(const DevPattern& P, const int* lvl, int nfronts, int maxf, const int* fm_off, const int4* recs,
+                     const int* xl, double2* F, int64_t Fc, const double* freqs, const double2* K, const double* M,
+                     int* flags, hipStream_t st) {
+  if (nfronts <= 0) return;
+  const size_t lds = (size_t)fm_lds_bytes(maxf);
+  static const bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_front_fm), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               160 * 1024) == hipSuccess;
+  }();
+  (void)attr;
+  LAUNCH_DYN(k_front_fm, dim3((unsigned)(nfronts * Fc)), dim3(FM_T), lds, st, P, lvl, fm_off, recs, xl, F, Fc, freqs, K, M,
+             flags, maxf);
 }
 
 void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F,
@@ -3011,7 +3227,6 @@ void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nro
          rhsP, beta, Y, accumulate);
 }
 
-int residual_parts(int n) { return (int)std::min<int64_t>((n + 3) / 4, 256); }
 
 void launch_residual(int mode, int rhs, const ResidDesc& d, const double2* X, int64_t Fc, double2* R, double* acc,
                      hipStream_t st, const double2* Mu, double2* cpart) {
@@ -3075,7 +3290,6 @@ void launch_gather_entries(const int4* ent, int nent, const double* stiff, int n
   LAUNCH(k_gather_entries, dim3((nent + 255) / 256), dim3(256), st, ent, nent, stiff, ns, se);
 }
 
-int contract_eg_parts(int nent) { return ((nent + CEG_EW - 1) / CEG_EW + 3) / 4; }   // workgroups of 4 waves
 
 void launch_contract_eg(const int4* ent, int nent, const double* se, int n_stiff, const double2* Lam, const double2* X,
                         int64_t Fc, int nvalid, double2* partial, hipStream_t st, const double2* msc) {

@@ -5,10 +5,6 @@
 
 namespace pfr {
 
-// The selective adjoint refinement works on at most this many 64-frequency groups per chunk (a compacted list;
-// its launches have this many grid rows instead of one per group)
-constexpr int REFINE_CAP = 4;
-
 struct RhsDesc {
   const double* rhsP = nullptr;   // RHS 0: permuted Dirichlet vector (device)
   double beta_re = 0, beta_im = 0, mass_sum = 0;
@@ -44,6 +40,12 @@ void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, i
 // largest pivot block (sizes the dynamic LDS: (maxns (maxns + 1) / 2 + 4 maxns) x 16 B)
 void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int maxns, double2* F, int64_t Fc, int* flags,
                        hipStream_t st);
+// the level's fronts frequency-major (symmetric analyses, operator form): one workgroup per (front, frequency), the
+// whole front gathered (records recs[fm_off[front] ..], one per lower-triangle entry: nz, two child sources, extra
+// list in xl or -1), factorised in LDS and written back; maxf = the level's largest front (sizes the LDS)
+void launch_front_fm(const DevPattern& P, const int* lvl, int nfronts, int maxf, const int* fm_off, const int4* recs,
+                     const int* xl, double2* F, int64_t Fc, const double* freqs, const double2* K, const double* M,
+                     int* flags, hipStream_t st);
 // L21 rows (and U12 columns in general mode) of a level's items; pipelined: the software-pipelined prefix
 // (symmetric, operator-form launches with few waves)
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
@@ -60,7 +62,6 @@ void launch_schur_blk(const DevPattern& P, const int4* blocks, int nblocks, cons
 // split > 1 (L and U solves): the update part of every front (L: the update rows; U: the pivot rows'
 // products with the update-row solution) runs first / last over `split` workgroups of SPLIT_W waves per
 // (front, frequency group) -- the top levels' few fronts otherwise pull their L21 blocks through one CU each
-constexpr int SPLIT_W = 4;
 // glist (may be NULL): the groups to solve, REFINE_CAP of them (-1: none), indexed by grid row (pass
 // ngroups = REFINE_CAP); the selective adjoint refinement's solves
 void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups,
@@ -73,7 +74,6 @@ void launch_lsolve_multi(int rhs_mode, const DevPattern& P, int nslices, const i
                          double2* const* Y, const int* const* reach, hipStream_t st, int split);
 // functional from the bottom-up passes: partial dot products (FN_PARTS x 3 x Fc), the functional / loss
 // / cotangent from them (fcoef: 3 x Fc, G at the support rows), and L^-1 g = sum_k c_k L^-1 a_k in Yk[0]
-constexpr int FN_PARTS_HOST = 16;
 void launch_fn_dot(const int2* rows, int nrows, const double2* F, const double2* Yb, const double2* const* Yk, int64_t Fc,
                    double2* parts, hipStream_t st);
 void launch_functional_fn(const FunctionalArgs& A, const double2* parts, int64_t Fc, int nvalid, int64_t q0,
@@ -94,8 +94,7 @@ void launch_functional_tangent(const FunctionalArgs& A, const double2* X, const 
                                int64_t q0, double2* G, hipStream_t st);
 void launch_functional(const FunctionalArgs& A, const double2* X, int64_t Fc, int nvalid, int64_t q0, double* fr_out,
                        double* loss_terms, double2* G, hipStream_t st);
-// gradient contraction with the frequency sum first (one partial per wave: contract_eg_parts of them)
-int contract_eg_parts(int nent);
+// gradient contraction with the frequency sum first (one partial per workgroup: contract_eg_parts of them)
 // msc (may be NULL): per-frequency factor of Lam (functional correction: the loss cotangent scale)
 void launch_contract_eg(const int4* ent, int nent, const double* se, int n_stiff, const double2* Lam, const double2* X,
                         int64_t Fc, int nvalid, double2* partial, hipStream_t st, const double2* msc = nullptr);
@@ -143,7 +142,6 @@ struct ResidDesc {
 };
 // Mu != NULL (mode 0, rhs 0): also the functional-correction dot products sum_p Mu_p r_p, one partial
 // per workgroup and frequency in cpart (residual_parts(n) x Fc), summed by launch_correct_finish
-int residual_parts(int n);
 // partial[t * n_stiff + k] = sum_{q in tile t} msc[q] sum_b kpart[b][k][q] (msc NULL: 1; tiles of 64
 // frequencies): the fused walk's contraction as Fc / 64 parts
 void launch_reduce_q(const double2* kpart, int nparts, int n_stiff, const double2* msc, int nvalid, int64_t Fc,
