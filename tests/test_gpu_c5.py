@@ -21,6 +21,11 @@
   difference; and the two trajectories' loss histories within that bound plus what their x difference
   (~1e-8) moves the loss, 2 sum_i |g_i| |xg_i - xo_i| with g the GPU gradient at the GPU iterate (the
   loss falls 200x over three steps, so 2e-8 in x moves the late iterates' loss by ~1e-5 of itself).
+* the losses along the trajectory against EXTENDED-PRECISION truth (tests/golden/c5_truth.npz,
+  make_c5_truth.py): at the 4 iterates of an oracle-driven 3-step L-BFGS run on the same subsample (fixed, so the
+  points do not depend on the GPU) the loss from fr solved with longdouble residuals to convergence; the GPU loss at
+  each iterate within C5_LOSS_RTOL of it, relative -- 3x the largest measured GPU error (the fp64 oracle's own
+  errors there, in the fixture: 1.3e-7 .. 1.6e-6).
 (The reference has no L-BFGS; its optimisers' trajectories are pinned at ny = 3 in
 tests/test_gpu_reference_run.py.)
 """
@@ -61,6 +66,26 @@ def test_c5_full_size_lbfgs_descends(c5):
     assert np.all(np.isfinite(f)) and len(f) >= 5
     assert np.all(np.diff(f) <= 0), f                      # Armijo steps: never an increase
     assert f[-1] < 0.1 * f[0], f
+
+
+# 3x the largest relative error of the GPU loss against the extended-precision loss at the fixture's iterates
+# (measured: see the test's report line)
+C5_LOSS_RTOL = 3 * 2.0e-7
+
+
+@pytest.mark.timeout(300)
+def test_c5_losses_match_extended_precision(c5):
+    import os
+    T = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c5_truth.npz"))
+    assert c5.mat_size == 19353 and str(T["material"]) == "orthotropic_d4"
+    assert np.allclose(np.asarray(c5.parameters), T["theta_true"], rtol=0, atol=0)
+    fn = c5.getLossFunction(T["freqs"], T["ref"], "MSE_LOG_AFC", T["theta0"])
+    fg = np.array([float(fn(torch.as_tensor(x))) for x in T["x"]])
+    rel = np.abs(fg / T["loss_true"] - 1)
+    rel_orc = np.abs(T["loss_oracle"] / T["loss_true"] - 1)
+    report("c5_loss_vs_truth", gpu_max_rel=float(rel.max()), gpu_last_rel=float(rel[-1]),
+           oracle_max_rel=float(rel_orc.max()), iterates=len(fg))
+    assert np.all(rel < C5_LOSS_RTOL), (rel, rel_orc)
 
 
 @pytest.mark.timeout(600)
