@@ -775,17 +775,23 @@ __global__ __launch_bounds__(FM_T, 2) void k_front_fm(DevPattern P, const int* _
       for (int x = 0; x < 4; ++x)
 #pragma unroll
         for (int y = 0; y < 4; ++y) acc[x][y] = A(ri[x], min(cj[y], ri[x]));
+      // two pivots' operands per step (16 accumulators + 16 operands: no spill at 2 waves / SIMD)
+#pragma unroll 1
+      for (int t0 = 0; t0 < FM_KB; t0 += 2) {
+        cplx li[2][4], wj[2][4];
 #pragma unroll
-      for (int t = 0; t < FM_KB; ++t) {
-        cplx li[4], wj[4];
+        for (int t = 0; t < 2; ++t) {
 #pragma unroll
-        for (int x = 0; x < 4; ++x) li[x] = A(ri[x], k0 + min(t, kb - 1));   // W = 0 past kb
+          for (int x = 0; x < 4; ++x) li[t][x] = A(ri[x], k0 + min(t0 + t, kb - 1));   // W = 0 past kb
 #pragma unroll
-        for (int y = 0; y < 4; ++y) wj[y] = sW[cj[y] * FM_KB + t];
+          for (int y = 0; y < 4; ++y) wj[t][y] = sW[cj[y] * FM_KB + t0 + t];
+        }
 #pragma unroll
-        for (int x = 0; x < 4; ++x)
+        for (int t = 0; t < 2; ++t)
 #pragma unroll
-          for (int y = 0; y < 4; ++y) acc[x][y] = cfms(acc[x][y], li[x], wj[y]);
+          for (int x = 0; x < 4; ++x)
+#pragma unroll
+            for (int y = 0; y < 4; ++y) acc[x][y] = cfms(acc[x][y], li[t][x], wj[t][y]);
       }
 #pragma unroll
       for (int x = 0; x < 4; ++x)
@@ -2332,7 +2338,7 @@ __device__ __forceinline__ cplx resid_entry(const ResidArgs& A, const cplx* __re
   return dq[nz];
 }
 
-constexpr int RES_WPE = 5;   // the fused walk at 96 VGPRs (5 waves/SIMD): its phase 9.5 -> 8.0 ms per step, lane-summed
+constexpr int RES_WPE = 4;   // the fused walk at 128 VGPRs with the compensated residual (round 3: 5 waves/SIMD, 96 VGPRs, 9.5 -> 8.0 ms)
 // NSK > 0 (with DOT, the loss sweep's forward walk under the functional correction): the gradient
 // contraction rides on the walk -- every entry (p, j, nz) it visits has x_j gathered and mu_p loaded
 // already, so s_k(q) += S_k(nz) mu_p x_j per lane (frequency), per workgroup; the loss cotangent scale
