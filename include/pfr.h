@@ -260,16 +260,14 @@ PFR_API int pfr_last_timings(const pfr_solver* s, double* ms_out /* 5 */);
 /* With pfr_set_timing(s, 3) the factorisation additionally brackets every launch with HIP events:
  * summed device times [ms] of the last call per kernel class (0 = A11 assembly, 1 = A11 LU,
  * 2 = L21/U12 rows/columns, 3 = Schur complement A22 of the large update blocks (16 x 16 LDS
- * blocks, symmetric mode), 4 = Schur complement A22 of the other fronts (4 x 4 tiles), 5 = the
- * frequency-major fronts of the narrow levels (the whole front per workgroup and frequency, symmetric
- * mode)) and their launch counts (NULL allowed). */
-PFR_API int pfr_last_kernel_timings(const pfr_solver* s, double* ms_out /* 6 */, int64_t* launches_out /* 6 */);
+ * blocks, symmetric mode), 4 = Schur complement A22 of the other fronts (4 x 4 tiles)) and their launch
+ * counts (NULL allowed). */
+PFR_API int pfr_last_kernel_timings(const pfr_solver* s, double* ms_out /* 5 */, int64_t* launches_out /* 5 */);
 
 /* Algorithmic HBM bytes per frequency of one factorisation, per kernel class as above: complex
  * entries each class must store plus the entries it must read once (children's update-matrix
- * entries it gathers, factor blocks it consumes); index data, shared by all frequencies, excluded.
- * The levels the frequency-major kernel takes count in class 5 alone. */
-PFR_API int pfr_solver_alg_bytes(const pfr_solver* s, int64_t* bytes_out /* 6 */);
+ * entries it gathers, factor blocks it consumes); index data, shared by all frequencies, excluded. */
+PFR_API int pfr_solver_alg_bytes(const pfr_solver* s, int64_t* bytes_out /* 5 */);
 
 /* Algorithmic HBM bytes per frequency of the triangular solves of one loss pfr_sweep under the
  * solver's current check mode: factor entries each pass must read (16 B each) plus rhs in / solution

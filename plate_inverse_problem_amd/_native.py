@@ -329,15 +329,15 @@ class Solver:
 
     def last_kernel_timings(self):
         """(ms, launches) per factorisation kernel class of the last call (needs kernels=True)."""
-        ms = np.zeros(6)
-        n = np.zeros(6, np.int64)
+        ms = np.zeros(5)
+        n = np.zeros(5, np.int64)
         check(lib().pfr_last_kernel_timings(self._h, ms.ctypes.data_as(_DP), n.ctypes.data_as(_P)),
               "pfr_last_kernel_timings")
         return ms, n
 
     def alg_bytes(self) -> np.ndarray:
         """Algorithmic HBM bytes per frequency of one factorisation, per kernel class."""
-        out = np.zeros(6, np.int64)
+        out = np.zeros(5, np.int64)
         check(lib().pfr_solver_alg_bytes(self._h, out.ctypes.data_as(_P)), "pfr_solver_alg_bytes")
         return out
 

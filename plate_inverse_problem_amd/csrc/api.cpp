@@ -173,13 +173,7 @@ struct pfr_solver {
   // algorithmic HBM bytes per frequency of each factorisation kernel class, per level (16 B per complex entry
   // loaded or stored; index data is shared by all frequencies and not counted)
   std::vector<std::array<int64_t, pfr::NKC>> lev_bytes;
-  // frequency-major fronts (k_front_fm) on the narrow levels (symmetric analyses, operator-form sweeps):
-  // PFR_FM_FRONTS = levels of at most this many fronts (0: off); per front its first gather record
-  std::vector<char> fm_level;
   pfr::Workspace ws;                    // element counts of the chunk buffers (plan.cpp; what is allocated)
-  int32_t* d_fm_off = nullptr;
-  int4* d_fm_rec = nullptr;             // per lower-triangle entry: (nz, child source, child source, extras or -1)
-  int32_t* d_fm_x = nullptr;            // extra child sources, each list ended by -1
   // launch-shape tuning knobs, read from the environment when the solver is created (so that a
   // process can build solvers with different settings, e.g. tests forcing each kernel variant):
   // PFR_SOLVE_WMAX (waves per solve workgroup, at most), PFR_FAC_WMAX (waves per A11 LU
@@ -189,6 +183,8 @@ struct pfr_solver {
   int fac_lds = -1;                     // PFR_FAC_LDS: which levels factor A11 in LDS (k_factor_sym_lds): n > 0
                                         // those whose largest pivot block has at least n pivots, 0 none, -1 auto
                                         // (default since round 3: 512-frequency sweeps +2.6 %, 4,096 unchanged)
+  int fac_wave = 16;                    // PFR_FAC_WAVE: A11 by one wave per frequency on the levels whose largest
+                                        // pivot block has at least this many pivots (0: never)
   int fac_lds_wg = 160;                 // PFR_FAC_LDS_WG: auto mode threshold (workgroups of k_factor_sym)
   int split_target = 256;               // PFR_SOLVE_SPLIT: solve launches with fewer (front, group) workgroups
                                         // than this (one per CU) split their update parts up to about this
@@ -293,6 +289,12 @@ int solve_split(const pfr_solver* s, int nf) { return pfr::solve_split(nf, s->Fc
 // top of the tree in small chunks: 512 frequencies levels 10-16, 2,048 level 16 -- faster per level there, slower
 // elsewhere; the default since the MMD ordering: 512-frequency sweeps 31.8k -> 32.6k freq-solves/s, 4,096
 // unchanged)
+// A11 of level l by one wave per frequency (k_factor_sym_wave): PFR_FAC_WAVE = n > 0: the levels whose largest
+// pivot block has n .. FAC_WAVE_MAX pivots; 0: none
+bool level_wave(const pfr_solver* s, int l) {
+  return s->sym && s->fac_wave > 0 && s->level_maxns[l] >= s->fac_wave && s->level_maxns[l] <= pfr::FAC_WAVE_MAX;
+}
+
 bool level_lds(const pfr_solver* s, int l) {
   const int64_t wgs = (int64_t)(s->level_ptr[l + 1] - s->level_ptr[l]) * (s->Fc / 64) * pfr::FAC_G;
   return s->sym && s->level_maxns[l] <= 64 &&
@@ -310,14 +312,6 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
   };
   for (int l = 0; l < L; ++l) {
     int nf = s->level_ptr[l + 1] - s->level_ptr[l];
-    if (mode == 0 && s->fm_level[l]) {
-      // the whole level frequency-major: one launch (classes 0-4 empty)
-      for (int c = 0; c <= pfr::NKC - 1; ++c) mark(l, c);
-      pfr::launch_front_fm(s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_maxf[l], s->d_fm_off, s->d_fm_rec,
-                           s->d_fm_x, s->F, s->Fc, s->freqs, s->K, s->M, s->flags, st);
-      mark(l, pfr::NKC);
-      continue;
-    }
     mark(l, 0);
     // panel: enough workgroups (front x 16 frequencies) to fill the chip -> one wave
     // each (no idle waves at the block barriers); few large fronts -> more waves
@@ -332,7 +326,10 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
                          s->d_asm_xp + s->asm_ptr[l] / 8, s->d_asm_x, ngroups, s->F, s->Fc, s->freqs, s->K, s->M,
                          data, ds, nvalid, st);
     mark(l, 1);
-    if (level_lds(s, l))
+    if (level_wave(s, l))
+      pfr::launch_factor_wave(s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_maxns[l], s->F, s->Fc, s->flags,
+                              st);
+    else if (level_lds(s, l))
       pfr::launch_factor_lds(s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_maxns[l], s->F, s->Fc, s->flags, st);
     else
       pfr::launch_factor(s->sym, s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st);
@@ -754,7 +751,8 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->fac_wmax = knob("PFR_FAC_WMAX", 16, 1, 16);
   s->us2_small = knob("PFR_US2_SMALL", 110, 0, pfr::MAX_FRONT);
   s->split_target = knob("PFR_SOLVE_SPLIT", 256, 0, 1 << 20);
-  s->fac_lds = knob("PFR_FAC_LDS", -1, -1, 64);   // LDS holds the lower triangle of up to 64 pivots
+  s->fac_lds = knob("PFR_FAC_LDS", -1, -1, 64);
+  s->fac_wave = knob("PFR_FAC_WAVE", 16, 0, pfr::FAC_WAVE_MAX);   // LDS holds the lower triangle of up to 64 pivots
   s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);
   s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);
   s->scale_corr = knob("PFR_SCALE_CORR", 1, 0, 1);
@@ -763,7 +761,6 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   const int blk_min = knob("PFR_SCHUR_BLK_MIN", 24, 0, pfr::MAX_FRONT);   // update blocks of >= this many rows: block kernel
   pfr::PlanOptions po;
   po.blk_min = blk_min;
-  po.fm_fronts = knob("PFR_FM_FRONTS", 4, 0, 1 << 30);
   s->n = S.n;
   s->nnz = S.nnz;
   s->Fc = round64(max_batch);
@@ -787,7 +784,6 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->asm_ptr = pl.asm_ptr;
   s->item_ptr = pl.item_ptr;
   s->lev_bytes = pl.lev_bytes;
-  s->fm_level = pl.fm_level;
   Front* d_fronts = nullptr;
   int rc = PFR_OK;
   std::vector<Front> fv(S.fronts);
@@ -805,9 +801,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       (rc = s->up_rec(&s->d_bg1, pl.bg1, -1)) || (rc = s->up(&s->d_bgxp, pl.bgxp)) || (rc = s->up_rec(&s->d_bgx, pl.bgx, z2)) ||
       (rc = s->up_rec(&s->d_asm, pl.asm_rec, n4)) || (rc = s->up(&s->d_asm_xp, pl.asm_xp)) ||
       (rc = s->up_rec(&s->d_asm_x, pl.asm_x, z2)) || (rc = s->up_rec(&s->d_items, pl.items, z4)) ||
-      (rc = s->up_rec(&s->d_orec, pl.orec, n2)) || (rc = s->up(&s->d_oxp, pl.oxp)) || (rc = s->up_rec(&s->d_ox, pl.ox, z2)) ||
-      (rc = s->up_rec(&s->d_fm_off, pl.fm_off, -1)) || (rc = s->up_rec(&s->d_fm_rec, pl.fm_rec, n4)) ||
-      (rc = s->up_rec(&s->d_fm_x, pl.fm_x, -1)))
+      (rc = s->up_rec(&s->d_orec, pl.orec, n2)) || (rc = s->up(&s->d_oxp, pl.oxp)) || (rc = s->up_rec(&s->d_ox, pl.ox, z2)))
     return bail(rc);
   std::vector<int32_t> cp(colptr, colptr + S.n + 1), ri(rowind, rowind + S.nnz);
   if ((rc = s->up(&s->d_colptr, cp)) || (rc = s->up(&s->d_rowind, ri))) return bail(rc);
@@ -931,10 +925,9 @@ int pfr_last_kernel_timings(const pfr_solver* s, double* ms, int64_t* launches) 
   for (int c = 0; c < s->n_tev; ++c) {
     if (!s->tev[c].used[0]) continue;
     for (int l = 0; l < L; ++l) {
-      const bool fm = s->fm_level[l];
-      const int work[pfr::NKC] = {fm ? 0 : s->asm_ptr[l + 1] - s->asm_ptr[l], fm ? 0 : s->level_ptr[l + 1] - s->level_ptr[l],
-                                  fm ? 0 : s->item_ptr[l + 1] - s->item_ptr[l], fm ? 0 : s->blk_ptr[l + 1] - s->blk_ptr[l],
-                                  fm ? 0 : s->tile_ptr[l + 1] - s->tile_ptr[l], fm ? s->level_ptr[l + 1] - s->level_ptr[l] : 0};
+      const int work[pfr::NKC] = {s->asm_ptr[l + 1] - s->asm_ptr[l], s->level_ptr[l + 1] - s->level_ptr[l],
+                                  s->item_ptr[l + 1] - s->item_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
+                                  s->tile_ptr[l + 1] - s->tile_ptr[l]};
       for (int k = 0; k < pfr::NKC; ++k) {
         float m = 0;
         HIP_TRY(hipEventElapsedTime(&m, s->tev[c].kev[(pfr::NKC + 1) * l + k], s->tev[c].kev[(pfr::NKC + 1) * l + k + 1]));
@@ -948,11 +941,9 @@ int pfr_last_kernel_timings(const pfr_solver* s, double* ms, int64_t* launches) 
 
 int pfr_solver_alg_bytes(const pfr_solver* s, int64_t* bytes) {
   if (!s || !bytes) return fail(PFR_ERR_ARG, "null argument");
-  // operator-form sweeps: a frequency-major level counts in class 5 alone
   for (int i = 0; i < pfr::NKC; ++i) bytes[i] = 0;
   for (int l = 0; l + 1 < (int)s->level_ptr.size(); ++l)
-    for (int i = 0; i < pfr::NKC; ++i)
-      if ((i == pfr::NKC - 1) == (s->fm_level[l] != 0)) bytes[i] += s->lev_bytes[l][i];
+    for (int i = 0; i < pfr::NKC; ++i) bytes[i] += s->lev_bytes[l][i];
   return PFR_OK;
 }
 

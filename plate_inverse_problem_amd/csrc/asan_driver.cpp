@@ -3,7 +3,7 @@
 // and pfr_solver_create this pfr::build_plan (api.cpp); tests/test_asan_host.py feeds it the plate patterns with
 // every ordering option the engine uses, compares the statistics with libpfr's, and has every plan checked
 // (pfr::check_plan) for every engine shape: chunks of 64 .. 4,096 frequencies (one or two lanes split a sweep
-// into such chunks), Schur block thresholds, frequency-major level limits and solve split targets.
+// into such chunks), Schur block thresholds and solve split targets.
 //
 // Input file (little-endian): int32 n, int64 nnz, int32 colptr[n + 1], int32 rowind[nnz],
 // int32 n_last, int32 last[n_last].  Each further argument is one option set
@@ -65,29 +65,25 @@ int main(int argc, char** argv) {
     int checked = 0;
     std::string err;
     const int blk_mins[] = {24, 0, 4};
-    const int fm_limits[] = {4, 0, 1000000};
     const int splits[] = {256, 0, 1000000};
     const int64_t chunks[] = {64, 512, 1024, 2048, 4096};
     for (int bm : blk_mins) {
-      for (int fm : fm_limits) {
-        pfr::PlanOptions po;
-        po.blk_min = bm;
-        po.fm_fronts = fm;
-        pfr::Plan P;
-        if (pfr::build_plan(S, po, P, err)) {
-          printf("plan error blk_min=%d fm=%d: %s\n", bm, fm, err.c_str());
-          goto next;
-        }
-        for (int64_t Fc : chunks)
-          for (int sp : splits) {
-            const std::string e = pfr::check_plan(S, P, Fc, sp);
-            if (!e.empty()) {
-              printf("plan error blk_min=%d fm=%d Fc=%lld split=%d: %s\n", bm, fm, (long long)Fc, sp, e.c_str());
-              goto next;
-            }
-            ++checked;
-          }
+      pfr::PlanOptions po;
+      po.blk_min = bm;
+      pfr::Plan P;
+      if (pfr::build_plan(S, po, P, err)) {
+        printf("plan error blk_min=%d: %s\n", bm, err.c_str());
+        goto next;
       }
+      for (int64_t Fc : chunks)
+        for (int sp : splits) {
+          const std::string e = pfr::check_plan(S, P, Fc, sp);
+          if (!e.empty()) {
+            printf("plan error blk_min=%d Fc=%lld split=%d: %s\n", bm, (long long)Fc, sp, e.c_str());
+            goto next;
+          }
+          ++checked;
+        }
     }
     {
       // reach lists of the loss support (the last nodes, when given) and of every 97th row

@@ -636,28 +636,7 @@ __global__ __launch_bounds__(256) void k_factor_sym_lds(DevPattern P, const int*
 #undef E
 }
 
-// ------------------------------------------------------------------ K2c: frequency-major fronts (narrow top)
-// The narrow top of the elimination tree -- levels of a few large fronts, which the frequency-minor kernels run
-// as five dependent launches of a few workgroups each (assembly, A11 LU, L21 rows, two Schur classes) -- as ONE
-// launch in which a workgroup is one front x ONE frequency.  The front's whole lower triangle (A11, L21, A22) is
-// gathered into LDS -- original entries K - omega^2 M plus every child's update-matrix entries, one record per
-// entry -- partially factorised there (LDL^T of the ns pivots in blocks of FM_KB, the update matrix formed in
-// place by rank-FM_KB updates of the trailing triangle) and written back once, in the frequency-minor layout
-// every other kernel reads: L11 below the diagonal, U(k, k) on it, U11 = diag(U) L11^T above it, L21, and the
-// update matrix (A22 lower).  Fc workgroups per front fill the chip on levels of one to a few fronts, and the
-// O(ns f^2) arithmetic runs out of LDS instead of global-memory round trips per pivot block.
-//  * global accesses are 16 B per lane at a stride of Fc entries; consecutive frequencies are consecutive
-//    logical workgroups on one XCD (xcd_swizzle), so each 128 B line is fetched into / written back from that
-//    XCD's L2 once for its 8 frequencies;
-//  * panel of a pivot block: every wave holds the block's FM_KB rows in lanes 0 .. FM_KB-1 (redundantly) and
-//    FM_PR panel rows in the other lanes, each lane its row's FM_KB entries in registers; the block's LDL^T and
-//    the panel solve run wave-synchronously, the pivot row values broadcast by v_readlane (no barrier per pivot);
-//  * trailing update: 4 x 4 tiles of the lower triangle per thread, A(i, j) -= sum_t L(i, t) W(j, t) with
-//    W(j, t) = U(t, t) L(j, t) kept beside the triangle (zero past a short last block).
-// Results equal the frequency-minor kernels' up to rounding (same pivots, same static order).
-constexpr int FM_T = 256;             // threads per workgroup
-constexpr int FM_PR = 64 - FM_KB;     // panel rows per wave
-
+// wave-uniform broadcast of lane l's value (l uniform)
 __device__ __forceinline__ double readlane_d(double v, int l) {
   const long long b = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
@@ -665,148 +644,128 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 }
 __device__ __forceinline__ cplx readlane_c(cplx v, int l) { return make_double2(readlane_d(v.x, l), readlane_d(v.y, l)); }
 
-__global__ __launch_bounds__(FM_T, 2) void k_front_fm(DevPattern P, const int* __restrict__ lvl,
-                                                  const int* __restrict__ fm_off, const int4* __restrict__ recs,
-                                                  const int* __restrict__ xl, cplx* __restrict__ F, int64_t Fc,
-                                                  const double* __restrict__ freqs, const cplx* __restrict__ K,
-                                                  const double* __restrict__ M, int* __restrict__ flags, int maxf) {
-  extern __shared__ cplx sA[];        // packed lower triangle of the front, then W (FM_KB per row)
-  cplx* __restrict__ sW = sA + (maxf * (maxf + 1)) / 2;
+// Orders one wave's LDS accesses across its lanes (the lanes of a wave exchange values through LDS without a
+// workgroup barrier: LDS operations of one wave complete in issue order; this keeps the compiler from moving
+// them across the exchange points)
+#define PFR_WAVE_SYNC()                                \
+  do {                                                 \
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); \
+    __builtin_amdgcn_wave_barrier();                   \
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); \
+  } while (0)
+
+// ------------------------------------------------------------------ K2a': symmetric A11 LU, one wave per frequency
+// A11 = L D L^T of the levels whose pivot blocks are mid-sized (FAC_WAVE_MIN .. 128 pivots): the frequency-minor
+// kernels walk those pivots through global memory -- one round trip per 4-pivot block phase, each phase behind a
+// workgroup barrier -- and are latency-bound there (0.04-0.2 ms per level of a few fronts at 2,048 frequencies,
+// against ~0.03 ms of bytes).  Here a workgroup is one front x WG consecutive frequencies and each WAVE owns one
+// frequency: its packed lower triangle of A11 (A(i, j) = sA[i (i + 1) / 2 + j]) sits in LDS, lane = row (RPL rows
+// per lane: lane + 64 r), and the factorisation runs without a single workgroup barrier:
+//  * panel of each FAC_WB-pivot block: lane i holds A(i, k0 .. k0 + FAC_WB) in registers and the block's pivots are
+//    eliminated one at a time wave-synchronously, pivot values and the pivot rows' W entries broadcast by
+//    v_readlane;  L(i, p) goes to the triangle, W(i, t) = U(p, p) L(i, p) to a per-wave scratch (FAC_WB per row);
+//  * trailing lower triangle: one entry (i, j) per lane at a time, A(i, j) -= sum_t L(i, k0 + t) W(j, t).
+// Global loads and stores are shared by the workgroup with the frequency fastest (WG x 16 B of each line per
+// access).  Entries written as k_factor_sym writes them: L11 below the diagonal, U(k, k) on it, U11 = diag(U) L11^T
+// above it; the operations per entry are k_factor_sym_lds's up to the block size (rounding differs).
+template <int WG, int RPL>
+__global__ __launch_bounds__(64 * WG) void k_factor_sym_wave(DevPattern P, const int* __restrict__ lvl,
+                                                            cplx* __restrict__ F, int64_t Fc, int* __restrict__ flags,
+                                                            int maxns) {
+  extern __shared__ cplx lds[];
+  const int per = maxns * (maxns + 1) / 2 + maxns * FAC_WB;   // wave_lds_entries(maxns)
+  const int ngq = (int)(Fc / WG);
   const int64_t lid = xcd_swizzle(blockIdx.x, gridDim.x);
-  const int slot = (int)(lid / Fc);
-  const int64_t q = lid - (int64_t)slot * Fc;
-  const int front = lvl[slot];
-  const Front fr = P.fronts[front];
-  const int f = fr.f, ns = fr.ns, nlow = f * (f + 1) / 2;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  cplx* __restrict__ base = F + fr.off * Fc + q;
-#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
-#define A(i, j) sA[((i) * ((i) + 1)) / 2 + (j)]
-  // 1. gather: per entry (nz of the original entry, two child sources, extra-source list or -1), 4 entries'
-  //    loads in flight per thread, masks as multipliers (loads unconditional from clamped addresses)
+  const int slot = (int)(lid / ngq);
+  const int64_t q0 = (lid % ngq) * WG;
+  const Front fr = P.fronts[lvl[slot]];
+  const int f = fr.f, ns = fr.ns, nlow = ns * (ns + 1) / 2;
+  cplx* __restrict__ base = F + fr.off * Fc + q0;
+  const int tid = threadIdx.x;
+#define E(a, b, qq) base[((int64_t)(a) * f + (b)) * Fc + (qq)]
   {
-    const int4* __restrict__ R = recs + fm_off[front];
-    const double om = 6.283185307179586 * freqs[q];
-    const double om2 = om * om;
-    constexpr int U = 4;
-    for (int e0 = tid; e0 < nlow; e0 += U * FM_T) {
-      int4 r[U];
+    // 1. the WG triangles: thread tid loads frequency tid % WG, UB entries in flight
+    constexpr int UB = 8;
+    const int qq = tid % WG;
+    cplx* __restrict__ sa = lds + qq * per;
+    for (int e0 = tid / WG; e0 < nlow; e0 += UB * 64) {
+      cplx v[UB];
 #pragma unroll
-      for (int u = 0; u < U; ++u) r[u] = R[min(e0 + u * FM_T, nlow - 1)];
-      cplx kk[U], c0[U], c1[U];
-      double mm[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        kk[u] = K[max(r[u].x, 0)];
-        mm[u] = M[max(r[u].x, 0)];
-        c0[u] = F[(int64_t)max(r[u].y, 0) * Fc + q];
-        c1[u] = F[(int64_t)max(r[u].z, 0) * Fc + q];
+      for (int u = 0; u < UB; ++u) {
+        const int e = min(e0 + u * 64, nlow - 1);
+        const int i = tri_row(e);
+        v[u] = E(i, e - i * (i + 1) / 2, qq);
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const double so = r[u].x >= 0 ? 1.0 : 0.0, s0 = r[u].y >= 0 ? 1.0 : 0.0, s1 = r[u].z >= 0 ? 1.0 : 0.0;
-        cplx v = make_double2(fma(so, fma(-om2, mm[u], kk[u].x), fma(s0, c0[u].x, s1 * c1[u].x)),
-                              fma(so, kk[u].y, fma(s0, c0[u].y, s1 * c1[u].y)));
-        if (r[u].w >= 0)     // rare: three or more children cover the entry
-          for (int x = r[u].w; xl[x] >= 0; ++x) v = cadd(v, F[(int64_t)xl[x] * Fc + q]);
-        if (e0 + u * FM_T < nlow) sA[e0 + u * FM_T] = v;
-      }
+      for (int u = 0; u < UB; ++u)
+        if (e0 + u * 64 < nlow) sa[e0 + u * 64] = v[u];
     }
   }
   __syncthreads();
-  // 2. partial LDL^T of the ns pivots
-  for (int k0 = 0; k0 < ns; k0 += FM_KB) {
-    const int kb = min(FM_KB, ns - k0), k1 = k0 + kb;
-    // panel: lane t < FM_KB the block row k0 + t, the others the rows k1 + FM_PR w + (lane - FM_KB)
-    const bool brow = lane < FM_KB;
-    const int prow = k1 + FM_PR * w + lane - FM_KB;
-    const int row = brow ? k0 + min(lane, kb - 1) : min(prow, f - 1);
-    cplx a[FM_KB], wv[FM_KB];
+  const int w = tid >> 6, lane = tid & 63;
+  cplx* __restrict__ sA = lds + w * per;
+  cplx* __restrict__ sW = sA + maxns * (maxns + 1) / 2;
+#define A(i, j) sA[((i) * ((i) + 1)) / 2 + (j)]
+  for (int k0 = 0; k0 < ns; k0 += FAC_WB) {
+    const int kb = min(FAC_WB, ns - k0), k1 = k0 + kb;
+    // 2. panel: rows >= k0 (rows outside [k0, ns) hold clamped copies that are never stored)
+    cplx a[RPL][FAC_WB];
+    int row[RPL];
 #pragma unroll
-    for (int u = 0; u < FM_KB; ++u) a[u] = A(row, min(k0 + min(u, kb - 1), row));   // block rows: right of the
-                                                                                     // diagonal unused
+    for (int r = 0; r < RPL; ++r) {
+      row[r] = lane + 64 * r;
+      const int ri = min(max(row[r], k0), ns - 1);
 #pragma unroll
-    for (int t = 0; t < FM_KB; ++t) {
-      if (t < kb) {                   // wave-uniform
-        const cplx d = readlane_c(a[t], t);        // U(k0 + t, k0 + t), updated by the earlier pivots
-        if (tid == 0) pivot_check(d, flags, q);
-        const cplx inv = crecip(d);
-        wv[t] = a[t];                              // U(t, t) L(row, t)
-        const cplx l = cmul(a[t], inv);
-#pragma unroll
-        for (int u = t + 1; u < FM_KB; ++u)
-          if (u < kb) a[u] = cfms(a[u], l, readlane_c(a[t], u));   // lane u: A(k0 + u, k0 + t) before its division
-        a[t] = l;
-      } else {
-        a[t] = make_double2(0.0, 0.0);
-        wv[t] = make_double2(0.0, 0.0);
-      }
+      for (int t = 0; t < FAC_WB; ++t) a[r][t] = A(ri, min(k0 + t, ri));
     }
-    __syncthreads();                  // every wave has read the block rows before wave 0 overwrites them
-    if (brow) {
-      if (w == 0 && lane < kb) {
 #pragma unroll
-        for (int u = 0; u < FM_KB; ++u) {
-          if (u < lane) A(k0 + lane, k0 + u) = a[u];
-          else if (u == lane) A(k0 + lane, k0 + lane) = wv[u];
+    for (int t = 0; t < FAC_WB; ++t) {
+      if (t < kb) {
+        const int p = k0 + t;
+        const cplx d = p < 64 ? readlane_c(a[0][t], p & 63) : readlane_c(a[RPL - 1][t], p & 63);
+        if (lane == 0) pivot_check(d, flags, q0 + w);
+        const cplx rd = crecip(d);
+        cplx b[FAC_WB];   // W(k0 + u, t): the pivot column's unscaled entries of the block rows below p
+#pragma unroll
+        for (int u = t + 1; u < FAC_WB; ++u)
+          b[u] = k0 + u < 64 ? readlane_c(a[0][t], (k0 + u) & 63) : readlane_c(a[RPL - 1][t], (k0 + u) & 63);
+#pragma unroll
+        for (int r = 0; r < RPL; ++r) {
+          const cplx wt = a[r][t], lt = cmul(wt, rd);
+#pragma unroll
+          for (int u = t + 1; u < FAC_WB; ++u) a[r][u] = cfms(a[r][u], lt, b[u]);
+          if (row[r] > p && row[r] < ns) {
+            A(row[r], p) = lt;
+            sW[row[r] * FAC_WB + t] = wt;
+          } else if (row[r] == p) {
+            A(p, p) = d;
+          }
         }
       }
-    } else if (prow < f) {
-#pragma unroll
-      for (int u = 0; u < FM_KB; ++u) {
-        if (u < kb) A(prow, k0 + u) = a[u];
-        sW[prow * FM_KB + u] = wv[u];
-      }
     }
-    __syncthreads();
-    // trailing lower triangle [k1, f): 4 x 4 tiles
-    const int m = f - k1, nb = (m + 3) >> 2, nt = nb * (nb + 1) / 2;
-    for (int tau = tid; tau < nt; tau += FM_T) {
-      const int bi = tri_row(tau), bj = tau - bi * (bi + 1) / 2;
-      const int i0 = k1 + 4 * bi, j0 = k1 + 4 * bj;
-      int ri[4], cj[4];
+    PFR_WAVE_SYNC();
+    // 3. trailing lower triangle (a short block is the last one: kb = FAC_WB whenever k1 < ns)
+    const int m = ns - k1, nt = m * (m + 1) / 2;
+    for (int e = lane; e < nt; e += 64) {
+      const int ii = tri_row(e), I = k1 + ii, J = k1 + e - ii * (ii + 1) / 2;
+      cplx v = A(I, J);
 #pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        ri[x] = min(i0 + x, f - 1);
-        cj[x] = min(j0 + x, f - 1);
-      }
-      cplx acc[4][4];
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 4; ++y) acc[x][y] = A(ri[x], min(cj[y], ri[x]));
-      // two pivots' operands per step (16 accumulators + 16 operands: no spill at 2 waves / SIMD)
-#pragma unroll 1
-      for (int t0 = 0; t0 < FM_KB; t0 += 2) {
-        cplx li[2][4], wj[2][4];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-#pragma unroll
-          for (int x = 0; x < 4; ++x) li[t][x] = A(ri[x], k0 + min(t0 + t, kb - 1));   // W = 0 past kb
-#pragma unroll
-          for (int y = 0; y < 4; ++y) wj[t][y] = sW[cj[y] * FM_KB + t0 + t];
-        }
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int x = 0; x < 4; ++x)
-#pragma unroll
-            for (int y = 0; y < 4; ++y) acc[x][y] = cfms(acc[x][y], li[t][x], wj[t][y]);
-      }
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 4; ++y)
-          if (i0 + x < f && j0 + y <= i0 + x) A(i0 + x, j0 + y) = acc[x][y];
+      for (int t = 0; t < FAC_WB; ++t) v = cfms(v, A(I, k0 + t), sW[J * FAC_WB + t]);
+      A(I, J) = v;
     }
-    __syncthreads();
+    PFR_WAVE_SYNC();
   }
-  // 3. write back: L11 / U(k, k) / L21 / update matrix (lower triangle), U11 = diag(U) L11^T above the diagonal
-  for (int e = tid; e < nlow; e += FM_T) {
-    const int i = tri_row(e), j = e - i * (i + 1) / 2;
-    const cplx v = sA[e];
-    E(i, j) = v;
-    if (j < i && i < ns) E(j, i) = cmul(A(j, j), v);
+  __syncthreads();
+  {
+    // 4. write back: L below the diagonal, U(k, k) on it, U(j, i) = U(j, j) L(i, j) above it
+    const int qq = tid % WG;
+    const cplx* __restrict__ sa = lds + qq * per;
+    for (int e = tid / WG; e < nlow; e += 64) {
+      const int i = tri_row(e), j = e - i * (i + 1) / 2;
+      const cplx v = sa[e];
+      E(i, j, qq) = v;
+      if (j < i) E(j, i, qq) = cmul(sa[j * (j + 1) / 2 + j], v);
+    }
   }
 #undef A
 #undef E
@@ -3084,18 +3043,25 @@ void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int max
   LAUNCH_DYN(k_factor_sym_lds<1>, dim3((unsigned)(nfronts * Fc)), dim3(256), lds, st, P, lvl, F, Fc, flags, maxns);
 }
 
-void launch_front_fm(const DevPattern& P, const int* lvl, int nfronts, int maxf, const int* fm_off, const int4* recs,
-                     const int* xl, double2* F, int64_t Fc, const double* freqs, const double2* K, const double* M,
-                     int* flags, hipStream_t st) {
-  if (nfronts <= 0) return;
-  const size_t lds = (size_t)fm_lds_bytes(maxf);
-  static const bool attr = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_front_fm), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               160 * 1024) == hipSuccess;
-  }();
-  (void)attr;
-  LAUNCH_DYN(k_front_fm, dim3((unsigned)(nfronts * Fc)), dim3(FM_T), lds, st, P, lvl, fm_off, recs, xl, F, Fc, freqs, K, M,
-             flags, maxf);
+void launch_factor_wave(const DevPattern& P, const int* lvl, int nfronts, int maxns, double2* F, int64_t Fc,
+                        int* flags, hipStream_t st) {
+  const int wg = wave_group(maxns);
+  const size_t lds = (size_t)(wg * wave_lds_entries(maxns) * 16);
+  const unsigned grid = (unsigned)(nfronts * (Fc / wg));
+#define FW(WG, RPL)                                                                                              \
+  do {                                                                                                           \
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_factor_sym_wave<WG, RPL>), \
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES); \
+    (void)attr;                                                                                                  \
+    LAUNCH_DYN((k_factor_sym_wave<WG, RPL>), dim3(grid), dim3(64 * WG), lds, st, P, lvl, F, Fc, flags, maxns);    \
+  } while (0)
+  if (maxns > 64) {
+    if (wg == 2) FW(2, 2); else FW(1, 2);
+  } else if (wg == 8) FW(8, 1);
+  else if (wg == 4) FW(4, 1);
+  else if (wg == 2) FW(2, 1);
+  else FW(1, 1);
+#undef FW
 }
 
 void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F,

@@ -40,12 +40,10 @@ void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, i
 // largest pivot block (sizes the dynamic LDS: (maxns (maxns + 1) / 2 + 4 maxns) x 16 B)
 void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int maxns, double2* F, int64_t Fc, int* flags,
                        hipStream_t st);
-// the level's fronts frequency-major (symmetric analyses, operator form): one workgroup per (front, frequency), the
-// whole front gathered (records recs[fm_off[front] ..], one per lower-triangle entry: nz, two child sources, extra
-// list in xl or -1), factorised in LDS and written back; maxf = the level's largest front (sizes the LDS)
-void launch_front_fm(const DevPattern& P, const int* lvl, int nfronts, int maxf, const int* fm_off, const int4* recs,
-                     const int* xl, double2* F, int64_t Fc, const double* freqs, const double2* K, const double* M,
-                     int* flags, hipStream_t st);
+// symmetric A11 LU, one wave per frequency (wave_group(maxns) frequencies of one front per workgroup, the
+// triangles in LDS); maxns <= FAC_WAVE_MAX
+void launch_factor_wave(const DevPattern& P, const int* lvl, int nfronts, int maxns, double2* F, int64_t Fc,
+                        int* flags, hipStream_t st);
 // L21 rows (and U12 columns in general mode) of a level's items; pipelined: the software-pipelined prefix
 // (symmetric, operator-form launches with few waves)
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,

@@ -257,60 +257,6 @@ int build_plan(const Symbolic& S, const PlanOptions& o, Plan& P, std::string& er
     b[4] += 16 * (g + P.gxp[P.tile_ptr[l + 1]] - P.gxp[P.tile_ptr[l]]);
   }
 
-  // ---- frequency-major levels (k_front_fm): levels of at most fm_fronts fronts whose largest front fits the LDS;
-  // per front and lower-triangle entry (a, b) one gather record -- the original entry (pivot rows: columns <= a;
-  // update rows: pivot columns) and the children's update-matrix entries landing there
-  P.fm_level.assign(L, 0);
-  P.fm_off.assign(nfr, -1);
-  if (sym && o.fm_fronts > 0) {
-    for (int l = 0; l < L; ++l)
-      P.fm_level[l] = S.level_ptr[l + 1] - S.level_ptr[l] <= o.fm_fronts && S.level_maxf[l] <= FM_MAXF;
-    std::vector<std::vector<int32_t>> src;
-    std::vector<int32_t> nz;
-    for (int l = 0; l < L; ++l) {
-      if (!P.fm_level[l]) continue;
-      for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
-        const int t = S.level_fronts[e];
-        const Front& F = S.fronts[t];
-        const int f = F.f, ns = F.ns, nlow = f * (f + 1) / 2;
-        nz.assign(nlow, -1);
-        src.assign(nlow, {});
-        for (int a = 0; a < f; ++a) {
-          const int r = F.row0 + a;
-          for (int x = S.asm_ptr[r]; x < S.asm_ptr[r + 1]; ++x) {
-            const int b = S.asm_col[x];
-            if (b <= a && b < ns) nz[a * (a + 1) / 2 + b] = S.asm_nz[x];
-          }
-        }
-        for (int c : kids[t]) {
-          const Front& C = S.fronts[c];
-          const int32_t* rp = S.relpos.data() + C.row0;
-          for (int ac = C.ns; ac < C.f; ++ac)
-            for (int bc = C.ns; bc <= ac; ++bc) {
-              const int i = std::max(rp[ac], rp[bc]), j = std::min(rp[ac], rp[bc]);
-              src[i * (i + 1) / 2 + j].push_back((int32_t)(C.off + (int64_t)ac * C.f + bc));
-            }
-        }
-        P.fm_off[t] = (int32_t)P.fm_rec.size();
-        int64_t g = 0;
-        for (int x = 0; x < nlow; ++x) {
-          const auto& v = src[x];
-          int xo = -1;
-          if (v.size() > 2) {
-            xo = (int)P.fm_x.size();
-            P.fm_x.insert(P.fm_x.end(), v.begin() + 2, v.end());
-            P.fm_x.push_back(-1);
-          }
-          P.fm_rec.push_back({nz[x], v.size() > 0 ? v[0] : -1, v.size() > 1 ? v[1] : -1, xo});
-          g += (int64_t)v.size();
-        }
-        // class 5: the children's entries gathered + every entry written (A11 both triangles)
-        const int64_t r = f - ns;
-        P.lev_bytes[l][NKC - 1] += 16 * (g + (int64_t)ns * ns + r * ns + r * (r + 1) / 2);
-      }
-    }
-  }
-
   // ---- symmetric mode: Dirichlet decoupling lists -- coupled rows (with their entries), per Dirichlet node the
   // entries of its column (adjoint correction), the coupled-row slot of every permuted row
   P.cslot.assign(S.n, -1);
@@ -488,31 +434,18 @@ std::string check_plan(const Symbolic& S, const Plan& P, int64_t Fc, int split_t
     if (P.tile_ptr[l] > P.tile_ptr[l + 1] || P.blk_ptr[l] > P.blk_ptr[l + 1] || P.item_ptr[l] > P.item_ptr[l + 1] ||
         P.asm_ptr[l] > P.asm_ptr[l + 1])
       return bad("level range order", l, P.tile_ptr[l], P.tile_ptr[l + 1]);
-  // frequency-major levels: every front's records inside fm_rec, extra lists terminated inside fm_x, LDS size
-  for (int l = 0; l < L; ++l) {
-    if (!P.fm_level[l]) continue;
-    if (!P.sym) return "frequency-major level in a general analysis";
-    if (fm_lds_bytes(S.level_maxf[l]) > LDS_BYTES) return bad("frequency-major LDS", l, fm_lds_bytes(S.level_maxf[l]), LDS_BYTES);
-    for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
-      const int t = S.level_fronts[e];
-      const Front& F = S.fronts[t];
-      const int64_t nlow = (int64_t)F.f * (F.f + 1) / 2;
-      if (P.fm_off[t] < 0 || P.fm_off[t] + nlow > (int64_t)P.fm_rec.size()) return bad("frequency-major records", t, P.fm_off[t], P.fm_rec.size());
-      for (int64_t x = P.fm_off[t]; x < P.fm_off[t] + nlow; ++x) {
-        const I4& r = P.fm_rec[x];
-        if (!nz_ok(r.x) || !id_ok(r.y) || !id_ok(r.z)) return bad("frequency-major record", x, r.y, FE);
-        if (r.w >= 0) {
-          int64_t k = r.w;
-          for (; k < (int64_t)P.fm_x.size() && P.fm_x[k] >= 0; ++k)
-            if (P.fm_x[k] >= FE) return bad("frequency-major extra", k, P.fm_x[k], FE);
-          if (k >= (int64_t)P.fm_x.size()) return bad("frequency-major extra list unterminated", x, r.w, P.fm_x.size());
-        }
-      }
-    }
-  }
   // A11 in LDS (k_factor_sym_lds) on the levels whose pivot blocks reach at most 64
   for (int l = 0; l < L; ++l)
     if (P.level_maxns[l] <= 64 && fac_lds_bytes(P.level_maxns[l]) > LDS_BYTES) return bad("A11 LDS", l, P.level_maxns[l], 64);
+  // A11 by one wave per frequency (k_factor_sym_wave) on the levels whose pivot blocks reach at most FAC_WAVE_MAX:
+  // the workgroup's triangles within the LDS, the frequencies of a chunk a whole number of workgroups
+  for (int l = 0; l < L; ++l) {
+    const int m = P.level_maxns[l];
+    if (m > FAC_WAVE_MAX) continue;
+    const int wg = wave_group(m);
+    if (wg * wave_lds_entries(m) * 16 > LDS_BYTES) return bad("A11 wave LDS", l, wg * wave_lds_entries(m) * 16, LDS_BYTES);
+    if (Fc % wg || (m > 64 && wg > 2)) return bad("A11 wave group", l, wg, Fc);
+  }
   // Dirichlet lists
   const Workspace W = workspace(S, Fc, P.n_crow);
   for (size_t d = 0; d < P.dir.size(); ++d)

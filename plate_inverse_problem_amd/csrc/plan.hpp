@@ -42,10 +42,10 @@ constexpr int OFF_G = 1;
 constexpr int OFF_RPL = 2;
 constexpr int FAC_G = 2;                      // A11 LU: lane groups per wave (64 / FAC_G frequencies each)
 constexpr int MAX_FRONT = 1024;               // largest front the solve kernels stage index lists for in LDS
-constexpr int FM_MAXF = 128;                  // largest front of a frequency-major level (LDS: lower triangle + W)
-constexpr int FM_KB = 8;                      // k_front_fm pivot block (W columns per row)
-constexpr int NKC = 6;                        // factorisation kernel classes: assembly, A11 LU, L21 rows, Schur
-                                              // blocks, Schur tiles, frequency-major fronts
+constexpr int FAC_WB = 8;                     // k_factor_sym_wave pivot block (W columns per row)
+constexpr int FAC_WAVE_MAX = 128;             // largest pivot block k_factor_sym_wave takes (two rows per lane)
+constexpr int NKC = 5;                        // factorisation kernel classes: assembly, A11 LU, L21 rows, Schur
+                                              // blocks, Schur tiles
 constexpr int FN_PARTS_HOST = 16;             // k_fn_dot partials per frequency group (kernels.hip: FN_PARTS)
 constexpr int REFINE_CAP = 4;                 // groups of the selective adjoint refinement per chunk
 constexpr int SPLIT_W = 4;                    // waves per workgroup of the split solve update parts
@@ -55,10 +55,16 @@ constexpr int64_t LDS_BYTES = 160 * 1024;
 // ---- launch geometry shared by the launchers and the checks
 inline int residual_parts(int n) { return (int)std::min<int64_t>((n + 3) / 4, 256); }   // k_residual grid.x
 inline int contract_eg_parts(int nent) { return ((nent + CEG_EW - 1) / CEG_EW + 3) / 4; }   // k_contract_eg grid
-// dynamic LDS of k_front_fm for a level whose largest front is maxf
-inline int64_t fm_lds_bytes(int maxf) { return ((int64_t)maxf * (maxf + 1) / 2 + (int64_t)maxf * FM_KB) * 16; }
 // dynamic LDS of k_factor_sym_lds for a level whose largest pivot block is maxns
 inline int64_t fac_lds_bytes(int maxns) { return ((int64_t)maxns * (maxns + 1) / 2 + (int64_t)maxns * 4) * 16; }
+// k_factor_sym_wave: LDS entries per wave (packed lower triangle + W) and frequencies (waves) per workgroup -- as
+// many as keep two workgroups' triangles within 80 KiB
+inline int64_t wave_lds_entries(int maxns) { return (int64_t)maxns * (maxns + 1) / 2 + (int64_t)maxns * FAC_WB; }
+inline int wave_group(int maxns) {
+  for (int wg = 8; wg > 1; wg /= 2)
+    if (wg * wave_lds_entries(maxns) * 16 <= 80 * 1024 && (maxns <= 64 || wg <= 2)) return wg;
+  return 1;
+}
 // waves per workgroup for a level whose largest front is maxf
 inline int waves_for(int maxf) { return std::max(1, std::min(8, (maxf + 23) / 24)); }
 // Workgroups per (front, frequency group) for the update part of a solve launch over nf fronts: 1 when the
@@ -78,7 +84,6 @@ inline int solve_waves(int level_w, int64_t nf, int64_t Fc, int wmax) {
 
 struct PlanOptions {
   int blk_min = 24;      // PFR_SCHUR_BLK_MIN: update blocks of at least this many rows through the block kernel
-  int fm_fronts = 4;     // PFR_FM_FRONTS: levels of at most this many fronts frequency-major (0: none)
 };
 
 struct Plan {
@@ -105,11 +110,6 @@ struct Plan {
   std::vector<I2> ox;                    // (pivot * OFF_G OFF_RPL + row slot, element id)
   // algorithmic bytes per frequency, level and kernel class (operator-form sweeps)
   std::vector<std::array<int64_t, NKC>> lev_bytes;
-  // frequency-major levels: per front its first record (-1: not frequency-major), records per lower-triangle
-  // entry (nz, child source, child source, extra list or -1), extra lists each ended by -1
-  std::vector<char> fm_level;
-  std::vector<int32_t> fm_off, fm_x;
-  std::vector<I4> fm_rec;
   // symmetric mode: Dirichlet decoupling lists
   int n_dir = 0, n_crow = 0;
   std::vector<I2> dir, ce, de;           // (permuted node, diagonal nz); (Dirichlet slot, nz); (permuted row, nz)

@@ -2,7 +2,7 @@
 the corrected fr of the bench's 4,096-frequency sweep and the raw / corrected fr of the 32 fixture frequencies
 with their backward errors.
 
-    python tools/fm_acc.py KNOB=V[,KNOB=V] ...
+    python tools/knob_acc.py KNOB=V[,KNOB=V] ...
 """
 import gc
 import os
