@@ -99,12 +99,12 @@ class _Engine:
         # (checked on the values): only L is formed, U = diag(U) L^T
         self.symmetric = bool(symmetric) and decoupled_symmetric(rows, cols, vals, n)
         # tuning knobs of the symbolic analysis (defaults in include/pfr.h): PFR_LEAF_SIZE,
-        # PFR_RELAX="small,mid,big" (supernode amalgamation pivot limits), PFR_MAX_NS, PFR_MD_DELTA,
-        # PFR_ORDERING (2: the exact-minimum-degree leaves of rounds 1-3, for A/B runs)
+        # PFR_RELAX="small,mid,big[,zmid,zbig]" (supernode amalgamation pivot limits and zero fractions), PFR_MAX_NS,
+        # PFR_MD_DELTA, PFR_ORDERING (2: the exact-minimum-degree leaves of rounds 1-3, for A/B runs)
         env = lambda k: os.environ.get(k)  # noqa: E731
         self._sym_args = (n, colptr, rows.astype(np.int32))
         self._sym_kw = dict(symmetric=self.symmetric, ordering=int(env("PFR_ORDERING") or 0),
-                            relax=tuple(int(v) for v in env("PFR_RELAX").split(",")) if env("PFR_RELAX") else None,
+                            relax=tuple(float(v) for v in env("PFR_RELAX").split(",")) if env("PFR_RELAX") else None,
                             max_ns=int(env("PFR_MAX_NS")) if env("PFR_MAX_NS") else None,
                             md_delta=int(env("PFR_MD_DELTA")) if env("PFR_MD_DELTA") else None)
         self._leaf_env = int(env("PFR_LEAF_SIZE")) if env("PFR_LEAF_SIZE") else None

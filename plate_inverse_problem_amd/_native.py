@@ -161,7 +161,9 @@ class Symbolic:
             opt.n_last = int(self.last.size)
             opt.last = lp
         if relax is not None:
-            opt.relax_small, opt.relax_mid, opt.relax_big = relax
+            opt.relax_small, opt.relax_mid, opt.relax_big = (int(v) for v in relax[:3])
+            if len(relax) > 3:
+                opt.zrelax_mid, opt.zrelax_big = (float(v) for v in relax[3:5])
         self.colptr, cp = _i32(colptr)
         self.rowind, ri = _i32(rowind)
         self.n = int(n)

@@ -2303,7 +2303,9 @@ constexpr int RES_WPE = 4;   // the fused walk at 128 VGPRs with the compensated
 // already, so s_k(q) += S_k(nz) mu_p x_j per lane (frequency), per workgroup; the loss cotangent scale
 // m_q is only known after this walk (k_correct_finish), so the partials stay per frequency and
 // k_reduce_q applies m_q.  Replaces k_contract_eg's separate entry walk.
-template <int MODE, int RHS, bool DOT = false, int NSK = 0>
+// CMP: the residual accumulated compensated (Dot2) -- the correction walk (DOT) and the refinement's residual (R):
+// both read the solve's own error, which a plain fp64 sum of the row's terms rounds away
+template <int MODE, int RHS, bool DOT = false, int NSK = 0, bool CMP = DOT>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSK > 0 ? RES_WPE : 1))) void k_residual(ResidArgs A, const cplx* __restrict__ X, int64_t Fc,
                                                   cplx* __restrict__ R, double* __restrict__ acc,
                                                   const cplx* __restrict__ Mu, cplx* __restrict__ cpart) {
@@ -2342,7 +2344,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSK > 0 ? R
     } else {
       b = A.G[(int64_t)p * Fc + q];
     }
-    cplx r = b, rl = make_double2(0.0, 0.0);    // DOT: r + rl compensated
+    cplx r = b, rl = make_double2(0.0, 0.0);    // CMP: r + rl compensated
     double den = cabs1(b);
     const int e1 = A.ptr[p + 1];
     int e = A.ptr[p];
@@ -2355,7 +2357,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSK > 0 ? R
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        if (DOT)
+        if (CMP)
           cfms_dd(r, rl, a[u], x[u]);
         else
           r = cfms(r, a[u], x[u]);
@@ -2377,7 +2379,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSK > 0 ? R
     for (; e < e1; ++e) {
       const cplx a = resid_entry<MODE>(A, dq, A.nzs[e], om2);
       const cplx x = X[(int64_t)A.idx[e] * Fc + q];
-      if (DOT)
+      if (CMP)
         cfms_dd(r, rl, a, x);
       else
         r = cfms(r, a, x);
@@ -2392,7 +2394,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSK > 0 ? R
         }
       }
     }
-    if (DOT) r = cadd(r, rl);
+    if (CMP) r = cadd(r, rl);
     if (R) R[(int64_t)p * Fc + q] = r;
     if (DOT) {
       const cplx m = NSK > 0 ? mup : Mu[(int64_t)p * Fc + q];
@@ -3214,7 +3216,12 @@ void launch_residual(int mode, int rhs, const ResidDesc& d, const double2* X, in
   else if (mode == 0 && rhs == 0 && Mu && d.kpart && d.n_stiff == 18)
     LAUNCH((k_residual<0, 0, true, 18>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
   else if (mode == 0 && rhs == 0 && Mu) LAUNCH((k_residual<0, 0, true>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
-  else if (mode == 0 && rhs == 0) LAUNCH((k_residual<0, 0>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
+  else if (R) {   // the refinement's residual: compensated
+    if (mode == 0 && rhs == 0) LAUNCH((k_residual<0, 0, false, 0, true>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
+    else if (mode == 0) LAUNCH((k_residual<0, 2, false, 0, true>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
+    else if (rhs == 1) LAUNCH((k_residual<1, 1, false, 0, true>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
+    else LAUNCH((k_residual<1, 2, false, 0, true>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
+  } else if (mode == 0 && rhs == 0) LAUNCH((k_residual<0, 0>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
   else if (mode == 0) LAUNCH((k_residual<0, 2>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
   else if (rhs == 1) LAUNCH((k_residual<1, 1>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
   else LAUNCH((k_residual<1, 2>), g, b, st, a, X, Fc, R, acc, Mu, cpart);
