@@ -183,8 +183,9 @@ struct pfr_solver {
   int fac_lds = -1;                     // PFR_FAC_LDS: which levels factor A11 in LDS (k_factor_sym_lds): n > 0
                                         // those whose largest pivot block has at least n pivots, 0 none, -1 auto
                                         // (default since round 3: 512-frequency sweeps +2.6 %, 4,096 unchanged)
-  int fac_wave = 16;                    // PFR_FAC_WAVE: A11 by one wave per frequency on the levels whose largest
-                                        // pivot block has at least this many pivots (0: never)
+  int fac_wave = -1;                    // PFR_FAC_WAVE: A11 by one wave per frequency (k_factor_sym_wave): n > 0 the
+                                        // levels whose largest pivot block has n .. 64 pivots, 0 none, -1 auto
+                                        // (the levels PFR_FAC_LDS=-1 picks)
   int fac_lds_wg = 160;                 // PFR_FAC_LDS_WG: auto mode threshold (workgroups of k_factor_sym)
   int split_target = 256;               // PFR_SOLVE_SPLIT: solve launches with fewer (front, group) workgroups
                                         // than this (one per CU) split their update parts up to about this
@@ -289,17 +290,20 @@ int solve_split(const pfr_solver* s, int nf) { return pfr::solve_split(nf, s->Fc
 // top of the tree in small chunks: 512 frequencies levels 10-16, 2,048 level 16 -- faster per level there, slower
 // elsewhere; the default since the MMD ordering: 512-frequency sweeps 31.8k -> 32.6k freq-solves/s, 4,096
 // unchanged)
-// A11 of level l by one wave per frequency (k_factor_sym_wave): PFR_FAC_WAVE = n > 0: the levels whose largest
-// pivot block has n .. FAC_WAVE_MAX pivots; 0: none
-bool level_wave(const pfr_solver* s, int l) {
-  return s->sym && s->fac_wave > 0 && s->level_maxns[l] >= s->fac_wave && s->level_maxns[l] <= pfr::FAC_WAVE_MAX;
-}
-
 bool level_lds(const pfr_solver* s, int l) {
   const int64_t wgs = (int64_t)(s->level_ptr[l + 1] - s->level_ptr[l]) * (s->Fc / 64) * pfr::FAC_G;
   return s->sym && s->level_maxns[l] <= 64 &&
          (s->fac_lds > 0 ? s->level_maxns[l] >= s->fac_lds
                          : s->fac_lds < 0 && s->level_maxns[l] >= 16 && wgs < s->fac_lds_wg);
+}
+
+// A11 of level l by one wave per frequency (k_factor_sym_wave): PFR_FAC_WAVE = n > 0: the levels whose largest
+// pivot block has n .. FAC_WAVE_MAX pivots; -1: the levels of the auto LDS rule above; 0: none
+bool level_wave(const pfr_solver* s, int l) {
+  if (!s->sym || s->fac_wave == 0 || s->level_maxns[l] > pfr::FAC_WAVE_MAX) return false;
+  if (s->fac_wave > 0) return s->level_maxns[l] >= s->fac_wave;
+  const int64_t wgs = (int64_t)(s->level_ptr[l + 1] - s->level_ptr[l]) * (s->Fc / 64) * pfr::FAC_G;
+  return s->level_maxns[l] >= 16 && wgs < s->fac_lds_wg;
 }
 
 int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nvalid, hipStream_t st) {
@@ -348,7 +352,6 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
                       s->d_g1 + (int64_t)s->tile_ptr[l] * pfr::SCHUR_TM * pfr::SCHUR_TN * pfr::SCHUR_SR * pfr::SCHUR_SC,
                       s->d_gxp + s->tile_ptr[l], s->d_gx, ngroups, s->F, s->Fc, st);
     mark(l, 5);
-    mark(l, 6);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -752,7 +755,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->us2_small = knob("PFR_US2_SMALL", 110, 0, pfr::MAX_FRONT);
   s->split_target = knob("PFR_SOLVE_SPLIT", 256, 0, 1 << 20);
   s->fac_lds = knob("PFR_FAC_LDS", -1, -1, 64);
-  s->fac_wave = knob("PFR_FAC_WAVE", 16, 0, pfr::FAC_WAVE_MAX);   // LDS holds the lower triangle of up to 64 pivots
+  s->fac_wave = knob("PFR_FAC_WAVE", -1, -1, pfr::FAC_WAVE_MAX);
   s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);
   s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);
   s->scale_corr = knob("PFR_SCALE_CORR", 1, 0, 1);

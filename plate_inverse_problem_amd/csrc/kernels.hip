@@ -655,19 +655,22 @@ __device__ __forceinline__ cplx readlane_c(cplx v, int l) { return make_double2(
   } while (0)
 
 // ------------------------------------------------------------------ K2a': symmetric A11 LU, one wave per frequency
-// A11 = L D L^T of the levels whose pivot blocks are mid-sized (FAC_WAVE_MIN .. 128 pivots): the frequency-minor
-// kernels walk those pivots through global memory -- one round trip per 4-pivot block phase, each phase behind a
-// workgroup barrier -- and are latency-bound there (0.04-0.2 ms per level of a few fronts at 2,048 frequencies,
-// against ~0.03 ms of bytes).  Here a workgroup is one front x WG consecutive frequencies and each WAVE owns one
+// A11 = L D L^T on the levels where the frequency-minor kernel gets few workgroups (the top of the tree: one or two
+// fronts of 16-64 pivots; it walks their pivots through global memory, a round trip per 4-pivot block phase behind
+// a workgroup barrier).  Here a workgroup is one front x WG consecutive frequencies and each WAVE owns one
 // frequency: its packed lower triangle of A11 (A(i, j) = sA[i (i + 1) / 2 + j]) sits in LDS, lane = row (RPL rows
-// per lane: lane + 64 r), and the factorisation runs without a single workgroup barrier:
+// per lane: lane + 64 r), and the factorisation runs without a workgroup barrier:
 //  * panel of each FAC_WB-pivot block: lane i holds A(i, k0 .. k0 + FAC_WB) in registers and the block's pivots are
 //    eliminated one at a time wave-synchronously, pivot values and the pivot rows' W entries broadcast by
-//    v_readlane;  L(i, p) goes to the triangle, W(i, t) = U(p, p) L(i, p) to a per-wave scratch (FAC_WB per row);
+//    v_readlane;  L(i, p) goes to the triangle, W(i, t) = U(p, p) L(i, p) to a per-wave scratch (column-major:
+//    consecutive rows in consecutive banks);
 //  * trailing lower triangle: one entry (i, j) per lane at a time, A(i, j) -= sum_t L(i, k0 + t) W(j, t).
 // Global loads and stores are shared by the workgroup with the frequency fastest (WG x 16 B of each line per
 // access).  Entries written as k_factor_sym writes them: L11 below the diagonal, U(k, k) on it, U11 = diag(U) L11^T
-// above it; the operations per entry are k_factor_sym_lds's up to the block size (rounding differs).
+// above it (rounding differs from the frequency-minor kernels: the elimination order within a block).
+// Measured (2,048 frequencies): 2-3x slower than k_factor_sym on levels of tens to hundreds of fronts (a wave per
+// front-frequency, LDS-limited occupancy), ~30 % faster than the one-frequency LDS kernel on one- and two-front
+// levels.
 template <int WG, int RPL>
 __global__ __launch_bounds__(64 * WG) void k_factor_sym_wave(DevPattern P, const int* __restrict__ lvl,
                                                             cplx* __restrict__ F, int64_t Fc, int* __restrict__ flags,
@@ -736,7 +739,7 @@ __global__ __launch_bounds__(64 * WG) void k_factor_sym_wave(DevPattern P, const
           for (int u = t + 1; u < FAC_WB; ++u) a[r][u] = cfms(a[r][u], lt, b[u]);
           if (row[r] > p && row[r] < ns) {
             A(row[r], p) = lt;
-            sW[row[r] * FAC_WB + t] = wt;
+            sW[t * maxns + row[r]] = wt;
           } else if (row[r] == p) {
             A(p, p) = d;
           }
@@ -750,7 +753,7 @@ __global__ __launch_bounds__(64 * WG) void k_factor_sym_wave(DevPattern P, const
       const int ii = tri_row(e), I = k1 + ii, J = k1 + e - ii * (ii + 1) / 2;
       cplx v = A(I, J);
 #pragma unroll
-      for (int t = 0; t < FAC_WB; ++t) v = cfms(v, A(I, k0 + t), sW[J * FAC_WB + t]);
+      for (int t = 0; t < FAC_WB; ++t) v = cfms(v, A(I, k0 + t), sW[t * maxns + J]);
       A(I, J) = v;
     }
     PFR_WAVE_SYNC();
@@ -3057,9 +3060,7 @@ void launch_factor_wave(const DevPattern& P, const int* lvl, int nfronts, int ma
     (void)attr;                                                                                                  \
     LAUNCH_DYN((k_factor_sym_wave<WG, RPL>), dim3(grid), dim3(64 * WG), lds, st, P, lvl, F, Fc, flags, maxns);    \
   } while (0)
-  if (maxns > 64) {
-    if (wg == 2) FW(2, 2); else FW(1, 2);
-  } else if (wg == 8) FW(8, 1);
+  if (wg == 8) FW(8, 1);
   else if (wg == 4) FW(4, 1);
   else if (wg == 2) FW(2, 1);
   else FW(1, 1);

@@ -444,7 +444,7 @@ std::string check_plan(const Symbolic& S, const Plan& P, int64_t Fc, int split_t
     if (m > FAC_WAVE_MAX) continue;
     const int wg = wave_group(m);
     if (wg * wave_lds_entries(m) * 16 > LDS_BYTES) return bad("A11 wave LDS", l, wg * wave_lds_entries(m) * 16, LDS_BYTES);
-    if (Fc % wg || (m > 64 && wg > 2)) return bad("A11 wave group", l, wg, Fc);
+    if (Fc % wg) return bad("A11 wave group", l, wg, Fc);
   }
   // Dirichlet lists
   const Workspace W = workspace(S, Fc, P.n_crow);

@@ -43,7 +43,7 @@ constexpr int OFF_RPL = 2;
 constexpr int FAC_G = 2;                      // A11 LU: lane groups per wave (64 / FAC_G frequencies each)
 constexpr int MAX_FRONT = 1024;               // largest front the solve kernels stage index lists for in LDS
 constexpr int FAC_WB = 8;                     // k_factor_sym_wave pivot block (W columns per row)
-constexpr int FAC_WAVE_MAX = 128;             // largest pivot block k_factor_sym_wave takes (two rows per lane)
+constexpr int FAC_WAVE_MAX = 64;              // largest pivot block k_factor_sym_wave takes (lane = row)
 constexpr int NKC = 5;                        // factorisation kernel classes: assembly, A11 LU, L21 rows, Schur
                                               // blocks, Schur tiles
 constexpr int FN_PARTS_HOST = 16;             // k_fn_dot partials per frequency group (kernels.hip: FN_PARTS)
@@ -62,7 +62,7 @@ inline int64_t fac_lds_bytes(int maxns) { return ((int64_t)maxns * (maxns + 1) /
 inline int64_t wave_lds_entries(int maxns) { return (int64_t)maxns * (maxns + 1) / 2 + (int64_t)maxns * FAC_WB; }
 inline int wave_group(int maxns) {
   for (int wg = 8; wg > 1; wg /= 2)
-    if (wg * wave_lds_entries(maxns) * 16 <= 80 * 1024 && (maxns <= 64 || wg <= 2)) return wg;
+    if (wg * wave_lds_entries(maxns) * 16 <= 80 * 1024) return wg;
   return 1;
 }
 // waves per workgroup for a level whose largest front is maxf
