@@ -183,9 +183,6 @@ struct pfr_solver {
   int fac_lds = -1;                     // PFR_FAC_LDS: which levels factor A11 in LDS (k_factor_sym_lds): n > 0
                                         // those whose largest pivot block has at least n pivots, 0 none, -1 auto
                                         // (default since round 3: 512-frequency sweeps +2.6 %, 4,096 unchanged)
-  int fac_wave = -1;                    // PFR_FAC_WAVE: A11 by one wave per frequency (k_factor_sym_wave): n > 0 the
-                                        // levels whose largest pivot block has n .. 64 pivots, 0 none, -1 auto
-                                        // (the levels PFR_FAC_LDS=-1 picks)
   int fac_lds_wg = 160;                 // PFR_FAC_LDS_WG: auto mode threshold (workgroups of k_factor_sym)
   int split_target = 256;               // PFR_SOLVE_SPLIT: solve launches with fewer (front, group) workgroups
                                         // than this (one per CU) split their update parts up to about this
@@ -297,15 +294,6 @@ bool level_lds(const pfr_solver* s, int l) {
                          : s->fac_lds < 0 && s->level_maxns[l] >= 16 && wgs < s->fac_lds_wg);
 }
 
-// A11 of level l by one wave per frequency (k_factor_sym_wave): PFR_FAC_WAVE = n > 0: the levels whose largest
-// pivot block has n .. FAC_WAVE_MAX pivots; -1: the levels of the auto LDS rule above; 0: none
-bool level_wave(const pfr_solver* s, int l) {
-  if (!s->sym || s->fac_wave == 0 || s->level_maxns[l] > pfr::FAC_WAVE_MAX) return false;
-  if (s->fac_wave > 0) return s->level_maxns[l] >= s->fac_wave;
-  const int64_t wgs = (int64_t)(s->level_ptr[l + 1] - s->level_ptr[l]) * (s->Fc / 64) * pfr::FAC_G;
-  return s->level_maxns[l] >= 16 && wgs < s->fac_lds_wg;
-}
-
 int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nvalid, hipStream_t st) {
   const int L = (int)s->level_ptr.size() - 1;
   const int ngroups = (int)(s->Fc / 64);
@@ -330,10 +318,7 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
                          s->d_asm_xp + s->asm_ptr[l] / 8, s->d_asm_x, ngroups, s->F, s->Fc, s->freqs, s->K, s->M,
                          data, ds, nvalid, st);
     mark(l, 1);
-    if (level_wave(s, l))
-      pfr::launch_factor_wave(s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_maxns[l], s->F, s->Fc, s->flags,
-                              st);
-    else if (level_lds(s, l))
+    if (level_lds(s, l))
       pfr::launch_factor_lds(s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_maxns[l], s->F, s->Fc, s->flags, st);
     else
       pfr::launch_factor(s->sym, s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st);
@@ -755,7 +740,6 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->us2_small = knob("PFR_US2_SMALL", 110, 0, pfr::MAX_FRONT);
   s->split_target = knob("PFR_SOLVE_SPLIT", 256, 0, 1 << 20);
   s->fac_lds = knob("PFR_FAC_LDS", -1, -1, 64);
-  s->fac_wave = knob("PFR_FAC_WAVE", -1, -1, pfr::FAC_WAVE_MAX);
   s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);
   s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);
   s->scale_corr = knob("PFR_SCALE_CORR", 1, 0, 1);

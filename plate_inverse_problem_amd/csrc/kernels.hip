@@ -636,144 +636,6 @@ __global__ __launch_bounds__(256) void k_factor_sym_lds(DevPattern P, const int*
 #undef E
 }
 
-// wave-uniform broadcast of lane l's value (l uniform)
-__device__ __forceinline__ double readlane_d(double v, int l) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
-}
-__device__ __forceinline__ cplx readlane_c(cplx v, int l) { return make_double2(readlane_d(v.x, l), readlane_d(v.y, l)); }
-
-// Orders one wave's LDS accesses across its lanes (the lanes of a wave exchange values through LDS without a
-// workgroup barrier: LDS operations of one wave complete in issue order; this keeps the compiler from moving
-// them across the exchange points)
-#define PFR_WAVE_SYNC()                                \
-  do {                                                 \
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); \
-    __builtin_amdgcn_wave_barrier();                   \
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront"); \
-  } while (0)
-
-// ------------------------------------------------------------------ K2a': symmetric A11 LU, one wave per frequency
-// A11 = L D L^T on the levels where the frequency-minor kernel gets few workgroups (the top of the tree: one or two
-// fronts of 16-64 pivots; it walks their pivots through global memory, a round trip per 4-pivot block phase behind
-// a workgroup barrier).  Here a workgroup is one front x WG consecutive frequencies and each WAVE owns one
-// frequency: its packed lower triangle of A11 (A(i, j) = sA[i (i + 1) / 2 + j]) sits in LDS, lane = row (RPL rows
-// per lane: lane + 64 r), and the factorisation runs without a workgroup barrier:
-//  * panel of each FAC_WB-pivot block: lane i holds A(i, k0 .. k0 + FAC_WB) in registers and the block's pivots are
-//    eliminated one at a time wave-synchronously, pivot values and the pivot rows' W entries broadcast by
-//    v_readlane;  L(i, p) goes to the triangle, W(i, t) = U(p, p) L(i, p) to a per-wave scratch (column-major:
-//    consecutive rows in consecutive banks);
-//  * trailing lower triangle: one entry (i, j) per lane at a time, A(i, j) -= sum_t L(i, k0 + t) W(j, t).
-// Global loads and stores are shared by the workgroup with the frequency fastest (WG x 16 B of each line per
-// access).  Entries written as k_factor_sym writes them: L11 below the diagonal, U(k, k) on it, U11 = diag(U) L11^T
-// above it (rounding differs from the frequency-minor kernels: the elimination order within a block).
-// Measured (2,048 frequencies): 2-3x slower than k_factor_sym on levels of tens to hundreds of fronts (a wave per
-// front-frequency, LDS-limited occupancy), ~30 % faster than the one-frequency LDS kernel on one- and two-front
-// levels.
-template <int WG, int RPL>
-__global__ __launch_bounds__(64 * WG) void k_factor_sym_wave(DevPattern P, const int* __restrict__ lvl,
-                                                            cplx* __restrict__ F, int64_t Fc, int* __restrict__ flags,
-                                                            int maxns) {
-  extern __shared__ cplx lds[];
-  const int per = maxns * (maxns + 1) / 2 + maxns * FAC_WB;   // wave_lds_entries(maxns)
-  const int ngq = (int)(Fc / WG);
-  const int64_t lid = xcd_swizzle(blockIdx.x, gridDim.x);
-  const int slot = (int)(lid / ngq);
-  const int64_t q0 = (lid % ngq) * WG;
-  const Front fr = P.fronts[lvl[slot]];
-  const int f = fr.f, ns = fr.ns, nlow = ns * (ns + 1) / 2;
-  cplx* __restrict__ base = F + fr.off * Fc + q0;
-  const int tid = threadIdx.x;
-#define E(a, b, qq) base[((int64_t)(a) * f + (b)) * Fc + (qq)]
-  {
-    // 1. the WG triangles: thread tid loads frequency tid % WG, UB entries in flight
-    constexpr int UB = 8;
-    const int qq = tid % WG;
-    cplx* __restrict__ sa = lds + qq * per;
-    for (int e0 = tid / WG; e0 < nlow; e0 += UB * 64) {
-      cplx v[UB];
-#pragma unroll
-      for (int u = 0; u < UB; ++u) {
-        const int e = min(e0 + u * 64, nlow - 1);
-        const int i = tri_row(e);
-        v[u] = E(i, e - i * (i + 1) / 2, qq);
-      }
-#pragma unroll
-      for (int u = 0; u < UB; ++u)
-        if (e0 + u * 64 < nlow) sa[e0 + u * 64] = v[u];
-    }
-  }
-  __syncthreads();
-  const int w = tid >> 6, lane = tid & 63;
-  cplx* __restrict__ sA = lds + w * per;
-  cplx* __restrict__ sW = sA + maxns * (maxns + 1) / 2;
-#define A(i, j) sA[((i) * ((i) + 1)) / 2 + (j)]
-  for (int k0 = 0; k0 < ns; k0 += FAC_WB) {
-    const int kb = min(FAC_WB, ns - k0), k1 = k0 + kb;
-    // 2. panel: rows >= k0 (rows outside [k0, ns) hold clamped copies that are never stored)
-    cplx a[RPL][FAC_WB];
-    int row[RPL];
-#pragma unroll
-    for (int r = 0; r < RPL; ++r) {
-      row[r] = lane + 64 * r;
-      const int ri = min(max(row[r], k0), ns - 1);
-#pragma unroll
-      for (int t = 0; t < FAC_WB; ++t) a[r][t] = A(ri, min(k0 + t, ri));
-    }
-#pragma unroll
-    for (int t = 0; t < FAC_WB; ++t) {
-      if (t < kb) {
-        const int p = k0 + t;
-        const cplx d = p < 64 ? readlane_c(a[0][t], p & 63) : readlane_c(a[RPL - 1][t], p & 63);
-        if (lane == 0) pivot_check(d, flags, q0 + w);
-        const cplx rd = crecip(d);
-        cplx b[FAC_WB];   // W(k0 + u, t): the pivot column's unscaled entries of the block rows below p
-#pragma unroll
-        for (int u = t + 1; u < FAC_WB; ++u)
-          b[u] = k0 + u < 64 ? readlane_c(a[0][t], (k0 + u) & 63) : readlane_c(a[RPL - 1][t], (k0 + u) & 63);
-#pragma unroll
-        for (int r = 0; r < RPL; ++r) {
-          const cplx wt = a[r][t], lt = cmul(wt, rd);
-#pragma unroll
-          for (int u = t + 1; u < FAC_WB; ++u) a[r][u] = cfms(a[r][u], lt, b[u]);
-          if (row[r] > p && row[r] < ns) {
-            A(row[r], p) = lt;
-            sW[t * maxns + row[r]] = wt;
-          } else if (row[r] == p) {
-            A(p, p) = d;
-          }
-        }
-      }
-    }
-    PFR_WAVE_SYNC();
-    // 3. trailing lower triangle (a short block is the last one: kb = FAC_WB whenever k1 < ns)
-    const int m = ns - k1, nt = m * (m + 1) / 2;
-    for (int e = lane; e < nt; e += 64) {
-      const int ii = tri_row(e), I = k1 + ii, J = k1 + e - ii * (ii + 1) / 2;
-      cplx v = A(I, J);
-#pragma unroll
-      for (int t = 0; t < FAC_WB; ++t) v = cfms(v, A(I, k0 + t), sW[t * maxns + J]);
-      A(I, J) = v;
-    }
-    PFR_WAVE_SYNC();
-  }
-  __syncthreads();
-  {
-    // 4. write back: L below the diagonal, U(k, k) on it, U(j, i) = U(j, j) L(i, j) above it
-    const int qq = tid % WG;
-    const cplx* __restrict__ sa = lds + qq * per;
-    for (int e = tid / WG; e < nlow; e += 64) {
-      const int i = tri_row(e), j = e - i * (i + 1) / 2;
-      const cplx v = sa[e];
-      E(i, j, qq) = v;
-      if (j < i) E(j, i, qq) = cmul(sa[j * (j + 1) / 2 + j], v);
-    }
-  }
-#undef A
-#undef E
-}
-
 // Off-diagonal panel blocks once A11 = L11 U11 is factored, every row of L21 and
 // every column of U12 independently (read once, written once):
 //   kind 0, row i >= ns:     L(i, :ns) = A(i, :ns) U11^{-1}
@@ -3046,25 +2908,6 @@ void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int max
   }();
   (void)attr;
   LAUNCH_DYN(k_factor_sym_lds<1>, dim3((unsigned)(nfronts * Fc)), dim3(256), lds, st, P, lvl, F, Fc, flags, maxns);
-}
-
-void launch_factor_wave(const DevPattern& P, const int* lvl, int nfronts, int maxns, double2* F, int64_t Fc,
-                        int* flags, hipStream_t st) {
-  const int wg = wave_group(maxns);
-  const size_t lds = (size_t)(wg * wave_lds_entries(maxns) * 16);
-  const unsigned grid = (unsigned)(nfronts * (Fc / wg));
-#define FW(WG, RPL)                                                                                              \
-  do {                                                                                                           \
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_factor_sym_wave<WG, RPL>), \
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES); \
-    (void)attr;                                                                                                  \
-    LAUNCH_DYN((k_factor_sym_wave<WG, RPL>), dim3(grid), dim3(64 * WG), lds, st, P, lvl, F, Fc, flags, maxns);    \
-  } while (0)
-  if (wg == 8) FW(8, 1);
-  else if (wg == 4) FW(4, 1);
-  else if (wg == 2) FW(2, 1);
-  else FW(1, 1);
-#undef FW
 }
 
 void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F,

@@ -40,10 +40,6 @@ void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, i
 // largest pivot block (sizes the dynamic LDS: (maxns (maxns + 1) / 2 + 4 maxns) x 16 B)
 void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int maxns, double2* F, int64_t Fc, int* flags,
                        hipStream_t st);
-// symmetric A11 LU, one wave per frequency (wave_group(maxns) frequencies of one front per workgroup, the
-// triangles in LDS); maxns <= FAC_WAVE_MAX
-void launch_factor_wave(const DevPattern& P, const int* lvl, int nfronts, int maxns, double2* F, int64_t Fc,
-                        int* flags, hipStream_t st);
 // L21 rows (and U12 columns in general mode) of a level's items; pipelined: the software-pipelined prefix
 // (symmetric, operator-form launches with few waves)
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,

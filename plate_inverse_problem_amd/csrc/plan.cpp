@@ -437,15 +437,6 @@ std::string check_plan(const Symbolic& S, const Plan& P, int64_t Fc, int split_t
   // A11 in LDS (k_factor_sym_lds) on the levels whose pivot blocks reach at most 64
   for (int l = 0; l < L; ++l)
     if (P.level_maxns[l] <= 64 && fac_lds_bytes(P.level_maxns[l]) > LDS_BYTES) return bad("A11 LDS", l, P.level_maxns[l], 64);
-  // A11 by one wave per frequency (k_factor_sym_wave) on the levels whose pivot blocks reach at most FAC_WAVE_MAX:
-  // the workgroup's triangles within the LDS, the frequencies of a chunk a whole number of workgroups
-  for (int l = 0; l < L; ++l) {
-    const int m = P.level_maxns[l];
-    if (m > FAC_WAVE_MAX) continue;
-    const int wg = wave_group(m);
-    if (wg * wave_lds_entries(m) * 16 > LDS_BYTES) return bad("A11 wave LDS", l, wg * wave_lds_entries(m) * 16, LDS_BYTES);
-    if (Fc % wg) return bad("A11 wave group", l, wg, Fc);
-  }
   // Dirichlet lists
   const Workspace W = workspace(S, Fc, P.n_crow);
   for (size_t d = 0; d < P.dir.size(); ++d)

@@ -42,8 +42,6 @@ constexpr int OFF_G = 1;
 constexpr int OFF_RPL = 2;
 constexpr int FAC_G = 2;                      // A11 LU: lane groups per wave (64 / FAC_G frequencies each)
 constexpr int MAX_FRONT = 1024;               // largest front the solve kernels stage index lists for in LDS
-constexpr int FAC_WB = 8;                     // k_factor_sym_wave pivot block (W columns per row)
-constexpr int FAC_WAVE_MAX = 64;              // largest pivot block k_factor_sym_wave takes (lane = row)
 constexpr int NKC = 5;                        // factorisation kernel classes: assembly, A11 LU, L21 rows, Schur
                                               // blocks, Schur tiles
 constexpr int FN_PARTS_HOST = 16;             // k_fn_dot partials per frequency group (kernels.hip: FN_PARTS)
@@ -57,14 +55,6 @@ inline int residual_parts(int n) { return (int)std::min<int64_t>((n + 3) / 4, 25
 inline int contract_eg_parts(int nent) { return ((nent + CEG_EW - 1) / CEG_EW + 3) / 4; }   // k_contract_eg grid
 // dynamic LDS of k_factor_sym_lds for a level whose largest pivot block is maxns
 inline int64_t fac_lds_bytes(int maxns) { return ((int64_t)maxns * (maxns + 1) / 2 + (int64_t)maxns * 4) * 16; }
-// k_factor_sym_wave: LDS entries per wave (packed lower triangle + W) and frequencies (waves) per workgroup -- as
-// many as keep two workgroups' triangles within 80 KiB
-inline int64_t wave_lds_entries(int maxns) { return (int64_t)maxns * (maxns + 1) / 2 + (int64_t)maxns * FAC_WB; }
-inline int wave_group(int maxns) {
-  for (int wg = 8; wg > 1; wg /= 2)
-    if (wg * wave_lds_entries(maxns) * 16 <= 80 * 1024) return wg;
-  return 1;
-}
 // waves per workgroup for a level whose largest front is maxf
 inline int waves_for(int maxf) { return std::max(1, std::min(8, (maxf + 23) / 24)); }
 // Workgroups per (front, frequency group) for the update part of a solve launch over nf fronts: 1 when the
