@@ -69,8 +69,10 @@ def test_c5_full_size_lbfgs_descends(c5):
 
 
 # 3x the largest relative error of the GPU loss against the extended-precision loss at the fixture's iterates
-# (measured: see the test's report line)
-C5_LOSS_RTOL = 3 * 2.0e-7
+# (measured round 5, gpurun_out/r5i_tests: 1.4e-7 / 3.7e-7 / 7.2e-8 / 6.9e-7 at the 4 iterates; the fp64 oracle
+# there 1.3e-7 / 1.1e-6 / 1.6e-6 / 3.6e-7).  The loss near the optimum (3.5e-5 of its start) is a mean of
+# squared small log-ratio differences, so its relative error is the fr error amplified ~10x.
+C5_LOSS_RTOL = 3 * 7.0e-7
 
 
 @pytest.mark.timeout(300)
