@@ -10,8 +10,8 @@ is the extended-precision fr at theta_true.
 
 Measure: relative max-norm error of the partials, ``max_k |w_k - w*_k| / max_k |w*_k|`` with
 ``w = sum_S w_f / |S|`` over a frequency set S, and the relative error of the loss and of the theta
-gradient.  Bound: the GPU partials within W_RTOL (6e-8) of the truth, or within twice the oracle's own
-error on the same set (asked for 2e-7).
+gradient.  Bound: the GPU partials, the theta gradient and the loss within W_RTOL / LOSS_RTOL (3e-8) of the
+truth, absolute (no allowance from the oracle's own error; VERDICT round 3 asked for 2e-7).
 
 C4 (BASELINE.json configs[3]): a rank of the 8-GPU run sweeps the 512-frequency block
 ``shard_range(4096, r, 8)``; a fresh engine sized for it takes the narrow-sweep path (1 lane, the
@@ -30,11 +30,12 @@ from helpers import make_problem, report
 pytestmark = pytest.mark.gpu
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-# gradient partials against the extended-precision truth (or 2x the oracle's error).  VERDICT round 3 asked for
-# 2e-7; with the solve-error scale of the cotangent (k_correct_finish) the GPU measures 1.2-2.5e-8 on every set
-# (profiles/r04), the oracle 0.9-2.7e-8, so the bound is 6e-8
-W_RTOL = 6e-8
-LOSS_RTOL = 1e-7
+# gradient partials against the extended-precision truth.  VERDICT round 3 asked for 2e-7; round 4 (the solve-error
+# scale of the cotangent) measured 1.2-2.5e-8 and bounded at 6e-8.  Round 5 (compensated correction residual)
+# measures partials 6.5e-9 .. 8.4e-9, theta gradient 4.3e-9 .. 1.6e-8, loss 5.9e-9 .. 7.3e-9 on every set
+# (gpurun_out/r5i_tests; the fp64 oracle: 0.9-2.7e-8), so both bounds are 3e-8, with no oracle allowance
+W_RTOL = 3e-8
+LOSS_RTOL = 3e-8
 FR_RTOL_C3 = 1e-7          # fr against c3_truth.npz (functional correction on, as in test_gpu_fullsize)
 
 
@@ -75,9 +76,9 @@ def _check_set(name, p, T, sel, theta):
     e = dict(w_gpu=_wrel(w, wt), w_oracle=_wrel(wo, wt), loss_gpu=abs(loss / lt - 1), loss_oracle=abs(lo / lt - 1),
              grad_gpu=_wrel(gg, gt), grad_oracle=_wrel(go, gt), n=sel.size)
     report(name, **e)
-    assert e["w_gpu"] <= max(W_RTOL, 2 * e["w_oracle"]), e
-    assert e["grad_gpu"] <= max(W_RTOL, 2 * e["grad_oracle"]), e
-    assert e["loss_gpu"] <= max(LOSS_RTOL, 2 * e["loss_oracle"]), e
+    assert e["w_gpu"] <= W_RTOL, e
+    assert e["grad_gpu"] <= W_RTOL, e
+    assert e["loss_gpu"] <= LOSS_RTOL, e
     return e
 
 
@@ -117,7 +118,7 @@ def test_c3_full_sweep_gradient_vs_truth(c3_fresh):
     go = np.real(T["w_oracle"].sum(0) / 4096 @ coeffs18_jacobian("orthotropic", p.geometry.height, theta))
     report("c3_grad_truth_api", grad_gpu=_wrel(x.grad.numpy(), gt), grad_oracle=_wrel(go, gt),
            loss_gpu=abs(val.item() / T["term_true"].mean() - 1))
-    assert _wrel(x.grad.numpy(), gt) <= max(W_RTOL, 2 * _wrel(go, gt))
+    assert _wrel(x.grad.numpy(), gt) <= W_RTOL
 
 
 def test_c4_rank_block_at_c3_size():
