@@ -1265,7 +1265,7 @@ __device__ __forceinline__ cplx rhs_staged(const RhsArgs& R, int p, double rv, i
 template <int RHS>
 __device__ __forceinline__ void gather_frontal(const DevPattern& P, const Front& fr, const RhsArgs& R,
                                                cplx* __restrict__ WV, int64_t Fc, const Ctx& c,
-                                               const int* __restrict__ reach) {
+                                               const int* __restrict__ reach, cplx* __restrict__ sv = nullptr) {
   __shared__ int s_ptr[MAX_FRONT + 1];
   __shared__ int s_src[GATHER_CAP];
   __shared__ int s_p[MAX_FRONT];
@@ -1284,6 +1284,7 @@ __device__ __forceinline__ void gather_frontal(const DevPattern& P, const Front&
         if (!reach || reach[P.row_front[src]]) v = cadd(v, WV[(int64_t)src * Fc + c.q]);
       }
       WV[(int64_t)r * Fc + c.q] = v;
+      if (sv && a < fr.ns) sv[a * 64 + c.lane] = v;
     }
     return;
   }
@@ -1315,6 +1316,7 @@ __device__ __forceinline__ void gather_frontal(const DevPattern& P, const Front&
       if (src >= 0) v = cadd(v, WV[(int64_t)src * Fc + c.q]);
     }
     WV[(int64_t)(fr.row0 + a) * Fc + c.q] = v;
+    if (sv && a < ns) sv[a * 64 + c.lane] = v;
   }
 }
 
@@ -1363,17 +1365,73 @@ __device__ __forceinline__ void lsolve_rows(const Front& fr, const cplx* __restr
 #undef V
 }
 
-template <int RHS>
+// NAR (the levels with few (front, group) workgroups, update rows split off): the pivot values resident in LDS
+// (sv, ns x 64) and each KBS block walked LEFT-looking -- the block's rows form their sums over the solved columns
+// (wave t row k0 + t: loads independent of the chain, solved values from LDS), then wave 0 solves the block's
+// triangle; the right-looking form below waits on a global round trip per row batch and per block (the top
+// levels of the bottom-up chain, ~35-100 us each at 2,048 frequencies).  Rounding differs from the default order.
+template <int RHS, bool NAR = false>
 __device__ __forceinline__ void lsolve_front(const DevPattern& P, const Front& fr, const cplx* __restrict__ F, int64_t Fc,
                                              cplx* __restrict__ WV, const RhsArgs& R, cplx* __restrict__ Y,
-                                             const int* __restrict__ reach, int rows_split, const Ctx& c) {
+                                             const int* __restrict__ reach, int rows_split, const Ctx& c,
+                                             cplx* __restrict__ sv = nullptr) {
   const int f = fr.f, ns = fr.ns;
   const cplx* __restrict__ base = F + fr.off * Fc + c.q;
   cplx* __restrict__ wv = WV + (int64_t)fr.row0 * Fc + c.q;
 #define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
 #define V(a) wv[(int64_t)(a) * Fc]
-  gather_frontal<RHS>(P, fr, R, WV, Fc, c, reach);
+  gather_frontal<RHS>(P, fr, R, WV, Fc, c, reach, NAR ? sv : nullptr);
   __syncthreads();
+  if (NAR) {
+#define SV(a) sv[(a) * 64 + c.lane]
+    for (int k0 = 0; k0 < ns; k0 += KBS) {
+      const int kb = min(KBS, ns - k0);
+      for (int t = c.w; t < kb; t += c.W) {
+        const int i = k0 + t;
+        cplx acc = make_double2(0.0, 0.0);
+        int j = 0;
+        for (; j + 4 <= k0; j += 4) {
+          cplx e[4], y[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            e[u] = E(i, j + u);
+            y[u] = SV(j + u);
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) acc = cfms(acc, e[u], y[u]);
+        }
+        for (; j < k0; ++j) acc = cfms(acc, E(i, j), SV(j));
+        SV(i) = cadd(SV(i), acc);
+      }
+      __syncthreads();
+      if (c.w == 0) {
+        cplx v[KBS];
+#pragma unroll
+        for (int t = 0; t < KBS; ++t) v[t] = SV(k0 + min(t, kb - 1));
+#pragma unroll
+        for (int i = 1; i < KBS; ++i) {
+          const int ri = k0 + min(i, kb - 1);
+#pragma unroll
+          for (int k = 0; k < i; ++k) v[i] = cfms(v[i], E(ri, k0 + min(k, kb - 1)), v[k]);
+        }
+#pragma unroll
+        for (int t = 0; t < KBS; ++t)
+          if (t < kb) SV(k0 + t) = v[t];
+      }
+      __syncthreads();
+    }
+    for (int a = c.w; a < ns; a += c.W) {
+      const cplx y = SV(a);
+      V(a) = y;
+      Y[(int64_t)(fr.col0 + a) * Fc + c.q] = y;
+    }
+#undef SV
+    if (!rows_split) {
+      __syncthreads();
+      lsolve_rows(fr, base, wv, Fc, ns + SRB * c.w, SRB * c.W);
+    }
+    return;
+  }
   for (int k0 = 0; k0 < ns; k0 += KBS) {
     const int kb = min(KBS, ns - k0), k1 = k0 + kb;
     if (c.w == 0) {
@@ -1431,14 +1489,15 @@ __global__ __launch_bounds__(512) void k_lsolve_level(DevPattern P, const int* _
 // that fr comes from  a_k^T x = (L^-1 a_k)^T diag(U)^-1 (L^-1 b)  without a top-down pass over the
 // support's fronts, and the adjoint's bottom-up result is a combination of the slices' (k_fn_combine).
 // Workgroups past a slice's front count return at once (the grid is sized for the largest slice).
-template <int RHS>
+template <int RHS, bool NAR = false>
 __global__ __launch_bounds__(512) void k_lsolve_level_z(DevPattern P, LSlices S, const cplx* __restrict__ F, int64_t Fc,
                                                         int rows_split) {
+  extern __shared__ cplx s_piv[];   // NAR: the pivot values (ns x 64)
   int bx;
   const Ctx c = ctx_xcd(bx);
   const int z = blockIdx.z;
   if (bx >= S.nf[z]) return;
-  lsolve_front<RHS>(P, P.fronts[S.lvl[z][bx]], F, Fc, S.WV[z], S.R[z], S.Y[z], S.reach[z], rows_split, c);
+  lsolve_front<RHS, NAR>(P, P.fronts[S.lvl[z][bx]], F, Fc, S.WV[z], S.R[z], S.Y[z], S.reach[z], rows_split, c, s_piv);
 }
 
 // Update rows of the L solve at the top levels, split over S workgroups per (front, frequency group)
@@ -1792,6 +1851,98 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
   __syncthreads();
   usolve2_tri(fr, base, Fc, c, act, Xs);
+}
+
+// The paired top-down pass's pivot blocks on the levels with few (front, group) workgroups -- the top of the tree,
+// after the split update part (k_usolve2_upd) -- with the pivot values resident in LDS.  k_usolve2_level walks a
+// pivot block right-looking: per KBS block, wave 0 solves the diagonal block from global memory, then every wave
+// updates its rows above with a loop whose iterations each wait for their own loads, so a 40-pivot block costs ~20
+// dependent global round trips (26-54 us per level at 2,048 frequencies, the whole pass's top is latency).  Here the
+// block is walked LEFT-looking with the values in LDS (2 vectors x ns x 64 frequencies): for each KBS block (from the
+// bottom), wave t forms row k0 + t's sum over the columns already solved (its U loads all independent of the chain,
+// the solved values read from LDS), then wave 0 solves the block's triangle.  Two barriers and about two global
+// latencies per block.  The operations per value are those of k_usolve2_level in another order (rounding differs).
+constexpr int US2_NAR_W = KBS;   // waves per workgroup: wave t owns row k0 + t of each block
+__global__ __launch_bounds__(64 * US2_NAR_W) void k_usolve2_nar(DevPattern P, const int* __restrict__ lvl,
+                                                               const cplx* __restrict__ F, int64_t Fc, UPair A,
+                                                               UPair B) {
+  extern __shared__ cplx sX[];   // [2][ns][64]
+  int bx;
+  const Ctx c = ctx_xcd(bx);
+  const int ft = lvl[bx];
+  const bool act[2] = {!A.skip || !A.skip[ft], !B.skip || !B.skip[ft]};
+  cplx* const Xs[2] = {A.X, B.X};
+  const Front fr = P.fronts[ft];
+  const int f = fr.f, ns = fr.ns;
+  const cplx* __restrict__ base = F + fr.off * Fc + c.q;
+#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+#define SX(v, a) sX[((v) * ns + (a)) * 64 + c.lane]
+#define XV(v, a) Xs[v][(int64_t)(fr.col0 + (a)) * Fc + c.q]
+  // the pivot values y_a + U12(a, :) x_upd the update part left in X
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+    if (act[v])
+      for (int a = c.w; a < ns; a += c.W) SX(v, a) = XV(v, a);
+  __syncthreads();
+  for (int k1 = ns; k1 > 0; k1 -= KBS) {
+    const int k0 = max(0, k1 - KBS), kb = k1 - k0;
+    if (c.w < kb) {
+      // row i of the block: minus its sum over the solved columns k1 .. ns
+      const int i = k0 + c.w;
+      cplx acc[2] = {make_double2(0.0, 0.0), make_double2(0.0, 0.0)};
+      int j = k1;
+      for (; j + 4 <= ns; j += 4) {
+        cplx e[4], x[2][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) e[u] = E(i, j + u);
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) x[v][u] = SX(v, j + u);   // inactive: unused
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) acc[v] = cfms(acc[v], e[u], x[v][u]);
+      }
+      for (; j < ns; ++j) {
+        const cplx e = E(i, j);
+#pragma unroll
+        for (int v = 0; v < 2; ++v) acc[v] = cfms(acc[v], e, SX(v, j));
+      }
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+        if (act[v]) SX(v, i) = cadd(SX(v, i), acc[v]);
+    }
+    __syncthreads();
+    if (c.w == 0) {
+      // the block's triangle (usolve2_tri's diagonal block)
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+        if (act[v]) {
+          cplx x[KBS];
+#pragma unroll
+          for (int t = 0; t < KBS; ++t) x[t] = SX(v, k0 + min(t, kb - 1));
+#pragma unroll
+          for (int i = KBS - 1; i >= 0; --i) {
+            const int ri = k0 + min(i, kb - 1);
+#pragma unroll
+            for (int k = i + 1; k < KBS; ++k) x[i] = cfms(x[i], E(ri, k0 + min(k, kb - 1)), x[k]);
+            x[i] = cscale(cmul(x[i], crecip(E(ri, ri))), i < kb ? 1.0 : 0.0);
+          }
+#pragma unroll
+          for (int t = 0; t < KBS; ++t)
+            if (t < kb) SX(v, k0 + t) = x[t];
+        }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+    if (act[v])
+      for (int a = c.w; a < ns; a += c.W) XV(v, a) = SX(v, a);
+#undef E
+#undef SX
+#undef XV
 }
 
 // The paired top-down pass on levels of tiny fronts (every pivot block <= NSM): ONE WAVE per (front, frequency
@@ -2977,7 +3128,8 @@ void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const 
 
 void launch_lsolve_multi(int rhs_mode, const DevPattern& P, int nslices, const int* const* lvl, const int* nf, int W,
                          int ngroups, const double2* F, int64_t Fc, double2* const* WV, const RhsDesc* rd,
-                         double2* const* Y, const int* const* reach, hipStream_t st, int split) {
+                         double2* const* Y, const int* const* reach, hipStream_t st, int split, bool nar,
+                         int maxns) {
   LSlices S{};
   int nmax = 0;
   for (int z = 0; z < nslices; ++z) {
@@ -2992,7 +3144,18 @@ void launch_lsolve_multi(int rhs_mode, const DevPattern& P, int nslices, const i
   if (nmax <= 0) return;
   const dim3 g(nmax, ngroups, nslices), b(64 * W);
   const int rs = split > 1;
-  if (rhs_mode == 0) LAUNCH(k_lsolve_level_z<0>, g, b, st, P, S, F, Fc, rs);
+  if (rs && nar) {
+    static const bool attr = [] {
+      return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lsolve_level_z<0, true>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)LS_NAR_DYN_MAX) == hipSuccess &&
+             hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lsolve_level_z<3, true>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)LS_NAR_DYN_MAX) == hipSuccess;
+    }();
+    (void)attr;
+    const size_t lds = (size_t)maxns * 64 * 16;
+    if (rhs_mode == 0) LAUNCH_DYN((k_lsolve_level_z<0, true>), g, b, lds, st, P, S, F, Fc, rs);
+    else LAUNCH_DYN((k_lsolve_level_z<3, true>), g, b, lds, st, P, S, F, Fc, rs);
+  } else if (rhs_mode == 0) LAUNCH(k_lsolve_level_z<0>, g, b, st, P, S, F, Fc, rs);
   else LAUNCH(k_lsolve_level_z<3>, g, b, st, P, S, F, Fc, rs);
   if (rs) LAUNCH(k_lsolve_rows_z, dim3(nmax * split, ngroups, nslices), dim3(64 * SPLIT_W), st, P, S, F, Fc, split);
 }
@@ -3016,7 +3179,8 @@ void launch_fn_combine(const int* rows, int nrows, const double2* fcoef, double2
 
 void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, bool small, int ngroups,
                     const double2* F, int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0,
-                    const double2* Y1, double2* X1, const int* reach1, hipStream_t st, int split, int tiny) {
+                    const double2* Y1, double2* X1, const int* reach1, hipStream_t st, int split, int tiny,
+                    bool nar, int maxns) {
   if (nfronts <= 0) return;
   UPair a{Y0, X0, reach0, skip0}, b{Y1, X1, reach1, nullptr};
   if (tiny > 0 && split <= 1) {
@@ -3034,7 +3198,12 @@ void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, boo
   // symmetric mode only (the paired top-down pass serves the symmetric loss + gradient sweep).  Small-front levels:
   // 8 pivot rows per pass share each gathered update-row value, 2 values per chunk, 3 waves/SIMD (18 % less traffic
   // than 2 rows x 4 values at 4 waves/SIMD, the same time: profiles/r04/solve_traffic/)
-  if (small) LAUNCH((k_usolve2_level<true, 8, 2, 3>), g, bl, st, P, lvl, F, Fc, a, b, rs);
+  if (rs && nar) {
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_usolve2_nar),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES);
+    (void)attr;
+    LAUNCH_DYN(k_usolve2_nar, g, dim3(64 * US2_NAR_W), (size_t)us2_nar_lds(maxns), st, P, lvl, F, Fc, a, b);
+  } else if (small) LAUNCH((k_usolve2_level<true, 8, 2, 3>), g, bl, st, P, lvl, F, Fc, a, b, rs);
   else LAUNCH((k_usolve2_level<true, 4, 8, 2>), g, bl, st, P, lvl, F, Fc, a, b, rs);
 }
 

@@ -65,7 +65,8 @@ void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const 
 // lvl[z][0 .. nf[z]), its work vectors WV[z], rhs rd[z] (rhs_mode 0 or 3 for every slice), solution Y[z])
 void launch_lsolve_multi(int rhs_mode, const DevPattern& P, int nslices, const int* const* lvl, const int* nf, int W,
                          int ngroups, const double2* F, int64_t Fc, double2* const* WV, const RhsDesc* rd,
-                         double2* const* Y, const int* const* reach, hipStream_t st, int split);
+                         double2* const* Y, const int* const* reach, hipStream_t st, int split, bool nar = false,
+                         int maxns = 0);   // nar (split > 1): pivot blocks in LDS (k_lsolve_level_z<., true>)
 // functional from the bottom-up passes: partial dot products (FN_PARTS x 3 x Fc), the functional / loss
 // / cotangent from them (fcoef: 3 x Fc, G at the support rows), and L^-1 g = sum_k c_k L^-1 a_k in Yk[0]
 void launch_fn_dot(const int2* rows, int nrows, const double2* F, const double2* Yb, const double2* const* Yk, int64_t Fc,
@@ -78,7 +79,8 @@ void launch_fn_combine(const int* rows, int nrows, const double2* fcoef, double2
 void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, bool small, int ngroups,
                     const double2* F, int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0,
                     const double2* Y1, double2* X1, const int* reach1, hipStream_t st, int split = 1,
-                    int tiny = 0);    // tiny 4 / 8: the level's pivot blocks all <= tiny (k_usolve2_tiny)
+                    int tiny = 0,     // tiny 4 / 8: the level's pivot blocks all <= tiny (k_usolve2_tiny)
+                    bool nar = false, int maxns = 0);   // nar (split > 1): pivot blocks in LDS (k_usolve2_nar)
 // Hessian sweep: tangent right-hand sides (rows of the permuted matrix, or of its
 // transpose with accumulate = 1) and the directional derivative of the loss cotangent
 void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nrows, const double2* Kd,
