@@ -290,13 +290,11 @@ int solve_split(const pfr_solver* s, int nf) { return pfr::solve_split(nf, s->Fc
 // top of the tree in small chunks: 512 frequencies levels 10-16, 2,048 level 16 -- faster per level there, slower
 // elsewhere; the default since the MMD ordering: 512-frequency sweeps 31.8k -> 32.6k freq-solves/s, 4,096
 // unchanged)
-// and, in auto mode, the levels whose pivot blocks exceed 64 pivots (up to FAC_LDS_MAX): the global-memory kernel's
-// chain of 4-pivot blocks is longest there (2,048 frequencies, C3 level 25, 76 pivots: 0.60 ms)
 bool level_lds(const pfr_solver* s, int l) {
   const int64_t wgs = (int64_t)(s->level_ptr[l + 1] - s->level_ptr[l]) * (s->Fc / 64) * pfr::FAC_G;
-  const int m = s->level_maxns[l];
-  return s->sym && m <= pfr::FAC_LDS_MAX &&
-         (s->fac_lds > 0 ? m >= s->fac_lds : s->fac_lds < 0 && ((m >= 16 && wgs < s->fac_lds_wg) || m > 64));
+  return s->sym && s->level_maxns[l] <= 64 &&
+         (s->fac_lds > 0 ? s->level_maxns[l] >= s->fac_lds
+                         : s->fac_lds < 0 && s->level_maxns[l] >= 16 && wgs < s->fac_lds_wg);
 }
 
 int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nvalid, hipStream_t st) {
@@ -747,7 +745,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->us2_small = knob("PFR_US2_SMALL", 110, 0, pfr::MAX_FRONT);
   s->split_target = knob("PFR_SOLVE_SPLIT", 256, 0, 1 << 20);
   s->us2_nar = knob("PFR_US2_NAR", 1, 0, 1);
-  s->fac_lds = knob("PFR_FAC_LDS", -1, -1, pfr::FAC_LDS_MAX);
+  s->fac_lds = knob("PFR_FAC_LDS", -1, -1, 64);
   s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);
   s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);
   s->scale_corr = knob("PFR_SCALE_CORR", 1, 0, 1);

@@ -434,10 +434,9 @@ std::string check_plan(const Symbolic& S, const Plan& P, int64_t Fc, int split_t
     if (P.tile_ptr[l] > P.tile_ptr[l + 1] || P.blk_ptr[l] > P.blk_ptr[l + 1] || P.item_ptr[l] > P.item_ptr[l + 1] ||
         P.asm_ptr[l] > P.asm_ptr[l + 1])
       return bad("level range order", l, P.tile_ptr[l], P.tile_ptr[l + 1]);
-  // A11 in LDS (k_factor_sym_lds) on the levels whose pivot blocks reach at most FAC_LDS_MAX
+  // A11 in LDS (k_factor_sym_lds) on the levels whose pivot blocks reach at most 64
   for (int l = 0; l < L; ++l)
-    if (P.level_maxns[l] <= FAC_LDS_MAX && fac_lds_bytes(P.level_maxns[l]) > LDS_BYTES)
-      return bad("A11 LDS", l, P.level_maxns[l], FAC_LDS_MAX);
+    if (P.level_maxns[l] <= 64 && fac_lds_bytes(P.level_maxns[l]) > LDS_BYTES) return bad("A11 LDS", l, P.level_maxns[l], 64);
   // Dirichlet lists
   const Workspace W = workspace(S, Fc, P.n_crow);
   for (size_t d = 0; d < P.dir.size(); ++d)

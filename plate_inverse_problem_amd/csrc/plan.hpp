@@ -42,7 +42,6 @@ constexpr int OFF_G = 1;
 constexpr int OFF_RPL = 2;
 constexpr int FAC_G = 2;                      // A11 LU: lane groups per wave (64 / FAC_G frequencies each)
 constexpr int MAX_FRONT = 1024;               // largest front the solve kernels stage index lists for in LDS
-constexpr int FAC_LDS_MAX = 96;               // largest pivot block k_factor_sym_lds takes (its triangle: 81 KB)
 constexpr int NKC = 5;                        // factorisation kernel classes: assembly, A11 LU, L21 rows, Schur
                                               // blocks, Schur tiles
 constexpr int FN_PARTS_HOST = 16;             // k_fn_dot partials per frequency group (kernels.hip: FN_PARTS)
