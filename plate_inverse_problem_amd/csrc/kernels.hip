@@ -1333,6 +1333,39 @@ constexpr int SRB = 4, SKC = 8;
 // 16-pivot block cost ~130 dependent memory round trips (~85 us) instead of a few.
 
 
+// acc_v -= sum_{j0 <= j < j1} E(i, j) x_v(j): one factor row (erow = &E(i, 0), column stride Fc) against NV vectors
+// resident in LDS (sx[v] + 64 j); the next 8 columns' loads are issued before the current 8 columns' products
+// (the narrow-level solves: their loop otherwise waits on every batch)
+template <int NV>
+__device__ __forceinline__ void dot_row_lds(cplx (&acc)[NV], const cplx* __restrict__ erow, int64_t Fc,
+                                            const cplx* const (&sx)[NV], int j0, int j1) {
+  constexpr int U = 8;
+  if (j0 >= j1) return;
+  cplx ea[U], eb[U];
+  auto ld = [&](cplx (&e)[U], int j) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) e[u] = erow[(int64_t)min(j + u, j1 - 1) * Fc];
+  };
+  auto fm = [&](const cplx (&e)[U], int j) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int jj = min(j + u, j1 - 1);
+      const cplx eu = cscale(e[u], j + u < j1 ? 1.0 : 0.0);
+#pragma unroll
+      for (int v = 0; v < NV; ++v) acc[v] = cfms(acc[v], eu, sx[v][jj * 64]);
+    }
+  };
+  ld(ea, j0);
+  int j = j0;
+  for (; j + U < j1; j += 2 * U) {
+    ld(eb, j + U);
+    fm(ea, j);
+    if (j + 2 * U < j1) ld(ea, j + 2 * U);
+    fm(eb, j + U);
+  }
+  if (j < j1) fm(ea, j);
+}
+
 // V(i) -= L21(i, :) y for the update rows i = i_begin, i_begin + i_step, ... (SRB rows per step; y = the
 // pivot part of the frontal vector, already solved)
 __device__ __forceinline__ void lsolve_rows(const Front& fr, const cplx* __restrict__ base, cplx* __restrict__ wv,
@@ -1388,20 +1421,10 @@ __device__ __forceinline__ void lsolve_front(const DevPattern& P, const Front& f
       const int kb = min(KBS, ns - k0);
       for (int t = c.w; t < kb; t += c.W) {
         const int i = k0 + t;
-        cplx acc = make_double2(0.0, 0.0);
-        int j = 0;
-        for (; j + 4 <= k0; j += 4) {
-          cplx e[4], y[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            e[u] = E(i, j + u);
-            y[u] = SV(j + u);
-          }
-#pragma unroll
-          for (int u = 0; u < 4; ++u) acc = cfms(acc, e[u], y[u]);
-        }
-        for (; j < k0; ++j) acc = cfms(acc, E(i, j), SV(j));
-        SV(i) = cadd(SV(i), acc);
+        cplx acc[1] = {make_double2(0.0, 0.0)};
+        const cplx* const sx[1] = {sv + c.lane};
+        dot_row_lds<1>(acc, base + (int64_t)i * f * Fc, Fc, sx, 0, k0);
+        SV(i) = cadd(SV(i), acc[0]);
       }
       __syncthreads();
       if (c.w == 0) {
@@ -1890,25 +1913,8 @@ __global__ __launch_bounds__(64 * US2_NAR_W) void k_usolve2_nar(DevPattern P, co
       // row i of the block: minus its sum over the solved columns k1 .. ns
       const int i = k0 + c.w;
       cplx acc[2] = {make_double2(0.0, 0.0), make_double2(0.0, 0.0)};
-      int j = k1;
-      for (; j + 4 <= ns; j += 4) {
-        cplx e[4], x[2][4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) e[u] = E(i, j + u);
-#pragma unroll
-        for (int v = 0; v < 2; ++v)
-#pragma unroll
-          for (int u = 0; u < 4; ++u) x[v][u] = SX(v, j + u);   // inactive: unused
-#pragma unroll
-        for (int v = 0; v < 2; ++v)
-#pragma unroll
-          for (int u = 0; u < 4; ++u) acc[v] = cfms(acc[v], e[u], x[v][u]);
-      }
-      for (; j < ns; ++j) {
-        const cplx e = E(i, j);
-#pragma unroll
-        for (int v = 0; v < 2; ++v) acc[v] = cfms(acc[v], e, SX(v, j));
-      }
+      const cplx* const sx[2] = {sX + c.lane, sX + (int64_t)ns * 64 + c.lane};   // inactive vector: unused
+      dot_row_lds<2>(acc, base + (int64_t)i * f * Fc, Fc, sx, k1, ns);
 #pragma unroll
       for (int v = 0; v < 2; ++v)
         if (act[v]) SX(v, i) = cadd(SX(v, i), acc[v]);
