@@ -679,14 +679,14 @@ __device__ __forceinline__ cplx off_source(const OffSrc& S, const cplx* __restri
 // One chunk of NB consecutive columns (kind 0) / rows (kind 1) c0 .. c0+NB-1 of
 // this lane's OFF_RPL rows (columns); the shared L11 / U11 values each step loads
 // serve all of them.
-template <int MODE, int NB, bool PRE = true, int PU = 2, int R = OFF_RPL>
-__device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int64_t (&so)[R], int64_t sc,
-                                              int64_t sa, int64_t sb, bool unit, const bool (&valid)[R],
+template <int MODE, int NB, bool PRE = true, int PU = 2>
+__device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int64_t (&so)[OFF_RPL], int64_t sc,
+                                              int64_t sa, int64_t sb, bool unit, const bool (&valid)[OFF_RPL],
                                               int c0, const OffSrc& S, const cplx* __restrict__ F, int64_t Fc,
                                               int64_t q) {
-  cplx x[R][NB];
+  cplx x[OFF_RPL][NB];
 #pragma unroll
-  for (int h = 0; h < R; ++h)
+  for (int h = 0; h < OFF_RPL; ++h)
 #pragma unroll
     for (int j = 0; j < NB; ++j) x[h][j] = off_source<MODE>(S, F, Fc, q, h, c0 + j);
   for (int e = S.ox0; e < S.ox1; ++e) {       // rare: several children cover one entry
@@ -695,7 +695,7 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
     if (c >= 0 && c < NB) {
       const cplx v = F[(int64_t)g.y * Fc + q];
 #pragma unroll
-      for (int h = 0; h < R; ++h)
+      for (int h = 0; h < OFF_RPL; ++h)
         if (slot == S.slot0 + OFF_G * h) {
 #pragma unroll
           for (int j = 0; j < NB; ++j)
@@ -709,16 +709,16 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
     // software-pipelined prefix: pivot t + 1's loads are issued before pivot t's products, so the products wait
     // only for the older loads (the compiler's s_waitcnt then counts the younger ones) -- two pivots' loads in
     // flight instead of the plain loop's drain at every iteration; same products, same order
-    cplx la[R], ua[NB], lb[R], ub[NB];
-    auto ld = [&](cplx (&l)[R], cplx (&u)[NB], int t) {
+    cplx la[OFF_RPL], ua[NB], lb[OFF_RPL], ub[NB];
+    auto ld = [&](cplx (&l)[OFF_RPL], cplx (&u)[NB], int t) {
 #pragma unroll
-      for (int h = 0; h < R; ++h) l[h] = base[(so[h] + (int64_t)t * sc) * Fc];
+      for (int h = 0; h < OFF_RPL; ++h) l[h] = base[(so[h] + (int64_t)t * sc) * Fc];
 #pragma unroll
       for (int j = 0; j < NB; ++j) u[j] = base[((int64_t)t * sa + (int64_t)(c0 + j) * sb) * Fc];
     };
-    auto fm = [&](const cplx (&l)[R], const cplx (&u)[NB]) {
+    auto fm = [&](const cplx (&l)[OFF_RPL], const cplx (&u)[NB]) {
 #pragma unroll
-      for (int h = 0; h < R; ++h)
+      for (int h = 0; h < OFF_RPL; ++h)
 #pragma unroll
         for (int j = 0; j < NB; ++j) x[h][j] = cfms(x[h][j], l[h], u[j]);
     };
@@ -735,13 +735,13 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
   }
 #pragma unroll 2
   for (int t = t0; t < (PRE ? c0 : 0); ++t) {
-    cplx l[R], u[NB];
+    cplx l[OFF_RPL], u[NB];
 #pragma unroll
-    for (int h = 0; h < R; ++h) l[h] = base[(so[h] + (int64_t)t * sc) * Fc];
+    for (int h = 0; h < OFF_RPL; ++h) l[h] = base[(so[h] + (int64_t)t * sc) * Fc];
 #pragma unroll
     for (int j = 0; j < NB; ++j) u[j] = base[((int64_t)t * sa + (int64_t)(c0 + j) * sb) * Fc];
 #pragma unroll
-    for (int h = 0; h < R; ++h)
+    for (int h = 0; h < OFF_RPL; ++h)
 #pragma unroll
       for (int j = 0; j < NB; ++j) x[h][j] = cfms(x[h][j], l[h], u[j]);
   }
@@ -753,16 +753,16 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
       if (a < j) {
         const cplx t = base[((int64_t)(c0 + a) * sa + (int64_t)(c0 + j) * sb) * Fc];
 #pragma unroll
-        for (int h = 0; h < R; ++h) x[h][j] = cfms(x[h][j], x[h][a], t);
+        for (int h = 0; h < OFF_RPL; ++h) x[h][j] = cfms(x[h][j], x[h][a], t);
       }
     if (!unit) {
       const cplx d = crecip(base[((int64_t)(c0 + j) * (sa + sb)) * Fc]);
 #pragma unroll
-      for (int h = 0; h < R; ++h) x[h][j] = cmul(x[h][j], d);
+      for (int h = 0; h < OFF_RPL; ++h) x[h][j] = cmul(x[h][j], d);
     }
   }
 #pragma unroll
-  for (int h = 0; h < R; ++h)
+  for (int h = 0; h < OFF_RPL; ++h)
     if (valid[h]) {
 #pragma unroll
       for (int j = 0; j < NB; ++j) base[(so[h] + (int64_t)(c0 + j) * sc) * Fc] = x[h][j];
@@ -780,13 +780,13 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
 // load chain, which more resident waves overlap.
 // One item (OFF_G OFF_RPL rows / columns of a front) of the panel for the frequency group `by`: the wave's
 // own work, no barrier
-template <int MODE, bool SMALL, int PU = 2, int R = OFF_RPL>
+template <int MODE, bool SMALL, int PU = 2>
 __device__ __forceinline__ void offdiag_item(const DevPattern& P, const int4* __restrict__ items, int wid,
                                              const int2* __restrict__ orec, const int* __restrict__ oxp,
                                              const int2* __restrict__ ox, cplx* __restrict__ F, int64_t Fc,
                                              const double* __restrict__ freqs, const cplx* __restrict__ K,
                                              const double* __restrict__ M, const cplx* __restrict__ data,
-                                             int64_t data_stride, int nvalid, int by, int hsel = 0) {
+                                             int64_t data_stride, int nvalid, int by) {
   const int lane = threadIdx.x & 63;
   constexpr int QG = 64 / OFF_G;                  // frequencies per lane group
   const int sub = lane / QG;
@@ -800,22 +800,21 @@ __device__ __forceinline__ void offdiag_item(const DevPattern& P, const int4* __
   const int64_t sc = it.z == 0 ? 1 : f;
   const int64_t sa = it.z == 0 ? f : 1, sb = it.z == 0 ? 1 : f;  // shared (a, b) at a * sa + b * sb
   const bool unit = it.z != 0;                                   // L11 has a unit diagonal
-  // R < OFF_RPL: this wave takes the item's rows hsel .. hsel + R - 1 only (more waves per item)
   OffSrc S;
-  int64_t so[R];
-  bool valid[R];
+  int64_t so[OFF_RPL];
+  bool valid[OFF_RPL];
 #pragma unroll
-  for (int h = 0; h < R; ++h) {
-    const int idx = it.y + OFF_G * (h + hsel) + sub;
+  for (int h = 0; h < OFF_RPL; ++h) {
+    const int idx = it.y + OFF_G * h + sub;
     valid[h] = idx < f;
     const int r = min(idx, f - 1);
     so[h] = it.z == 0 ? (int64_t)r * f : r;                      // own element c at so + c * sc
-    S.rec[h] = orec + it.w + (int64_t)(OFF_G * (h + hsel) + sub) * ns;
+    S.rec[h] = orec + it.w + (int64_t)(OFF_G * h + sub) * ns;
   }
   S.ox = ox;
   S.ox0 = oxp[wid];
   S.ox1 = oxp[wid + 1];
-  S.slot0 = OFF_G * hsel + sub;
+  S.slot0 = sub;
   S.om2 = 0.0;
   if (MODE == 0) {
     const double om = 6.283185307179586 * freqs[q];
@@ -827,7 +826,7 @@ __device__ __forceinline__ void offdiag_item(const DevPattern& P, const int4* __
   if (SMALL) {
     switch (ns) {
 #define SMALLC(n) \
-  case n: offdiag_chunk<MODE, n, false, 2, R>(base, so, sc, sa, sb, unit, valid, 0, S, F, Fc, q); break;
+  case n: offdiag_chunk<MODE, n, false>(base, so, sc, sa, sb, unit, valid, 0, S, F, Fc, q); break;
       SMALLC(1) SMALLC(2) SMALLC(3) SMALLC(4) SMALLC(5) SMALLC(6) SMALLC(7) SMALLC(8)
 #undef SMALLC
       default: break;
@@ -835,10 +834,10 @@ __device__ __forceinline__ void offdiag_item(const DevPattern& P, const int4* __
     return;
   }
   int c0 = 0;
-  for (; c0 + OB <= ns; c0 += OB) offdiag_chunk<MODE, OB, true, PU, R>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q);
+  for (; c0 + OB <= ns; c0 += OB) offdiag_chunk<MODE, OB, true, PU>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q);
   switch (ns - c0) {     // wave-uniform tail width
 #define TAIL(n) \
-  case n: offdiag_chunk<MODE, n, true, PU, R>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q); break;
+  case n: offdiag_chunk<MODE, n, true, PU>(base, so, sc, sa, sb, unit, valid, c0, S, F, Fc, q); break;
     TAIL(1) TAIL(2) TAIL(3) TAIL(4) TAIL(5) TAIL(6) TAIL(7)
 #undef TAIL
     default: break;
@@ -846,23 +845,17 @@ __device__ __forceinline__ void offdiag_item(const DevPattern& P, const int4* __
 }
 
 // XCD-aware order: a frequency group's items on one XCD, sharing its L2
-// R = 1 (launches with few waves): two waves per item, one row each -- twice the waves on the narrow levels, each
-// U11 value loaded once per row instead of once per two rows
-template <int MODE, bool SMALL, int PU = 2, int R = OFF_RPL>
+template <int MODE, bool SMALL, int PU = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMALL ? 5 : 1))) void k_offdiag_level(
     DevPattern P, const int4* __restrict__ items, int nitems, const int2* __restrict__ orec, const int* __restrict__ oxp,
     const int2* __restrict__ ox, cplx* __restrict__ F, int64_t Fc, const double* __restrict__ freqs,
     const cplx* __restrict__ K, const double* __restrict__ M, const cplx* __restrict__ data, int64_t data_stride,
     int nvalid) {
-  static_assert(OFF_RPL % R == 0, "waves per item");
   const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
   const int bx = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
-  const int wv = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
-  constexpr int WPI = OFF_RPL / R;                  // waves per item
-  const int wid = wv / WPI, hsel = (wv % WPI) * R;
+  const int wid = __builtin_amdgcn_readfirstlane(bx * (blockDim.x >> 6) + (threadIdx.x >> 6));
   if (wid < nitems)
-    offdiag_item<MODE, SMALL, PU, R>(P, items, wid, orec, oxp, ox, F, Fc, freqs, K, M, data, data_stride, nvalid, by,
-                                     hsel);
+    offdiag_item<MODE, SMALL, PU>(P, items, wid, orec, oxp, ox, F, Fc, freqs, K, M, data, data_stride, nvalid, by);
 }
 
 // ------------------------------------------------------------------ K2b: Schur complement
@@ -3082,22 +3075,12 @@ void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, i
 
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
                     const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,
-                    const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st, bool pipelined,
-                    bool one_row) {
+                    const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st, bool pipelined) {
   if (nitems <= 0) return;
   const bool small = maxns <= 8;
   dim3 g((nitems + 3) / 4, ngroups * OFF_G), b(256);
   static_assert(OB >= 8, "the SMALL variant covers pivot blocks of up to 8");
 #define OL(MD, SM, PU) LAUNCH((k_offdiag_level<MD, SM, PU>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid)
-  // one_row: a wave per row (symmetric operator form, launches with few waves)
-  if (mode == 0 && !small && one_row) {
-    const dim3 g1((nitems * OFF_RPL + 3) / 4, ngroups * OFF_G);
-    if (pipelined)
-      LAUNCH((k_offdiag_level<0, false, 3, 1>), g1, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid);
-    else
-      LAUNCH((k_offdiag_level<0, false, 2, 1>), g1, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid);
-    return;
-  }
   // pipelined: the prefix loop with the next pivot's loads issued before the current pivot's products (the
   // narrow levels, where few waves are resident)
   if (mode == 0 && small) OL(0, true, 2);
