@@ -204,16 +204,10 @@ PFR_API int pfr_set_functional(pfr_solver* s, int32_t n_support, const int32_t* 
                                const double* a_host /* 3 x n_support: aU, aV, aW */, double ts);
 /* nfreq frequencies [Hz] (device).  loss_type PFR_LOSS_NONE: forward only (fr_dev).  Otherwise ref_dev
  * (complex nfreq) and the reverse pass: loss_dev[0] += sum of terms * scale ... (raw sum, unscaled),
- * w_dev (complex n_stiff) += gradient partials.  fr_dev / loss_dev / w_dev / flags_dev may be NULL.
- * A single-chunk sweep (nfreq <= max batch) that repeats the previous call's shape, modes and solver state
- * (no setter called in between) is captured into a HIP graph on its second occurrence and replayed after
- * (PFR_GRAPH=0: never); results are bit-identical to the direct launches.  The stream must not be the null
- * stream for that. */
+ * w_dev (complex n_stiff) += gradient partials.  fr_dev / loss_dev / w_dev / flags_dev may be NULL. */
 PFR_API int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t loss_type,
                       const double* ref_dev, double scale, double* fr_dev, double* loss_dev, double* w_dev,
                       int32_t* flags_dev, void* stream);
-/* the sweep graph of the solver: 0 none, 1 a key recorded (the next identical sweep is captured), 2 captured */
-PFR_API int32_t pfr_sweep_graph_state(const pfr_solver* s);
 
 /* Exact second derivatives with the factors of the sweep reused (replaces the reference's
  * forward-over-reverse Hessian, `jax.jacobian(grad)` in Optimizers.py:125-136, whose mode-4

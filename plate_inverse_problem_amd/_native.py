@@ -66,7 +66,6 @@ _PROTOS = {
     "pfr_solver_destroy": (None, [_P]),
     "pfr_solver_workspace_bytes": (C.c_int64, [_P, C.c_int32]),
     "pfr_solver_max_batch": (C.c_int32, [_P]),
-    "pfr_sweep_graph_state": (C.c_int32, [_P]),
     "pfr_solve": (C.c_int, [_P, C.c_int32, _P, C.c_int64, _P, C.c_int64, _P, C.c_int32, _P, _P]),
     "pfr_matvec": (C.c_int, [_P, C.c_int32, _P, C.c_int64, _P, C.c_int64, _P, C.c_int32, _P]),
     "pfr_set_stiffness": (C.c_int, [_P, C.c_int32, _P, _DP]),
@@ -276,10 +275,6 @@ class Solver:
     def sweep(self, freqs, loss_type=LOSS_NONE, ref=None, scale=1.0, fr=None, loss=None, w=None, flags=None):
         check(lib().pfr_sweep(self._h, int(freqs.numel()), _ptr(freqs), int(loss_type), _ptr(ref), float(scale),
                               _ptr(fr), _ptr(loss), _ptr(w), _ptr(flags), self._stream(freqs)), "pfr_sweep")
-
-    def graph_state(self) -> int:
-        """0 no sweep graph, 1 a sweep key recorded (the next identical sweep is captured), 2 captured."""
-        return int(lib().pfr_sweep_graph_state(self._h))
 
     def hessian_sweep(self, freqs, loss_type, ref, scale, dcoef, loss=None, w=None, h=None, flags=None):
         """Loss, gradient partials w (18 complex) and second-order partials h (n_dir x 18 complex) with the

@@ -174,27 +174,6 @@ struct pfr_solver {
   // loaded or stored; index data is shared by all frequencies and not counted)
   std::vector<std::array<int64_t, pfr::NKC>> lev_bytes;
   pfr::Workspace ws;                    // element counts of the chunk buffers (plan.cpp; what is allocated)
-  // graph-captured sweeps (pfr_sweep): the last single-chunk sweep's key, its instantiated graph, the staging
-  // buffers its inputs / outputs go through, and a generation bumped by every setter whose values launches take
-  // by value (a changed generation re-keys the sweep)
-  struct GraphKey {
-    int nv = -1, loss_type = 0;
-    double scale = 0;
-    int io = 0, check = 0;
-    uint64_t gen = 0;
-    bool operator==(const GraphKey& o) const {
-      return nv == o.nv && loss_type == o.loss_type && scale == o.scale && io == o.io && check == o.check && gen == o.gen;
-    }
-  };
-  int graph_on = 1;                     // PFR_GRAPH
-  uint64_t gen = 0;
-  GraphKey gkey;
-  bool gkey_seen = false;
-  hipGraphExec_t gexec = nullptr;
-  double2* g_ref = nullptr;             // Fc
-  double* g_fr = nullptr;               // Fc
-  int32_t* g_flags = nullptr;           // Fc
-  double* g_lw = nullptr;               // w (18 complex), then loss (Fc doubles allocated)
   // launch-shape tuning knobs, read from the environment when the solver is created (so that a
   // process can build solvers with different settings, e.g. tests forcing each kernel variant):
   // PFR_SOLVE_WMAX (waves per solve workgroup, at most), PFR_FAC_WMAX (waves per A11 LU
@@ -223,7 +202,6 @@ struct pfr_solver {
   double* d_berr_acc = nullptr;
 
   ~pfr_solver() {
-    if (gexec) (void)hipGraphExecDestroy(gexec);
     for (void* p : owned) (void)hipFree(p);
     for (auto& c : tev) {
       for (auto& x : c.ev)
@@ -617,8 +595,6 @@ void contract_rows(pfr_solver* s, const double2* lam, const double2* x, int nv, 
 namespace pfr {
 void launch_pad_freqs(double* freqs, int nvalid, int64_t Fc, hipStream_t st);
 void launch_flags_merge(const int* chunk, int nvalid, int* out, hipStream_t st);
-void launch_sweep_out(const double* lw, int n_stiff, double* loss, double2* w, const int* fl, int nvalid, int* flags,
-                      hipStream_t st);   // a graph-replayed sweep's staged outputs: loss +=, w +=, flags |=
 }
 
 extern "C" {
@@ -769,7 +745,6 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->us2_small = knob("PFR_US2_SMALL", 110, 0, pfr::MAX_FRONT);
   s->split_target = knob("PFR_SOLVE_SPLIT", 256, 0, 1 << 20);
   s->us2_nar = knob("PFR_US2_NAR", 1, 0, 1);
-  s->graph_on = knob("PFR_GRAPH", 1, 0, 1);
   s->fac_lds = knob("PFR_FAC_LDS", -1, -1, 64);
   s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);
   s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);
@@ -866,9 +841,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       (rc = s->alloc(&s->freqs, Fc)) || (rc = s->alloc(&s->loss_terms, Fc)) || (rc = s->alloc(&s->flags, Fc)) ||
       (rc = s->alloc(&s->tq, Fc)) || (rc = s->alloc(&s->d_berr_acc, 2 * Fc)) || (rc = s->alloc(&s->fr0, Fc)) ||
       (rc = s->alloc(&s->mscale, Fc)) || (rc = s->alloc(&s->cpart, s->ws.cpart)) ||
-      (rc = s->alloc(&s->gind, Fc / 64)) || (rc = s->alloc(&s->glist, pfr::REFINE_CAP)) ||
-      (rc = s->alloc(&s->g_ref, Fc)) || (rc = s->alloc(&s->g_fr, Fc)) || (rc = s->alloc(&s->g_flags, Fc)) ||
-      (rc = s->alloc(&s->g_lw, Fc)))   // >= 37 (Fc >= 64)
+      (rc = s->alloc(&s->gind, Fc / 64)) || (rc = s->alloc(&s->glist, pfr::REFINE_CAP)))
     return bail(rc);
   HIP_TRY(hipMemset(s->d_berr_acc, 0, 2 * Fc * sizeof(double)));
   *out = s;
@@ -884,10 +857,7 @@ void pfr_solver_destroy(pfr_solver* s) {
 
 int32_t pfr_solver_max_batch(const pfr_solver* s) { return s ? (int32_t)s->Fc : 0; }
 
-int32_t pfr_sweep_graph_state(const pfr_solver* s) { return !s ? 0 : s->gexec ? 2 : s->gkey_seen ? 1 : 0; }
-
 int pfr_set_timing(pfr_solver* s, int32_t enable) {
-  if (s) ++s->gen;   // re-keys the captured sweep graph
   if (!s) return fail(PFR_ERR_ARG, "null solver");
   s->timing = enable == 0 ? 0 : (enable | 1);
   return PFR_OK;
@@ -909,14 +879,12 @@ int pfr_debug_solution(pfr_solver* s, int32_t which, int32_t q, double* out) {
 }
 
 int pfr_set_refine_tol(pfr_solver* s, double tol) {
-  if (s) ++s->gen;   // re-keys the captured sweep graph
   if (!s || !(tol >= 0.0)) return fail(PFR_ERR_ARG, "bad refine tolerance");
   s->refine_tol = tol;
   return PFR_OK;
 }
 
 int pfr_set_check(pfr_solver* s, int32_t mode, double tol, double* berr_dev) {
-  if (s) ++s->gen;   // re-keys the captured sweep graph
   if (!s || mode < 0 || mode > 31 || !(tol >= 0.0)) return fail(PFR_ERR_ARG, "bad check arguments");
   s->check_mode = mode;
   s->check_tol = tol;
@@ -1015,7 +983,6 @@ int pfr_solver_solve_bytes(const pfr_solver* s, int64_t* bytes) {
 }
 
 int pfr_set_stiffness(pfr_solver* s, int32_t n_stiff, const double* stiff_dev, const double* w) {
-  if (s) ++s->gen;   // re-keys the captured sweep graph
   if (!s || (n_stiff != 12 && n_stiff != 18) || !stiff_dev || !w)
     return fail(PFR_ERR_ARG, "bad stiffness arguments (n_stiff must be 12 or 18)");
   s->stiff = stiff_dev;
@@ -1056,7 +1023,6 @@ int pfr_combine(pfr_solver* s, const double* coef, double* K_out, void* stream) 
 }
 
 int pfr_set_operator(pfr_solver* s, const double* K_dev, const double* M_dev) {
-  if (s) ++s->gen;   // re-keys the captured sweep graph
   if (!s || !K_dev || !M_dev) return fail(PFR_ERR_ARG, "null argument");
   s->K = reinterpret_cast<const double2*>(K_dev);
   s->M = M_dev;
@@ -1064,7 +1030,6 @@ int pfr_set_operator(pfr_solver* s, const double* K_dev, const double* M_dev) {
 }
 
 int pfr_set_rhs(pfr_solver* s, const double* rhs, double beta_re, double beta_im, double mass_sum) {
-  if (s) ++s->gen;   // re-keys the captured sweep graph
   if (!s || !rhs) return fail(PFR_ERR_ARG, "null argument");
   s->beta_re = beta_re;
   s->beta_im = beta_im;
@@ -1110,7 +1075,6 @@ int pfr_set_rhs(pfr_solver* s, const double* rhs, double beta_re, double beta_im
 }
 
 int pfr_set_functional(pfr_solver* s, int32_t n_support, const int32_t* index, const double* a, double ts) {
-  if (s) ++s->gen;   // re-keys the captured sweep graph
   if (!s || n_support <= 0 || !index || !a) return fail(PFR_ERR_ARG, "bad functional arguments");
   HIP_TRY(hipSetDevice(s->device));
   std::vector<int32_t> pidx(n_support);
@@ -1161,237 +1125,177 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
   if (fn_fast)
     if (int rc0 = fn_setup(s)) return rc0;
   bool used[5] = {true, true, true, adj, adj};
-  // one chunk of the sweep: every launch on st, no host synchronisation (captured into a graph below)
-  auto run_chunk = [&](int64_t q0, int nv, const double* ref_dev, double* fr_dev, double* loss_dev, double* w_dev,
-                       int32_t* flags_dev) -> int {
-      pfr::launch_pad_freqs(s->freqs, nv, Fc, st);
-      HIP_TRY(hipMemsetAsync(s->flags, 0, Fc * sizeof(int32_t), st));
-      if (int rc0 = begin_chunk(s)) return rc0;
-      record(s, 0, st);
-      pfr::RhsDesc rd;
-      rd.rhsP = s->rhsP;
-      rd.beta_re = s->beta_re;
-      rd.beta_im = s->beta_im;
-      rd.mass_sum = s->mass_sum;
-      rd.freqs = s->freqs;
-      pfr::RhsDesc rf = rd;
-      int rc;
-      if (paired) {
-        pfr::launch_dirichlet_rhs(0, dir_desc(s), s->n_crow, rd, nullptr, s->Bc, s->Fc, st);
-        rf.cslot = s->d_cslot;
-        rf.Bc = s->Bc;
-        if ((rc = factor_all(s, 0, nullptr, 0, nv, st))) return rc;
-        record(s, 1, st);   // the forward bottom-up pass belongs to the solve phases (sptrsv_roofline)
-        if (fn_fast) {
-          if ((rc = fn_bottom_up(s, s->n_crow > 0 ? 3 : 0, rf, st))) return rc;
-        } else if ((rc = solve_all(s, 0, s->n_crow > 0 ? 3 : 0, rf, nullptr, s->Y, st, 0))) {
-          return rc;
-        }
-      } else {
-        rc = factor_all(s, 0, nullptr, 0, nv, st);
-        if (rc) return rc;
-        record(s, 1, st);
-      }
-      // symmetric mode with an adjoint: forward top-down only over the loss support's fronts, then one
-      // combined top-down pass (sym_top_down_pair); otherwise the full forward solve first
-      if (paired) {
-        if (!fn_fast && (rc = sym_top_down_support(s, rf, st))) return rc;
-      } else {
-        if ((rc = forward_solve(s, 0, rd, s->X, st, 0))) return rc;
-        if (refine) {
-          // one refinement step on the same factors: r = b - A x (into G), A d = r (into XA), x += d
-          check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, s->G, q0, st);
-          pfr::RhsDesc rr;
-          rr.G = s->G;
-          if ((rc = forward_solve(s, 2, rr, s->XA, st))) return rc;
-          pfr::launch_axpy_vec(s->X, s->XA, (int64_t)s->n * Fc, st);
-        }
-        if (!fwd_late && (s->check_mode & PFR_CHECK_FORWARD))
-          check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st);
-      }
-      record(s, 2, st);
-      pfr::FunctionalArgs fa = s->fn;
-      fa.loss_type = reverse ? loss_type : -1;
-      fa.ref = reinterpret_cast<const double2*>(ref_dev);
-      fa.scale = scale;
-      if (adj) HIP_TRY(hipMemsetAsync(s->G, 0, (size_t)s->n * Fc * 16, st));
-      if (fn_fast) {
-        const double2* Yk[3] = {s->Y2, s->YVk, s->YVk + (int64_t)s->n * Fc};
-        pfr::launch_fn_dot(s->d_fn_rows, s->n_fn_rows, s->F, s->Y, Yk, Fc, s->fn_parts, st);
-        pfr::FunctionalArgs fs = fa;
-        if (correct) fs.fr0 = s->fr0;
-        pfr::launch_functional_fn(fs, s->fn_parts, Fc, nv, q0, correct ? nullptr : fr_dev, correct ? nullptr : s->loss_terms,
-                                  s->G, s->fcoef, st);
-      } else if (correct) {
-        pfr::FunctionalArgs fs = fa;
-        fs.fr0 = s->fr0;          // seed: fr of this solve kept, G = d fr / d x
-        pfr::launch_functional(fs, s->X, Fc, nv, q0, nullptr, nullptr, s->G, st);
-      } else {
-        pfr::launch_functional(fa, s->X, Fc, nv, q0, fr_dev, s->loss_terms, s->G, st);
-      }
-      record(s, 3, st);
-      if (adj) {
-        pfr::RhsDesc rg;
-        rg.G = s->G;
-        if (fn_fast) {
-          double2* Yk[3] = {s->Y2, s->YVk, s->YVk + (int64_t)s->n * Fc};
-          pfr::launch_fn_combine(s->d_sup_rows, s->n_sup_rows, s->fcoef, Yk, Fc, st);
-          if ((rc = sym_top_down_pair(s, st, true))) return rc;
-          pfr::launch_dirichlet_post(dir_desc(s), s->n_dir, s->XA, s->Fc, st);
-          if (correct) {
-            // the correction fr(x) + Re(mu^T r) needs fr OF the solution x whose residual r is walked (the
-            // dot product's fr has its own rounding error, which the correction does not see): fr0 from x
-            pfr::FunctionalArgs fs = fa;
-            fs.fr0 = s->fr0;
-            pfr::launch_functional(fs, s->X, Fc, nv, q0, nullptr, nullptr, nullptr, st);
-          }
-        } else if (paired) {
-          if ((rc = solve_all(s, 0, 2, rg, nullptr, s->Y2, st, 1)) || (rc = sym_top_down_pair(s, st))) return rc;
-          pfr::launch_dirichlet_post(dir_desc(s), s->n_dir, s->XA, s->Fc, st);
-        } else {
-          if ((rc = adjoint_solve(s, rg, s->XA, st, 1))) return rc;
-          if (refine) {
-            // l += A^{-T} (g - A^T l): residual into Y2, correction into XR
-            check_solution(s, 1, 0, 2, rg, nullptr, 0, nv, s->XA, s->Y2, q0, st);
-            pfr::RhsDesc rr;
-            rr.G = s->Y2;
-            if ((rc = adjoint_solve(s, rr, s->XR, st))) return rc;
-            pfr::launch_axpy_vec(s->XA, s->XR, (int64_t)s->n * Fc, st);
-          }
-        }
-        record(s, 4, st);
-        bool want_f = fwd_late && (s->check_mode & PFR_CHECK_FORWARD);
-        bool want_a = (s->check_mode & PFR_CHECK_ADJOINT) != 0;
-        // the gradient contraction rides on the forward residual walk (loss sweeps with the correction)
-        const bool cwalk = reverse && correct && s->contract_walk &&
-                           (s->n_stiff == 12 || s->n_stiff == 18);
-        if (cwalk && !s->kpart) {
-          if ((rc = s->alloc(&s->kpart, s->ws.kpart))) return rc;
-        }
-        // selective adjoint refinement (PFR_CHECK_REFINE_ADJ): the groups next to a resonance, where the unrefined
-        // solves' first-order error dominates the gradient, get one refinement step of mu
-        const bool refine_adj = reverse && correct && cwalk && fn_fast && (s->check_mode & PFR_CHECK_REFINE_ADJ);
-        // the solve-error scale of the cotangent (k_correct_finish): t_q = mu^T rhsP in, m_q t_q out
-        const bool scorr = reverse && correct && s->scale_corr;
-        pfr::RhsScale bsc;
-        bsc.freqs = s->freqs;
-        bsc.mass_sum = s->mass_sum;
-        bsc.beta_re = s->beta_re;
-        bsc.beta_im = s->beta_im;
-        if (correct) {
-          // the forward residual walk: backward error (when checked) + the correction's dot products,
-          // then the corrected fr, its loss terms and the per-frequency cotangent scales
-          check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st, s->XA, want_f, cwalk);
-          want_f = false;
-          if (scorr) pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st);
-          pfr::launch_correct_finish(fa, s->fr0, s->cpart, pfr::residual_parts(s->n), Fc, nv, q0, fr_dev, s->loss_terms,
-                                     s->mscale, st, refine_adj ? s->gind : nullptr, scorr ? s->tq : nullptr, bsc);
-        }
-        if (refine_adj) {
-          // the listed groups (largest first-order fr error estimates above the tolerance, at most REFINE_CAP):
-          // mu += A^-T (G - A^T mu) with the fr seed G = d fr / d x of THIS x (k_functional seed mode; the adjoint
-          // was solved for the seed of the bottom-up dot products, whose rounding differs), then their correction
-          // dot products and gradient contraction again with the refined mu, and their fr / m_q
-          pfr::launch_select_groups(s->gind, (int)(Fc / 64), s->refine_tol, s->glist, st);
-          if (!s->Gx) {
-            if ((rc = s->alloc(&s->Gx, s->ws.nvec))) return rc;
-            HIP_TRY(hipMemsetAsync(s->Gx, 0, (size_t)s->n * Fc * 16, st));   // only the support rows are ever written
-          }
-          pfr::FunctionalArgs fs = fa;
-          fs.fr0 = s->fr0;
-          pfr::launch_functional(fs, s->X, Fc, nv, q0, nullptr, nullptr, s->Gx, st);
-          pfr::RhsDesc rgx;
-          rgx.G = s->Gx;
-          check_solution(s, 1, 0, 2, rgx, nullptr, 0, nv, s->XA, s->XR, q0, st, nullptr, false, false, s->glist);
-          pfr::RhsDesc rr;
-          rr.G = s->XR;
-          if ((rc = adjoint_solve(s, rr, s->Y2, st, -1, s->glist))) return rc;
-          pfr::launch_axpy_vec(s->XA, s->Y2, (int64_t)s->n * Fc, st, s->glist, Fc);
-          check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st, s->XA, false, true, s->glist);
-          if (scorr) pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st);
-          pfr::launch_correct_finish(fa, s->fr0, s->cpart, pfr::residual_parts(s->n), Fc, nv, q0, fr_dev, s->loss_terms,
-                                     s->mscale, st, nullptr, scorr ? s->tq : nullptr, bsc);
-        }
-        const double2* msc = correct ? s->mscale : nullptr;
-        if (cwalk)
-          pfr::launch_reduce_q(s->kpart, pfr::residual_parts(s->n), s->n_stiff, msc, nv, Fc, s->partial, st);
-        else if (reverse)
-          pfr::launch_contract_eg(s->d_uent, s->n_uent, s->d_se, s->n_stiff, s->XA, s->X, Fc, nv, s->partial, st, msc);
-        // the checks as row / column walks of the original pattern (k_residual)
-        if (want_f) check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st);
-        if (want_a) check_solution(s, 1, 0, 2, rg, nullptr, 0, nv, s->XA, nullptr, q0, st);
-        if (reverse) {
-          if (!scorr) pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st, msc);
-          pfr::launch_reduce(s->partial, cwalk ? (int)(Fc / 64) : pfr::contract_eg_parts(s->n_uent), s->n_stiff, s->tq, s->e,
-                             s->loss_terms, nv, Fc, reinterpret_cast<double2*>(w_dev), loss_dev, st);
-        }
-      } else {
-        record(s, 4, st);
-      }
-      record(s, 5, st);
-      if (flags_dev) pfr::launch_flags_merge(s->flags, nv, flags_dev + q0, st);
-      HIP_TRY(hipGetLastError());
-    return PFR_OK;
-  };
-  // graph-captured sweeps (PFR_GRAPH): a single-chunk sweep with the same shape, modes and solver state as the
-  // previous call is replayed from a HIP graph captured on the second such call (one launch instead of ~300 on
-  // the stream; the dispatch gaps between dependent kernels shrink).  The per-call inputs and outputs go through
-  // solver-owned staging buffers, so the graph's pointers never change: freqs and ref copied in before, fr copied
-  // out, loss / w / flags accumulated into the caller's buffers by one small kernel after (same += / |=
-  // semantics as the direct path).  Timing, per-call backward errors and the selective refinement run eagerly.
-  const bool graphable = s->graph_on && st != nullptr && !s->timing && nfreq <= Fc && !s->berr_out &&
-                         !(s->check_mode & PFR_CHECK_REFINE_ADJ);
-  if (graphable) {
-    const int io = (ref_dev ? 1 : 0) | (fr_dev ? 2 : 0) | (loss_dev ? 4 : 0) | (w_dev ? 8 : 0) | (flags_dev ? 16 : 0);
-    const pfr_solver::GraphKey key{nfreq, loss_type, scale, io, s->check_mode, s->gen};
-    HIP_TRY(hipMemcpyAsync(s->freqs, freqs_dev, nfreq * sizeof(double), hipMemcpyDeviceToDevice, st));
-    if (ref_dev) HIP_TRY(hipMemcpyAsync(s->g_ref, ref_dev, (size_t)nfreq * 16, hipMemcpyDeviceToDevice, st));
-    const bool have = s->gexec && key == s->gkey;
-    auto staged = [&]() -> int {
-      if (loss_dev || w_dev) HIP_TRY(hipMemsetAsync(s->g_lw, 0, sizeof(double) * (1 + 2 * 18), st));
-      if (flags_dev) HIP_TRY(hipMemsetAsync(s->g_flags, 0, sizeof(int32_t) * Fc, st));
-      return run_chunk(0, nfreq, ref_dev ? reinterpret_cast<const double*>(s->g_ref) : nullptr, fr_dev ? s->g_fr : nullptr,
-                       loss_dev ? s->g_lw + 2 * 18 : nullptr, w_dev ? s->g_lw : nullptr, flags_dev ? s->g_flags : nullptr);
-    };
-    int rc = PFR_OK;
-    if (!have && s->gkey_seen && key == s->gkey) {
-      // second identical call: capture (nothing runs during capture), then launch
-      hipGraph_t g = nullptr;
-      HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-      rc = staged();
-      const hipError_t e = hipStreamEndCapture(st, &g);
-      if (rc == PFR_OK && e == hipSuccess && g && hipGraphInstantiate(&s->gexec, g, nullptr, nullptr, 0) == hipSuccess) {
-        (void)hipGraphDestroy(g);
-        HIP_TRY(hipGraphLaunch(s->gexec, st));
-      } else {
-        // capture not possible here: this solver runs its sweeps eagerly from now on
-        if (g) (void)hipGraphDestroy(g);
-        (void)hipGetLastError();
-        s->gexec = nullptr;
-        s->graph_on = 0;
-        if ((rc = staged())) return rc;
-      }
-    } else if (have) {
-      HIP_TRY(hipGraphLaunch(s->gexec, st));
-    } else {
-      // a new key: run eagerly, remember it (captured if the next call repeats it)
-      if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
-      s->gexec = nullptr;
-      s->gkey = key;
-      s->gkey_seen = true;
-      if ((rc = staged())) return rc;
-    }
-    if (fr_dev) HIP_TRY(hipMemcpyAsync(fr_dev, s->g_fr, (size_t)nfreq * sizeof(double), hipMemcpyDeviceToDevice, st));
-    pfr::launch_sweep_out(s->g_lw, s->n_stiff, loss_dev, reinterpret_cast<double2*>(w_dev), s->g_flags, nfreq, flags_dev,
-                          st);
-    HIP_TRY(hipGetLastError());
-    return PFR_OK;
-  }
   for (int64_t q0 = 0; q0 < nfreq; q0 += Fc) {
     const int nv = (int)std::min<int64_t>(Fc, nfreq - q0);
     HIP_TRY(hipMemcpyAsync(s->freqs, freqs_dev + q0, nv * sizeof(double), hipMemcpyDeviceToDevice, st));
-    if (int rc = run_chunk(q0, nv, ref_dev, fr_dev, loss_dev, w_dev, flags_dev)) return rc;
-    if (int rc = finish_timing(s, used)) return rc;
+    pfr::launch_pad_freqs(s->freqs, nv, Fc, st);
+    HIP_TRY(hipMemsetAsync(s->flags, 0, Fc * sizeof(int32_t), st));
+    if (int rc0 = begin_chunk(s)) return rc0;
+    record(s, 0, st);
+    pfr::RhsDesc rd;
+    rd.rhsP = s->rhsP;
+    rd.beta_re = s->beta_re;
+    rd.beta_im = s->beta_im;
+    rd.mass_sum = s->mass_sum;
+    rd.freqs = s->freqs;
+    pfr::RhsDesc rf = rd;
+    int rc;
+    if (paired) {
+      pfr::launch_dirichlet_rhs(0, dir_desc(s), s->n_crow, rd, nullptr, s->Bc, s->Fc, st);
+      rf.cslot = s->d_cslot;
+      rf.Bc = s->Bc;
+      if ((rc = factor_all(s, 0, nullptr, 0, nv, st))) return rc;
+      record(s, 1, st);   // the forward bottom-up pass belongs to the solve phases (sptrsv_roofline)
+      if (fn_fast) {
+        if ((rc = fn_bottom_up(s, s->n_crow > 0 ? 3 : 0, rf, st))) return rc;
+      } else if ((rc = solve_all(s, 0, s->n_crow > 0 ? 3 : 0, rf, nullptr, s->Y, st, 0))) {
+        return rc;
+      }
+    } else {
+      rc = factor_all(s, 0, nullptr, 0, nv, st);
+      if (rc) return rc;
+      record(s, 1, st);
+    }
+    // symmetric mode with an adjoint: forward top-down only over the loss support's fronts, then one
+    // combined top-down pass (sym_top_down_pair); otherwise the full forward solve first
+    if (paired) {
+      if (!fn_fast && (rc = sym_top_down_support(s, rf, st))) return rc;
+    } else {
+      if ((rc = forward_solve(s, 0, rd, s->X, st, 0))) return rc;
+      if (refine) {
+        // one refinement step on the same factors: r = b - A x (into G), A d = r (into XA), x += d
+        check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, s->G, q0, st);
+        pfr::RhsDesc rr;
+        rr.G = s->G;
+        if ((rc = forward_solve(s, 2, rr, s->XA, st))) return rc;
+        pfr::launch_axpy_vec(s->X, s->XA, (int64_t)s->n * Fc, st);
+      }
+      if (!fwd_late && (s->check_mode & PFR_CHECK_FORWARD))
+        check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st);
+    }
+    record(s, 2, st);
+    pfr::FunctionalArgs fa = s->fn;
+    fa.loss_type = reverse ? loss_type : -1;
+    fa.ref = reinterpret_cast<const double2*>(ref_dev);
+    fa.scale = scale;
+    if (adj) HIP_TRY(hipMemsetAsync(s->G, 0, (size_t)s->n * Fc * 16, st));
+    if (fn_fast) {
+      const double2* Yk[3] = {s->Y2, s->YVk, s->YVk + (int64_t)s->n * Fc};
+      pfr::launch_fn_dot(s->d_fn_rows, s->n_fn_rows, s->F, s->Y, Yk, Fc, s->fn_parts, st);
+      pfr::FunctionalArgs fs = fa;
+      if (correct) fs.fr0 = s->fr0;
+      pfr::launch_functional_fn(fs, s->fn_parts, Fc, nv, q0, correct ? nullptr : fr_dev, correct ? nullptr : s->loss_terms,
+                                s->G, s->fcoef, st);
+    } else if (correct) {
+      pfr::FunctionalArgs fs = fa;
+      fs.fr0 = s->fr0;          // seed: fr of this solve kept, G = d fr / d x
+      pfr::launch_functional(fs, s->X, Fc, nv, q0, nullptr, nullptr, s->G, st);
+    } else {
+      pfr::launch_functional(fa, s->X, Fc, nv, q0, fr_dev, s->loss_terms, s->G, st);
+    }
+    record(s, 3, st);
+    if (adj) {
+      pfr::RhsDesc rg;
+      rg.G = s->G;
+      if (fn_fast) {
+        double2* Yk[3] = {s->Y2, s->YVk, s->YVk + (int64_t)s->n * Fc};
+        pfr::launch_fn_combine(s->d_sup_rows, s->n_sup_rows, s->fcoef, Yk, Fc, st);
+        if ((rc = sym_top_down_pair(s, st, true))) return rc;
+        pfr::launch_dirichlet_post(dir_desc(s), s->n_dir, s->XA, s->Fc, st);
+        if (correct) {
+          // the correction fr(x) + Re(mu^T r) needs fr OF the solution x whose residual r is walked (the
+          // dot product's fr has its own rounding error, which the correction does not see): fr0 from x
+          pfr::FunctionalArgs fs = fa;
+          fs.fr0 = s->fr0;
+          pfr::launch_functional(fs, s->X, Fc, nv, q0, nullptr, nullptr, nullptr, st);
+        }
+      } else if (paired) {
+        if ((rc = solve_all(s, 0, 2, rg, nullptr, s->Y2, st, 1)) || (rc = sym_top_down_pair(s, st))) return rc;
+        pfr::launch_dirichlet_post(dir_desc(s), s->n_dir, s->XA, s->Fc, st);
+      } else {
+        if ((rc = adjoint_solve(s, rg, s->XA, st, 1))) return rc;
+        if (refine) {
+          // l += A^{-T} (g - A^T l): residual into Y2, correction into XR
+          check_solution(s, 1, 0, 2, rg, nullptr, 0, nv, s->XA, s->Y2, q0, st);
+          pfr::RhsDesc rr;
+          rr.G = s->Y2;
+          if ((rc = adjoint_solve(s, rr, s->XR, st))) return rc;
+          pfr::launch_axpy_vec(s->XA, s->XR, (int64_t)s->n * Fc, st);
+        }
+      }
+      record(s, 4, st);
+      bool want_f = fwd_late && (s->check_mode & PFR_CHECK_FORWARD);
+      bool want_a = (s->check_mode & PFR_CHECK_ADJOINT) != 0;
+      // the gradient contraction rides on the forward residual walk (loss sweeps with the correction)
+      const bool cwalk = reverse && correct && s->contract_walk &&
+                         (s->n_stiff == 12 || s->n_stiff == 18);
+      if (cwalk && !s->kpart) {
+        if ((rc = s->alloc(&s->kpart, s->ws.kpart))) return rc;
+      }
+      // selective adjoint refinement (PFR_CHECK_REFINE_ADJ): the groups next to a resonance, where the unrefined
+      // solves' first-order error dominates the gradient, get one refinement step of mu
+      const bool refine_adj = reverse && correct && cwalk && fn_fast && (s->check_mode & PFR_CHECK_REFINE_ADJ);
+      // the solve-error scale of the cotangent (k_correct_finish): t_q = mu^T rhsP in, m_q t_q out
+      const bool scorr = reverse && correct && s->scale_corr;
+      pfr::RhsScale bsc;
+      bsc.freqs = s->freqs;
+      bsc.mass_sum = s->mass_sum;
+      bsc.beta_re = s->beta_re;
+      bsc.beta_im = s->beta_im;
+      if (correct) {
+        // the forward residual walk: backward error (when checked) + the correction's dot products,
+        // then the corrected fr, its loss terms and the per-frequency cotangent scales
+        check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st, s->XA, want_f, cwalk);
+        want_f = false;
+        if (scorr) pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st);
+        pfr::launch_correct_finish(fa, s->fr0, s->cpart, pfr::residual_parts(s->n), Fc, nv, q0, fr_dev, s->loss_terms,
+                                   s->mscale, st, refine_adj ? s->gind : nullptr, scorr ? s->tq : nullptr, bsc);
+      }
+      if (refine_adj) {
+        // the listed groups (largest first-order fr error estimates above the tolerance, at most REFINE_CAP):
+        // mu += A^-T (G - A^T mu) with the fr seed G = d fr / d x of THIS x (k_functional seed mode; the adjoint
+        // was solved for the seed of the bottom-up dot products, whose rounding differs), then their correction
+        // dot products and gradient contraction again with the refined mu, and their fr / m_q
+        pfr::launch_select_groups(s->gind, (int)(Fc / 64), s->refine_tol, s->glist, st);
+        if (!s->Gx) {
+          if ((rc = s->alloc(&s->Gx, s->ws.nvec))) return rc;
+          HIP_TRY(hipMemsetAsync(s->Gx, 0, (size_t)s->n * Fc * 16, st));   // only the support rows are ever written
+        }
+        pfr::FunctionalArgs fs = fa;
+        fs.fr0 = s->fr0;
+        pfr::launch_functional(fs, s->X, Fc, nv, q0, nullptr, nullptr, s->Gx, st);
+        pfr::RhsDesc rgx;
+        rgx.G = s->Gx;
+        check_solution(s, 1, 0, 2, rgx, nullptr, 0, nv, s->XA, s->XR, q0, st, nullptr, false, false, s->glist);
+        pfr::RhsDesc rr;
+        rr.G = s->XR;
+        if ((rc = adjoint_solve(s, rr, s->Y2, st, -1, s->glist))) return rc;
+        pfr::launch_axpy_vec(s->XA, s->Y2, (int64_t)s->n * Fc, st, s->glist, Fc);
+        check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st, s->XA, false, true, s->glist);
+        if (scorr) pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st);
+        pfr::launch_correct_finish(fa, s->fr0, s->cpart, pfr::residual_parts(s->n), Fc, nv, q0, fr_dev, s->loss_terms,
+                                   s->mscale, st, nullptr, scorr ? s->tq : nullptr, bsc);
+      }
+      const double2* msc = correct ? s->mscale : nullptr;
+      if (cwalk)
+        pfr::launch_reduce_q(s->kpart, pfr::residual_parts(s->n), s->n_stiff, msc, nv, Fc, s->partial, st);
+      else if (reverse)
+        pfr::launch_contract_eg(s->d_uent, s->n_uent, s->d_se, s->n_stiff, s->XA, s->X, Fc, nv, s->partial, st, msc);
+      // the checks as row / column walks of the original pattern (k_residual)
+      if (want_f) check_solution(s, 0, 0, 0, rd, nullptr, 0, nv, s->X, nullptr, q0, st);
+      if (want_a) check_solution(s, 1, 0, 2, rg, nullptr, 0, nv, s->XA, nullptr, q0, st);
+      if (reverse) {
+        if (!scorr) pfr::launch_rhs_dot(s->rhs_sup, s->rhs_val, s->n_rhs_sup, s->XA, Fc, s->tq, st, msc);
+        pfr::launch_reduce(s->partial, cwalk ? (int)(Fc / 64) : pfr::contract_eg_parts(s->n_uent), s->n_stiff, s->tq, s->e,
+                           s->loss_terms, nv, Fc, reinterpret_cast<double2*>(w_dev), loss_dev, st);
+      }
+    } else {
+      record(s, 4, st);
+    }
+    record(s, 5, st);
+    if (flags_dev) pfr::launch_flags_merge(s->flags, nv, flags_dev + q0, st);
+    HIP_TRY(hipGetLastError());
+    if ((rc = finish_timing(s, used))) return rc;
   }
   return PFR_OK;
 }

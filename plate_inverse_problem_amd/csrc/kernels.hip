@@ -3353,22 +3353,6 @@ __global__ void k_pad_freqs(double* freqs, int nvalid, int64_t Fc) {
 void launch_pad_freqs(double* freqs, int nvalid, int64_t Fc, hipStream_t st) {
   LAUNCH(k_pad_freqs, dim3((unsigned)((Fc + 63) / 64)), dim3(64), st, freqs, nvalid, Fc);
 }
-// a graph-replayed sweep's staged outputs into the caller's buffers: w += (n_stiff complex, lw[0 ..]), loss +=
-// (lw[36]), flags |=
-__global__ void k_sweep_out(const double* __restrict__ lw, int n_stiff, double* __restrict__ loss, cplx* __restrict__ w,
-                            const int* __restrict__ fl, int nvalid, int* __restrict__ flags) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t == 0 && loss) loss[0] += lw[2 * 18];
-  if (w && t < n_stiff) w[t] = cadd(w[t], reinterpret_cast<const cplx*>(lw)[t]);
-  if (flags)
-    for (int q = t; q < nvalid; q += gridDim.x * blockDim.x) flags[q] |= fl[q];
-}
-void launch_sweep_out(const double* lw, int n_stiff, double* loss, double2* w, const int* fl, int nvalid, int* flags,
-                      hipStream_t st) {
-  if (!loss && !w && !flags) return;
-  LAUNCH(k_sweep_out, dim3(flags ? (nvalid + 255) / 256 : 1), dim3(256), st, lw, n_stiff, loss, w, fl, nvalid, flags);
-}
-
 __global__ void k_flags_merge(const int* chunk, int nvalid, int* out) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q < nvalid) out[q] |= chunk[q];

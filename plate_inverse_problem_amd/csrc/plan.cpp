@@ -29,7 +29,6 @@ Workspace workspace(const Symbolic& S, int64_t Fc, int n_crow) {
   }
   int64_t b = 16 * (w.F + w.WV + w.n_nvec * w.nvec + w.cpart + w.kpart + w.WVk + w.YVk + w.fn_parts + w.fcoef + w.Bc);
   b += Fc * (8 + 8 + 4 + 16) + Fc * (8 + 16) + 8 * (w.berr_acc + w.gind);   // freqs, loss, flags, tq; fr0, mscale
-  b += Fc * (16 + 8 + 4 + 8);                                // graph staging: ref, fr, flags, w + loss
   w.bytes = b;
   return w;
 }
