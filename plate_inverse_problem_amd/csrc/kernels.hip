@@ -2027,6 +2027,93 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSM <= 4 ? 
 #undef E
 }
 
+// The pivot rows' update part on the split levels with the update COLUMNS split over the waves (the NAR path):
+// a workgroup = UPC_SR pivot rows of one front x one frequency group, its UPC_W waves each summing every
+// UPC_W-th chunk of UPC_SK update columns for those rows (each chunk's gathers and L21 loads independent of the
+// others), the partial sums added in wave order through LDS.  k_usolve2_upd gives each wave a row pair and the
+// whole column range: r / 4 dependent load rounds per wave (16-18 on the narrow levels of C3, 22-64 us per level).
+constexpr int UPC_SR = 2, UPC_SK = 8, UPC_W = 8;
+__global__ __launch_bounds__(64 * UPC_W) void k_usolve2_updc(DevPattern P, const int* __restrict__ lvl,
+                                                            const cplx* __restrict__ F, int64_t Fc, UPair A, UPair B,
+                                                            int RB) {
+  int bx;
+  const Ctx c = ctx_xcd(bx);
+  const int slot = bx / RB, rb = bx % RB;
+  const int ft = lvl[slot];
+  const Front fr = P.fronts[ft];
+  const int f = fr.f, ns = fr.ns;
+  const int a0 = rb * UPC_SR;
+  if (a0 >= ns) return;                         // the whole workgroup (the level's largest pivot block sizes RB)
+  const bool act[2] = {!A.skip || !A.skip[ft], !B.skip || !B.skip[ft]};
+  const bool live[2] = {!A.reach || A.reach[ft], !B.reach || B.reach[ft]};
+  const cplx* const Ys[2] = {A.Y, B.Y};
+  cplx* const Xs[2] = {A.X, B.X};
+  const cplx* __restrict__ base = F + fr.off * Fc + c.q;
+  __shared__ int six[MAX_FRONT];
+  __shared__ cplx part[UPC_W][2][UPC_SR][64];
+  for (int a = threadIdx.x; a < f; a += blockDim.x) six[a] = P.idx[fr.row0 + a];
+  __syncthreads();
+  int ra[UPC_SR];
+  const cplx* pu[UPC_SR];
+#pragma unroll
+  for (int r = 0; r < UPC_SR; ++r) {
+    ra[r] = min(a0 + r, ns - 1);
+    pu[r] = base + (int64_t)ra[r] * Fc;         // column ra of L21: E(b, ra) at pu + b f Fc
+  }
+  const int64_t su = (int64_t)f * Fc;
+  cplx acc[2][UPC_SR];
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+#pragma unroll
+    for (int r = 0; r < UPC_SR; ++r) acc[v][r] = make_double2(0.0, 0.0);
+  for (int b0 = ns + UPC_SK * c.w; b0 < f; b0 += UPC_SK * UPC_W) {
+    int iv[UPC_SK];
+    cplx xv[2][UPC_SK], ev[UPC_SR][UPC_SK];
+#pragma unroll
+    for (int u = 0; u < UPC_SK; ++u) iv[u] = __builtin_amdgcn_readfirstlane(six[min(b0 + u, f - 1)]);
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int u = 0; u < UPC_SK; ++u) xv[v][u] = Xs[v][(int64_t)iv[u] * Fc + c.q];   // inactive: unused
+#pragma unroll
+    for (int r = 0; r < UPC_SR; ++r)
+#pragma unroll
+      for (int u = 0; u < UPC_SK; ++u) ev[r][u] = pu[r][min(b0 + u, f - 1) * su];
+#pragma unroll
+    for (int u = 0; u < UPC_SK; ++u) {
+      const double m = b0 + u < f ? 1.0 : 0.0;
+#pragma unroll
+      for (int v = 0; v < 2; ++v) xv[v][u] = cscale(xv[v][u], m);
+    }
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+#pragma unroll
+      for (int r = 0; r < UPC_SR; ++r)
+#pragma unroll
+        for (int u = 0; u < UPC_SK; ++u) acc[v][r] = cfms(acc[v][r], ev[r][u], xv[v][u]);
+  }
+#pragma unroll
+  for (int v = 0; v < 2; ++v)
+#pragma unroll
+    for (int r = 0; r < UPC_SR; ++r) part[c.w][v][r][c.lane] = acc[v][r];
+  __syncthreads();
+  if (c.w == 0) {
+#pragma unroll
+    for (int r = 0; r < UPC_SR; ++r)
+      if (a0 + r < ns) {
+        const cplx urr = base[((int64_t)ra[r] * f + ra[r]) * Fc];
+#pragma unroll
+        for (int v = 0; v < 2; ++v)
+          if (act[v]) {
+            cplx t = part[0][v][r][c.lane];
+            for (int w = 1; w < UPC_W; ++w) t = cadd(t, part[w][v][r][c.lane]);
+            const cplx y = live[v] ? Ys[v][(int64_t)(fr.col0 + a0 + r) * Fc + c.q] : make_double2(0.0, 0.0);
+            Xs[v][(int64_t)(fr.col0 + a0 + r) * Fc + c.q] = cadd(y, cmul(urr, t));
+          }
+      }
+  }
+}
+
 // the pivot rows' update part of k_usolve2_level split over S workgroups per (front, frequency group)
 template <bool SYM, int SR, int SK>
 __global__ __launch_bounds__(256) void k_usolve2_upd(DevPattern P, const int* __restrict__ lvl, const cplx* __restrict__ F,
@@ -3200,7 +3287,12 @@ void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, boo
   const int rs = split > 1;
   // split > 1: the pivot rows' update part over `split` workgroups per front first (the small-front
   // register shape: many short waves)
-  if (rs) LAUNCH((k_usolve2_upd<true, 2, 4>), dim3(nfronts * split, ngroups), dim3(64 * SPLIT_W), st, P, lvl, F, Fc, a, b, split);
+  if (rs && nar) {
+    const int RB = (maxns + UPC_SR - 1) / UPC_SR;
+    LAUNCH(k_usolve2_updc, dim3(nfronts * RB, ngroups), dim3(64 * UPC_W), st, P, lvl, F, Fc, a, b, RB);
+  } else if (rs) {
+    LAUNCH((k_usolve2_upd<true, 2, 4>), dim3(nfronts * split, ngroups), dim3(64 * SPLIT_W), st, P, lvl, F, Fc, a, b, split);
+  }
   // symmetric mode only (the paired top-down pass serves the symmetric loss + gradient sweep).  Small-front levels:
   // 8 pivot rows per pass share each gathered update-row value, 2 values per chunk, 3 waves/SIMD (18 % less traffic
   // than 2 rows x 4 values at 4 waves/SIMD, the same time: profiles/r04/solve_traffic/)
