@@ -486,7 +486,7 @@ int fn_bottom_up(pfr_solver* s, int rhs_mode, const pfr::RhsDesc& rf, hipStream_
     if (nmax == 0) continue;
     pfr::launch_lsolve_multi(rhs_mode, s->P, 4, lvl, nf, solve_W(s, l, nmax), ngroups, s->F, s->Fc, WV, rd, Y, reach,
                              st, solve_split(s, nf[0] + 3 * nf[1]), s->us2_nar && pfr::ls_nar_fits(s->level_maxns[l]),
-                             s->level_maxns[l]);
+                             s->level_maxns[l], s->level_maxf[l]);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;

@@ -1550,6 +1550,65 @@ __global__ __launch_bounds__(256) void k_lsolve_rows_z(DevPattern P, LSlices S, 
               SRB * c.W * split);
 }
 
+// The bottom-up update rows on the split levels with the pivot COLUMNS split over the waves (the NAR path): a
+// workgroup = LRC_SR update rows of one front x one frequency group x one slice, its LRC_W waves each summing every
+// LRC_W-th chunk of LRC_SK pivot columns, the partial sums added in wave order through LDS (k_lsolve_rows_z: each
+// wave's rows walk all ns columns, a dependent load round per 8 columns).
+constexpr int LRC_SR = 4, LRC_SK = 8, LRC_W = 4;
+__global__ __launch_bounds__(64 * LRC_W) void k_lsolve_rows_zc(DevPattern P, LSlices S, const cplx* __restrict__ F,
+                                                              int64_t Fc, int RB) {
+  int bx;
+  const Ctx c = ctx_xcd(bx);
+  const int z = blockIdx.z;
+  const int slot = bx / RB, rb = bx % RB;
+  if (slot >= S.nf[z]) return;
+  const Front fr = P.fronts[S.lvl[z][slot]];
+  const int f = fr.f, ns = fr.ns;
+  const int i0 = ns + rb * LRC_SR;
+  if (i0 >= f) return;                          // the whole workgroup (the level's largest front sizes RB)
+  const cplx* __restrict__ base = F + fr.off * Fc + c.q;
+  cplx* __restrict__ wv = S.WV[z] + (int64_t)fr.row0 * Fc + c.q;
+#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+#define V(a) wv[(int64_t)(a) * Fc]
+  __shared__ cplx part[LRC_W][LRC_SR][64];
+  int ri[LRC_SR];
+  cplx acc[LRC_SR];
+#pragma unroll
+  for (int r = 0; r < LRC_SR; ++r) {
+    ri[r] = min(i0 + r, f - 1);
+    acc[r] = make_double2(0.0, 0.0);
+  }
+  for (int k0 = LRC_SK * c.w; k0 < ns; k0 += LRC_SK * LRC_W) {
+    cplx y[LRC_SK], e[LRC_SR][LRC_SK];
+#pragma unroll
+    for (int u = 0; u < LRC_SK; ++u) y[u] = V(min(k0 + u, ns - 1));
+#pragma unroll
+    for (int r = 0; r < LRC_SR; ++r)
+#pragma unroll
+      for (int u = 0; u < LRC_SK; ++u) e[r][u] = E(ri[r], min(k0 + u, ns - 1));
+#pragma unroll
+    for (int u = 0; u < LRC_SK; ++u) y[u] = cscale(y[u], k0 + u < ns ? 1.0 : 0.0);
+#pragma unroll
+    for (int r = 0; r < LRC_SR; ++r)
+#pragma unroll
+      for (int u = 0; u < LRC_SK; ++u) acc[r] = cfms(acc[r], e[r][u], y[u]);
+  }
+#pragma unroll
+  for (int r = 0; r < LRC_SR; ++r) part[c.w][r][c.lane] = acc[r];
+  __syncthreads();
+  if (c.w == 0) {
+#pragma unroll
+    for (int r = 0; r < LRC_SR; ++r)
+      if (i0 + r < f) {
+        cplx t = V(i0 + r);
+        for (int w = 0; w < LRC_W; ++w) t = cadd(t, part[w][r][c.lane]);
+        V(i0 + r) = t;
+      }
+  }
+#undef E
+#undef V
+}
+
 // v - sum_{b in [ns, f)} e[b * es] * X[ix[b]]: the update-row solution values are
 // gathered 8 at a time (one scalar index load, then 16 independent vector loads)
 __device__ __forceinline__ cplx offdiag_dot(cplx v, const cplx* __restrict__ e, int64_t es,
@@ -3222,7 +3281,7 @@ void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const 
 void launch_lsolve_multi(int rhs_mode, const DevPattern& P, int nslices, const int* const* lvl, const int* nf, int W,
                          int ngroups, const double2* F, int64_t Fc, double2* const* WV, const RhsDesc* rd,
                          double2* const* Y, const int* const* reach, hipStream_t st, int split, bool nar,
-                         int maxns) {
+                         int maxns, int maxf) {
   LSlices S{};
   int nmax = 0;
   for (int z = 0; z < nslices; ++z) {
@@ -3250,7 +3309,12 @@ void launch_lsolve_multi(int rhs_mode, const DevPattern& P, int nslices, const i
     else LAUNCH_DYN((k_lsolve_level_z<3, true>), g, b, lds, st, P, S, F, Fc, rs);
   } else if (rhs_mode == 0) LAUNCH(k_lsolve_level_z<0>, g, b, st, P, S, F, Fc, rs);
   else LAUNCH(k_lsolve_level_z<3>, g, b, st, P, S, F, Fc, rs);
-  if (rs) LAUNCH(k_lsolve_rows_z, dim3(nmax * split, ngroups, nslices), dim3(64 * SPLIT_W), st, P, S, F, Fc, split);
+  if (rs && nar) {
+    const int RB = (std::max(1, maxf - 1) + LRC_SR - 1) / LRC_SR;
+    LAUNCH(k_lsolve_rows_zc, dim3(nmax * RB, ngroups, nslices), dim3(64 * LRC_W), st, P, S, F, Fc, RB);
+  } else if (rs) {
+    LAUNCH(k_lsolve_rows_z, dim3(nmax * split, ngroups, nslices), dim3(64 * SPLIT_W), st, P, S, F, Fc, split);
+  }
 }
 
 void launch_fn_dot(const int2* rows, int nrows, const double2* F, const double2* Yb, const double2* const* Yk, int64_t Fc,

@@ -66,7 +66,8 @@ void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const 
 void launch_lsolve_multi(int rhs_mode, const DevPattern& P, int nslices, const int* const* lvl, const int* nf, int W,
                          int ngroups, const double2* F, int64_t Fc, double2* const* WV, const RhsDesc* rd,
                          double2* const* Y, const int* const* reach, hipStream_t st, int split, bool nar = false,
-                         int maxns = 0);   // nar (split > 1): pivot blocks in LDS (k_lsolve_level_z<., true>)
+                         int maxns = 0, int maxf = 0);   // nar (split > 1): pivot blocks in LDS, update rows
+                                                         // column-split (k_lsolve_level_z<., true>, k_lsolve_rows_zc)
 // functional from the bottom-up passes: partial dot products (FN_PARTS x 3 x Fc), the functional / loss
 // / cotangent from them (fcoef: 3 x Fc, G at the support rows), and L^-1 g = sum_k c_k L^-1 a_k in Yk[0]
 void launch_fn_dot(const int2* rows, int nrows, const double2* F, const double2* Yb, const double2* const* Yk, int64_t Fc,
