@@ -184,9 +184,10 @@ struct pfr_solver {
                                         // those whose largest pivot block has at least n pivots, 0 none, -1 auto
                                         // (default since round 3: 512-frequency sweeps +2.6 %, 4,096 unchanged)
   int fac_lds_wg = 160;                 // PFR_FAC_LDS_WG: auto mode threshold (workgroups of k_factor_sym)
-  int us2_nar = 1;                      // PFR_US2_NAR: both solve passes' pivot blocks in LDS, left-looking, on the
-                                        // split (few-workgroup) levels: k_usolve2_nar, k_lsolve_level_z<., true>
-                                        // (0: the right-looking global-memory forms)
+  int us2_nar = 256;                    // PFR_US2_NAR: solve launches with fewer (front, group) workgroups than this
+                                        // take the narrow-level forms -- pivot blocks in LDS, left-looking, the
+                                        // update parts with their columns split over the waves (k_usolve2_updc +
+                                        // k_usolve2_nar, k_lsolve_level_z<., true> + k_lsolve_rows_zc); 0: never
   int split_target = 256;               // PFR_SOLVE_SPLIT: solve launches with fewer (front, group) workgroups
                                         // than this (one per CU) split their update parts up to about this
                                         // many workgroups (0: off)
@@ -484,8 +485,10 @@ int fn_bottom_up(pfr_solver* s, int rhs_mode, const pfr::RhsDesc& rf, hipStream_
     }
     const int nmax = std::max(nf[0], nf[1]);
     if (nmax == 0) continue;
+    const int nsum = nf[0] + 3 * nf[1];
+    const bool nar = (int64_t)nsum * ngroups < s->us2_nar && pfr::ls_nar_fits(s->level_maxns[l]);
     pfr::launch_lsolve_multi(rhs_mode, s->P, 4, lvl, nf, solve_W(s, l, nmax), ngroups, s->F, s->Fc, WV, rd, Y, reach,
-                             st, solve_split(s, nf[0] + 3 * nf[1]), s->us2_nar && pfr::ls_nar_fits(s->level_maxns[l]),
+                             st, nar ? std::max(2, solve_split(s, nsum)) : solve_split(s, nsum), nar,
                              s->level_maxns[l], s->level_maxf[l]);
   }
   HIP_TRY(hipGetLastError());
@@ -515,10 +518,11 @@ int sym_top_down_pair(pfr_solver* s, hipStream_t st, bool fwd_all = false) {
     const int nf = s->level_ptr[l + 1] - s->level_ptr[l];
     const bool small = s->level_maxf[l] <= s->us2_small;
     const int tiny = s->us2_tiny > 0 && s->level_maxns[l] <= s->us2_tiny ? (s->level_maxns[l] <= 4 ? 4 : 8) : 0;
-    const bool nar = s->us2_nar && pfr::us2_nar_lds(s->level_maxns[l]) <= pfr::LDS_BYTES;
+    const bool nar = (int64_t)nf * ngroups < s->us2_nar && pfr::us2_nar_lds(s->level_maxns[l]) <= pfr::LDS_BYTES;
     pfr::launch_usolve2(s->P, s->d_level_fronts + s->level_ptr[l], nf, solve_W(s, l, nf), small, ngroups, s->F, s->Fc,
                         s->Y, s->X, s->d_reach[0], fwd_all ? nullptr : s->d_reach[1], s->Y2, s->XA, s->d_reach[1], st,
-                        solve_split(s, nf), tiny, nar, s->level_maxns[l]);
+                        nar ? std::max(2, solve_split(s, nf)) : solve_split(s, nf), nar ? 0 : tiny, nar,
+                        s->level_maxns[l]);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
@@ -744,7 +748,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->fac_wmax = knob("PFR_FAC_WMAX", 16, 1, 16);
   s->us2_small = knob("PFR_US2_SMALL", 110, 0, pfr::MAX_FRONT);
   s->split_target = knob("PFR_SOLVE_SPLIT", 256, 0, 1 << 20);
-  s->us2_nar = knob("PFR_US2_NAR", 1, 0, 1);
+  s->us2_nar = knob("PFR_US2_NAR", 256, 0, 1 << 30);
   s->fac_lds = knob("PFR_FAC_LDS", -1, -1, 64);
   s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);
   s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);

@@ -173,7 +173,8 @@ def test_c2_forward_sweep_matches_truth():
     {"PFR_US2_TINY": "8"},             # paired top-down pass one wave per front where pivot blocks are <= 8
     {"PFR_OFF_PU_WAVES": "1000000000"},   # the pipelined L21 prefix on every launch
     {"PFR_US2_TINY": "0"},
-    {"PFR_US2_NAR": "0"},               # the split levels' pivot blocks right-looking from global memory
+    {"PFR_US2_NAR": "0"},               # the narrow-level solve forms never (right-looking, global memory)
+    {"PFR_US2_NAR": "1000000000"},      # ... on every level whose pivot block fits the LDS
 ])
 def test_kernel_variants_match_oracle(env, monkeypatch):
     from oracle.plate_oracle import loss_and_grad
