@@ -142,8 +142,6 @@ struct pfr_solver {
   int scale_corr = 1;                   // PFR_SCALE_CORR: the solve-error scale of the loss sweeps' cotangent
   int us2_tiny = 8;                     // PFR_US2_TINY (0 / 4 / 8): levels whose pivot blocks are <= this, one wave per front
   int off_pu_waves = 0;                 // PFR_OFF_PU_WAVES: L21 launches with fewer waves run the pipelined prefix
-  int off_nar_waves = 0;                // PFR_OFF_NAR_WAVES: L21 launches with fewer waves: a workgroup per item,
-                                        // the prefix split over its waves (k_offdiag_nar)
   int32_t* flags = nullptr;
   // operator / rhs / functional / stiffness state
   const double2* K = nullptr;
@@ -333,8 +331,7 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     const int64_t owaves = (int64_t)(s->item_ptr[l + 1] - s->item_ptr[l]) * ngroups;
     pfr::launch_offdiag(mode, s->P, s->d_items + s->item_ptr[l], s->item_ptr[l + 1] - s->item_ptr[l], s->d_orec,
                         s->d_oxp + s->item_ptr[l], s->d_ox, ngroups, s->F, s->Fc, s->freqs, s->K, s->M, data, ds,
-                        nvalid, s->level_maxns[l], st, s->sym && owaves < s->off_pu_waves,
-                        s->sym && mode == 0 && owaves < s->off_nar_waves);
+                        nvalid, s->level_maxns[l], st, s->sym && owaves < s->off_pu_waves);
     mark(l, 3);
     pfr::launch_schur_blk(s->P, s->d_blocks + s->blk_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
                           s->d_bg1 + (int64_t)s->blk_ptr[l] * 16 * 16, s->d_bgxp + s->blk_ptr[l], s->d_bgx, ngroups, s->F,
@@ -768,7 +765,6 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   // levels of C4's per-rank sweeps: 512 frequencies 35.3-35.7k -> 36.2-36.6k freq-solves/s; 2,048-frequency
   // chunks unchanged, profiles/r04/offdiag_layout/pu3_*)
   s->off_pu_waves = knob("PFR_OFF_PU_WAVES", s->Fc <= 1024 ? 8000 : 0, 0, 1 << 30);
-  s->off_nar_waves = knob("PFR_OFF_NAR_WAVES", 0, 0, 1 << 30);
   s->level_ptr = S.level_ptr;
   s->level_maxf = S.level_maxf;
   s->perm = S.perm;

@@ -844,106 +844,6 @@ __device__ __forceinline__ void offdiag_item(const DevPattern& P, const int4* __
   }
 }
 
-// L21 rows on the narrow levels (symmetric operator form): a WORKGROUP per item (OFF_RPL rows x 64 frequencies),
-// OFF_NW waves per row splitting each OB-column chunk's prefix sum over the pivots t < c0 (every OFF_NW-th pivot
-// each; all their loads independent of the chain), the partial sums added in wave order through LDS; the row's
-// first wave starts from the chunk's sources, adds the partials, solves the chunk's triangle and stores it, visible
-// to the next chunk's prefix after the barrier.  k_offdiag_level walks the whole prefix in one wave: c0 dependent
-// pivot steps per chunk, on levels whose launches have a few thousand waves.  Rounding differs from
-// k_offdiag_level (the prefix's summation order).
-constexpr int OFF_NW = 4;
-__global__ __launch_bounds__(64 * OFF_NW * OFF_RPL) void k_offdiag_nar(
-    DevPattern P, const int4* __restrict__ items, int nitems, const int2* __restrict__ orec, const int* __restrict__ oxp,
-    const int2* __restrict__ ox, cplx* __restrict__ F, int64_t Fc, const double* __restrict__ freqs,
-    const cplx* __restrict__ K, const double* __restrict__ M) {
-  static_assert(OFF_G == 1, "lane = frequency");
-  const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
-  const int wid = (int)(lid % gridDim.x), by = (int)(lid / gridDim.x);
-  if (wid >= nitems) return;
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int h = w / OFF_NW, wr = w % OFF_NW;    // this wave's row of the item, its share of the prefix
-  const int64_t q = (int64_t)by * 64 + lane;
-  const int4 it = items[wid];
-  const Front fr = P.fronts[it.x];
-  const int f = fr.f, ns = fr.ns;
-  cplx* __restrict__ base = F + fr.off * Fc + q;
-#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
-  const int idx = it.y + h;
-  const bool valid = idx < f;
-  const int64_t so = (int64_t)min(idx, f - 1) * f;   // own element c at so + c
-  OffSrc S;
-  S.rec[0] = orec + it.w + (int64_t)h * ns;
-  S.ox = ox;
-  S.ox0 = oxp[wid];
-  S.ox1 = oxp[wid + 1];
-  S.slot0 = h;
-  const double om = 6.283185307179586 * freqs[q];
-  S.om2 = om * om;
-  S.K = K;
-  S.M = M;
-  S.dq = nullptr;
-  __shared__ cplx part[OFF_RPL][OFF_NW - 1][OB][64];   // waves 1 .. NW-1 of each row (48 KiB)
-  for (int c0 = 0; c0 < ns; c0 += OB) {
-    const int kb = min(OB, ns - c0);
-    // 1. the row's first wave starts from the chunk's sources (original entries + children's update entries), the
-    //    others from zero; each subtracts its share of the prefix, sum_{t = wr, wr + NW, ... < c0} L(row, t) U(t, c0 + j)
-    cplx acc[OB];
-    if (wr == 0) {
-#pragma unroll
-      for (int j = 0; j < OB; ++j) acc[j] = off_source<0>(S, F, Fc, q, 0, c0 + min(j, kb - 1));
-      for (int e = S.ox0; e < S.ox1; ++e) {     // rare: several children cover one entry
-        const int2 g = S.ox[e];
-        const int c = g.x / (OFF_G * OFF_RPL) - c0, slot = g.x % (OFF_G * OFF_RPL);
-        if (c >= 0 && c < kb && slot == S.slot0) {
-          const cplx v = F[(int64_t)g.y * Fc + q];
-#pragma unroll
-          for (int j = 0; j < OB; ++j)
-            if (j == c) acc[j] = cadd(acc[j], v);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < OB; ++j) acc[j] = make_double2(0.0, 0.0);
-    }
-#pragma unroll 2
-    for (int t = wr; t < c0; t += OFF_NW) {
-      const cplx l = base[(so + t) * Fc];
-      cplx u[OB];
-#pragma unroll
-      for (int j = 0; j < OB; ++j) u[j] = E(t, c0 + min(j, kb - 1));
-#pragma unroll
-      for (int j = 0; j < OB; ++j) acc[j] = cfms(acc[j], l, u[j]);
-    }
-    if (wr > 0) {
-#pragma unroll
-      for (int j = 0; j < OB; ++j) part[h][wr - 1][j][lane] = acc[j];
-    }
-    __syncthreads();
-    if (wr == 0) {
-      // 2. + the other waves' partials (wave order), then the chunk's triangle, stored
-#pragma unroll
-      for (int v = 0; v < OFF_NW - 1; ++v)
-#pragma unroll
-        for (int j = 0; j < OB; ++j) acc[j] = cadd(acc[j], part[h][v][j][lane]);
-#pragma unroll
-      for (int j = 0; j < OB; ++j) {
-        const int cj = c0 + min(j, kb - 1);
-#pragma unroll
-        for (int a = 0; a < OB; ++a)
-          if (a < j) acc[j] = cfms(acc[j], acc[a], E(c0 + min(a, kb - 1), cj));
-        acc[j] = cmul(acc[j], crecip(E(cj, cj)));
-      }
-      if (valid) {
-#pragma unroll
-        for (int j = 0; j < OB; ++j)
-          if (j < kb) base[(so + c0 + j) * Fc] = acc[j];
-      }
-    }
-    __syncthreads();
-  }
-#undef E
-}
-
 // XCD-aware order: a frequency group's items on one XCD, sharing its L2
 template <int MODE, bool SMALL, int PU = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMALL ? 5 : 1))) void k_offdiag_level(
@@ -3321,15 +3221,9 @@ void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, i
 
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
                     const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,
-                    const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st, bool pipelined,
-                    bool nar) {
+                    const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st, bool pipelined) {
   if (nitems <= 0) return;
   const bool small = maxns <= 8;
-  if (mode == 0 && !small && nar) {
-    LAUNCH(k_offdiag_nar, dim3(nitems, ngroups), dim3(64 * OFF_NW * OFF_RPL), st, P, items, nitems, orec, oxp, ox, F, Fc,
-           freqs, K, M);
-    return;
-  }
   dim3 g((nitems + 3) / 4, ngroups * OFF_G), b(256);
   static_assert(OB >= 8, "the SMALL variant covers pivot blocks of up to 8");
 #define OL(MD, SM, PU) LAUNCH((k_offdiag_level<MD, SM, PU>), g, b, st, P, items, nitems, orec, oxp, ox, F, Fc, freqs, K, M, data, ds, nvalid)

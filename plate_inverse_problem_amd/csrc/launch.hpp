@@ -45,7 +45,7 @@ void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int max
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
                     const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,
                     const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st,
-                    bool pipelined = false, bool nar = false);   // nar: a workgroup per item (k_offdiag_nar)
+                    bool pipelined = false);
 // Schur complement A22 -= L21 U12 for a level's tile list (TM x TN = 4 x 4 tiles)
 void launch_schur(bool sym, const DevPattern& P, const int4* tiles, int ntiles, const int* g1, const int* gxp,
                   const int2* gx, int ngroups, double2* F, int64_t Fc, hipStream_t st);

@@ -172,7 +172,6 @@ def test_c2_forward_sweep_matches_truth():
     {"PFR_SCALE_CORR": "0"},           # the cotangent without the solve-error scale
     {"PFR_US2_TINY": "8"},             # paired top-down pass one wave per front where pivot blocks are <= 8
     {"PFR_OFF_PU_WAVES": "1000000000"},   # the pipelined L21 prefix on every launch
-    {"PFR_OFF_NAR_WAVES": "1000000000"},  # L21 rows a workgroup per item, the prefix split over its waves
     {"PFR_US2_TINY": "0"},
     {"PFR_US2_NAR": "0"},               # the narrow-level solve forms never (right-looking, global memory)
     {"PFR_US2_NAR": "1000000000"},      # ... on every level whose pivot block fits the LDS
