@@ -489,8 +489,7 @@ int fn_bottom_up(pfr_solver* s, int rhs_mode, const pfr::RhsDesc& rf, hipStream_
     const int nsum = nf[0] + 3 * nf[1];
     const bool nar = (int64_t)nsum * ngroups < s->ls_nar && pfr::ls_nar_fits(s->level_maxns[l]);
     pfr::launch_lsolve_multi(rhs_mode, s->P, 4, lvl, nf, solve_W(s, l, nmax), ngroups, s->F, s->Fc, WV, rd, Y, reach,
-                             st, nar ? std::max(2, solve_split(s, nsum)) : solve_split(s, nsum), nar,
-                             s->level_maxns[l], s->level_maxf[l]);
+                             st, solve_split(s, nsum), nar, s->level_maxns[l], s->level_maxf[l]);
   }
   HIP_TRY(hipGetLastError());
   return PFR_OK;
