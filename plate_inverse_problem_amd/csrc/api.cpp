@@ -183,8 +183,6 @@ struct pfr_solver {
   int fac_lds = -1;                     // PFR_FAC_LDS: which levels factor A11 in LDS (k_factor_sym_lds): n > 0
                                         // those whose largest pivot block has at least n pivots, 0 none, -1 auto
                                         // (default since round 3: 512-frequency sweeps +2.6 %, 4,096 unchanged)
-  int fac_sb16 = 0;                     // PFR_FAC_SB16: levels whose largest pivot block has at least this many pivots
-                                        // factor A11 in 16-pivot super-blocks (0: never)
   int fac_lds_wg = 160;                 // PFR_FAC_LDS_WG: auto mode threshold (workgroups of k_factor_sym)
   int us2_nar = 256;                    // PFR_US2_NAR / PFR_LS_NAR: paired top-down / bottom-up launches with fewer
   int ls_nar = 256;                     // (front, group) workgroups than this take the narrow-level forms -- pivot
@@ -328,8 +326,7 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     if (level_lds(s, l))
       pfr::launch_factor_lds(s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_maxns[l], s->F, s->Fc, s->flags, st);
     else
-      pfr::launch_factor(s->sym, s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st,
-                         s->fac_sb16 > 0 && s->level_maxns[l] >= s->fac_sb16);
+      pfr::launch_factor(s->sym, s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st);
     mark(l, 2);
     // the software-pipelined L21 prefix on the launches with few waves (symmetric analyses, operator form)
     const int64_t owaves = (int64_t)(s->item_ptr[l + 1] - s->item_ptr[l]) * ngroups;
@@ -754,7 +751,6 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->us2_nar = knob("PFR_US2_NAR", 256, 0, 1 << 30);
   s->ls_nar = knob("PFR_LS_NAR", 256, 0, 1 << 30);
   s->fac_lds = knob("PFR_FAC_LDS", -1, -1, 64);
-  s->fac_sb16 = knob("PFR_FAC_SB16", 0, 0, 1 << 20);
   s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);
   s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);
   s->scale_corr = knob("PFR_SCALE_CORR", 1, 0, 1);

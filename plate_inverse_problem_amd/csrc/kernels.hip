@@ -393,7 +393,6 @@ constexpr int FAC_SB = 2;    // 4-pivot blocks per super-block (rank of the trai
 
 // One front's A11 LU for the 64 / FAC_G frequencies of c.q's lane group: c.w / c.W the wave's index and count
 // among the waves working on these frequencies (every wave of the workgroup reaches the same barriers)
-template <int SB = FAC_SB>
 __device__ __forceinline__ void factor_sym_front(const DevPattern& P, int front, cplx* __restrict__ F, int64_t Fc,
                                                  int* __restrict__ flags, const Ctx& c, int sub) {
   const Front fr = P.fronts[front];
@@ -464,7 +463,7 @@ __device__ __forceinline__ void factor_sym_front(const DevPattern& P, int front,
         }
     }
   };
-  constexpr int R = SB * KB;
+  constexpr int SB = FAC_SB, R = SB * KB;
   for (int k0 = 0; k0 < ns; k0 += R) {
     const int kr = min(R, ns - k0);
 #pragma unroll 1
@@ -502,10 +501,7 @@ __device__ __forceinline__ void factor_sym_front(const DevPattern& P, int front,
 #undef E
 }
 
-// SB = 4 (16-pivot super-blocks: the trailing triangle read and written once per 16 pivots instead of 8) on the levels
-// of large pivot blocks, at most 8 waves per workgroup (its rows' 16 L values and 16 U values in registers)
-template <int SB = FAC_SB>
-__global__ __launch_bounds__(SB > 2 ? 512 : 1024) void k_factor_sym(DevPattern P, const int* __restrict__ lvl, cplx* __restrict__ F,
+__global__ __launch_bounds__(1024) void k_factor_sym(DevPattern P, const int* __restrict__ lvl, cplx* __restrict__ F,
                                                int64_t Fc, int* __restrict__ flags) {
   Ctx c;
   c.lane = threadIdx.x & 63;
@@ -513,7 +509,7 @@ __global__ __launch_bounds__(SB > 2 ? 512 : 1024) void k_factor_sym(DevPattern P
   c.W = blockDim.x >> 6;
   constexpr int QG = 64 / FAC_G;     // frequencies per lane group
   c.q = (int64_t)blockIdx.y * QG + c.lane % QG;
-  factor_sym_front<SB>(P, lvl[blockIdx.x], F, Fc, flags, c, c.lane / QG);
+  factor_sym_front(P, lvl[blockIdx.x], F, Fc, flags, c, c.lane / QG);
 }
 
 // Symmetric A11 LU with the pivot block resident in LDS, for the levels of large pivot blocks (the
@@ -3218,10 +3214,8 @@ void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int max
 }
 
 void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F,
-                   int64_t Fc, int* flags, hipStream_t st, bool wide) {
-  if (sym && wide)
-    LAUNCH(k_factor_sym<4>, dim3(nfronts, ngroups * FAC_G), dim3(64 * std::min(W, 8)), st, P, lvl, F, Fc, flags);
-  else if (sym) LAUNCH(k_factor_sym<>, dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
+                   int64_t Fc, int* flags, hipStream_t st) {
+  if (sym) LAUNCH(k_factor_sym, dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
   else LAUNCH(k_factor_level<true>, dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
 }
 
