@@ -184,11 +184,12 @@ struct pfr_solver {
                                         // those whose largest pivot block has at least n pivots, 0 none, -1 auto
                                         // (default since round 3: 512-frequency sweeps +2.6 %, 4,096 unchanged)
   int fac_lds_wg = 160;                 // PFR_FAC_LDS_WG: auto mode threshold (workgroups of k_factor_sym)
-  int us2_nar = 256;                    // PFR_US2_NAR / PFR_LS_NAR: paired top-down / bottom-up launches with fewer
-  int ls_nar = 256;                     // (front, group) workgroups than this take the narrow-level forms -- pivot
+  int us2_nar = 256;                    // PFR_US2_NAR: solve launches (paired top-down, bottom-up chain) with fewer
+                                        // (front, group) workgroups than this take the narrow-level forms -- pivot
                                         // blocks in LDS, left-looking, the update parts with their columns split
                                         // over the waves (k_usolve2_updc + k_usolve2_nar, k_lsolve_level_z<., true>
-                                        // + k_lsolve_rows_zc); 0: never
+                                        // + k_lsolve_rows_zc); 0: never.  Measured best at 256 for both passes
+                                        // (1,024 / 4,096: no gain at 512 frequencies, slower at 4,096)
   int split_target = 256;               // PFR_SOLVE_SPLIT: solve launches with fewer (front, group) workgroups
                                         // than this (one per CU) split their update parts up to about this
                                         // many workgroups (0: off)
@@ -487,7 +488,7 @@ int fn_bottom_up(pfr_solver* s, int rhs_mode, const pfr::RhsDesc& rf, hipStream_
     const int nmax = std::max(nf[0], nf[1]);
     if (nmax == 0) continue;
     const int nsum = nf[0] + 3 * nf[1];
-    const bool nar = (int64_t)nsum * ngroups < s->ls_nar && pfr::ls_nar_fits(s->level_maxns[l]);
+    const bool nar = (int64_t)nsum * ngroups < s->us2_nar && pfr::ls_nar_fits(s->level_maxns[l]);
     pfr::launch_lsolve_multi(rhs_mode, s->P, 4, lvl, nf, solve_W(s, l, nmax), ngroups, s->F, s->Fc, WV, rd, Y, reach,
                              st, solve_split(s, nsum), nar, s->level_maxns[l], s->level_maxf[l]);
   }
@@ -749,7 +750,6 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->us2_small = knob("PFR_US2_SMALL", 110, 0, pfr::MAX_FRONT);
   s->split_target = knob("PFR_SOLVE_SPLIT", 256, 0, 1 << 20);
   s->us2_nar = knob("PFR_US2_NAR", 256, 0, 1 << 30);
-  s->ls_nar = knob("PFR_LS_NAR", 256, 0, 1 << 30);
   s->fac_lds = knob("PFR_FAC_LDS", -1, -1, 64);
   s->fn_dot = knob("PFR_FN_DOT", 1, 0, 1);
   s->contract_walk = knob("PFR_CONTRACT_WALK", 1, 0, 1);
