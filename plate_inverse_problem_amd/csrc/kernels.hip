@@ -512,14 +512,10 @@ __global__ __launch_bounds__(1024) void k_factor_sym(DevPattern P, const int* __
   factor_sym_front(P, lvl[blockIdx.x], F, Fc, flags, c, c.lane / QG);
 }
 
-// Symmetric A11 LU with the pivot block resident in LDS, for the levels of large pivot blocks (the
-// top of the elimination tree: few fronts, long pivot chains).  Workgroup = one front x QF consecutive
-// frequencies (QF = 4: a 64 B piece of each 128 B line; the workgroups of the two halves of a line are
-// neighbours in dispatch order, i.e. on the same XCD at the same time, so the line is fetched once);
-// the lower triangle of A11 (packed, idx(i, j) = i (i + 1) / 2 + j) is read once into LDS, factored
-// there in 4-pivot blocks (diagonal block, panel rows, trailing update of the lower triangle), and
-// written once: L11 below the diagonal, U11 = diag(U) L11^T above it, U(k, k) on it -- the same
-// entries k_factor_sym writes.  Thread t = (slot t / QF, frequency t % QF).
+// Symmetric A11 LU with the pivot block resident in LDS, for the levels where the frequency-minor kernel gets few
+// workgroups (the top of the elimination tree: few fronts, long pivot chains).  The lower triangle of A11 (packed,
+// idx(i, j) = i (i + 1) / 2 + j) is read once into LDS, factored there and written once: L11 below the diagonal,
+// U11 = diag(U) L11^T above it, U(k, k) on it -- the same entries k_factor_sym writes.
 __device__ __forceinline__ int tri_row(int e) {
   int i = (int)((sqrtf(8.0f * e + 1.0f) - 1.0f) * 0.5f);
   if ((i + 1) * (i + 2) / 2 <= e) ++i;
@@ -527,27 +523,37 @@ __device__ __forceinline__ int tri_row(int e) {
   return i;
 }
 
-template <int QF>
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+__device__ __forceinline__ cplx readlane_c(cplx v, int l) { return make_double2(readlane_d(v.x, l), readlane_d(v.y, l)); }
+
+// Workgroup = one front x one frequency, 4 waves; the packed lower triangle in LDS.  Per block of FAC_LB pivots:
+// wave 0 (lane = row, rows < 64) eliminates the block's pivots and forms the panel rows wave-synchronously -- each
+// lane holds its row's FAC_LB block entries in registers, the pivot and the pivot rows' entries broadcast by
+// v_readlane -- writing L(i, p) to the triangle and W(i, t) = U(p, p) L(i, p) to a column-major scratch; then all
+// threads update the trailing lower triangle, A(i, j) -= sum_t L(i, k0 + t) W(j, t).  Two barriers per 8 pivots.
+constexpr int FAC_LB = 8;
 __global__ __launch_bounds__(256) void k_factor_sym_lds(DevPattern P, const int* __restrict__ lvl,
                                                         cplx* __restrict__ F, int64_t Fc, int* __restrict__ flags,
                                                         int maxns) {
   extern __shared__ cplx sA[];
-  cplx* __restrict__ sW = sA + (int64_t)maxns * (maxns + 1) / 2 * QF;   // W(i, t) = U(k0 + t, k0 + t) L(i, k0 + t)
-  const int ngq = (int)(Fc / QF);
+  cplx* __restrict__ sW = sA + (int64_t)maxns * (maxns + 1) / 2;   // W(i, t) at sW[t * maxns + i]
   const int64_t lid = xcd_swizzle(blockIdx.x, gridDim.x);
-  const int slot = (int)(lid / ngq), qg = (int)(lid % ngq);
+  const int slot = (int)(lid / Fc);
+  const int64_t q = lid % Fc;
   const Front fr = P.fronts[lvl[slot]];
   const int f = fr.f, ns = fr.ns;
-  const int qq = threadIdx.x % QF, s = threadIdx.x / QF, S = blockDim.x / QF;
-  const int64_t q = (int64_t)qg * QF + qq;
+  const int tid = threadIdx.x, S = blockDim.x, lane = tid & 63;
   cplx* __restrict__ base = F + fr.off * Fc + q;
   const int nlow = ns * (ns + 1) / 2;
 #define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
-#define A(i, j) sA[(((i) * ((i) + 1)) / 2 + (j)) * QF + qq]
-#define W(i, t) sW[((i) * KB + (t)) * QF + qq]
-  // UB loads in flight per thread before their LDS stores (a plain loop waits for every load)
+#define A(i, j) sA[((i) * ((i) + 1)) / 2 + (j)]
+  // UB loads in flight per thread before their LDS stores
   constexpr int UB = 8;
-  for (int e0 = s; e0 < nlow; e0 += UB * S) {
+  for (int e0 = tid; e0 < nlow; e0 += UB * S) {
     cplx v[UB];
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
@@ -557,81 +563,57 @@ __global__ __launch_bounds__(256) void k_factor_sym_lds(DevPattern P, const int*
     }
 #pragma unroll
     for (int u = 0; u < UB; ++u)
-      if (e0 + u * S < nlow) sA[(e0 + u * S) * QF + qq] = v[u];
+      if (e0 + u * S < nlow) sA[e0 + u * S] = v[u];
   }
   __syncthreads();
-  for (int k0 = 0; k0 < ns; k0 += KB) {
-    const int kb = min(KB, ns - k0), k1 = k0 + kb;
-    if (s == 0) {
-      // diagonal block: L D L^T of the kb x kb lower triangle, in registers
-      cplx D[KB][KB];
+  for (int k0 = 0; k0 < ns; k0 += FAC_LB) {
+    const int kb = min(FAC_LB, ns - k0), k1 = k0 + kb;
+    if (tid < 64) {
+      // the block's pivots and the panel rows, lane = row (rows outside [k0, ns) hold clamped copies, never stored)
+      const int row = lane, ri = min(max(row, k0), ns - 1);
+      cplx a[FAC_LB];
 #pragma unroll
-      for (int i = 0; i < KB; ++i)
+      for (int t = 0; t < FAC_LB; ++t) a[t] = A(ri, min(k0 + t, ri));
 #pragma unroll
-        for (int j = 0; j <= i; ++j) D[i][j] = i < kb ? A(k0 + i, k0 + j) : make_double2(0.0, 0.0);
-#pragma unroll
-      for (int k = 0; k < KB; ++k)
-        if (k < kb) {
-          pivot_check(D[k][k], flags, q);
-          const cplx inv = crecip(D[k][k]);
-#pragma unroll
-          for (int i = k + 1; i < KB; ++i)
-            if (i < kb) {
-              const cplx lik = cmul(D[i][k], inv);
-#pragma unroll
-              for (int j = k + 1; j <= i; ++j) D[i][j] = cfms(D[i][j], lik, D[j][k]);   // D[j][k] still U-scaled
-            }
-#pragma unroll
-          for (int i = k + 1; i < KB; ++i)
-            if (i < kb) D[i][k] = cmul(D[i][k], inv);
-        }
-#pragma unroll
-      for (int i = 0; i < KB; ++i)
-#pragma unroll
-        for (int j = 0; j <= i; ++j)
-          if (i < kb) A(k0 + i, k0 + j) = D[i][j];
-    }
-    __syncthreads();
-    // panel rows: L(i, k0 + t) = (A(i, k0 + t) - sum_{u < t} L(i, k0 + u) U(k0 + u, k0 + t)) / U(k0 + t, k0 + t),
-    // U(u, t) = U(u, u) L(t, u); W(i, t) = U(k0 + t, k0 + t) L(i, k0 + t) for the trailing update
-    for (int i = k1 + s; i < ns; i += S) {
-      cplx l[KB], d[KB];
-#pragma unroll
-      for (int t = 0; t < KB; ++t) {
-        l[t] = t < kb ? A(i, k0 + t) : make_double2(0.0, 0.0);
-        d[t] = A(k0 + min(t, kb - 1), k0 + min(t, kb - 1));
-      }
-#pragma unroll
-      for (int t = 0; t < KB; ++t)
+      for (int t = 0; t < FAC_LB; ++t)
         if (t < kb) {
+          const int p = k0 + t;
+          const cplx d = readlane_c(a[t], p);
+          if (lane == 0) pivot_check(d, flags, q);
+          const cplx rd = crecip(d);
+          cplx b[FAC_LB];      // W(k0 + u, t): the pivot column's unscaled entries of the block rows below p
 #pragma unroll
-          for (int u = 0; u < t; ++u) l[t] = cfms(l[t], l[u], cmul(d[u], A(k0 + t, k0 + u)));
-          l[t] = cmul(l[t], crecip(d[t]));
-          A(i, k0 + t) = l[t];
-          W(i, t) = cmul(d[t], l[t]);
+          for (int u = t + 1; u < FAC_LB; ++u) b[u] = readlane_c(a[t], min(k0 + u, 63));
+          const cplx wt = a[t], lt = cmul(wt, rd);
+#pragma unroll
+          for (int u = t + 1; u < FAC_LB; ++u) a[u] = cfms(a[u], lt, b[u]);
+          if (row > p && row < ns) {
+            A(row, p) = lt;
+            sW[t * maxns + row] = wt;
+          } else if (row == p) {
+            A(p, p) = d;
+          }
         }
     }
     __syncthreads();
-    // trailing lower triangle: A(i, j) -= sum_t L(i, k0 + t) W(j, t), k1 <= j <= i
-    const int nt = ns - k1, ntl = nt * (nt + 1) / 2;
-    for (int e = s; e < ntl; e += S) {
-      const int ii = tri_row(e), i = k1 + ii, j = k1 + e - ii * (ii + 1) / 2;
-      cplx v = A(i, j);
+    // trailing lower triangle (a short block is the last one: kb = FAC_LB whenever k1 < ns)
+    const int m = ns - k1, nt = m * (m + 1) / 2;
+    for (int e = tid; e < nt; e += S) {
+      const int ii = tri_row(e), I = k1 + ii, J = k1 + e - ii * (ii + 1) / 2;
+      cplx v = A(I, J);
 #pragma unroll
-      for (int t = 0; t < KB; ++t)
-        if (t < kb) v = cfms(v, A(i, k0 + t), W(j, t));
-      A(i, j) = v;
+      for (int t = 0; t < FAC_LB; ++t) v = cfms(v, A(I, k0 + t), sW[t * maxns + J]);
+      A(I, J) = v;
     }
     __syncthreads();
   }
   // write back: L below the diagonal, U(k, k) on it, U(j, i) = U(j, j) L(i, j) above it
-  for (int e = s; e < nlow; e += S) {
+  for (int e = tid; e < nlow; e += S) {
     const int i = tri_row(e), j = e - i * (i + 1) / 2;
-    const cplx v = sA[e * QF + qq];
+    const cplx v = sA[e];
     E(i, j) = v;
     if (j < i) E(j, i) = cmul(A(j, j), v);
   }
-#undef W
 #undef A
 #undef E
 }
@@ -3204,13 +3186,13 @@ void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, cons
 void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int maxns, double2* F, int64_t Fc, int* flags,
                        hipStream_t st) {
   const size_t lds = (size_t)fac_lds_bytes(maxns);
-  static_assert(KB == 4, "fac_lds_bytes: 4 W columns per row");
+  static_assert(FAC_LB == 8, "fac_lds_bytes: 8 W columns per row");
   static const bool attr = [] {   // dynamic LDS beyond the default 64 KiB (up to 64 pivots: 37 KiB; headroom)
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_factor_sym_lds<1>),
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_factor_sym_lds),
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
   }();
   (void)attr;
-  LAUNCH_DYN(k_factor_sym_lds<1>, dim3((unsigned)(nfronts * Fc)), dim3(256), lds, st, P, lvl, F, Fc, flags, maxns);
+  LAUNCH_DYN(k_factor_sym_lds, dim3((unsigned)(nfronts * Fc)), dim3(256), lds, st, P, lvl, F, Fc, flags, maxns);
 }
 
 void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F,
