@@ -136,7 +136,7 @@ def test_c4_rank_block_at_c3_size():
         sel = np.arange(lo, hi)
         e = _check_set("c4_rank2_grad_truth", p, T, sel, theta)
         eng = p.engine()
-        assert eng.n_lanes == 1 and eng.max_batch == 512
+        assert eng.n_lanes == 2 and eng.max_batch == 256       # two lanes of 256 (Problem._lanes_for)
         assert eng.leaf_size_for(512) == 200 and eng.sym is eng._syms[200]
         assert eng.stats["n_levels"] < 38          # the shallow tree, not the deep one
         # fr at the fixture frequencies inside the block (forward sweep on the same engine)
