@@ -157,11 +157,14 @@ class _Engine:
         41.1k / 42.8k / 43.5k / 44.0k, 2,048 - / 49.8k / 51.4k / 52.7k.  Round 4 (current kernels, alternated
         runs, profiles/r04/experiments/leaf*.txt): 512 frequencies leaf 96 / 150 / 200 / 250 / 300: 32.2-33.4k /
         34.2k / 34.9-35.1k / 33.4k / 33.3-33.9k; 1,024 leaf 600 / 1,000 / 2,000 / 10,000: 43.2k / 45.8-46.1k / 46.7k /
-        44.5-44.9k; 2,048 leaf 1,000 / 2,000 / 10,000: 53.0k / 55.2k / 55.4-55.8k; 4,096: 10,000 best."""
+        44.5-44.9k; 2,048 leaf 1,000 / 2,000 / 10,000: 53.0k / 55.2k / 55.4-55.8k; 4,096: 10,000 best.  Round 5, with
+        512 frequencies on two lanes of 256: leaf 120 / 200 / 350 / 700 / 1,000 / 2,000 / 5,000 / 10,000: 36.1-36.2k /
+        36.8-37.0k / 36.7-37.2k / 36.8-36.9k / 37.9-38.4k / 36.2-38.0k / 38.1-38.3k / 33.5k; 1,024 leaf 1,000 / 2,000 /
+        5,000 / 10,000: 48.4-48.6k / 50.3-50.4k / 50.2-50.8k / 48.5k; 2,048: 5,000 = 10,000 (gpurun_out/r6_leaf*)."""
         if self._leaf_env is not None:
             return self._leaf_env
         n_freqs = max(1, n_freqs)
-        return 200 if n_freqs <= 512 else 2000 if n_freqs <= 1024 else 10000
+        return 200 if n_freqs <= 256 else 1000 if n_freqs <= 512 else 2000 if n_freqs <= 1024 else 10000
 
     def _use_symbolic(self, n_freqs: int) -> bool:
         """Select (building once) the symbolic analysis for a sweep width; True if it changed."""

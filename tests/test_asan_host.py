@@ -65,7 +65,8 @@ def _fnv(perm):
 # (leaf, ordering, symmetric, max_ns, md_delta, use_last)
 OPTION_SETS = [
     (10000, 0, 1, 256, 4, 0),   # the engine above 512 frequencies (deep MMD tree)
-    (200, 0, 1, 256, 4, 0),     # the engine up to 512 frequencies (C4's per-rank share)
+    (200, 0, 1, 256, 4, 0),     # the engine up to 256 frequencies
+    (1000, 0, 1, 256, 4, 0),    # the engine at 257-512 frequencies (C4's per-rank share)
     (2000, 0, 1, 256, 4, 0),    # the engine at 513-1,024 frequencies
     (96, 0, 1, 256, 4, 0),      # the width rule of round 3 at <= 512
     (16, 0, 1, 256, 4, 0),

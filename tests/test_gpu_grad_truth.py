@@ -14,8 +14,8 @@ gradient.  Bound: the GPU partials, the theta gradient and the loss within W_RTO
 truth, absolute (no allowance from the oracle's own error; VERDICT round 3 asked for 2e-7).
 
 C4 (BASELINE.json configs[3]): a rank of the 8-GPU run sweeps the 512-frequency block
-``shard_range(4096, r, 8)``; a fresh engine sized for it takes the narrow-sweep path (1 lane, the
-leaf-200 ordering, one 512-frequency chunk, the A11 LU in LDS on its few-workgroup levels).  Block 2
+``shard_range(4096, r, 8)``; a fresh engine sized for it takes the narrow-sweep path (2 lanes of 256, the
+leaf-1,000 ordering, the A11 LU in LDS on its few-workgroup levels).  Block 2
 holds the resonance (sample 1179).
 """
 import gc
@@ -137,7 +137,7 @@ def test_c4_rank_block_at_c3_size():
         e = _check_set("c4_rank2_grad_truth", p, T, sel, theta)
         eng = p.engine()
         assert eng.n_lanes == 2 and eng.max_batch == 256       # two lanes of 256 (Problem._lanes_for)
-        assert eng.leaf_size_for(512) == 200 and eng.sym is eng._syms[200]
+        assert eng.leaf_size_for(512) == 1000 and eng.sym is eng._syms[1000]
         assert eng.stats["n_levels"] < 38          # the shallow tree, not the deep one
         # fr at the fixture frequencies inside the block (forward sweep on the same engine)
         inside = (F["index"] >= lo) & (F["index"] < hi)
@@ -149,7 +149,7 @@ def test_c4_rank_block_at_c3_size():
         report("c4_rank2_fr_vs_truth", gpu_max=err.max(), oracle_max=err_o.max(), n=int(inside.sum()),
                **{k: v for k, v in e.items() if k != "n"})
         # absolute FR_RTOL_C3 at every fixture frequency (round 4 needed max(1e-7, 2x the oracle's error) for the
-        # leaf-200 ordering's 1.04e-7 at 200 Hz; the compensated residual of the functional correction makes the
+        # leaf-200 ordering's 1.04e-7 at 200 Hz, since round 5 at 1,000; the compensated residual of the functional correction makes the
         # corrected fr independent of the factorisation's rounding order)
         assert np.all(err < FR_RTOL_C3), (err, err_o)
     finally:
