@@ -194,7 +194,10 @@ class _Engine:
         per_lane = -(-n_freqs // n_lanes)
         free, _ = torch.cuda.mem_get_info(self.device)
         free += sum(self.sym.workspace_bytes(sv.max_batch) for sv in self.solvers)   # ours, if rebuilt
-        cap = max(64, min(4096, int(0.85 * free / n_lanes / self.sym.workspace_bytes(64)) * 64))
+        per64 = self.sym.workspace_bytes(64)
+        if getattr(self, "check_mode", 0) & _native.PFR_CHECK_REFINE_ADJ:
+            per64 += self._sym_args[0] * 64 * 16     # the refinement's fr seed vector (n x Fc), allocated on first use
+        cap = max(64, min(4096, int(0.85 * free / n_lanes / per64) * 64))
         n_chunks = -(-per_lane // cap)
         return n_lanes, (-(-per_lane // n_chunks) + 63) // 64 * 64
 
