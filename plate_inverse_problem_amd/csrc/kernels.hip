@@ -2447,10 +2447,7 @@ __device__ __forceinline__ cplx resid_entry(const ResidArgs& A, const cplx* __re
   return dq[nz];
 }
 
-// the fused walk at 5 waves/SIMD: 96 VGPRs + 56 B/lane of spills (round 3: 5 waves, 96 VGPRs, 9.5 -> 8.0 ms; round 5,
-// with the compensated residual: 4 waves at 114 VGPRs against 5 with the spills, the contract phase ~7-9 -> ~6-7 ms);
-// the 18-matrix walk (anisotropic materials) stays at 4 (5 would spill 320 B/lane)
-constexpr int RES_WPE = 5;
+constexpr int RES_WPE = 4;   // the fused walk at 114 VGPRs with the compensated residual (round 3: 5 waves/SIMD, 96 VGPRs, 9.5 -> 8.0 ms)
 // NSK > 0 (with DOT, the loss sweep's forward walk under the functional correction): the gradient
 // contraction rides on the walk -- every entry (p, j, nz) it visits has x_j gathered and mu_p loaded
 // already, so s_k(q) += S_k(nz) mu_p x_j per lane (frequency), per workgroup; the loss cotangent scale
@@ -2459,7 +2456,7 @@ constexpr int RES_WPE = 5;
 // CMP: the residual accumulated compensated (Dot2) -- the correction walk (DOT) and the refinement's residual (R):
 // both read the solve's own error, which a plain fp64 sum of the row's terms rounds away
 template <int MODE, int RHS, bool DOT = false, int NSK = 0, bool CMP = DOT>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSK > 12 ? 4 : NSK > 0 ? RES_WPE : 1))) void k_residual(ResidArgs A, const cplx* __restrict__ X, int64_t Fc,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSK > 0 ? RES_WPE : 1))) void k_residual(ResidArgs A, const cplx* __restrict__ X, int64_t Fc,
                                                   cplx* __restrict__ R, double* __restrict__ acc,
                                                   const cplx* __restrict__ Mu, cplx* __restrict__ cpart) {
   // XCD-aware order: the workgroups of one 64-frequency group run together on one XCD, so the
