@@ -62,9 +62,9 @@ PMC_FILE = (sorted(glob.glob(os.path.join(REPO, "profiles", "r[0-9][0-9]", "pmc_
             or [os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")])[-1]
 # kernel classes of the factorisation (libpfr per-class HIP-event timings, pfr_last_kernel_timings
 # order); the rocprof names of a class's kernels start with one of its prefixes
-KERNELS = (("k_assemble_level",), ("k_factor_level", "k_factor_sym"), ("k_offdiag_level",), ("k_schur_sym_blk",),
+KERNELS = (("k_assemble_level", "k_front0"), ("k_factor_level", "k_factor_sym"), ("k_offdiag_level",), ("k_schur_sym_blk",),
            ("k_schur_level", "k_schur_sym_level"))
-KERNEL_NAMES = ("k_assemble_level", "k_factor_level", "k_offdiag_level", "k_schur_sym_blk",
+KERNEL_NAMES = ("k_assemble_level + k_front0 (level 0 fused)", "k_factor_level", "k_offdiag_level", "k_schur_sym_blk",
                 "k_schur_sym_level / k_schur_level")
 # every launch of the triangular solves: level passes, split update parts, the sliced bottom-up chain and
 # the combination of its functional slices

@@ -62,6 +62,9 @@ struct pfr_solver {
   int4* d_tiles = nullptr;              // Schur tiles (front, i0, j0, 0), grouped by level
   int4* d_items = nullptr;              // off-diagonal panel items (front, first row/col, kind, record offset)
   int2* d_orec = nullptr;               // per item x lane group x pivot: (nz, first child source) of the entry
+  bool fused0 = false;                  // level 0 through k_front0 (Plan::fused0)
+  int n_f0 = 0, f0_small = 0;
+  int32_t *d_f0_front = nullptr, *d_f0_ptr = nullptr, *d_f0_nz = nullptr;
   int32_t* d_oxp = nullptr;             // per item: range of further child sources in d_ox
   int2* d_ox = nullptr;                 // (pivot * OFF_G OFF_RPL + row slot, element id)
   int32_t* d_g1 = nullptr;              // per super-tile, lane group, position: first child source (or -1)
@@ -311,6 +314,13 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
   for (int l = 0; l < L; ++l) {
     int nf = s->level_ptr[l + 1] - s->level_ptr[l];
     mark(l, 0);
+    if (l == 0 && s->fused0 && mode == 0) {
+      // the bottom level's leaf fronts in one pass (k_front0): A11, L21 and update block per frequency in registers
+      pfr::launch_front0(s->P, s->d_f0_front, s->n_f0, s->f0_small, s->d_f0_ptr, s->d_f0_nz, ngroups, s->F, s->Fc,
+                         s->freqs, s->K, s->M, s->flags, st);
+      for (int c = 1; c <= 5; ++c) mark(l, c);
+      continue;
+    }
     // panel: enough workgroups (front x 16 frequencies) to fill the chip -> one wave
     // each (no idle waves at the block barriers); few large fronts -> more waves
     // (symmetric kernel: up to 16 waves -- the top levels' few fronts are latency-bound, every
@@ -782,6 +792,9 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->asm_ptr = pl.asm_ptr;
   s->item_ptr = pl.item_ptr;
   s->lev_bytes = pl.lev_bytes;
+  s->fused0 = pl.fused0;
+  s->n_f0 = (int)pl.f0_front.size();
+  s->f0_small = pl.f0_small;
   Front* d_fronts = nullptr;
   int rc = PFR_OK;
   std::vector<Front> fv(S.fronts);
@@ -800,6 +813,9 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
       (rc = s->up_rec(&s->d_asm, pl.asm_rec, n4)) || (rc = s->up(&s->d_asm_xp, pl.asm_xp)) ||
       (rc = s->up_rec(&s->d_asm_x, pl.asm_x, z2)) || (rc = s->up_rec(&s->d_items, pl.items, z4)) ||
       (rc = s->up_rec(&s->d_orec, pl.orec, n2)) || (rc = s->up(&s->d_oxp, pl.oxp)) || (rc = s->up_rec(&s->d_ox, pl.ox, z2)))
+    return bail(rc);
+  if (s->fused0 && ((rc = s->up(&s->d_f0_front, pl.f0_front)) || (rc = s->up(&s->d_f0_ptr, pl.f0_ptr)) ||
+                    (rc = s->up(&s->d_f0_nz, pl.f0_nz))))
     return bail(rc);
   std::vector<int32_t> cp(colptr, colptr + S.n + 1), ri(rowind, rowind + S.nnz);
   if ((rc = s->up(&s->d_colptr, cp)) || (rc = s->up(&s->d_rowind, ri))) return bail(rc);

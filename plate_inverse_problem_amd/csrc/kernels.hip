@@ -840,6 +840,100 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SMALL ? 5 :
     offdiag_item<MODE, SMALL, PU>(P, items, wid, orec, oxp, ox, F, Fc, freqs, K, M, data, data_stride, nvalid, by);
 }
 
+// ------------------------------------------------------------------ K0: the bottom level fused
+// Level 0's ~3,000 leaf fronts (1-4 pivots, at most F0_RM update rows, no children) in ONE pass instead of the
+// four class launches: one wave per (front, 64 frequencies), four fronts per workgroup, everything in registers --
+// the panel's original entries (K - omega^2 M), the A11 LU (k_factor_sym's 4-pivot diagonal block), the L21 rows
+// (k_offdiag_level's column order) and the lower update block (k_schur_sym_level's pivot order), each stored once
+// and nothing read back.  Same operations in the same order as the four kernels: bit-for-bit the same factors.
+template <int NS>
+__global__ __launch_bounds__(256) void k_front0(DevPattern P, const int* __restrict__ fl, int nfronts,
+                                                const int* __restrict__ fptr, const int* __restrict__ fnz,
+                                                cplx* __restrict__ F, int64_t Fc, const double* __restrict__ freqs,
+                                                const cplx* __restrict__ K, const double* __restrict__ M,
+                                                int* __restrict__ flags) {
+  static_assert(NS <= F0_NS && NS <= KB, "one diagonal block");
+  int bx;
+  const Ctx c = ctx_xcd(bx);
+  const int slot = bx * 4 + c.w;
+  if (slot >= nfronts) return;
+  const Front fr = P.fronts[fl[slot]];
+  const int f = fr.f, ns = fr.ns, r = f - ns;
+  const int* __restrict__ rec = fnz + fptr[slot];
+  const int nrec = ns * (ns + 1) / 2 + r * ns;
+  const double om = 6.283185307179586 * freqs[c.q];
+  const double om2 = om * om;
+  // every load unconditional from a clamped record, masked arithmetically
+  auto val = [&](int e) {
+    const int nz = rec[min(e, nrec - 1)];
+    const cplx k = K[max(nz, 0)];
+    const double m = M[max(nz, 0)];
+    return cscale(make_double2(fma(-om2, m, k.x), k.y), nz >= 0 ? 1.0 : 0.0);
+  };
+  cplx* __restrict__ base = F + fr.off * Fc + c.q;
+#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
+  cplx D[NS][NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i)
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+      const int a = max(min(i, ns - 1), min(j, ns - 1)), b = min(min(i, ns - 1), min(j, ns - 1));
+      D[i][j] = val(a * (a + 1) / 2 + b);
+    }
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    if (k < ns) {
+      pivot_check(D[k][k], flags, c.q);
+      const cplx inv = crecip(D[k][k]);
+#pragma unroll
+      for (int i = k + 1; i < NS; ++i) {
+        D[i][k] = cmul(D[i][k], inv);
+#pragma unroll
+        for (int j = k + 1; j < NS; ++j) D[i][j] = cfms(D[i][j], D[i][k], D[k][j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NS; ++i)
+#pragma unroll
+    for (int j = 0; j < NS; ++j)
+      if (i < ns && j < ns) E(i, j) = D[i][j];
+  // L21 rows: L(i, t) = (A(i, t) - sum_{s < t} L(i, s) U(s, t)) / U(t, t); columns past ns zero
+  const int e0 = ns * (ns + 1) / 2;
+  cplx L[F0_RM][NS];
+#pragma unroll
+  for (int i = 0; i < F0_RM; ++i) {
+#pragma unroll
+    for (int t = 0; t < NS; ++t) L[i][t] = val(e0 + min(i, max(r - 1, 0)) * ns + min(t, ns - 1));
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+#pragma unroll
+      for (int s = 0; s < t; ++s) L[i][t] = cfms(L[i][t], L[i][s], D[s][t]);
+      // columns past ns: the clamped copies' "pivot" can be 0 (a multiplicative mask would keep the NaN)
+      const cplx lt = cmul(L[i][t], crecip(t < ns ? D[t][t] : make_double2(1.0, 0.0)));
+      L[i][t] = t < ns ? lt : make_double2(0.0, 0.0);
+    }
+#pragma unroll
+    for (int t = 0; t < NS; ++t)
+      if (i < r && t < ns) E(ns + i, t) = L[i][t];
+  }
+  // the update block, lower: A22(i, j) = - sum_t (L(i, t) U(t, t)) L(j, t)
+#pragma unroll
+  for (int i = 0; i < F0_RM; ++i) {
+    cplx lu[NS];
+#pragma unroll
+    for (int t = 0; t < NS; ++t) lu[t] = cmul(L[i][t], t < ns ? D[t][t] : make_double2(0.0, 0.0));
+#pragma unroll
+    for (int j = 0; j <= i; ++j) {
+      cplx acc = make_double2(0.0, 0.0);
+#pragma unroll
+      for (int t = 0; t < NS; ++t) acc = cfms(acc, lu[t], L[j][t]);
+      if (i < r) E(ns + i, ns + j) = acc;
+    }
+  }
+#undef E
+}
+
 // ------------------------------------------------------------------ K2b: Schur complement
 // A22 -= L21 U12 over all ns pivots of the front: one wavefront per TM x TN tile
 // of A22 (64 lanes = 64 frequencies), accumulators in registers, no stores in
@@ -3199,6 +3293,17 @@ void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, i
                    int64_t Fc, int* flags, hipStream_t st) {
   if (sym) LAUNCH(k_factor_sym, dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
   else LAUNCH(k_factor_level<true>, dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
+}
+
+void launch_front0(const DevPattern& P, const int* fl, int nfronts, int nsmall, const int* fptr, const int* fnz,
+                   int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K, const double* M,
+                   int* flags, hipStream_t st) {
+  if (nsmall > 0)
+    LAUNCH((k_front0<2>), dim3((nsmall + 3) / 4, ngroups), dim3(256), st, P, fl, nsmall, fptr, fnz, F, Fc, freqs, K,
+           M, flags);
+  if (nfronts > nsmall)
+    LAUNCH((k_front0<F0_NS>), dim3((nfronts - nsmall + 3) / 4, ngroups), dim3(256), st, P, fl + nsmall,
+           nfronts - nsmall, fptr + nsmall, fnz, F, Fc, freqs, K, M, flags);
 }
 
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,

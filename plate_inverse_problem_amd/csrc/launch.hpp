@@ -42,6 +42,10 @@ void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int max
                        hipStream_t st);
 // L21 rows (and U12 columns in general mode) of a level's items; pipelined: the software-pipelined prefix
 // (symmetric, operator-form launches with few waves)
+// the bottom level fused (k_front0, Plan::fused0): fl = level-0 fronts, the first nsmall with <= 2 pivots
+void launch_front0(const DevPattern& P, const int* fl, int nfronts, int nsmall, const int* fptr, const int* fnz,
+                   int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K, const double* M,
+                   int* flags, hipStream_t st);
 void launch_offdiag(int mode, const DevPattern& P, const int4* items, int nitems, const int2* orec, const int* oxp,
                     const int2* ox, int ngroups, double2* F, int64_t Fc, const double* freqs, const double2* K,
                     const double* M, const double2* data, int64_t ds, int nvalid, int maxns, hipStream_t st,

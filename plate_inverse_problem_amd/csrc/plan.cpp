@@ -163,6 +163,8 @@ int build_plan(const Symbolic& S, const PlanOptions& o, Plan& P, std::string& er
   P.item_ptr.assign(1, 0);
   std::vector<int32_t> nzm, s1m;
   std::vector<std::pair<int32_t, int32_t>> morem;   // (a * f + b, id)
+  bool ok0 = sym;
+  std::vector<std::pair<int32_t, std::vector<int32_t>>> f0;   // level-0 fronts: (front, records)
   for (int l = 0; l < L; ++l) {
     for (int e = S.level_ptr[l]; e < S.level_ptr[l + 1]; ++e) {
       const int t = S.level_fronts[e];
@@ -195,6 +197,16 @@ int build_plan(const Symbolic& S, const PlanOptions& o, Plan& P, std::string& er
         }
       }
       std::sort(morem.begin(), morem.end());
+      if (l == 0 && ok0) {
+        ok0 = ns <= F0_NS && f - ns <= F0_RM && morem.empty();
+        std::vector<int32_t> rec;
+        for (int a = 0; a < f && ok0; ++a)
+          for (int b = 0; b < std::min(a + 1, ns); ++b) {
+            ok0 = ok0 && s1m[(size_t)a * f + b] < 0;   // leaves: no child entries
+            rec.push_back(nzm[(size_t)a * f + b]);
+          }
+        if (ok0) f0.emplace_back(t, std::move(rec));
+      }
       for (int a = 0; a < ns; ++a)
         for (int b = 0; b < (sym ? a + 1 : ns); ++b) {   // symmetric: A11's lower triangle only
           const int k = (int)(P.asm_rec.size() % 8);
@@ -227,6 +239,19 @@ int build_plan(const Symbolic& S, const PlanOptions& o, Plan& P, std::string& er
     P.item_ptr.push_back((int32_t)P.items.size());
   }
 
+  // ---- the fused bottom level
+  P.fused0 = ok0 && !f0.empty() && L > 0;
+  if (P.fused0) {
+    std::stable_partition(f0.begin(), f0.end(), [&](const auto& x) { return S.fronts[x.first].ns <= 2; });
+    P.f0_ptr.assign(1, 0);
+    for (const auto& x : f0) {
+      P.f0_front.push_back(x.first);
+      P.f0_nz.insert(P.f0_nz.end(), x.second.begin(), x.second.end());
+      P.f0_ptr.push_back((int32_t)P.f0_nz.size());
+      P.f0_small += S.fronts[x.first].ns <= 2;
+    }
+  }
+
   // ---- algorithmic bytes per frequency and level of classes 0-4 (16 B per complex entry loaded or stored)
   P.lev_bytes.assign(L, std::array<int64_t, NKC>{});
   for (int t = 0; t < nfr; ++t) {
@@ -255,6 +280,14 @@ int build_plan(const Symbolic& S, const PlanOptions& o, Plan& P, std::string& er
     g = 0;
     for (size_t x = (size_t)P.tile_ptr[l] * SCHUR_TILE; x < (size_t)P.tile_ptr[l + 1] * SCHUR_TILE; ++x) g += P.g1[x] >= 0;
     b[4] += 16 * (g + P.gxp[P.tile_ptr[l + 1]] - P.gxp[P.tile_ptr[l]]);
+  }
+  if (P.fused0) {   // level 0 in one pass (class 0): A11 block, L21 rows and update block stored once, nothing read back
+    auto& b = P.lev_bytes[0];
+    b = {};
+    for (const int32_t t : P.f0_front) {
+      const int64_t ns = S.fronts[t].ns, r = S.fronts[t].f - ns;
+      b[0] += 16 * (ns * ns + r * ns + r * (r + 1) / 2);
+    }
   }
 
   // ---- symmetric mode: Dirichlet decoupling lists -- coupled rows (with their entries), per Dirichlet node the
@@ -426,6 +459,24 @@ std::string check_plan(const Symbolic& S, const Plan& P, int64_t Fc, int split_t
     if (P.gx[x].x < 0 || P.gx[x].x >= SCHUR_TILE || P.gx[x].y < 0 || P.gx[x].y >= FE) return bad("tile extra", x, P.gx[x].y, FE);
   for (size_t x = 0; x < P.bgx.size(); ++x)
     if (P.bgx[x].x < 0 || P.bgx[x].x >= SCHUR_BLK_IDS || P.bgx[x].y < 0 || P.bgx[x].y >= FE) return bad("block extra", x, P.bgx[x].y, FE);
+  // the fused bottom level: every level-0 front listed once, <= 2-pivot fronts first, records of its panel
+  if (P.fused0) {
+    const int n0 = (int)P.f0_front.size();
+    if ((int)P.f0_ptr.size() != n0 + 1 || P.f0_ptr[0] != 0 || P.f0_ptr[n0] != (int)P.f0_nz.size() ||
+        n0 != S.level_ptr[1] - S.level_ptr[0] || P.f0_small < 0 || P.f0_small > n0)
+      return "fused level 0 lists";
+    for (int i = 0; i < n0; ++i) {
+      const int t = P.f0_front[i];
+      if (t < 0 || t >= (int)S.fronts.size()) return bad("fused level 0 front", i, t, (int64_t)S.fronts.size());
+      const Front& F = S.fronts[t];
+      const int r = F.f - F.ns;
+      if (F.level != 0 || F.ns > F0_NS || r > F0_RM || (F.ns <= 2) != (i < P.f0_small) ||
+          P.f0_ptr[i + 1] - P.f0_ptr[i] != F.ns * (F.ns + 1) / 2 + r * F.ns)
+        return bad("fused level 0 front", i, F.ns, r);
+    }
+    for (size_t x = 0; x < P.f0_nz.size(); ++x)
+      if (P.f0_nz[x] < -1 || P.f0_nz[x] >= S.nnz) return bad("fused level 0 nz", x, P.f0_nz[x], S.nnz);
+  }
   // per-level ranges monotone and complete
   if ((int)P.tile_ptr.size() != L + 1 || (int)P.blk_ptr.size() != L + 1 || (int)P.item_ptr.size() != L + 1 ||
       (int)P.asm_ptr.size() != L + 1)

@@ -78,6 +78,10 @@ inline int solve_waves(int level_w, int64_t nf, int64_t Fc, int wmax) {
   return (int)std::max<int64_t>(level_w, std::min<int64_t>(wmax, fill));
 }
 
+// The bottom level fused (k_front0): symmetric analyses whose level-0 fronts (leaves) all have at most F0_NS pivots
+// and F0_RM update rows -- per (front, frequency) A11, L21 and the update block formed in registers, one pass
+constexpr int F0_NS = 4, F0_RM = 10;
+
 struct PlanOptions {
   int blk_min = 24;      // PFR_SCHUR_BLK_MIN: update blocks of at least this many rows through the block kernel
 };
@@ -103,6 +107,10 @@ struct Plan {
   std::vector<I4> items;
   std::vector<I2> orec;
   std::vector<int32_t> oxp, item_ptr;
+  bool fused0 = false;                   // level 0 through k_front0 (operator-form sweeps)
+  int f0_small = 0;                      // the first f0_small listed fronts have <= 2 pivots
+  std::vector<int32_t> f0_front, f0_ptr; // level-0 fronts (<= 2 pivots first); their first record
+  std::vector<int32_t> f0_nz;            // per front: A11 lower (a >= b) then the L21 rows: original nz or -1
   std::vector<I2> ox;                    // (pivot * OFF_G OFF_RPL + row slot, element id)
   // algorithmic bytes per frequency, level and kernel class (operator-form sweeps)
   std::vector<std::array<int64_t, NKC>> lev_bytes;
