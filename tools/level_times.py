@@ -8,7 +8,7 @@ import csv
 import sys
 
 
-LU = ("k_factor_sym", "k_factor_sym_lds", "k_factor_level")
+LU = ("k_factor_sym", "k_factor_sym_lds", "k_factor_level", "k_front0")   # k_front0: the fused bottom level
 
 
 def main(path, L=None):
@@ -18,7 +18,7 @@ def main(path, L=None):
     # one A11 LU launch per level (the assembly may be fused into it): the level marker; the level count is
     # that of the last sweep (k_pad_freqs starts every chunk)
     pads = [i for i, n in enumerate(names) if n == "k_pad_freqs"]
-    lus = [i for i, n in enumerate(names) if n in LU]
+    lus = [i for i, n in enumerate(names) if n in LU and not (n == "k_front0" and names[i - 1] == "k_front0")]
     if L is None:
         L = sum(1 for i in lus if i > pads[-1]) if pads else 17
     st = lus[-L]
@@ -29,11 +29,11 @@ def main(path, L=None):
     tab, lvl = {}, -1
     for i, (r, n) in enumerate(zip(rows[st:end], names[st:end])):
         if n in LU or (n == "k_assemble_level" and (st + i + 1 >= end or names[st + i + 1] in LU)):
-            if not (n in LU and i > 0 and names[st + i - 1] == "k_assemble_level"):
+            if not (n in LU and i > 0 and names[st + i - 1] in ("k_assemble_level", "k_front0")):
                 lvl += 1
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
         t = tab.setdefault(n, {})
-        key = lvl if n.startswith(("k_assemble", "k_factor", "k_offdiag", "k_schur")) else "x"
+        key = lvl if n.startswith(("k_assemble", "k_factor", "k_offdiag", "k_schur", "k_front0")) else "x"
         t[key] = t.get(key, 0.0) + d
     print("%-20s %7s " % ("kernel", "total") + " ".join("%5d" % l for l in range(L)))
     for n, t in sorted(tab.items(), key=lambda kv: -sum(kv[1].values())):
