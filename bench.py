@@ -45,6 +45,7 @@ import argparse
 import glob
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -176,6 +177,26 @@ def gpu_parity(prob, sample, theta):
                        "frequencies; relative, max-norm over k"}
 
 
+def strong_proxy(headline, ny, steps=10, warmup=2):
+    """C4's per-rank work on this GPU, driver-timed: rank 0's block ``shard_range(4096, 0, 8)`` (512
+    frequencies; every rank's block has the same work) as a loss + gradient sweep on a fresh engine sized for
+    it, in a fresh process as a rank is (tools/strong_proxy.py --one).  share = its per-frequency rate over
+    the headline's; predicted_c4 = 8 x the per-rank rate (the 304-B all-reduce per step left out)."""
+    cmd = [sys.executable, os.path.join(REPO, "tools", "strong_proxy.py"), "--one", "512", "0", "--steps", str(steps),
+           "--warmup", str(warmup), "--ny", str(ny)]
+    t0 = time.perf_counter()
+    res = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, timeout=600)
+    if res.returncode != 0:
+        return {"error": f"tools/strong_proxy.py exited {res.returncode}"}
+    r = json.loads(res.stdout.strip().splitlines()[-1])
+    rate = r["freq_solves_per_s"]
+    return {"freqs_per_rank": 512, "value": rate, "unit": "freq-solves/s", "ms_per_step": r["ms_per_step"],
+            "steps": steps, "warmup": warmup, "share": rate / headline, "predicted_c4": 8 * rate,
+            "lanes": r["lanes"], "chunk": r["chunk"], "wall_s": time.perf_counter() - t0,
+            "measure": "rank 0's block of linspace(40, 600, 4096) for N = 8 (shard_range(4096, 0, 8)), loss + "
+                       "gradient per step, a fresh process and engine; share = per-rank rate / the headline's"}
+
+
 def timed(step, steps, warmup, world, device):
     """W untimed steps, then K steps bracketed by barrier + synchronize; max over ranks."""
     for _ in range(warmup):
@@ -206,6 +227,7 @@ def main():
     ap.add_argument("--weak", action="store_true", help="--freqs per GPU instead of in total")
     ap.add_argument("--ny", type=int, default=25, help="mesh cells across the width (25 -> 19,353 DOF)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-strong-proxy", action="store_true", help="skip the 512-frequency per-rank sweep (C4 share)")
     ap.add_argument("--chunk", type=int, default=None, help="frequencies per chunk (default: from free HBM)")
     args = ap.parse_args()
 
@@ -378,6 +400,8 @@ def main():
         el_w = timed(step_w, args.steps, args.warmup, world, device)
         out["weak"] = {"value": n_w / (el_w / args.steps), "ms_per_step": 1e3 * el_w / args.steps,
                        "freqs_per_gpu": args.freqs, "freqs_total": n_w}
+    if rank == 0 and world == 1 and not args.weak and args.freqs == 4096 and not args.no_strong_proxy:
+        out["strong_proxy"] = strong_proxy(value, args.ny)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"], sample = cpu_baseline(prob, freqs, ref, theta)
         out["parity"] = gpu_parity(prob, sample, theta)

@@ -114,6 +114,7 @@ class _Engine:
         self._fixed_batch = max_batch
         self.solvers, self.streams, self._pool = [], [], None
         self.n_lanes = 0
+        self._seeded = False
         self._sized_for = set()
         # the coefficient matrices contracted for the gradient: all 18, or the 12 of A and D when the
         # coupling coefficients B vanish identically (mid-plane symmetric materials: dB/dtheta = 0, so
@@ -134,7 +135,8 @@ class _Engine:
         self._ts = prob.accelerometer.transverse_sensitivity
         self.rhs = prob.vec
         self._coef_key = None
-        self.last_berr = None          # (F, 2) componentwise backward errors of the last sweep (device)
+        self.last_berr = None          # (F, 2) componentwise backward errors of the last sweep (device; a loss
+                                       # step's buffer is reused -- overwritten -- by the next loss step)
         self.last_flags = None         # its status flags (host)
         # backward-error checks of every solve (pfr_set_check) and the functional correction (fr to
         # second order in the solve's error, the accuracy of the reference's refined UMFPACK solves) by
@@ -193,15 +195,18 @@ class _Engine:
             return n_lanes, int(self._fixed_batch)
         per_lane = -(-n_freqs // n_lanes)
         free, _ = torch.cuda.mem_get_info(self.device)
-        free += sum(self.sym.workspace_bytes(sv.max_batch) for sv in self.solvers)   # ours, if rebuilt
+        n = self._sym_args[0]
+        # ours, if rebuilt: the workspaces, and the refinement's seed vectors the solvers already hold
+        free += sum(self.sym.workspace_bytes(sv.max_batch) + (n * sv.max_batch * 16 if self._seeded else 0)
+                    for sv in self.solvers)
         per64 = self.sym.workspace_bytes(64)
         if getattr(self, "check_mode", 0) & _native.PFR_CHECK_REFINE_ADJ:
-            per64 += self._sym_args[0] * 64 * 16     # the refinement's fr seed vector (n x Fc), allocated on first use
+            per64 += n * 64 * 16     # the refinement's fr seed vector (n x Fc), allocated on first use
         cap = max(64, min(4096, int(0.85 * free / n_lanes / per64) * 64))
         n_chunks = -(-per_lane // cap)
         return n_lanes, (-(-per_lane // n_chunks) + 63) // 64 * 64
 
-    def ensure(self, n_freqs: int):
+    def ensure(self, n_freqs: int, refit: bool = False):
         """Size the lanes for a sweep of ``n_freqs`` frequencies.  The solvers are rebuilt only when
         the sweep needs more lanes or larger chunks than the current ones have (a small first call
         must not pin 1 lane and 64-frequency chunks on every later large sweep); smaller sweeps run
@@ -209,7 +214,7 @@ class _Engine:
         elimination tree (a C4 rank, whose engine is first sized for its 512-frequency share, gets the
         shallow narrow-sweep tree; a 512-frequency sweep after a 4,096-frequency one runs on the deep
         tree, correct but slower)."""
-        if self.solvers:
+        if self.solvers and not refit:
             per_lane = -(-max(1, n_freqs) // self.n_lanes)
             if n_freqs in self._sized_for or (self._lanes_for(n_freqs) <= self.n_lanes and per_lane <= self.max_batch):
                 return
@@ -218,10 +223,17 @@ class _Engine:
         if self.solvers:
             self._use_symbolic(n_freqs)   # a rebuild for a wider sweep may take a deeper ordering
         lanes, batch = self._shape_for(n_freqs)
-        if self.solvers and lanes <= self.n_lanes and batch <= self.max_batch and self.sym is old:
-            return
-        lanes = max(lanes, self.n_lanes)
-        batch = max(batch, self.max_batch if self.solvers else 0)
+        if refit:
+            # re-sized for what now has to fit beside the workspaces (set_check adding the refinement's seed
+            # vectors): smaller chunks only when the current ones no longer fit
+            if self.solvers and batch >= self.max_batch:
+                return
+            lanes = max(lanes, self.n_lanes)
+        else:
+            if self.solvers and lanes <= self.n_lanes and batch <= self.max_batch and self.sym is old:
+                return
+            lanes = max(lanes, self.n_lanes)
+            batch = max(batch, self.max_batch if self.solvers else 0)
         if self.solvers:
             torch.cuda.synchronize(self.device)
         self.solvers, self.streams = [], []       # free the old workspaces before allocating
@@ -230,6 +242,7 @@ class _Engine:
             self._pool = None
         self.n_lanes = lanes
         self.solvers = [_native.Solver(self.sym, self.device.index, batch) for _ in range(lanes)]
+        self._seeded = False           # no refinement seed vector allocated in the new solvers yet
         self.streams = [torch.cuda.Stream(self.device) for i in range(lanes)]
         if lanes > 1 and os.environ.get("PFR_PAR_LAUNCH", "1") != "0":
             from concurrent.futures import ThreadPoolExecutor
@@ -243,13 +256,19 @@ class _Engine:
         self._coef_key = None          # new solvers: rhs scale not set yet
 
     def set_check(self, mode: int | None = None, tol: float | None = None):
-        """Backward-error check mode (PFR_CHECK_* bits) and flag tolerance of every lane."""
+        """Backward-error check mode (PFR_CHECK_* bits) and flag tolerance of every lane.  Turning on the
+        selective adjoint refinement (PFR_CHECK_REFINE_ADJ) re-sizes the chunks when its seed vectors (n x chunk
+        per lane, allocated on first use) would not fit beside the current workspaces."""
+        adds_refine = mode is not None and bool(int(mode) & _native.PFR_CHECK_REFINE_ADJ) \
+            and not (self.check_mode & _native.PFR_CHECK_REFINE_ADJ)
         if mode is not None:
             self.check_mode = int(mode)
         if tol is not None:
             self.check_tol = float(tol)
         for sv in self.solvers:
             sv.set_check(self.check_mode, self.check_tol)
+        if adds_refine and self.solvers:
+            self.ensure(max(self._sized_for) if self._sized_for else self.n_lanes * self.max_batch, refit=True)
 
     @property
     def solver(self):
@@ -288,20 +307,25 @@ class _Engine:
         per = (-(-n // self.n_lanes) + 63) // 64 * 64
         return [(min(n, i * per), min(n, (i + 1) * per)) for i in range(self.n_lanes)]
 
-    def _run(self, call, n, accum):
+    def _run(self, call, n, accum, lane_bufs=None):
         """``call(solver, lo, hi, bufs)`` on every lane's stream; per-lane ``accum``
-        buffers (zeros like each given tensor) are summed into the given tensors.  With several
-        lanes each lane's launches are issued from its own host thread (the C calls release the
-        GIL): issued one after the other, the second lane started a whole sweep's enqueue time
-        (~9 ms) after the first and finished that much later."""
+        buffers (zeros like each given tensor) are summed into the given tensors -- or, with
+        ``lane_bufs`` (the caller's zeroed per-lane buffers, one list per lane), accumulated there and
+        left to the caller.  With several lanes each lane's launches are issued from its own host
+        thread (the C calls release the GIL): issued one after the other, the second lane started a
+        whole sweep's enqueue time (~9 ms) after the first and finished that much later."""
         cur = torch.cuda.current_stream(self.device)
         jobs = []
-        spans = [(sv, st, lo, hi) for sv, st, (lo, hi) in zip(self.solvers, self.streams, self._split(n)) if hi > lo]
-        for sv, st, lo, hi in spans:
+        spans = [(i, sv, st, lo, hi) for i, (sv, st, (lo, hi)) in
+                 enumerate(zip(self.solvers, self.streams, self._split(n))) if hi > lo]
+        for i, sv, st, lo, hi in spans:
             # the lane's accumulation buffers are zero-filled on the current stream BEFORE the lane
             # stream is ordered after it (k_reduce accumulates into them with +=); one lane accumulates
             # straight into the given tensors
-            bufs = list(accum) if len(spans) == 1 else [None if a is None else torch.zeros_like(a) for a in accum]
+            if lane_bufs is not None:
+                bufs = lane_bufs[i]
+            else:
+                bufs = list(accum) if len(spans) == 1 else [None if a is None else torch.zeros_like(a) for a in accum]
             st.wait_stream(cur)
             jobs.append((sv, st, lo, hi, bufs))
 
@@ -331,15 +355,61 @@ class _Engine:
                     b.record_stream(cur)
         if err is not None:
             raise err
+        if lane_bufs is not None:
+            return
         for _, st, _, _, bufs in jobs:
             for a, b in zip(accum, bufs):
                 if a is not None and b is not a:
                     a.add_(b)
 
+    def loss_step(self, freqs, loss_type, ref, scale):
+        """One loss + gradient sweep with the step buffers reused across calls (the optimiser / bench loop:
+        the host's step-to-step turnaround is GPU idle time).  Per lane, loss and the contracted partials
+        accumulate into one slot of a single device buffer whose last entry receives the number of flagged
+        frequencies; one fill per buffer, one device->host copy.  Returns (loss sum, w (18,) complex, flags
+        device tensor, flagged count); the backward errors land in ``last_berr``."""
+        n = freqs.numel()
+        key = (n, self.n_lanes, id(self.solvers[0]))
+        b = self._step_bufs.get(key) if hasattr(self, "_step_bufs") else None
+        if b is None:
+            L, m = self.n_lanes, 2 + 2 * self.n_stiff
+            acc = torch.empty(L * m + 1, dtype=torch.float64, device=self.device)
+            lanes = [[acc[l * m:l * m + 1], acc[l * m + 2:(l + 1) * m].view(self.n_stiff, 2)] for l in range(L)]
+            b = (acc, lanes, torch.empty(n, dtype=torch.int32, device=self.device),
+                 torch.empty((n, 2), dtype=torch.float64, device=self.device))
+            self._step_bufs = {key: b}            # one shape at a time (a new size replaces it)
+        acc, lanes, flags, berr = b
+        acc.zero_()
+        flags.zero_()
+        berr.fill_(float('nan'))
+
+        def call(sv, lo, hi, bufs):
+            sv.set_check(self.check_mode, self.check_tol, berr[lo:hi])
+            try:
+                sv.sweep(freqs[lo:hi], loss_type, ref=ref[lo:hi], scale=scale, loss=bufs[0], w=bufs[1],
+                         flags=flags[lo:hi])
+            finally:
+                sv.set_check(self.check_mode, self.check_tol)
+        if self.check_mode & _native.PFR_CHECK_REFINE_ADJ:
+            self._seeded = True
+        self._run(call, n, None, lane_bufs=lanes)
+        torch.sum(flags != 0, dtype=torch.float64, out=acc[-1])
+        h = acc.cpu().numpy()
+        L, m = self.n_lanes, 2 + 2 * self.n_stiff
+        per = h[:L * m].reshape(L, m)
+        wk = (per[:, 2::2] + 1j * per[:, 3::2]).sum(axis=0)
+        w = np.zeros(18, dtype=np.complex128)
+        w[self.kidx] = wk
+        self.last_berr = berr
+        return float(per[:, 0].sum()), w, flags, int(h[-1])
+
     def sweep(self, freqs, loss_type=_native.LOSS_NONE, ref=None, scale=1.0, fr=None, loss=None, w=None,
               flags=None, berr=None):
         """``Solver.sweep`` over all lanes (fr / flags / berr (F, 2) written in place, loss / w
         accumulated)."""
+        if self.check_mode & _native.PFR_CHECK_REFINE_ADJ:
+            self._seeded = True        # the lanes allocate their refinement seed vectors in this sweep
+
         def call(sv, lo, hi, bufs):
             if berr is not None:
                 sv.set_check(self.check_mode, self.check_tol, berr[lo:hi])
@@ -422,6 +492,12 @@ class _SweepLoss(torch.autograd.Function):
     def forward(ctx, c, engine, freqs, ref, loss_id, n_total, reduce_fn):
         cn = c.detach().cpu().numpy()
         engine.set_coefficients(cn)
+        if reduce_fn is None:
+            # the single-process step: reused buffers, one device->host copy (_Engine.loss_step)
+            lsum, w, flags, nflag = engine.loss_step(freqs, loss_id, torch.view_as_real(ref), 1.0 / n_total)
+            engine.last_flags = _check_flags(flags) if nflag else np.zeros(flags.numel(), np.int32)
+            ctx.save_for_backward(torch.from_numpy(w))
+            return torch.tensor(lsum / n_total, dtype=torch.float64)
         w = torch.zeros(engine.n_stiff, dtype=torch.complex128, device=engine.device)
         loss = torch.zeros(1, dtype=torch.float64, device=engine.device)
         flags = torch.zeros(freqs.numel(), dtype=torch.int32, device=engine.device)

@@ -27,6 +27,14 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+// after a group of launches: a refused launch configuration (pfr::launch_refused) or a launch error
+#define LAUNCH_TRY()                                                                      \
+  do {                                                                                    \
+    if (const char* _k = pfr::launch_refused())                                           \
+      return fail(PFR_ERR_HIP, std::string("hipFuncSetAttribute refused the dynamic LDS size of ") + _k); \
+    HIP_TRY(hipGetLastError());                                                           \
+  } while (0)
+
 #define HIP_TRY(expr)                                                                     \
   do {                                                                                    \
     hipError_t _e = (expr);                                                               \
@@ -169,6 +177,7 @@ struct pfr_solver {
     hipEvent_t ev[6]{};
     std::vector<hipEvent_t> kev;        // factorisation kernel classes: NKC + 1 events per level
     bool used[5]{};
+    bool f0 = false;                    // level 0 ran fused (k_front0): its launches are all class 0
   };
   int timing = 0;
   std::vector<ChunkEvents> tev;
@@ -190,9 +199,11 @@ struct pfr_solver {
   int us2_nar = 256;                    // PFR_US2_NAR: solve launches (paired top-down, bottom-up chain) with fewer
                                         // (front, group) workgroups than this take the narrow-level forms -- pivot
                                         // blocks in LDS, left-looking, the update parts with their columns split
-                                        // over the waves (k_usolve2_updc + k_usolve2_nar, k_lsolve_level_z<., true>
+                                        // over the waves (k_usolve2_updc + k_usolve2_rl, k_lsolve_level_z<., true>
                                         // + k_lsolve_rows_zc); 0: never.  Measured best at 256 for both passes
                                         // (1,024 / 4,096: no gain at 512 frequencies, slower at 4,096)
+  int us2_rl = 1;                       // PFR_US2_RL: k_usolve2_rl for the narrow levels' paired pivot blocks
+  int ls_rl = 1;                        // PFR_LS_RL: k_lsolve_rl_z for the bottom-up chain's narrow pivot blocks
   int split_target = 256;               // PFR_SOLVE_SPLIT: solve launches with fewer (front, group) workgroups
                                         // than this (one per CU) split their update parts up to about this
                                         // many workgroups (0: off)
@@ -311,10 +322,12 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
   auto mark = [&](int l, int c) {
     if (kt) (void)hipEventRecord(kev[(pfr::NKC + 1) * l + c], st);
   };
+  if (kt) s->tev[s->n_tev].f0 = false;
   for (int l = 0; l < L; ++l) {
     int nf = s->level_ptr[l + 1] - s->level_ptr[l];
     mark(l, 0);
     if (l == 0 && s->fused0 && mode == 0) {
+      if (kt) s->tev[s->n_tev].f0 = true;
       // the bottom level's leaf fronts in one pass (k_front0): A11, L21 and update block per frequency in registers
       pfr::launch_front0(s->P, s->d_f0_front, s->n_f0, s->f0_small, s->d_f0_ptr, s->d_f0_nz, ngroups, s->F, s->Fc,
                          s->freqs, s->K, s->M, s->flags, st);
@@ -354,7 +367,7 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
                       s->d_gxp + s->tile_ptr[l], s->d_gx, ngroups, s->F, s->Fc, st);
     mark(l, 5);
   }
-  HIP_TRY(hipGetLastError());
+  LAUNCH_TRY();
   return PFR_OK;
 }
 
@@ -380,7 +393,7 @@ int solve_all(pfr_solver* s, int which, int rhs_mode, const pfr::RhsDesc& rd, co
     pfr::launch_solve(which, rhs_mode, s->sym, s->P, lvl, nf, solve_W(s, l, nf), ngroups, s->F, s->Fc, s->WV, rd, Yin, Out,
                       reach, st, split, glist);
   }
-  HIP_TRY(hipGetLastError());
+  LAUNCH_TRY();
   return PFR_OK;
 }
 
@@ -500,9 +513,9 @@ int fn_bottom_up(pfr_solver* s, int rhs_mode, const pfr::RhsDesc& rf, hipStream_
     const int nsum = nf[0] + 3 * nf[1];
     const bool nar = (int64_t)nsum * ngroups < s->us2_nar && pfr::ls_nar_fits(s->level_maxns[l]);
     pfr::launch_lsolve_multi(rhs_mode, s->P, 4, lvl, nf, solve_W(s, l, nmax), ngroups, s->F, s->Fc, WV, rd, Y, reach,
-                             st, solve_split(s, nsum), nar, s->level_maxns[l], s->level_maxf[l]);
+                             st, solve_split(s, nsum), nar, s->level_maxns[l], s->level_maxf[l], s->ls_rl != 0);
   }
-  HIP_TRY(hipGetLastError());
+  LAUNCH_TRY();
   return PFR_OK;
 }
 
@@ -518,7 +531,7 @@ int sym_top_down_support(pfr_solver* s, const pfr::RhsDesc& rd, hipStream_t st) 
     pfr::launch_solve(1, 0, true, s->P, s->d_reach_fronts[1] + s->reach_ptr[1][l], nf, solve_W(s, l, nf), ngroups, s->F,
                       s->Fc, s->WV, rd, s->Y, s->X, s->d_reach[0], st, solve_split(s, nf));
   }
-  HIP_TRY(hipGetLastError());
+  LAUNCH_TRY();
   return PFR_OK;
 }
 
@@ -529,13 +542,13 @@ int sym_top_down_pair(pfr_solver* s, hipStream_t st, bool fwd_all = false) {
     const int nf = s->level_ptr[l + 1] - s->level_ptr[l];
     const bool small = s->level_maxf[l] <= s->us2_small;
     const int tiny = s->us2_tiny > 0 && s->level_maxns[l] <= s->us2_tiny ? (s->level_maxns[l] <= 4 ? 4 : 8) : 0;
-    const bool nar = (int64_t)nf * ngroups < s->us2_nar && pfr::us2_nar_lds(s->level_maxns[l]) <= pfr::LDS_BYTES;
+    const bool nar = (int64_t)nf * ngroups < s->us2_nar;
     pfr::launch_usolve2(s->P, s->d_level_fronts + s->level_ptr[l], nf, solve_W(s, l, nf), small, ngroups, s->F, s->Fc,
                         s->Y, s->X, s->d_reach[0], fwd_all ? nullptr : s->d_reach[1], s->Y2, s->XA, s->d_reach[1], st,
                         nar ? std::max(2, solve_split(s, nf)) : solve_split(s, nf), nar ? 0 : tiny, nar,
-                        s->level_maxns[l]);
+                        s->level_maxns[l], s->us2_rl != 0);
   }
-  HIP_TRY(hipGetLastError());
+  LAUNCH_TRY();
   return PFR_OK;
 }
 
@@ -766,12 +779,19 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->scale_corr = knob("PFR_SCALE_CORR", 1, 0, 1);
   // 8: the bottom two levels at 2,048 frequencies 685 / 612 -> 509 / 489 us (profiles/r04/experiments/us2_tiny_*)
   s->us2_tiny = knob("PFR_US2_TINY", 8, 0, 8);
+  // the narrow levels' paired top-down pivot blocks right-looking with prefetched factor entries (k_usolve2_rl)
+  s->us2_rl = knob("PFR_US2_RL", 1, 0, 1);
   const int blk_min = knob("PFR_SCHUR_BLK_MIN", 24, 0, pfr::MAX_FRONT);   // update blocks of >= this many rows: block kernel
   pfr::PlanOptions po;
   po.blk_min = blk_min;
   s->n = S.n;
   s->nnz = S.nnz;
   s->Fc = round64(max_batch);
+  // the same for the bottom-up chain's pivot blocks (k_lsolve_rl_z), on chunks of up to 1,024 frequencies: 512-
+  // frequency sweeps forward solves 1.65 -> 1.33 ms per step, 41.6k against 38.9-39.7k freq-solves/s; on 2,048-
+  // frequency chunks 0.37 -> 0.50 ms per sweep (four slices x 128 groups of 16 frequencies each stage the frontal
+  // index chains: profiles/EXPERIMENTS.md, round 6)
+  s->ls_rl = knob("PFR_LS_RL", s->Fc <= 1024 ? 1 : 0, 0, 1);
   // the pipelined L21 prefix on launches of fewer than 8,000 waves in chunks of <= 1,024 frequencies (the narrow
   // levels of C4's per-rank sweeps: 512 frequencies 35.3-35.7k -> 36.2-36.6k freq-solves/s; 2,048-frequency
   // chunks unchanged, profiles/r04/offdiag_layout/pu3_*)
@@ -792,7 +812,9 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->asm_ptr = pl.asm_ptr;
   s->item_ptr = pl.item_ptr;
   s->lev_bytes = pl.lev_bytes;
-  s->fused0 = pl.fused0;
+  // PFR_FRONT0=0: level 0 through the four class kernels instead of the fused k_front0 (tests/test_gpu_bitwise.py
+  // checks the two give the same factors bit for bit)
+  s->fused0 = pl.fused0 && knob("PFR_FRONT0", 1, 0, 1);
   s->n_f0 = (int)pl.f0_front.size();
   s->f0_small = pl.f0_small;
   Front* d_fronts = nullptr;
@@ -939,14 +961,18 @@ int pfr_last_kernel_timings(const pfr_solver* s, double* ms, int64_t* launches) 
   for (int c = 0; c < s->n_tev; ++c) {
     if (!s->tev[c].used[0]) continue;
     for (int l = 0; l < L; ++l) {
-      const int work[pfr::NKC] = {s->asm_ptr[l + 1] - s->asm_ptr[l], s->level_ptr[l + 1] - s->level_ptr[l],
-                                  s->item_ptr[l + 1] - s->item_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
-                                  s->tile_ptr[l + 1] - s->tile_ptr[l]};
+      int work[pfr::NKC] = {s->asm_ptr[l + 1] - s->asm_ptr[l], s->level_ptr[l + 1] - s->level_ptr[l],
+                            s->item_ptr[l + 1] - s->item_ptr[l], s->blk_ptr[l + 1] - s->blk_ptr[l],
+                            s->tile_ptr[l + 1] - s->tile_ptr[l]};
+      if (l == 0 && s->tev[c].f0) {   // the fused bottom level: one or two k_front0 launches, all in class 0
+        work[0] = (s->f0_small > 0) + (s->n_f0 > s->f0_small);
+        for (int k = 1; k < pfr::NKC; ++k) work[k] = 0;
+      }
       for (int k = 0; k < pfr::NKC; ++k) {
         float m = 0;
         HIP_TRY(hipEventElapsedTime(&m, s->tev[c].kev[(pfr::NKC + 1) * l + k], s->tev[c].kev[(pfr::NKC + 1) * l + k + 1]));
         ms[k] += m;
-        if (launches) launches[k] += work[k] > 0;    // empty classes launch nothing
+        if (launches) launches[k] += l == 0 && s->tev[c].f0 ? work[k] : work[k] > 0;   // empty classes launch nothing
       }
     }
   }
@@ -1039,7 +1065,7 @@ int pfr_combine(pfr_solver* s, const double* coef, double* K_out, void* stream) 
     c.im[k] = coef[2 * k + 1];
   }
   pfr::launch_combine(s->stiff, s->n_stiff, s->nnz, c, reinterpret_cast<double2*>(K_out), (hipStream_t)stream);
-  HIP_TRY(hipGetLastError());
+  LAUNCH_TRY();
   return PFR_OK;
 }
 
@@ -1315,7 +1341,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
     }
     record(s, 5, st);
     if (flags_dev) pfr::launch_flags_merge(s->flags, nv, flags_dev + q0, st);
-    HIP_TRY(hipGetLastError());
+    LAUNCH_TRY();
     if ((rc = finish_timing(s, used))) return rc;
   }
   return PFR_OK;
@@ -1429,7 +1455,7 @@ int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int
                          H + (int64_t)i * s->n_stiff, nullptr, st);
     }
     if (flags_dev) pfr::launch_flags_merge(s->flags, nv, flags_dev + q0, st);
-    HIP_TRY(hipGetLastError());
+    LAUNCH_TRY();
   }
   return PFR_OK;
 }
@@ -1499,7 +1525,7 @@ int pfr_solve_multi(pfr_solver* s, int32_t batch, int32_t nrhs, const double* da
     record(s, 4, st);
     record(s, 5, st);
     if (flags_dev) pfr::launch_flags_merge(s->flags, nv, flags_dev + q0, st);
-    HIP_TRY(hipGetLastError());
+    LAUNCH_TRY();
     if ((rc = finish_timing(s, used))) return rc;
   }
   return PFR_OK;
@@ -1520,7 +1546,7 @@ int pfr_matvec(pfr_solver* s, int32_t batch, const double* data_dev, int64_t dat
   pfr::launch_matvec(s->d_colptr, s->d_rowind, s->n, reinterpret_cast<const double2*>(data_dev), data_stride,
                      reinterpret_cast<const double2*>(x_dev), x_stride, reinterpret_cast<double2*>(y_dev),
                      transpose, batch, st);
-  HIP_TRY(hipGetLastError());
+  LAUNCH_TRY();
   return PFR_OK;
 }
 

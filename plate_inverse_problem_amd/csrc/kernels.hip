@@ -20,6 +20,7 @@
 #include <cstdlib>
 
 #include <algorithm>
+#include <atomic>
 
 #include "launch.hpp"
 
@@ -2011,79 +2012,215 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(WPE))) void
   usolve2_tri(fr, base, Fc, c, act, Xs);
 }
 
-// The paired top-down pass's pivot blocks on the levels with few (front, group) workgroups -- the top of the tree,
-// after the split update part (k_usolve2_upd) -- with the pivot values resident in LDS.  k_usolve2_level walks a
-// pivot block right-looking: per KBS block, wave 0 solves the diagonal block from global memory, then every wave
-// updates its rows above with a loop whose iterations each wait for their own loads, so a 40-pivot block costs ~20
-// dependent global round trips (26-54 us per level at 2,048 frequencies, the whole pass's top is latency).  Here the
-// block is walked LEFT-looking with the values in LDS (2 vectors x ns x 64 frequencies): for each KBS block (from the
-// bottom), wave t forms row k0 + t's sum over the columns already solved (its U loads all independent of the chain,
-// the solved values read from LDS), then wave 0 solves the block's triangle.  Two barriers and about two global
-// latencies per block.  The operations per value are those of k_usolve2_level in another order (rounding differs).
-constexpr int US2_NAR_W = KBS;   // waves per workgroup: wave t owns row k0 + t of each block
-__global__ __launch_bounds__(64 * US2_NAR_W) void k_usolve2_nar(DevPattern P, const int* __restrict__ lvl,
-                                                               const cplx* __restrict__ F, int64_t Fc, UPair A,
-                                                               UPair B) {
-  extern __shared__ cplx sX[];   // [2][ns][64]
-  int bx;
-  const Ctx c = ctx_xcd(bx);
-  const int ft = lvl[bx];
-  const bool act[2] = {!A.skip || !A.skip[ft], !B.skip || !B.skip[ft]};
-  cplx* const Xs[2] = {A.X, B.X};
-  const Front fr = P.fronts[ft];
-  const int f = fr.f, ns = fr.ns;
-  const cplx* __restrict__ base = F + fr.off * Fc + c.q;
-#define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
-#define SX(v, a) sX[((v) * ns + (a)) * 64 + c.lane]
-#define XV(v, a) Xs[v][(int64_t)(fr.col0 + (a)) * Fc + c.q]
-  // the pivot values y_a + U12(a, :) x_upd the update part left in X
+// Pivot-block triangular solves of the narrow levels, RIGHT-looking by single pivots with the factor entries
+// prefetched: a workgroup = one front x 16 frequencies, W waves, lane = (one of 16 frequencies, one of 4 row slots);
+// the lane of slot s = 4 w + (lane >> 4) owns rows i = s + 4 W r (r < RPL) and keeps their running sums acc[v][r] in
+// registers.  Per pivot p (UP: ns - 1 .. 0, U11 backward, x_p = acc_p / U(p, p), then acc_i -= U(i, p) x_p on the
+// rows i < p; !UP: 0 .. ns - 1, unit L11 forward, y_p = acc_p, then acc_i -= L(i, p) y_p on the rows p < i < ns) the
+// owner forms x_p, stores it and broadcasts it through LDS: one barrier per pivot.  Every lane's column entries
+// E(i, p) of the next PF pivots are already in registers (a ring loaded PF pivots ahead, independent of the chain),
+// so the chain carries no global-memory latency -- the left-looking form of round 5 (the pivot values in LDS, per
+// 8-pivot block the rows' sums over the solved columns, then wave 0's triangle) waited on about two global round
+// trips per block: the paired pass's 28 narrow levels 1.06 -> 0.67 ms per 2,048-frequency chunk.  The 16-frequency workgroups also give the narrow levels 4x the workgroups.
+// dst[v] (and dst2 for vector 0 when not NULL): the solution's pivot rows (already offset by the first pivot row and the lane's
+// frequency).
+constexpr int RL_Q = 16, RL_WMAX = 8, RL_RING = 16;   // ring entries per lane: PF = RL_RING / RPL pivots ahead
+// rows per lane slot for a level whose largest pivot block is maxns (1, 2 or 4: maxns <= 128), and the waves
+inline int rl_rpl(int maxns) { return maxns <= 4 * RL_WMAX ? 1 : maxns <= 8 * RL_WMAX ? 2 : 4; }
+inline int rl_waves(int maxns) { return std::min(RL_WMAX, (maxns + 4 * rl_rpl(maxns) - 1) / (4 * rl_rpl(maxns))); }
+template <bool UP, int NV, int RPL, int PF>
+__device__ __forceinline__ void tri_rl16(const cplx* __restrict__ base, int f, int ns, int64_t Fc, int w, int W,
+                                         int lane, const bool (&act)[NV], cplx (&acc)[NV][RPL],
+                                         cplx* const (&dst)[NV], cplx (*sx)[NV][RL_Q],
+                                         cplx* __restrict__ dst2 = nullptr) {
+  const int slot = 4 * w + (lane >> 4), nsl = 4 * W, ql = lane & (RL_Q - 1);
+  int ir[RPL], ic[RPL];
 #pragma unroll
-  for (int v = 0; v < 2; ++v)
-    if (act[v])
-      for (int a = c.w; a < ns; a += c.W) SX(v, a) = XV(v, a);
-  __syncthreads();
-  for (int k1 = ns; k1 > 0; k1 -= KBS) {
-    const int k0 = max(0, k1 - KBS), kb = k1 - k0;
-    if (c.w < kb) {
-      // row i of the block: minus its sum over the solved columns k1 .. ns
-      const int i = k0 + c.w;
-      cplx acc[2] = {make_double2(0.0, 0.0), make_double2(0.0, 0.0)};
-      const cplx* const sx[2] = {sX + c.lane, sX + (int64_t)ns * 64 + c.lane};   // inactive vector: unused
-      dot_row_lds<2>(acc, base + (int64_t)i * f * Fc, Fc, sx, k1, ns);
+  for (int r = 0; r < RPL; ++r) {
+    ir[r] = slot + nsl * r;
+    ic[r] = min(ir[r], ns - 1);
+  }
+  cplx dinv[RPL];
 #pragma unroll
-      for (int v = 0; v < 2; ++v)
-        if (act[v]) SX(v, i) = cadd(SX(v, i), acc[v]);
-    }
-    __syncthreads();
-    if (c.w == 0) {
-      // the block's triangle (usolve2_tri's diagonal block)
+  for (int r = 0; r < RPL; ++r) dinv[r] = UP ? crecip(base[((int64_t)ic[r] * f + ic[r]) * Fc]) : make_double2(1.0, 0.0);
+  cplx pre[PF][RPL];
+  // the ring's next column pointer per row (the pivot of step t + PF, clamped into the block), advanced by one
+  // column per step; the owner slot p % nsl likewise (no per-step index arithmetic: every wave of every
+  // workgroup runs each step's instructions, so they set the step time)
+  const int64_t dcol = UP ? -Fc : Fc;
+  const cplx* lp[RPL];
+  auto col = [&](int t) { const int tc = min(t, ns - 1); return UP ? ns - 1 - tc : tc; };
 #pragma unroll
-      for (int v = 0; v < 2; ++v)
+  for (int r = 0; r < RPL; ++r) lp[r] = base + (int64_t)ic[r] * f * Fc;
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) pre[u][r] = lp[r][(int64_t)col(u) * Fc];
+#pragma unroll
+  for (int r = 0; r < RPL; ++r) lp[r] += (int64_t)col(PF) * Fc;
+  int os = col(0) % nsl;
+  // one pivot step t with the column entries e; the owner's solved value through LDS (buffer t & 1)
+  auto step = [&](int t, const cplx (&e)[RPL]) {
+    const int p = UP ? ns - 1 - t : t, par = t & 1;
+    // the owner lane (row ir[r] == p) turns acc into x_p and broadcasts it; every row's candidate is formed and the
+    // owner's picked by lane predicates (an index by p / nsl makes the compiler address acc in scratch memory)
+    if (slot == os) {
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
         if (act[v]) {
-          cplx x[KBS];
+          cplx xs = make_double2(0.0, 0.0);
 #pragma unroll
-          for (int t = 0; t < KBS; ++t) x[t] = SX(v, k0 + min(t, kb - 1));
-#pragma unroll
-          for (int i = KBS - 1; i >= 0; --i) {
-            const int ri = k0 + min(i, kb - 1);
-#pragma unroll
-            for (int k = i + 1; k < KBS; ++k) x[i] = cfms(x[i], E(ri, k0 + min(k, kb - 1)), x[k]);
-            x[i] = cscale(cmul(x[i], crecip(E(ri, ri))), i < kb ? 1.0 : 0.0);
+          for (int r = 0; r < RPL; ++r) {
+            const bool own = ir[r] == p;
+            const cplx x = UP ? cmul(acc[v][r], dinv[r]) : acc[v][r];
+            acc[v][r].x = own ? x.x : acc[v][r].x;
+            acc[v][r].y = own ? x.y : acc[v][r].y;
+            xs.x = own ? x.x : xs.x;
+            xs.y = own ? x.y : xs.y;
           }
-#pragma unroll
-          for (int t = 0; t < KBS; ++t)
-            if (t < kb) SX(v, k0 + t) = x[t];
+          sx[par][v][ql] = xs;
         }
     }
-    __syncthreads();
+    os = UP ? (os == 0 ? nsl - 1 : os - 1) : (os == nsl - 1 ? 0 : os + 1);
+    PFR_BARRIER();
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+      if (act[v]) {
+        const cplx x = sx[par][v][ql];
+#pragma unroll
+        for (int r = 0; r < RPL; ++r)
+          if (UP ? ir[r] < p : (ir[r] > p && ir[r] < ns)) acc[v][r] = cfms(acc[v][r], e[r], x);
+      }
+  };
+  // whole rounds of PF steps (the ring slot u refilled PF steps ahead: straight-line code, so that the waits on
+  // the ring are counted, not drained), then the tail from the ring without refills
+  int t0 = 0;
+  for (; t0 + PF <= ns; t0 += PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      cplx e[RPL];
+#pragma unroll
+      for (int r = 0; r < RPL; ++r) {
+        e[r] = pre[u][r];
+        pre[u][r] = *lp[r];
+        if (t0 + u + PF + 1 < ns) lp[r] += dcol;
+      }
+      step(t0 + u, e);
+    }
   }
 #pragma unroll
-  for (int v = 0; v < 2; ++v)
+  for (int u = 0; u < PF; ++u)
+    if (t0 + u < ns) step(t0 + u, pre[u]);
+  // every lane's solved rows out
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
     if (act[v])
-      for (int a = c.w; a < ns; a += c.W) XV(v, a) = SX(v, a);
-#undef E
-#undef SX
-#undef XV
+#pragma unroll
+      for (int r = 0; r < RPL; ++r)
+        if (ir[r] < ns) {
+          dst[v][(int64_t)ir[r] * Fc] = acc[v][r];
+          if (dst2 && v == 0) dst2[(int64_t)ir[r] * Fc] = acc[v][r];
+        }
+}
+
+// The paired top-down pass's pivot blocks on the narrow levels (after k_usolve2_updc left y_a + U12(a, :) x_upd in
+// X): tri_rl16 over both vectors.  Grid (fronts, Fc / 16), 64 W threads with 4 W RPL >= the level's largest ns.
+template <int RPL>
+__global__ __launch_bounds__(64 * RL_WMAX) void k_usolve2_rl(DevPattern P, const int* __restrict__ lvl,
+                                                    const cplx* __restrict__ F, int64_t Fc, UPair A, UPair B) {
+  __shared__ cplx sx[2][2][RL_Q];
+  const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
+  const int bx = (int)(lid % gridDim.x);
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), W = blockDim.x >> 6;
+  const int64_t q = (lid / gridDim.x) * RL_Q + (lane & (RL_Q - 1));
+  const int ft = lvl[bx];
+  const bool act[2] = {!A.skip || !A.skip[ft], !B.skip || !B.skip[ft]};
+  const Front fr = P.fronts[ft];
+  const int ns = fr.ns;
+  cplx* const dst[2] = {A.X + (int64_t)fr.col0 * Fc + q, B.X + (int64_t)fr.col0 * Fc + q};
+  cplx acc[2][RPL];
+  const int slot = 4 * w + (lane >> 4);
+#pragma unroll
+  for (int r = 0; r < RPL; ++r) {
+    const int i = min(slot + 4 * W * r, ns - 1);
+#pragma unroll
+    for (int v = 0; v < 2; ++v) acc[v][r] = act[v] ? dst[v][(int64_t)i * Fc] : make_double2(0.0, 0.0);
+  }
+  tri_rl16<true, 2, RPL, RL_RING / RPL>(F + fr.off * Fc + q, fr.f, ns, Fc, w, W, lane, act, acc, dst, sx);
+}
+
+// The bottom-up chain's pivot blocks on the narrow levels (k_lsolve_level_z<., true>'s role, the update rows left to
+// k_lsolve_rows_zc): per (front, 16 frequencies, slice) the frontal vector gathered -- pivot rows into the owning
+// lanes' registers, update rows into WV -- then tri_rl16's unit forward substitution, y to Y and to WV's pivot rows.
+// Grid (largest slice's fronts, Fc / 16, slices), 64 W threads with 4 W RPL >= the level's largest ns.
+template <int RHS, int RPL>
+__global__ __launch_bounds__(64 * RL_WMAX) void k_lsolve_rl_z(DevPattern P, LSlices S, const cplx* __restrict__ F, int64_t Fc) {
+  __shared__ cplx sx[2][1][RL_Q];
+  __shared__ int s_ptr[MAX_FRONT + 1];
+  __shared__ int s_src[GATHER_CAP];
+  __shared__ int s_p[MAX_FRONT];
+  __shared__ double s_rv[MAX_FRONT];
+  __shared__ int s_cs[MAX_FRONT];
+  const int64_t lid = xcd_swizzle(blockIdx.x + (int64_t)gridDim.x * blockIdx.y, (int64_t)gridDim.x * gridDim.y);
+  const int bx = (int)(lid % gridDim.x), z = blockIdx.z;
+  if (bx >= S.nf[z]) return;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), W = blockDim.x >> 6;
+  const int64_t q = (lid / gridDim.x) * RL_Q + (lane & (RL_Q - 1));
+  const Front fr = P.fronts[S.lvl[z][bx]];
+  const int f = fr.f, ns = fr.ns, slot = 4 * w + (lane >> 4), nsl = 4 * W;
+  const RhsArgs& R = S.R[z];
+  const int* __restrict__ reach = S.reach[z];
+  cplx* __restrict__ WV = S.WV[z];
+  // the frontal gather (gather_frontal's chains resolved into LDS by all threads; rows per lane slot, so the row
+  // indices are not wave-uniform here)
+  const int E0 = P.ea_ptr[fr.row0], nE = P.ea_ptr[fr.row0 + f] - E0;
+  const bool staged = nE <= GATHER_CAP;
+  if (staged) {
+    for (int t = threadIdx.x; t <= f; t += blockDim.x) s_ptr[t] = P.ea_ptr[fr.row0 + t] - E0;
+    for (int t = threadIdx.x; t < nE; t += blockDim.x) {
+      const int src = P.ea_src[E0 + t];
+      s_src[t] = (!reach || reach[P.row_front[src]]) ? src : -1;
+    }
+  }
+  for (int t = threadIdx.x; t < ns; t += blockDim.x) {
+    const int p = P.idx[fr.row0 + t];
+    s_p[t] = p;
+    s_rv[t] = R.rhsP[p];
+    s_cs[t] = RHS == 3 ? R.cslot[p] : -1;
+  }
+  const double om = 6.283185307179586 * R.freqs[q], om2 = om * om;
+  __syncthreads();
+  auto gather = [&](int a) {
+    cplx v = make_double2(0.0, 0.0);
+    if (a < ns) v = rhs_staged<RHS>(R, s_p[a], s_rv[a], s_cs[a], om2, q, Fc);
+    if (staged) {
+      for (int e = s_ptr[a]; e < s_ptr[a + 1]; ++e) {
+        const int src = s_src[e];
+        if (src >= 0) v = cadd(v, WV[(int64_t)src * Fc + q]);
+      }
+    } else {
+      for (int e = P.ea_ptr[fr.row0 + a]; e < P.ea_ptr[fr.row0 + a + 1]; ++e) {
+        const int src = P.ea_src[e];
+        if (!reach || reach[P.row_front[src]]) v = cadd(v, WV[(int64_t)src * Fc + q]);
+      }
+    }
+    return v;
+  };
+  // pivot rows through LDS to their owners (gathered by row slot like the update rows, which go to WV)
+  __shared__ cplx s_b[4 * RL_WMAX * RPL][RL_Q];
+  for (int a = slot; a < f; a += nsl) {
+    const cplx v = gather(a);
+    if (a < ns) s_b[a][lane & (RL_Q - 1)] = v;
+    else WV[(int64_t)(fr.row0 + a) * Fc + q] = v;
+  }
+  __syncthreads();
+  cplx acc[1][RPL];
+#pragma unroll
+  for (int r = 0; r < RPL; ++r) acc[0][r] = s_b[min(slot + nsl * r, ns - 1)][lane & (RL_Q - 1)];
+  const bool act[1] = {true};
+  cplx* const dst[1] = {S.Y[z] + (int64_t)fr.col0 * Fc + q};
+  tri_rl16<false, 1, RPL, RL_RING / RPL>(F + fr.off * Fc + q, f, ns, Fc, w, W, lane, act, acc, dst, sx,
+                                         WV + (int64_t)fr.row0 * Fc + q);
 }
 
 // The paired top-down pass on levels of tiny fronts (every pivot block <= NSM): ONE WAVE per (front, frequency
@@ -3249,6 +3386,18 @@ __global__ void k_matvec(const int* __restrict__ colptr, const int* __restrict__
 #define LAUNCH(kern, grid, block, st, ...) hipLaunchKernelGGL(kern, grid, block, 0, st, __VA_ARGS__)
 #define LAUNCH_DYN(kern, grid, block, lds, st, ...) hipLaunchKernelGGL(kern, grid, block, lds, st, __VA_ARGS__)
 
+// The first launch configuration the runtime refused since the last launch_refused() call (a kernel whose dynamic
+// LDS could not be raised above the default): the launch is skipped and the C ABI call that issued it fails with
+// this name (api.cpp LAUNCH_TRY), instead of a later generic launch error.
+static std::atomic<const char*> g_refused{nullptr};
+const char* launch_refused() { return g_refused.exchange(nullptr); }
+static bool dyn_lds(const void* fn, int bytes, const char* name) {
+  if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes) == hipSuccess) return true;
+  const char* none = nullptr;
+  g_refused.compare_exchange_strong(none, name);
+  return false;
+}
+
 void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPack& coef, double2* K, hipStream_t st) {
   LAUNCH(k_combine, dim3((unsigned)((nnz + 255) / 256)), dim3(256), st, stiff, n_stiff, nnz, coef, K);
 }
@@ -3281,11 +3430,13 @@ void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int max
                        hipStream_t st) {
   const size_t lds = (size_t)fac_lds_bytes(maxns);
   static_assert(FAC_LB == 8, "fac_lds_bytes: 8 W columns per row");
-  static const bool attr = [] {   // dynamic LDS beyond the default 64 KiB (up to 64 pivots: 37 KiB; headroom)
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_factor_sym_lds),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
-  }();
-  (void)attr;
+  // dynamic LDS beyond the default 64 KiB (up to 64 pivots: 37 KiB; headroom)
+  static const bool attr = dyn_lds(reinterpret_cast<const void*>(&k_factor_sym_lds), 160 * 1024, "k_factor_sym_lds");
+  if (!attr) {
+    const char* none = nullptr;
+    g_refused.compare_exchange_strong(none, "k_factor_sym_lds");
+    return;
+  }
   LAUNCH_DYN(k_factor_sym_lds, dim3((unsigned)(nfronts * Fc)), dim3(256), lds, st, P, lvl, F, Fc, flags, maxns);
 }
 
@@ -3368,7 +3519,7 @@ void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const 
 void launch_lsolve_multi(int rhs_mode, const DevPattern& P, int nslices, const int* const* lvl, const int* nf, int W,
                          int ngroups, const double2* F, int64_t Fc, double2* const* WV, const RhsDesc* rd,
                          double2* const* Y, const int* const* reach, hipStream_t st, int split, bool nar,
-                         int maxns, int maxf) {
+                         int maxns, int maxf, bool rl) {
   LSlices S{};
   int nmax = 0;
   for (int z = 0; z < nslices; ++z) {
@@ -3383,14 +3534,26 @@ void launch_lsolve_multi(int rhs_mode, const DevPattern& P, int nslices, const i
   if (nmax <= 0) return;
   const dim3 g(nmax, ngroups, nslices), b(64 * W);
   const int rs = split > 1;
-  if (rs && nar) {
-    static const bool attr = [] {
-      return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lsolve_level_z<0, true>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)LS_NAR_DYN_MAX) == hipSuccess &&
-             hipFuncSetAttribute(reinterpret_cast<const void*>(&k_lsolve_level_z<3, true>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)LS_NAR_DYN_MAX) == hipSuccess;
-    }();
-    (void)attr;
+  if (rl && maxns > 16 * RL_WMAX) rl = false;   // k_lsolve_rl_z: at most 4 rows per lane slot
+  if (rs && nar && rl) {
+    const int rpl = rl_rpl(maxns);
+    const dim3 gq(nmax, (unsigned)(Fc / RL_Q), nslices), bq(64 * rl_waves(maxns));
+#define LRL(RH, RP) LAUNCH((k_lsolve_rl_z<RH, RP>), gq, bq, st, P, S, F, Fc)
+    if (rhs_mode == 0) {
+      if (rpl == 1) LRL(0, 1); else if (rpl == 2) LRL(0, 2); else LRL(0, 4);
+    } else {
+      if (rpl == 1) LRL(3, 1); else if (rpl == 2) LRL(3, 2); else LRL(3, 4);
+    }
+#undef LRL
+  } else if (rs && nar) {
+    static const bool attr =
+        dyn_lds(reinterpret_cast<const void*>(&k_lsolve_level_z<0, true>), (int)LS_NAR_DYN_MAX, "k_lsolve_level_z<0,NAR>") &&
+        dyn_lds(reinterpret_cast<const void*>(&k_lsolve_level_z<3, true>), (int)LS_NAR_DYN_MAX, "k_lsolve_level_z<3,NAR>");
+    if (!attr) {
+      const char* none = nullptr;
+      g_refused.compare_exchange_strong(none, "k_lsolve_level_z<NAR>");
+      return;
+    }
     const size_t lds = (size_t)maxns * 64 * 16;
     if (rhs_mode == 0) LAUNCH_DYN((k_lsolve_level_z<0, true>), g, b, lds, st, P, S, F, Fc, rs);
     else LAUNCH_DYN((k_lsolve_level_z<3, true>), g, b, lds, st, P, S, F, Fc, rs);
@@ -3424,8 +3587,10 @@ void launch_fn_combine(const int* rows, int nrows, const double2* fcoef, double2
 void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, bool small, int ngroups,
                     const double2* F, int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0,
                     const double2* Y1, double2* X1, const int* reach1, hipStream_t st, int split, int tiny,
-                    bool nar, int maxns) {
+                    bool nar, int maxns, bool rl) {
   if (nfronts <= 0) return;
+  if (rl && maxns > 16 * RL_WMAX) rl = false;   // k_usolve2_rl: at most 4 rows per lane slot
+  // nar && !rl: the column-split update part (k_usolve2_updc), then k_usolve2_level's pivot block
   UPair a{Y0, X0, reach0, skip0}, b{Y1, X1, reach1, nullptr};
   if (tiny > 0 && split <= 1) {
     // every pivot block of the level <= tiny (4 or 8): one wave per (front, group)
@@ -3447,11 +3612,12 @@ void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, boo
   // symmetric mode only (the paired top-down pass serves the symmetric loss + gradient sweep).  Small-front levels:
   // 8 pivot rows per pass share each gathered update-row value, 2 values per chunk, 3 waves/SIMD (18 % less traffic
   // than 2 rows x 4 values at 4 waves/SIMD, the same time: profiles/r04/solve_traffic/)
-  if (rs && nar) {
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_usolve2_nar),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES);
-    (void)attr;
-    LAUNCH_DYN(k_usolve2_nar, g, dim3(64 * US2_NAR_W), (size_t)us2_nar_lds(maxns), st, P, lvl, F, Fc, a, b);
+  if (rs && nar && rl) {
+    const int rpl = rl_rpl(maxns);
+    const dim3 gq(nfronts, (unsigned)(Fc / RL_Q)), bq(64 * rl_waves(maxns));
+    if (rpl == 1) LAUNCH((k_usolve2_rl<1>), gq, bq, st, P, lvl, F, Fc, a, b);
+    else if (rpl == 2) LAUNCH((k_usolve2_rl<2>), gq, bq, st, P, lvl, F, Fc, a, b);
+    else LAUNCH((k_usolve2_rl<4>), gq, bq, st, P, lvl, F, Fc, a, b);
   } else if (small) LAUNCH((k_usolve2_level<true, 8, 2, 3>), g, bl, st, P, lvl, F, Fc, a, b, rs);
   else LAUNCH((k_usolve2_level<true, 4, 8, 2>), g, bl, st, P, lvl, F, Fc, a, b, rs);
 }

@@ -30,6 +30,10 @@ struct DirDesc {
   const double* freqs = nullptr;
 };
 
+// the first launch configuration refused since the last call (a kernel's dynamic LDS size), NULL: none; the
+// refused launch was skipped
+const char* launch_refused();
+
 void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPack& coef, double2* K, hipStream_t st);
 void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, const int2* xl, int ngroups, double2* F,
                      int64_t Fc, const double* freqs, const double2* K, const double* M, const double2* data,
@@ -70,8 +74,9 @@ void launch_solve(int which, int rhs_mode, bool sym, const DevPattern& P, const 
 void launch_lsolve_multi(int rhs_mode, const DevPattern& P, int nslices, const int* const* lvl, const int* nf, int W,
                          int ngroups, const double2* F, int64_t Fc, double2* const* WV, const RhsDesc* rd,
                          double2* const* Y, const int* const* reach, hipStream_t st, int split, bool nar = false,
-                         int maxns = 0, int maxf = 0);   // nar (split > 1): pivot blocks in LDS, update rows
+                         int maxns = 0, int maxf = 0,    // nar (split > 1): pivot blocks in LDS, update rows
                                                          // column-split (k_lsolve_level_z<., true>, k_lsolve_rows_zc)
+                         bool rl = true);                // nar + rl: pivot blocks right-looking (k_lsolve_rl_z)
 // functional from the bottom-up passes: partial dot products (FN_PARTS x 3 x Fc), the functional / loss
 // / cotangent from them (fcoef: 3 x Fc, G at the support rows), and L^-1 g = sum_k c_k L^-1 a_k in Yk[0]
 void launch_fn_dot(const int2* rows, int nrows, const double2* F, const double2* Yb, const double2* const* Yk, int64_t Fc,
@@ -85,7 +90,8 @@ void launch_usolve2(const DevPattern& P, const int* lvl, int nfronts, int W, boo
                     const double2* F, int64_t Fc, const double2* Y0, double2* X0, const int* reach0, const int* skip0,
                     const double2* Y1, double2* X1, const int* reach1, hipStream_t st, int split = 1,
                     int tiny = 0,     // tiny 4 / 8: the level's pivot blocks all <= tiny (k_usolve2_tiny)
-                    bool nar = false, int maxns = 0);   // nar (split > 1): pivot blocks in LDS (k_usolve2_nar)
+                    bool nar = false, int maxns = 0,    // nar (split > 1): the update part column-split (k_usolve2_updc)
+                    bool rl = true);                    // nar + rl: pivot blocks right-looking, prefetched (k_usolve2_rl)
 // Hessian sweep: tangent right-hand sides (rows of the permuted matrix, or of its
 // transpose with accumulate = 1) and the directional derivative of the loss cotangent
 void launch_tangent_spmv(const int* ptr, const int* idx, const int* nzs, int nrows, const double2* Kd,

@@ -55,8 +55,6 @@ inline int residual_parts(int n) { return (int)std::min<int64_t>((n + 3) / 4, 25
 inline int contract_eg_parts(int nent) { return ((nent + CEG_EW - 1) / CEG_EW + 3) / 4; }   // k_contract_eg grid
 // dynamic LDS of k_factor_sym_lds for a level whose largest pivot block is maxns (triangle + 8 W columns)
 inline int64_t fac_lds_bytes(int maxns) { return ((int64_t)maxns * (maxns + 1) / 2 + (int64_t)maxns * 8) * 16; }
-// dynamic LDS of k_usolve2_nar (the paired top-down pass's pivot values of the level's largest pivot block)
-inline int64_t us2_nar_lds(int maxns) { return 2 * (int64_t)maxns * 64 * 16; }
 // k_lsolve_level_z's NAR form: the level's largest pivot block's values in dynamic LDS (ns x 64 x 16 B), beside
 // the frontal gather's static index staging (~36 KiB)
 constexpr int64_t LS_NAR_DYN_MAX = 112 * 1024;

@@ -61,4 +61,5 @@ def report(name, **vals):
     if path:
         import json
         with open(path, "a") as f:
-            f.write(json.dumps({"test": name, **{k: float(v) for k, v in vals.items()}}) + "\n")
+            f.write(json.dumps({"test": name, **{k: [float(x) for x in v] if isinstance(v, (list, tuple)) else float(v)
+                                                 for k, v in vals.items()}}) + "\n")

@@ -6,7 +6,9 @@ operations per entry in the same order, so a difference means a wrong index, a l
   * PFR_US2_TINY: the paired top-down pass one wave per front on the levels whose pivot blocks are <= 4 / 8
     (k_usolve2_tiny) against the workgroup kernel (k_usolve2_level);
   * PFR_OFF_PU_WAVES: the software-pipelined L21 prefix (k_offdiag_level<0, false, 3>) on every launch against
-    none.
+    none;
+  * PFR_FRONT0: the bottom level fused into one kernel (k_front0: A11, L21 and the update block per frequency in
+    registers) against the four class kernels (assembly, A11 LU, L21 rows, Schur update) on level 0.
 The measured-slower variants of round 4 (dependency-driven passes, right-looking / shared-U11 L21 rows, prefix
 batches, fused A11 gather, pipelined paired updates) were removed with their tests.
 """
@@ -77,3 +79,9 @@ def test_tiny_front_top_down_bitwise(monkeypatch, lo, hi):
 def test_offdiag_pipelined_prefix_bitwise(monkeypatch, lo, hi):
     base = _run(monkeypatch, lo, hi, env={"PFR_OFF_PU_WAVES": "0"})
     _same(f"offdiag_pu3_{lo}_{hi}", base, _run(monkeypatch, lo, hi, env={"PFR_OFF_PU_WAVES": "1000000000"}))
+
+
+@pytest.mark.parametrize("lo,hi", [(1024, 1536), (0, 2048)])
+def test_front0_fused_bottom_level_bitwise(monkeypatch, lo, hi):
+    base = _run(monkeypatch, lo, hi, env={"PFR_FRONT0": "0"})
+    _same(f"front0_{lo}_{hi}", base, _run(monkeypatch, lo, hi, env={"PFR_FRONT0": "1"}))

@@ -20,7 +20,8 @@
   fixed 1e-6 would be below what the two fp64 solvers determine about a loss that is a small
   difference; and the two trajectories (x within 1e-7) with loss histories within 1e-4 of each other,
   relative (the loss falls 200x over three steps, so ~2e-8 in x and the two sides' non-smooth 1e-8-level
-  fr errors move the late iterates' loss by ~1e-5 of itself).
+  fr errors move the late iterates' loss by ~1e-5 of itself); the trajectories' loss difference within
+  (R_gpu + R_orc) f + 2 |g| |dx|, R from the extended-precision fixture below (derivation in the test).
 * the losses along the trajectory against EXTENDED-PRECISION truth (tests/golden/c5_truth.npz,
   make_c5_truth.py): at the 4 iterates of an oracle-driven 3-step L-BFGS run on the same subsample (fixed, so the
   points do not depend on the GPU) the loss from fr solved with longdouble residuals to convergence; the GPU loss at
@@ -30,6 +31,7 @@
 tests/test_gpu_reference_run.py.)
 """
 import gc
+import os
 
 import numpy as np
 import pytest
@@ -77,7 +79,6 @@ C5_LOSS_RTOL = 3 * 7.0e-7
 
 @pytest.mark.timeout(300)
 def test_c5_losses_match_extended_precision(c5):
-    import os
     T = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c5_truth.npz"))
     assert c5.mat_size == 19353 and str(T["material"]) == "orthotropic_d4"
     assert np.allclose(np.asarray(c5.parameters), T["theta_true"], rtol=0, atol=0)
@@ -129,10 +130,21 @@ def test_c5_full_mesh_iterates_match_oracle_driven(c5):
         gpu_fn(xt).backward()
         moved.append(2 * float(np.sum(np.abs(xt.grad.numpy()) * np.abs(x - xo_i))))
     moved = np.array(moved)
+    # The trajectory bound from the extended-precision fixture (tests/golden/c5_truth.npz: the losses at the
+    # iterates of an oracle-driven run on this subsample, x within ~3e-8 of both trajectories here).  With f_t
+    # the exact loss:  fg(xg) - fo(xo) = [fg(xg) - f_t(xg)] + [f_t(xg) - f_t(xo)] + [f_t(xo) - fo(xo)], so
+    #   |fg - fo| <= R_gpu f + R_orc f + moved,
+    # R_gpu = C5_LOSS_RTOL (3x the GPU's largest measured relative loss error there), R_orc = 3x the oracle's
+    # (1.56e-6 measured, its refinement's rounding), moved = 2 sum_i |g_i| |xg_i - xo_i| (first order, 2x for
+    # curvature).  Round 5's failure of the fr-error bound `bound` (1.15x once) came from taking the oracle's fr
+    # error at C3's orthotropic truth (1.7e-7) for this material: the fixture shows its LOSS errors along this
+    # trajectory reach 1.6e-6 relative (fr errors ~8e-8 amplified by 1/|d_q| near the optimum) -- the oracle side,
+    # not the GPU's (6.9e-7 at most, C5_LOSS_RTOL).
+    T = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c5_truth.npz"))
+    r_orc = 3 * float(np.max(np.abs(T["loss_oracle"] / T["loss_true"] - 1)))
+    traj_bound = (C5_LOSS_RTOL + r_orc) * np.maximum(fg, fo) + moved
     report("c5_trajectories", f_diff_max=float(np.max(np.abs(fg - fo))), moved_max=float(moved.max()),
-           over_bound=float(np.max(np.abs(fg - fo) / (bound + moved))), f_rel_max=float(np.max(np.abs(fg / fo - 1))))
-    # the trajectories' losses within 1e-4 of each other, relative, at every iterate (measured 6e-6 .. 2.4e-5
-    # over rounds 4-5).  The first-order bound above (fr errors + |g| |dx|) is reported, not asserted: it ran at
-    # 0.25-0.74 of itself and once (round 5) at 1.15 -- near the optimum both sides' 1e-8-level fr errors, which
-    # the oracle's refinement makes non-smooth in x, move the small loss by ~1e-5 of itself between the two paths
-    assert np.all(np.abs(fg / fo - 1) < 1e-4), (fg, fo)
+           over_bound=float(np.max(np.abs(fg - fo) / (bound + moved))), f_rel_max=float(np.max(np.abs(fg / fo - 1))),
+           over_traj_bound=float(np.max(np.abs(fg - fo) / traj_bound)), f_diff=np.abs(fg - fo).tolist(),
+           fo=fo.tolist(), moved=moved.tolist(), r_orc=r_orc)
+    assert np.all(np.abs(fg - fo) <= traj_bound), (np.abs(fg - fo), traj_bound)

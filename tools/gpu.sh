@@ -39,7 +39,7 @@ tests() {
 bench() { timeout -k 10 400 python3 -u bench.py "$@" > "$O/bench.json" 2> "$O/bench.err"; local rc=$?; cat "$O/bench.json"; tail -3 "$O/bench.err"; return $rc; }
 stats() {
   PFR_LANES=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/stats" -o run -- \
-    python3 bench.py --no-cpu-baseline --chunk 2048 "$@" > "$O/bench_lanes1_chunk2048.json" 2> "$O/stats.err"
+    python3 bench.py --no-cpu-baseline --no-strong-proxy --chunk 2048 "$@" > "$O/bench_lanes1_chunk2048.json" 2> "$O/stats.err"
 }
 traffic() {
   PFR_LANES=1 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$O/fetch" -o run -- \
@@ -64,7 +64,7 @@ envs() {
   local i=0 cfg
   for cfg in "$@"; do
     i=$((i + 1))
-    env $cfg timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --steps "${STEPS:-3}" --freqs "${FREQS:-2048}" \
+    env $cfg timeout -k 10 200 python3 -u bench.py --no-cpu-baseline --no-strong-proxy --steps "${STEPS:-3}" --freqs "${FREQS:-2048}" \
       > "$O/e$i.json" 2> "$O/e$i.err" || { tail -5 "$O/e$i.err"; return 1; }
     python3 -c "import json;d=json.load(open('$O/e$i.json'));f=d['factor_roofline'];p=d['phase_ms'];print('$cfg |', round(d['value']), [round(x,2) for x in f['ms']], {k:round(v,2) for k,v in p.items() if k!='note'})"
   done
@@ -77,7 +77,7 @@ case $CMD in
     timeout -k 10 600 python3 -u -m pytest tests/test_gpu_fullsize.py tests/test_gpu_parity.py tests/test_gpu_symmetric.py \
       -x -q --timeout 300 --timeout-method thread > "$O/tests.log" 2>&1
     rc=$?; tail -3 "$O/tests.log"; stop $rc
-    bench --no-cpu-baseline --steps 6 --warmup 2 ;;
+    bench --no-cpu-baseline --no-strong-proxy --steps 6 --warmup 2 ;;
   bench) bench "$@" ;;
   stats) stats "$@" ;;
   traffic) traffic ;;

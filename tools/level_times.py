@@ -42,26 +42,44 @@ def main(path, L=None):
             continue
         per = " ".join("%5.2f" % t.get(l, 0.0) for l in range(L)) if "x" not in t else ""
         print("%-20s %7.2f %s" % (n[:20], tot, per))
-    # whole-sweep view: device span of every sweep (first k_pad_freqs .. last kernel before the next
-    # one), the kernels' busy time inside it, and the idle time between consecutive sweeps (host side)
+    # whole-sweep view.  A sweep = the native kernels from its k_pad_freqs to its last pfr kernel (k_*); the
+    # TURNAROUND before sweep k = the GPU's idle time between the end of sweep k-1's last native kernel and
+    # the start of sweep k's k_pad_freqs -- the host's step-to-step work (the result copy, Python, autograd,
+    # the next step's buffer fills and copies); the torch / copy kernels run in that interval count as busy,
+    # not idle.  (Round 5's "idle before" was measured from the previous sweep's LAST kernel of any kind,
+    # which put the turnaround inside the span.)
     pads = [i for i, n in enumerate(names) if n == "k_pad_freqs"]
+    native = [i for i, n in enumerate(names) if n.startswith("k_")]
     spans = []
     for a, b in zip(pads, pads[1:] + [len(rows)]):
+        last = max(i for i in native if a <= i < b)
         t0 = int(rows[a]["Start_Timestamp"])
-        t1 = max(int(r["End_Timestamp"]) for r in rows[a:b])
-        busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows[a:b])
-        spans.append((t0, t1, busy, b - a))
-    for k, (t0, t1, busy, nk) in enumerate(spans):
-        gap = (t0 - spans[k - 1][1]) / 1e6 if k else float("nan")
-        print("sweep %2d: span %7.3f ms  busy %7.3f ms  kernels %4d  idle before %7.3f ms"
-              % (k, (t1 - t0) / 1e6, busy / 1e6, nk, gap))
+        t1 = int(rows[last]["End_Timestamp"])
+        busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows[a:last + 1])
+        spans.append((t0, t1, busy, last + 1 - a, a, last))
+    turn = []
+    for k, (t0, t1, busy, nk, a, last) in enumerate(spans):
+        idle = float("nan")
+        if k:
+            p_end, p_last = spans[k - 1][1], spans[k - 1][5]
+            between = rows[p_last + 1:a]
+            other = sum(min(int(r["End_Timestamp"]), t0) - max(int(r["Start_Timestamp"]), p_end) for r in between
+                        if int(r["End_Timestamp"]) > p_end and int(r["Start_Timestamp"]) < t0)
+            idle = (t0 - p_end - other) / 1e6
+            turn.append(((t0 - p_end) / 1e6, idle))
+        print("sweep %2d: span %7.3f ms  busy %7.3f ms  kernels %4d  turnaround before: %7.3f ms (GPU idle %7.3f ms)"
+              % (k, (t1 - t0) / 1e6, busy / 1e6, nk, (t0 - spans[k - 1][1]) / 1e6 if k else float("nan"), idle))
         if GAPS:
-            a = pads[k]
             b = pads[k + 1] if k + 1 < len(pads) else len(rows)
             for i in range(a + 1, b):
                 g = (int(rows[i]["Start_Timestamp"]) - int(rows[i - 1]["End_Timestamp"])) / 1e3
                 if g > 10:
                     print("    gap %8.1f us  %-24s -> %s" % (g, names[i - 1][:24], names[i][:24]))
+    if turn:
+        steady = turn[1:] or turn
+        print("turnaround between consecutive sweeps (steady, sweeps 2..): mean %.3f ms, GPU idle mean %.3f ms, max %.3f ms"
+              % (sum(t for t, _ in steady) / len(steady), sum(i for _, i in steady) / len(steady),
+                 max(i for _, i in steady)))
 
 
 GAPS = "--gaps" in sys.argv
