@@ -337,10 +337,16 @@ class _Engine:
         err = None
         if len(jobs) > 1 and self._pool is not None:
             from concurrent.futures import wait
-            futs = [self._pool.submit(lane, j) for j in jobs]
+            # lanes 1.. on the pool, lane 0 on this thread meanwhile (one thread handoff less before the
+            # first launch: the GPU idles from the previous step's result until then)
+            futs = [self._pool.submit(lane, j) for j in jobs[1:]]
+            try:
+                lane(jobs[0])
+            except Exception as e:           # noqa: BLE001 -- re-raised once every lane is joined
+                err = e
             wait(futs)                       # every lane has issued its work (or failed) ...
             errs = [f.exception() for f in futs if f.exception() is not None]
-            err = errs[0] if errs else None
+            err = err if err is not None else (errs[0] if errs else None)
         else:
             for j in jobs:
                 try:
@@ -382,18 +388,25 @@ class _Engine:
         acc.zero_()
         flags.zero_()
         berr.fill_(float('nan'))
+        # the lanes' views of this step's tensors, made once per (buffers, freqs, ref): slicing costs host time
+        # on the step-to-step turnaround
+        vkey = (key, freqs.data_ptr(), ref.data_ptr(), freqs.numel())
+        views = self._step_views.get(vkey) if hasattr(self, "_step_views") else None
+        if views is None:
+            views = {lo: (berr[lo:hi], freqs[lo:hi], ref[lo:hi], flags[lo:hi]) for lo, hi in self._split(n)}
+            self._step_views = {vkey: views}
 
         def call(sv, lo, hi, bufs):
-            sv.set_check(self.check_mode, self.check_tol, berr[lo:hi])
+            vb, vf, vr, vfl = views[lo]
+            sv.set_check(self.check_mode, self.check_tol, vb)
             try:
-                sv.sweep(freqs[lo:hi], loss_type, ref=ref[lo:hi], scale=scale, loss=bufs[0], w=bufs[1],
-                         flags=flags[lo:hi])
+                sv.sweep(vf, loss_type, ref=vr, scale=scale, loss=bufs[0], w=bufs[1], flags=vfl)
             finally:
                 sv.set_check(self.check_mode, self.check_tol)
         if self.check_mode & _native.PFR_CHECK_REFINE_ADJ:
             self._seeded = True
         self._run(call, n, None, lane_bufs=lanes)
-        torch.sum(flags != 0, dtype=torch.float64, out=acc[-1])
+        torch.sum(flags != 0, dim=0, dtype=torch.float64, out=acc[-1])
         h = acc.cpu().numpy()
         L, m = self.n_lanes, 2 + 2 * self.n_stiff
         per = h[:L * m].reshape(L, m)
