@@ -154,8 +154,11 @@ def test_c5_trajectory_matches_extended_precision(c5):
     d_q = log|fr_q| - log|ref_q|, so relative fr errors e_q move it by at most mean_q (2 |d_q| e_q + e_q^2) -- near
     the optimum (|d_q| ~ 1e-2, loss ~ 3e-5) an fr error of 1e-8 is ~1e-5 of the loss, and it varies between points
     1e-9 apart (the round-6 run of a loss-relative bound: 3.5e-6 and 2.1e-5 of the loss at iterates 1 and 3, with
-    the iterates within 7e-9 of the truth's).  E = 3x the GPU's largest relative fr error against fr_t at the
-    fixture's iterates (measured in this test); then with the GPU iterates x_g within 1e-7 of x_t:
+    the iterates within 7e-9 of the truth's).  E = the fr error bound this build asserts against the
+    extended-precision truth at C3 (FR_RTOL_C3 = 1e-7, 6.2e-8 measured: test_gpu_fullsize.py), or 3x the largest
+    error measured here at the fixture's iterates if larger -- the error at the GPU's own iterates is a fresh draw
+    of the rounding (3x the fixture points' largest alone was exceeded by 1.6 % at iterate 1 in round 6); then
+    with the GPU iterates x_g within 1e-7 of x_t:
       |f_gpu(x_g) - f_t(x_t)| <= mean_q (2 |d_q(x_g)| E + E^2) + moved,
     moved = 2 sum_i |g_i| |x_g - x_t|_i (first order in the iterate difference, 2x for curvature)."""
     from plate_inverse_problem_amd import Optimizers
@@ -164,7 +167,7 @@ def test_c5_trajectory_matches_extended_precision(c5):
     freqs, ref, th0 = T["freqs"], T["ref"], T["theta0"]
     e_fr = max(float(np.max(np.abs(np.abs(c5.solveForward(freqs, x * th0)) / np.abs(T["fr_true"][i]) - 1)))
                for i, x in enumerate(T["x"]))
-    E = 3 * e_fr
+    E = max(1e-7, 3 * e_fr)
     fn = c5.getLossFunction(freqs, ref, "MSE_LOG_AFC", th0)
     res = Optimizers.optimize_lbfgs(fn, np.ones(8), N_steps=len(T["x"]) - 1)
     xg = np.array([np.asarray(v, dtype=np.float64) for v in res.x_history + [res.x]])

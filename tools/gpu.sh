@@ -15,7 +15,7 @@
 #                                                     (FREQS frequencies, STEPS timed steps)
 #   bash tools/gpu.sh strong  OUT                     1-GPU strong-scaling proxy (tools/strong_proxy.py)
 #   bash tools/gpu.sh round   R                       round measurement: tests, traffic (-> profiles/R),
-#                                                     bench, stats, C5, strong proxy
+#                                                     bench, stats, C5, strong proxy, 6-step 512 trace
 #
 # Every GPU step runs under its own time limit; the script stops at the first failure and never
 # starts another GPU step after a timeout / abort / fault (exit 124, 134, 137, 139).
@@ -95,6 +95,7 @@ case $CMD in
     timeout -k 10 600 python3 -u tools/c5_lbfgs.py > "$O/c5.json" 2> "$O/c5.err"; stop $?
     cat "$O/c5.json"
     strong; stop $?
+    mkdir -p "$O/tr512" && (O=$O/tr512; STEPS=6 trace 512) > "$O/tr512/levels.txt" 2>&1; stop $?
     echo DONE ;;
   *) echo "unknown command $CMD"; exit 2 ;;
 esac
