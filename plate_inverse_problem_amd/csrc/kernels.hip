@@ -2047,17 +2047,21 @@ __device__ __forceinline__ void tri_rl16(const cplx* __restrict__ base, int f, i
   // the ring's next column pointer per row (the pivot of step t + PF, clamped into the block), advanced by one
   // column per step; the owner slot p % nsl likewise (no per-step index arithmetic: every wave of every
   // workgroup runs each step's instructions, so they set the step time)
+  // A row uses the column entry of pivot p only on one side of the diagonal (UP: rows i < p; !UP: rows i > p); on the
+  // other side its ring loads its own diagonal entry instead (one address, cached), so the ring reads the factor
+  // triangle once rather than whole columns: column max(p, i) (UP) / min(p, i) (!UP) of row i.
   const int64_t dcol = UP ? -Fc : Fc;
   const cplx* lp[RPL];
   auto col = [&](int t) { const int tc = min(t, ns - 1); return UP ? ns - 1 - tc : tc; };
+  auto cc = [&](int t, int i) { return UP ? max(col(t), i) : min(col(t), i); };
 #pragma unroll
   for (int r = 0; r < RPL; ++r) lp[r] = base + (int64_t)ic[r] * f * Fc;
 #pragma unroll
   for (int u = 0; u < PF; ++u)
 #pragma unroll
-    for (int r = 0; r < RPL; ++r) pre[u][r] = lp[r][(int64_t)col(u) * Fc];
+    for (int r = 0; r < RPL; ++r) pre[u][r] = lp[r][(int64_t)cc(u, ic[r]) * Fc];
 #pragma unroll
-  for (int r = 0; r < RPL; ++r) lp[r] += (int64_t)col(PF) * Fc;
+  for (int r = 0; r < RPL; ++r) lp[r] += (int64_t)cc(PF, ic[r]) * Fc;
   int os = col(0) % nsl;
   // one pivot step t with the column entries e; the owner's solved value through LDS (buffer t & 1)
   auto step = [&](int t, const cplx (&e)[RPL]) {
@@ -2099,11 +2103,12 @@ __device__ __forceinline__ void tri_rl16(const cplx* __restrict__ base, int f, i
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
       cplx e[RPL];
+      const int tn = t0 + u + PF + 1, pn = UP ? ns - 1 - tn : tn;   // the pointers move to step tn's column
 #pragma unroll
       for (int r = 0; r < RPL; ++r) {
         e[r] = pre[u][r];
         pre[u][r] = *lp[r];
-        if (t0 + u + PF + 1 < ns) lp[r] += dcol;
+        if (tn < ns && (UP ? pn >= ic[r] : pn <= ic[r])) lp[r] += dcol;
       }
       step(t0 + u, e);
     }

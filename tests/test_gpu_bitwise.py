@@ -85,3 +85,4 @@ def test_offdiag_pipelined_prefix_bitwise(monkeypatch, lo, hi):
 def test_front0_fused_bottom_level_bitwise(monkeypatch, lo, hi):
     base = _run(monkeypatch, lo, hi, env={"PFR_FRONT0": "0"})
     _same(f"front0_{lo}_{hi}", base, _run(monkeypatch, lo, hi, env={"PFR_FRONT0": "1"}))
+
