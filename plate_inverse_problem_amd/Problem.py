@@ -179,11 +179,13 @@ class _Engine:
         return changed
 
     def _lanes_for(self, n_freqs: int) -> int:
-        """Solver lanes for a sweep of ``n_freqs``: a lane per 256 frequencies at most.  Round 3 kept 512
+        """Solver lanes for a sweep of ``n_freqs``: a lane per 512 frequencies at most.  Round 3 kept 512
         frequencies on one lane (27.1k against 26.4k freq-solves/s with two); with round 5's kernels two lanes of
-        256 overlap each other's narrow-level chains and kernel drains: 36.2-36.8k → 36.6-37.6k over five
-        alternations, four lanes of 128 27.5k (profiles/EXPERIMENTS.md, round 5)."""
-        return max(1, min(self._lanes_req, -(-max(1, n_freqs) // 256)))
+        256 overlapped each other's narrow-level chains and kernel drains: 36.2-36.8k → 36.6-37.6k over five
+        alternations, four lanes of 128 27.5k (profiles/EXPERIMENTS.md, round 5).  Round 6's right-looking
+        narrow-level solves shortened the one-lane chain: 512 frequencies on one lane 41.7-41.8k against
+        41.1-41.2k on two (alternated, gpurun_out/r6k_e512)."""
+        return max(1, min(self._lanes_req, -(-max(1, n_freqs) // 512)))
 
     def _shape_for(self, n_freqs: int):
         """(lanes, frequencies per chunk) for a sweep of ``n_freqs``: up to ``lanes`` lanes of at
