@@ -8,7 +8,7 @@ import csv
 import sys
 
 
-LU = ("k_factor_sym", "k_factor_sym_lds", "k_factor_level", "k_front0")   # k_front0: the fused bottom level
+LU = ("k_factor_sym", "k_factor_sym_lds", "k_factor_sym_rl", "k_factor_level", "k_front0")   # k_front0: the fused bottom level
 
 
 def main(path, L=None):
