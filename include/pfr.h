@@ -208,6 +208,12 @@ PFR_API int pfr_set_functional(pfr_solver* s, int32_t n_support, const int32_t* 
 PFR_API int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t loss_type,
                       const double* ref_dev, double scale, double* fr_dev, double* loss_dev, double* w_dev,
                       int32_t* flags_dev, void* stream);
+/* Sweeps of this solver replayed from its captured hipGraph so far.  A pfr_sweep called again with the same
+ * arguments, stream and solver state (no setter called in between; pfr_set_check's mode, tolerance and berr
+ * pointer are part of the arguments) is captured into a hipGraph on that second call and replayed with one
+ * hipGraphLaunch afterwards -- the same kernels with the same arguments; only with PFR_GRAPH=1 (off by default).  The
+ * reference's analogue is none: its sweep is a host loop of UMFPACK calls (InnerState.h:276-288). */
+PFR_API int64_t pfr_sweep_graph_launches(const pfr_solver* s);
 
 /* Exact second derivatives with the factors of the sweep reused (replaces the reference's
  * forward-over-reverse Hessian, `jax.jacobian(grad)` in Optimizers.py:125-136, whose mode-4

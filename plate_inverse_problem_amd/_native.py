@@ -74,6 +74,7 @@ _PROTOS = {
     "pfr_set_rhs": (C.c_int, [_P, _DP, C.c_double, C.c_double, C.c_double]),
     "pfr_set_functional": (C.c_int, [_P, C.c_int32, _I32P, _DP, C.c_double]),
     "pfr_sweep": (C.c_int, [_P, C.c_int32, _P, C.c_int32, _P, C.c_double, _P, _P, _P, _P, _P]),
+    "pfr_sweep_graph_launches": (C.c_int64, [_P]),
     "pfr_solve_multi": (C.c_int, [_P, C.c_int32, C.c_int32, _P, C.c_int64, _P, C.c_int64, C.c_int64, _P, C.c_int64,
                                   C.c_int32, _P, _P]),
     "pfr_hessian_sweep": (C.c_int, [_P, C.c_int32, _P, C.c_int32, _P, C.c_double, C.c_int32, _P, _P, _P, _P, _P,
@@ -316,6 +317,10 @@ class Solver:
         """PFR_CHECK_* bits, flag tolerance; ``berr`` (device float64, 2 per frequency of each later
         call, or None) receives the componentwise backward errors (forward, adjoint)."""
         check(lib().pfr_set_check(self._h, int(mode), float(tol), _ptr(berr)), "pfr_set_check")
+
+    def graph_launches(self) -> int:
+        """Sweeps of this solver replayed from its captured hipGraph (pfr_sweep_graph_launches)."""
+        return int(lib().pfr_sweep_graph_launches(self._h))
 
     # ---- timing
     def set_timing(self, on, kernels: bool = False):

@@ -217,8 +217,27 @@ struct pfr_solver {
   double2* Gx = nullptr;                // the fr seed of the forward solution (support rows; zero elsewhere)
   double* berr_out = nullptr;
   double* d_berr_acc = nullptr;
+  // sweep graphs (PFR_GRAPH=1): a pfr_sweep called again with the same arguments and solver state (gen:
+  // bumped by every setter that changes what a sweep enqueues) is captured once into a hipGraph and from then on
+  // replayed with one hipGraphLaunch instead of ~160-290 kernel launches; any other sweep runs the launches
+  // directly.  graph_off: a capture failed on this solver, no further attempts.
+  int graph_mode = 0;
+  bool graph_off = false;
+  uint64_t gen = 0;
+  std::array<uint64_t, 14> gkey{};
+  bool gkey_valid = false;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  int64_t graph_launches = 0;           // sweeps replayed from the graph (pfr_sweep_graph_launches)
 
+  void drop_graph() {
+    if (gexec) (void)hipGraphExecDestroy(gexec);
+    if (graph) (void)hipGraphDestroy(graph);
+    gexec = nullptr;
+    graph = nullptr;
+  }
   ~pfr_solver() {
+    drop_graph();
     for (void* p : owned) (void)hipFree(p);
     for (auto& c : tev) {
       for (auto& x : c.ev)
@@ -621,8 +640,11 @@ void contract_rows(pfr_solver* s, const double2* lam, const double2* x, int nv, 
 }  // namespace
 
 namespace pfr {
-void launch_pad_freqs(double* freqs, int nvalid, int64_t Fc, hipStream_t st);
 void launch_flags_merge(const int* chunk, int nvalid, int* out, hipStream_t st);
+// a chunk's frequencies (padded with the last) and its flags cleared, one kernel
+void launch_chunk_start(double* freqs, const double* src, int nvalid, int64_t Fc, int* flags, hipStream_t st);
+// p[0 .. n) = 0 (complex entries)
+void launch_zero(double2* p, int64_t n, hipStream_t st);
 }
 
 extern "C" {
@@ -815,6 +837,10 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   // PFR_FRONT0=0: level 0 through the four class kernels instead of the fused k_front0 (tests/test_gpu_bitwise.py
   // checks the two give the same factors bit for bit)
   s->fused0 = pl.fused0 && knob("PFR_FRONT0", 1, 0, 1);
+  // PFR_GRAPH=1: repeated sweeps captured into and replayed from a hipGraph (off by default: bitwise the same
+  // results and the host's enqueue of a 512-frequency sweep 427 -> 75 us, but 512 frequencies within the spread
+  // and 4,096 frequencies 1 % slower on the device, 67.0-67.6k -> 66.5-66.8k, gpurun_out/r6r_e4096)
+  s->graph_mode = knob("PFR_GRAPH", 0, 0, 1);
   s->n_f0 = (int)pl.f0_front.size();
   s->f0_small = pl.f0_small;
   Front* d_fronts = nullptr;
@@ -902,6 +928,7 @@ int32_t pfr_solver_max_batch(const pfr_solver* s) { return s ? (int32_t)s->Fc : 
 
 int pfr_set_timing(pfr_solver* s, int32_t enable) {
   if (!s) return fail(PFR_ERR_ARG, "null solver");
+  ++s->gen;
   s->timing = enable == 0 ? 0 : (enable | 1);
   return PFR_OK;
 }
@@ -923,6 +950,7 @@ int pfr_debug_solution(pfr_solver* s, int32_t which, int32_t q, double* out) {
 
 int pfr_set_refine_tol(pfr_solver* s, double tol) {
   if (!s || !(tol >= 0.0)) return fail(PFR_ERR_ARG, "bad refine tolerance");
+  ++s->gen;
   s->refine_tol = tol;
   return PFR_OK;
 }
@@ -1032,6 +1060,7 @@ int pfr_solver_solve_bytes(const pfr_solver* s, int64_t* bytes) {
 int pfr_set_stiffness(pfr_solver* s, int32_t n_stiff, const double* stiff_dev, const double* w) {
   if (!s || (n_stiff != 12 && n_stiff != 18) || !stiff_dev || !w)
     return fail(PFR_ERR_ARG, "bad stiffness arguments (n_stiff must be 12 or 18)");
+  ++s->gen;
   s->stiff = stiff_dev;
   s->n_stiff = n_stiff;
   std::memset(&s->e, 0, sizeof(s->e));
@@ -1071,6 +1100,7 @@ int pfr_combine(pfr_solver* s, const double* coef, double* K_out, void* stream) 
 
 int pfr_set_operator(pfr_solver* s, const double* K_dev, const double* M_dev) {
   if (!s || !K_dev || !M_dev) return fail(PFR_ERR_ARG, "null argument");
+  ++s->gen;
   s->K = reinterpret_cast<const double2*>(K_dev);
   s->M = M_dev;
   return PFR_OK;
@@ -1078,6 +1108,7 @@ int pfr_set_operator(pfr_solver* s, const double* K_dev, const double* M_dev) {
 
 int pfr_set_rhs(pfr_solver* s, const double* rhs, double beta_re, double beta_im, double mass_sum) {
   if (!s || !rhs) return fail(PFR_ERR_ARG, "null argument");
+  ++s->gen;
   s->beta_re = beta_re;
   s->beta_im = beta_im;
   s->mass_sum = mass_sum;
@@ -1123,6 +1154,7 @@ int pfr_set_rhs(pfr_solver* s, const double* rhs, double beta_re, double beta_im
 
 int pfr_set_functional(pfr_solver* s, int32_t n_support, const int32_t* index, const double* a, double ts) {
   if (!s || n_support <= 0 || !index || !a) return fail(PFR_ERR_ARG, "bad functional arguments");
+  ++s->gen;
   HIP_TRY(hipSetDevice(s->device));
   std::vector<int32_t> pidx(n_support);
   for (int i = 0; i < n_support; ++i) {
@@ -1147,18 +1179,13 @@ int pfr_set_functional(pfr_solver* s, int32_t n_support, const int32_t* index, c
   return PFR_OK;
 }
 
-int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t loss_type, const double* ref_dev,
-              double scale, double* fr_dev, double* loss_dev, double* w_dev, int32_t* flags_dev, void* stream) {
-  if (!s || nfreq <= 0 || !freqs_dev) return fail(PFR_ERR_ARG, "bad sweep arguments");
-  if (!s->K || !s->M) return fail(PFR_ERR_STATE, "operator not set (pfr_set_operator)");
-  if (!s->has_rhs) return fail(PFR_ERR_STATE, "rhs not set (pfr_set_rhs)");
-  if (!s->has_fn) return fail(PFR_ERR_STATE, "functional not set (pfr_set_functional)");
+}  // extern "C"
+
+namespace {
+// The launches of one sweep (pfr_sweep after its argument checks), direct or under stream capture.
+int sweep_launches(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t loss_type, const double* ref_dev,
+                   double scale, double* fr_dev, double* loss_dev, double* w_dev, int32_t* flags_dev, hipStream_t st) {
   const bool reverse = loss_type != PFR_LOSS_NONE;
-  if (reverse && (loss_type < 0 || loss_type > PFR_LOSS_COTANGENT || !ref_dev))
-    return fail(PFR_ERR_ARG, "bad loss type / missing ref");
-  if (reverse && (!s->stiff || !w_dev)) return fail(PFR_ERR_STATE, "reverse pass needs pfr_set_stiffness and w_dev");
-  HIP_TRY(hipSetDevice(s->device));
-  hipStream_t st = (hipStream_t)stream;
   reset_timing(s);
   const int64_t Fc = s->Fc;
   const bool refine = (s->check_mode & PFR_CHECK_REFINE) != 0;
@@ -1174,9 +1201,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
   bool used[5] = {true, true, true, adj, adj};
   for (int64_t q0 = 0; q0 < nfreq; q0 += Fc) {
     const int nv = (int)std::min<int64_t>(Fc, nfreq - q0);
-    HIP_TRY(hipMemcpyAsync(s->freqs, freqs_dev + q0, nv * sizeof(double), hipMemcpyDeviceToDevice, st));
-    pfr::launch_pad_freqs(s->freqs, nv, Fc, st);
-    HIP_TRY(hipMemsetAsync(s->flags, 0, Fc * sizeof(int32_t), st));
+    pfr::launch_chunk_start(s->freqs, freqs_dev + q0, nv, Fc, s->flags, st);
     if (int rc0 = begin_chunk(s)) return rc0;
     record(s, 0, st);
     pfr::RhsDesc rd;
@@ -1225,7 +1250,7 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
     fa.loss_type = reverse ? loss_type : -1;
     fa.ref = reinterpret_cast<const double2*>(ref_dev);
     fa.scale = scale;
-    if (adj) HIP_TRY(hipMemsetAsync(s->G, 0, (size_t)s->n * Fc * 16, st));
+    if (adj) pfr::launch_zero(s->G, (int64_t)s->n * Fc, st);
     if (fn_fast) {
       const double2* Yk[3] = {s->Y2, s->YVk, s->YVk + (int64_t)s->n * Fc};
       pfr::launch_fn_dot(s->d_fn_rows, s->n_fn_rows, s->F, s->Y, Yk, Fc, s->fn_parts, st);
@@ -1347,11 +1372,75 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
   return PFR_OK;
 }
 
+template <class T>
+uint64_t key_bits(T v) {
+  uint64_t b = 0;
+  static_assert(sizeof(T) <= sizeof(b), "key word");
+  std::memcpy(&b, &v, sizeof(T));
+  return b;
+}
+}  // namespace
+
+extern "C" {
+
+int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t loss_type, const double* ref_dev,
+              double scale, double* fr_dev, double* loss_dev, double* w_dev, int32_t* flags_dev, void* stream) {
+  if (!s || nfreq <= 0 || !freqs_dev) return fail(PFR_ERR_ARG, "bad sweep arguments");
+  if (!s->K || !s->M) return fail(PFR_ERR_STATE, "operator not set (pfr_set_operator)");
+  if (!s->has_rhs) return fail(PFR_ERR_STATE, "rhs not set (pfr_set_rhs)");
+  if (!s->has_fn) return fail(PFR_ERR_STATE, "functional not set (pfr_set_functional)");
+  const bool reverse = loss_type != PFR_LOSS_NONE;
+  if (reverse && (loss_type < 0 || loss_type > PFR_LOSS_COTANGENT || !ref_dev))
+    return fail(PFR_ERR_ARG, "bad loss type / missing ref");
+  if (reverse && (!s->stiff || !w_dev)) return fail(PFR_ERR_STATE, "reverse pass needs pfr_set_stiffness and w_dev");
+  HIP_TRY(hipSetDevice(s->device));
+  hipStream_t st = (hipStream_t)stream;
+  auto direct = [&] { return sweep_launches(s, nfreq, freqs_dev, loss_type, ref_dev, scale, fr_dev, loss_dev, w_dev,
+                                            flags_dev, st); };
+  // per-launch timing events are host work between the launches: never under a graph
+  if (!s->graph_mode || s->graph_off || s->timing) return direct();
+  const std::array<uint64_t, 14> key = {s->gen, key_bits(s->check_mode), key_bits(s->check_tol), key_bits(s->berr_out),
+                                        key_bits(nfreq), key_bits(freqs_dev), key_bits(loss_type), key_bits(ref_dev),
+                                        key_bits(scale), key_bits(fr_dev), key_bits(loss_dev), key_bits(w_dev),
+                                        key_bits(flags_dev), key_bits(st)};
+  if (!s->gkey_valid || key != s->gkey) {
+    // a new sweep configuration: run it directly (its first run also makes the lazy allocations and uploads,
+    // which a capture must not contain); the same configuration again is captured
+    s->drop_graph();
+    s->gkey = key;
+    s->gkey_valid = true;
+    return direct();
+  }
+  if (!s->gexec) {
+    hipGraph_t g = nullptr;
+    HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    const int rc = direct();
+    const hipError_t e = hipStreamEndCapture(st, &g);
+    hipGraphExec_t x = nullptr;
+    if (rc == PFR_OK && e == hipSuccess && g && hipGraphInstantiate(&x, g, nullptr, nullptr, 0) == hipSuccess) {
+      s->graph = g;
+      s->gexec = x;
+    } else {
+      // nothing of the captured work ran: no graphs on this solver from now on, and this sweep directly
+      if (g) (void)hipGraphDestroy(g);
+      (void)hipGetLastError();
+      s->graph_off = true;
+      return direct();
+    }
+  }
+  HIP_TRY(hipGraphLaunch(s->gexec, st));
+  ++s->graph_launches;
+  return PFR_OK;
+}
+
+int64_t pfr_sweep_graph_launches(const pfr_solver* s) { return s ? s->graph_launches : 0; }
+
 int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t loss_type, const double* ref_dev,
                       double scale, int32_t n_dir, const double* dcoef, double* loss_dev, double* w_dev,
                       double* h_dev, int32_t* flags_dev, void* stream) {
   if (!s || nfreq <= 0 || !freqs_dev || !ref_dev || !w_dev || !h_dev || n_dir <= 0 || !dcoef)
     return fail(PFR_ERR_ARG, "bad hessian sweep arguments");
+  ++s->gen;
   if (loss_type < PFR_LOSS_MSE || loss_type > PFR_LOSS_MSE_LOG_AFC)
     return fail(PFR_ERR_ARG, "hessian sweep needs a loss type (MSE, RMSE, MSE_AFC, MSE_LOG_AFC)");
   if (!s->K || !s->M) return fail(PFR_ERR_STATE, "operator not set (pfr_set_operator)");
@@ -1386,9 +1475,7 @@ int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int
   double2* H = reinterpret_cast<double2*>(h_dev);
   for (int64_t q0 = 0; q0 < nfreq; q0 += Fc) {
     const int nv = (int)std::min<int64_t>(Fc, nfreq - q0);
-    HIP_TRY(hipMemcpyAsync(s->freqs, freqs_dev + q0, nv * sizeof(double), hipMemcpyDeviceToDevice, st));
-    pfr::launch_pad_freqs(s->freqs, nv, Fc, st);
-    HIP_TRY(hipMemsetAsync(s->flags, 0, Fc * sizeof(int32_t), st));
+    pfr::launch_chunk_start(s->freqs, freqs_dev + q0, nv, Fc, s->flags, st);
     if ((rc = factor_all(s, 0, nullptr, 0, nv, st))) return rc;
     // forward solve, loss, adjoint, gradient partials (as pfr_sweep)
     pfr::RhsDesc rd;
@@ -1466,6 +1553,7 @@ int pfr_solve_multi(pfr_solver* s, int32_t batch, int32_t nrhs, const double* da
   if (!s || batch <= 0 || nrhs <= 0 || !data_dev || !b_dev || !x_dev || data_stride < 0 || b_stride < 0 ||
       b_rhs_stride < 0 || x_rhs_stride < 0)
     return fail(PFR_ERR_ARG, "bad solve arguments");
+  ++s->gen;
   if (data_stride != 0 && data_stride < s->nnz) return fail(PFR_ERR_ARG, "data_stride < nnz");
   if (b_stride != 0 && b_stride < s->n) return fail(PFR_ERR_ARG, "b_stride < n");
   if (nrhs > 1 && x_rhs_stride < (int64_t)batch * s->n) return fail(PFR_ERR_ARG, "x_rhs_stride < batch * n");
@@ -1540,6 +1628,7 @@ int pfr_solve(pfr_solver* s, int32_t batch, const double* data_dev, int64_t data
 int pfr_matvec(pfr_solver* s, int32_t batch, const double* data_dev, int64_t data_stride, const double* x_dev,
                int64_t x_stride, double* y_dev, int32_t transpose, void* stream) {
   if (!s || batch <= 0 || !data_dev || !x_dev || !y_dev) return fail(PFR_ERR_ARG, "bad matvec arguments");
+  ++s->gen;
   HIP_TRY(hipSetDevice(s->device));
   hipStream_t st = (hipStream_t)stream;
   if (!transpose) HIP_TRY(hipMemsetAsync(y_dev, 0, (size_t)batch * s->n * 16, st));

@@ -3760,12 +3760,26 @@ void launch_dirichlet_post(const DirDesc& d, int n_dir, double2* X, int64_t Fc, 
 }
 
 // fill padded frequency slots with the last valid frequency (keeps padded lanes well-posed)
-__global__ void k_pad_freqs(double* freqs, int nvalid, int64_t Fc) {
+// A chunk's start in one kernel (no memcpy / memset nodes in a captured sweep): its frequencies from the caller's
+// array, padded to Fc with the last one, and its flags cleared
+__global__ void k_chunk_start(double* __restrict__ freqs, const double* __restrict__ src, int nvalid, int64_t Fc,
+                              int* __restrict__ flags) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= nvalid && q < Fc) freqs[q] = freqs[nvalid - 1];
+  if (q < Fc) {
+    freqs[q] = src[q < nvalid ? q : nvalid - 1];
+    flags[q] = 0;
+  }
 }
-void launch_pad_freqs(double* freqs, int nvalid, int64_t Fc, hipStream_t st) {
-  LAUNCH(k_pad_freqs, dim3((unsigned)((Fc + 63) / 64)), dim3(64), st, freqs, nvalid, Fc);
+void launch_chunk_start(double* freqs, const double* src, int nvalid, int64_t Fc, int* flags, hipStream_t st) {
+  LAUNCH(k_chunk_start, dim3((unsigned)((Fc + 255) / 256)), dim3(256), st, freqs, src, nvalid, Fc, flags);
+}
+__global__ void k_zero(double2* __restrict__ p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = make_double2(0.0, 0.0);
+}
+void launch_zero(double2* p, int64_t n, hipStream_t st) {
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 8192);
+  LAUNCH(k_zero, dim3((unsigned)blocks), dim3(256), st, p, n);
 }
 __global__ void k_flags_merge(const int* chunk, int nvalid, int* out) {
   const int q = blockIdx.x * blockDim.x + threadIdx.x;

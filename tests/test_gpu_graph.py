@@ -1,0 +1,103 @@
+"""GPU: sweep graphs (PFR_GRAPH, api.cpp pfr_sweep).  A loss + gradient step repeated with the same arguments is
+captured into a hipGraph on its second call and replayed afterwards; the replay runs the same kernels with the same
+arguments, so loss, gradient and backward errors must EQUAL the direct launches' bit for bit.  A step at a new
+theta (pfr_set_rhs in between: a new solver state) must leave the graph and run directly, and the same theta
+again must be captured again.  Workload: C4's per-rank block (512 frequencies of the C3 sweep, the one with the
+resonance), the loop an optimiser or the bench runs (Problem.getLossFunction + backward)."""
+import gc
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import make_problem, report
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _steps(monkeypatch, graph, thetas):
+    from plate_inverse_problem_amd.distributed import shard_range
+    monkeypatch.setenv("PFR_GRAPH", graph)
+    T = np.load(os.path.join(GOLDEN, "c3_grad_truth.npz"))
+    lo, hi = shard_range(4096, 2, 8)
+    sel = np.arange(lo, hi)
+    p = make_problem("orthotropic", ny=25, device="cuda:0")
+    try:
+        fn = p.getLossFunction(T["freqs"][sel], T["ref"][sel], "MSE_LOG_AFC")
+        out = []
+        for th in thetas:
+            x = torch.tensor(th, requires_grad=True)
+            v = fn(x)
+            v.backward()
+            eng = p.engine()
+            out.append((v.item(), x.grad.numpy().copy(), eng.last_berr.cpu().numpy().copy()))
+        eng = p.engine()
+        return out, sum(sv.graph_launches() for sv in eng.solvers), eng.n_lanes
+    finally:
+        p._engine = None
+        del p
+        gc.collect()
+        torch.cuda.empty_cache()
+
+
+def test_graph_replay_bitwise_and_state_changes(monkeypatch):
+    T = np.load(os.path.join(GOLDEN, "c3_grad_truth.npz"))
+    t0 = np.asarray(T["theta"], dtype=np.float64)
+    t1 = t0 * (1 + 0.01 * np.arange(1, t0.size + 1))
+    # t0 x4: direct, captured, replayed, replayed; t1 x3: direct (new rhs scale), captured, replayed; t0: direct
+    thetas = [t0, t0, t0, t0, t1, t1, t1, t0]
+    direct, n0, lanes = _steps(monkeypatch, "0", thetas)
+    graph, n1, lanes1 = _steps(monkeypatch, "1", thetas)
+    assert n0 == 0 and lanes == lanes1
+    assert n1 == 5 * lanes, n1
+    dl = max(abs(g[0] - d[0]) for g, d in zip(graph, direct))
+    dw = max(float(np.max(np.abs(g[1] - d[1]))) for g, d in zip(graph, direct))
+    db = max(float(np.nanmax(np.abs(g[2] - d[2]))) for g, d in zip(graph, direct))
+    report("graph_replay_vs_direct", loss_diff=dl, grad_diff=dw, berr_diff=db, graph_launches=n1, lanes=lanes)
+    for k, (g, d) in enumerate(zip(graph, direct)):
+        assert g[0] == d[0], (k, g[0], d[0])
+        assert np.array_equal(g[1], d[1]), k
+        assert np.array_equal(np.isnan(g[2]), np.isnan(d[2])) and np.array_equal(np.nan_to_num(g[2]),
+                                                                                  np.nan_to_num(d[2])), k
+    # the steps at one theta agree among themselves (replays of one graph and the direct run before them)
+    assert graph[0][0] == graph[3][0] and np.array_equal(graph[0][1], graph[3][1])
+    assert graph[4][0] != graph[0][0]
+
+
+def test_graph_two_lanes_repeated_steps(monkeypatch):
+    """C3's 4,096 frequencies on two lanes (two solvers, two host threads, each capturing and replaying its own
+    graph): twelve steps at one theta -- every step's loss and gradient equal to the first (direct) step's, no
+    frequency flagged by the on-device backward-error checks."""
+    import bench
+    monkeypatch.setenv("PFR_GRAPH", "1")
+    p = bench.build_problem(25, torch.device("cuda", 0))
+    try:
+        th0 = p.parameters.copy()
+        freqs = np.linspace(40.0, 600.0, 4096)
+        ref = p.solveForward(freqs, th0)
+        fn = p.getLossFunction(freqs, ref, "MSE_LOG_AFC")
+        theta = th0 * (1 + np.array([0.1, 0.1, 0.2, 0.1, 0.1]))
+        vals, grads, nflag = [], [], []
+        for _ in range(12):
+            x = torch.tensor(theta, requires_grad=True)
+            v = fn(x)
+            v.backward()
+            eng = p.engine()
+            vals.append(v.item())
+            grads.append(x.grad.numpy().copy())
+            nflag.append(int(np.count_nonzero(eng.last_flags)))
+        n_graph = sum(sv.graph_launches() for sv in eng.solvers)
+        report("graph_two_lanes", lanes=eng.n_lanes, graph_launches=n_graph, flagged=max(nflag),
+               loss_spread=max(vals) - min(vals))
+        assert eng.n_lanes == 2 and n_graph == 2 * 11      # step 1 direct (new theta), 2 captured, 3-12 replayed
+        assert max(nflag) == 0, nflag
+        for k in range(1, 12):
+            assert vals[k] == vals[0] and np.array_equal(grads[k], grads[0]), k
+    finally:
+        p._engine = None
+        del p
+        gc.collect()
+        torch.cuda.empty_cache()

@@ -31,7 +31,9 @@ def loss_step(self, *a, **k):
 
 def sweep(self, *a, **k):
     mark("native_sweep_in")
-    return _orig_sw(self, *a, **k)
+    r = _orig_sw(self, *a, **k)
+    mark("native_sweep_out")       # the sweep's launches enqueued (host side)
+    return r
 
 
 PM._Engine.loss_step = loss_step
@@ -77,6 +79,10 @@ def main():
         print(r)
     print("mean host time from result to the next step's first native sweep call: %.1f us"
           % np.mean([r["first_native_us"] for r in rows]))
+    ins = [t for tag, t in T if tag == "native_sweep_in"]
+    outs_n = [t for tag, t in T if tag == "native_sweep_out"]
+    print("mean host enqueue time of one lane's sweep (pfr_sweep call to return): %.1f us"
+          % (1e6 * np.mean(np.subtract(outs_n, ins))))
 
 
 if __name__ == "__main__":

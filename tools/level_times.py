@@ -16,8 +16,8 @@ def main(path, L=None):
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     names = [r["Kernel_Name"].split("(")[0].replace("void ", "").replace("pfr::", "").split("<")[0] for r in rows]
     # one A11 LU launch per level (the assembly may be fused into it): the level marker; the level count is
-    # that of the last sweep (k_pad_freqs starts every chunk)
-    pads = [i for i, n in enumerate(names) if n == "k_pad_freqs"]
+    # that of the last sweep (k_chunk_start -- k_pad_freqs before round 6 -- starts every chunk)
+    pads = [i for i, n in enumerate(names) if n in ("k_chunk_start", "k_pad_freqs")]
     lus = [i for i, n in enumerate(names) if n in LU and not (n == "k_front0" and names[i - 1] == "k_front0")]
     if L is None:
         L = sum(1 for i in lus if i > pads[-1]) if pads else 17
@@ -42,13 +42,13 @@ def main(path, L=None):
             continue
         per = " ".join("%5.2f" % t.get(l, 0.0) for l in range(L)) if "x" not in t else ""
         print("%-20s %7.2f %s" % (n[:20], tot, per))
-    # whole-sweep view.  A sweep = the native kernels from its k_pad_freqs to its last pfr kernel (k_*); the
+    # whole-sweep view.  A sweep = the native kernels from its k_chunk_start to its last pfr kernel (k_*); the
     # TURNAROUND before sweep k = the GPU's idle time between the end of sweep k-1's last native kernel and
-    # the start of sweep k's k_pad_freqs -- the host's step-to-step work (the result copy, Python, autograd,
+    # the start of sweep k's k_chunk_start -- the host's step-to-step work (the result copy, Python, autograd,
     # the next step's buffer fills and copies); the torch / copy kernels run in that interval count as busy,
     # not idle.  (Round 5's "idle before" was measured from the previous sweep's LAST kernel of any kind,
     # which put the turnaround inside the span.)
-    pads = [i for i, n in enumerate(names) if n == "k_pad_freqs"]
+    pads = [i for i, n in enumerate(names) if n in ("k_chunk_start", "k_pad_freqs")]
     native = [i for i, n in enumerate(names) if n.startswith("k_")]
     spans = []
     for a, b in zip(pads, pads[1:] + [len(rows)]):
@@ -92,7 +92,7 @@ def solves(path):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     names = [r["Kernel_Name"].split("(")[0].replace("void ", "").replace("pfr::", "") for r in rows]
-    pads = [i for i, n in enumerate(names) if n.startswith("k_pad_freqs")]
+    pads = [i for i, n in enumerate(names) if n.startswith(("k_chunk_start", "k_pad_freqs"))]
     a = pads[-1] if pads else 0
     seq = {}
     for r, n in zip(rows[a:], names[a:]):
