@@ -111,6 +111,7 @@ class _Engine:
         self._syms = {}
         self._use_symbolic(n_freqs)
         self._lanes_req = int(os.environ.get("PFR_LANES", "2")) if lanes is None else int(lanes)
+        self._lane_freqs = max(64, int(os.environ.get("PFR_LANE_FREQS", "256")))   # frequencies per lane at least
         self._fixed_batch = max_batch
         self.solvers, self.streams, self._pool = [], [], None
         self.n_lanes = 0
@@ -179,13 +180,14 @@ class _Engine:
         return changed
 
     def _lanes_for(self, n_freqs: int) -> int:
-        """Solver lanes for a sweep of ``n_freqs``: a lane per 512 frequencies at most.  Round 3 kept 512
-        frequencies on one lane (27.1k against 26.4k freq-solves/s with two); with round 5's kernels two lanes of
-        256 overlapped each other's narrow-level chains and kernel drains: 36.2-36.8k → 36.6-37.6k over five
-        alternations, four lanes of 128 27.5k (profiles/EXPERIMENTS.md, round 5).  Round 6's right-looking
-        narrow-level solves shortened the one-lane chain: 512 frequencies on one lane 41.7-41.8k against
-        41.1-41.2k on two (alternated, gpurun_out/r6k_e512)."""
-        return max(1, min(self._lanes_req, -(-max(1, n_freqs) // 512)))
+        """Solver lanes for a sweep of ``n_freqs``: a lane per PFR_LANE_FREQS (256) frequencies at most.  Round 3
+        kept 512 frequencies on one lane (27.1k against 26.4k freq-solves/s with two); with round 5's kernels two
+        lanes of 256 overlap each other's narrow-level chains and kernel drains: 36.2-36.8k -> 36.6-37.6k over five
+        alternations, four lanes of 128 27.5k (profiles/EXPERIMENTS.md, round 5).  Round 6, C4's rank block
+        (tools/strong_proxy.py --one 512, three alternations): two lanes of 256 41.5-41.6k, one lane of 512
+        40.6-40.7k (gpurun_out/r6u); 512 frequencies spread over the band favoured one lane (41.7-41.8k against
+        41.1-41.2k, gpurun_out/r6k_e512) -- the rank block is the C4 workload."""
+        return max(1, min(self._lanes_req, -(-max(1, n_freqs) // self._lane_freqs)))
 
     def _shape_for(self, n_freqs: int):
         """(lanes, frequencies per chunk) for a sweep of ``n_freqs``: up to ``lanes`` lanes of at

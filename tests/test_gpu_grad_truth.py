@@ -14,7 +14,7 @@ gradient.  Bound: the GPU partials, the theta gradient and the loss within W_RTO
 truth, absolute (no allowance from the oracle's own error; VERDICT round 3 asked for 2e-7).
 
 C4 (BASELINE.json configs[3]): a rank of the 8-GPU run sweeps the 512-frequency block
-``shard_range(4096, r, 8)``; a fresh engine sized for it takes the narrow-sweep path (one lane of 512, the
+``shard_range(4096, r, 8)``; a fresh engine sized for it takes the narrow-sweep path (2 lanes of 256, the
 leaf-1,000 ordering, the A11 LU in LDS on its few-workgroup levels).  Block 2
 holds the resonance (sample 1179).
 """
@@ -136,7 +136,7 @@ def test_c4_rank_block_at_c3_size():
         sel = np.arange(lo, hi)
         e = _check_set("c4_rank2_grad_truth", p, T, sel, theta)
         eng = p.engine()
-        assert eng.n_lanes == 1 and eng.max_batch == 512       # one lane of 512 (Problem._lanes_for)
+        assert eng.n_lanes == 2 and eng.max_batch == 256       # two lanes of 256 (Problem._lanes_for)
         assert eng.leaf_size_for(512) == 1000 and eng.sym is eng._syms[1000]
         assert eng.stats["n_levels"] < 38          # the shallow tree, not the deep one
         # fr at the fixture frequencies inside the block (forward sweep on the same engine)
