@@ -689,15 +689,29 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
   // x -= own(0:c0) * shared(0:c0, c0:c0+NB)   (PRE = false: c0 = 0, no prefix); PU = 3: software-pipelined
   int t0 = 0;
   if (PU == 3 && PRE && c0 > 0) {
-    // software-pipelined prefix: pivot t + 1's loads are issued before pivot t's products, so the products wait
-    // only for the older loads (the compiler's s_waitcnt then counts the younger ones) -- two pivots' loads in
-    // flight instead of the plain loop's drain at every iteration; same products, same order
-    cplx la[OFF_RPL], ua[NB], lb[OFF_RPL], ub[NB];
-    auto ld = [&](cplx (&l)[OFF_RPL], cplx (&u)[NB], int t) {
+    // software-pipelined prefix: the next D pivots' loads are in flight while a pivot's products run, so the
+    // products wait only for the oldest loads (the compiler's s_waitcnt counts the younger ones) instead of the
+    // plain loop's drain at every pivot; same products, same order.  c0 is a multiple of OB, so the rounds of D
+    // pivots are whole: no conditional load (a load under a branch makes the compiler drain every load at the
+    // join).  Running element pointers, advanced once per pivot: no 64-bit index product per load (round 6: 94
+    // instead of 180 instructions per pivot).  D = 4 measured slower (255 VGPRs; profiles/EXPERIMENTS.md).
+    constexpr int D = 2;
+    static_assert(OB % D == 0, "whole rounds");
+    cplx lb[D][OFF_RPL], ub[D][NB];
+    const cplx* lq[OFF_RPL];
 #pragma unroll
-      for (int h = 0; h < OFF_RPL; ++h) l[h] = base[(so[h] + (int64_t)t * sc) * Fc];
+    for (int h = 0; h < OFF_RPL; ++h) lq[h] = base + so[h] * Fc;
+    const cplx* uq = base + (int64_t)c0 * sb * Fc;
+    const int64_t lstep = sc * Fc, ustep = sa * Fc, ucol = sb * Fc;
+    auto ld = [&](cplx (&l)[OFF_RPL], cplx (&u)[NB]) {
 #pragma unroll
-      for (int j = 0; j < NB; ++j) u[j] = base[((int64_t)t * sa + (int64_t)(c0 + j) * sb) * Fc];
+      for (int h = 0; h < OFF_RPL; ++h) {
+        l[h] = *lq[h];
+        lq[h] += lstep;
+      }
+#pragma unroll
+      for (int j = 0; j < NB; ++j) u[j] = uq[j * ucol];
+      uq += ustep;
     };
     auto fm = [&](const cplx (&l)[OFF_RPL], const cplx (&u)[NB]) {
 #pragma unroll
@@ -705,15 +719,17 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
 #pragma unroll
         for (int j = 0; j < NB; ++j) x[h][j] = cfms(x[h][j], l[h], u[j]);
     };
-    ld(la, ua, 0);
-    int t = 0;
-    for (; t + 2 <= c0; t += 2) {
-      ld(lb, ub, t + 1);
-      fm(la, ua);
-      if (t + 2 < c0) ld(la, ua, t + 2);
-      fm(lb, ub);
+#pragma unroll
+    for (int d = 0; d < D; ++d) ld(lb[d], ub[d]);
+    for (int t = 0; t + 2 * D <= c0; t += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        fm(lb[d], ub[d]);
+        ld(lb[d], ub[d]);
+      }
     }
-    if (t < c0) fm(la, ua);
+#pragma unroll
+    for (int d = 0; d < D; ++d) fm(lb[d], ub[d]);
     t0 = c0;
   }
 #pragma unroll 2
