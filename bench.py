@@ -97,12 +97,13 @@ def pmc_traffic(chunk, symmetric):
 
 def pmc_solve_traffic(symmetric):
     """Measured HBM bytes per frequency of one sweep's triangular solves (every launch of the solve
-    kernels; chunks counted by their k_pad_freqs launches, one per chunk of freqs_per_sweep)."""
+    kernels; chunks counted by their k_chunk_start launches -- k_pad_freqs before round 6 --, one per chunk of
+    freqs_per_sweep)."""
     d = _pmc()
     if d is None or d.get("factorisation") != ("symmetric" if symmetric else "general"):
         return None
     k = d["kernels"]
-    sweeps = sum(e["dispatches"] for n, e in k.items() if n == "k_pad_freqs")
+    sweeps = sum(e["dispatches"] for n, e in k.items() if n in ("k_chunk_start", "k_pad_freqs"))
     if not sweeps:
         return None
     byts = sum(e["read_bytes"] + e["write_bytes"] for n, e in k.items() if n.startswith(SOLVE_KERNELS))

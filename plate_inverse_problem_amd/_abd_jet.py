@@ -170,14 +170,29 @@ def abd_and_jacobian(material, h: float, theta):
             np.stack([np.asarray(x.d, dtype=np.complex128) for x in jets]))
 
 
+def _cached_abd(material, h: float, theta: np.ndarray):
+    """abd_and_jacobian memoised on the last call per material (a pure function of the material's type and laminate,
+    h and theta): a loss + gradient loop re-evaluated at one theta -- a benchmark, a line search's repeated point,
+    the fr and loss of one iterate -- skips the jet pass (~100-200 us of Python per evaluation)."""
+    key = (material.atype, float(h), theta.tobytes(),
+           tuple(np.asarray(getattr(material, "angles", ()), dtype=np.float64).ravel().tolist()),
+           bool(getattr(material, "is_mps", False)))
+    last = material.__dict__.get("_abd_last")
+    if last is not None and last[0] == key:
+        return last[1], last[2]
+    c, J = abd_and_jacobian(material, h, theta)
+    material.__dict__["_abd_last"] = (key, c, J)
+    return c, J
+
+
 class _Coeffs(torch.autograd.Function):
     """theta (real, n) -> c (18 complex): values and Jacobian from the jet pass; backward one product."""
 
     @staticmethod
     def forward(ctx, theta, material, h):
-        c, J = abd_and_jacobian(material, h, theta.detach().cpu().numpy())
+        c, J = _cached_abd(material, h, theta.detach().cpu().numpy().astype(np.float64))
         ctx.J = J
-        return torch.from_numpy(c)
+        return torch.from_numpy(c.copy())
 
     @staticmethod
     def backward(ctx, grad_c):
