@@ -208,6 +208,12 @@ PFR_API int pfr_set_functional(pfr_solver* s, int32_t n_support, const int32_t* 
 PFR_API int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t loss_type,
                       const double* ref_dev, double scale, double* fr_dev, double* loss_dev, double* w_dev,
                       int32_t* flags_dev, void* stream);
+/* pfr_sweep with fresh outputs: loss_dev[0], w_dev (n_stiff complex) and flags_dev[0 .. nfreq) zeroed and the
+ * pfr_set_check backward-error buffer set to NaN by the sweep's first kernel, then filled as pfr_sweep accumulates
+ * them -- the loss step's initialisation without separate fills before the sweep (Problem._Engine.loss_step). */
+PFR_API int pfr_sweep_fresh(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t loss_type,
+                            const double* ref_dev, double scale, double* fr_dev, double* loss_dev, double* w_dev,
+                            int32_t* flags_dev, void* stream);
 /* Sweeps of this solver replayed from its captured hipGraph so far.  A pfr_sweep called again with the same
  * arguments, stream and solver state (no setter called in between; pfr_set_check's mode, tolerance and berr
  * pointer are part of the arguments) is captured into a hipGraph on that second call and replayed with one

@@ -389,9 +389,8 @@ class _Engine:
                  torch.empty((n, 2), dtype=torch.float64, device=self.device))
             self._step_bufs = {key: b}            # one shape at a time (a new size replaces it)
         acc, lanes, flags, berr = b
-        acc.zero_()
-        flags.zero_()
-        berr.fill_(float('nan'))
+        # no fills here: every lane's sweep initialises its loss / w slots, flags and backward errors in its first
+        # kernel (pfr_sweep_fresh); acc[-1] is written by the flag count below
         # the lanes' views of this step's tensors, made once per (buffers, freqs, ref): slicing costs host time
         # on the step-to-step turnaround
         vkey = (key, freqs.data_ptr(), ref.data_ptr(), freqs.numel())
@@ -404,7 +403,7 @@ class _Engine:
             vb, vf, vr, vfl = views[lo]
             sv.set_check(self.check_mode, self.check_tol, vb)
             try:
-                sv.sweep(vf, loss_type, ref=vr, scale=scale, loss=bufs[0], w=bufs[1], flags=vfl)
+                sv.sweep(vf, loss_type, ref=vr, scale=scale, loss=bufs[0], w=bufs[1], flags=vfl, fresh=True)
             finally:
                 sv.set_check(self.check_mode, self.check_tol)
         if self.check_mode & _native.PFR_CHECK_REFINE_ADJ:
@@ -413,7 +412,8 @@ class _Engine:
         torch.sum(flags != 0, dim=0, dtype=torch.float64, out=acc[-1])
         h = acc.cpu().numpy()
         L, m = self.n_lanes, 2 + 2 * self.n_stiff
-        per = h[:L * m].reshape(L, m)
+        # the lanes that swept (a lane with no frequencies ran nothing: its slot was never initialised)
+        per = h[:L * m].reshape(L, m)[[hi > lo for lo, hi in self._split(n)]]
         wk = (per[:, 2::2] + 1j * per[:, 3::2]).sum(axis=0)
         w = np.zeros(18, dtype=np.complex128)
         w[self.kidx] = wk

@@ -75,6 +75,7 @@ _PROTOS = {
     "pfr_set_functional": (C.c_int, [_P, C.c_int32, _I32P, _DP, C.c_double]),
     "pfr_sweep": (C.c_int, [_P, C.c_int32, _P, C.c_int32, _P, C.c_double, _P, _P, _P, _P, _P]),
     "pfr_sweep_graph_launches": (C.c_int64, [_P]),
+    "pfr_sweep_fresh": (C.c_int, [_P, C.c_int32, _P, C.c_int32, _P, C.c_double, _P, _P, _P, _P, _P]),
     "pfr_solve_multi": (C.c_int, [_P, C.c_int32, C.c_int32, _P, C.c_int64, _P, C.c_int64, C.c_int64, _P, C.c_int64,
                                   C.c_int32, _P, _P]),
     "pfr_hessian_sweep": (C.c_int, [_P, C.c_int32, _P, C.c_int32, _P, C.c_double, C.c_int32, _P, _P, _P, _P, _P,
@@ -273,9 +274,13 @@ class Solver:
         a, ap = _f64(np.asarray(a3).reshape(-1))
         check(lib().pfr_set_functional(self._h, int(i.size), ip, ap, float(ts)), "pfr_set_functional")
 
-    def sweep(self, freqs, loss_type=LOSS_NONE, ref=None, scale=1.0, fr=None, loss=None, w=None, flags=None):
-        check(lib().pfr_sweep(self._h, int(freqs.numel()), _ptr(freqs), int(loss_type), _ptr(ref), float(scale),
-                              _ptr(fr), _ptr(loss), _ptr(w), _ptr(flags), self._stream(freqs)), "pfr_sweep")
+    def sweep(self, freqs, loss_type=LOSS_NONE, ref=None, scale=1.0, fr=None, loss=None, w=None, flags=None,
+              fresh=False):
+        """pfr_sweep (loss / w / flags accumulated into), or with ``fresh`` pfr_sweep_fresh (they and the
+        pfr_set_check backward errors initialised by the sweep's first kernel)."""
+        fn = lib().pfr_sweep_fresh if fresh else lib().pfr_sweep
+        check(fn(self._h, int(freqs.numel()), _ptr(freqs), int(loss_type), _ptr(ref), float(scale),
+                 _ptr(fr), _ptr(loss), _ptr(w), _ptr(flags), self._stream(freqs)), "pfr_sweep")
 
     def hessian_sweep(self, freqs, loss_type, ref, scale, dcoef, loss=None, w=None, h=None, flags=None):
         """Loss, gradient partials w (18 complex) and second-order partials h (n_dir x 18 complex) with the

@@ -642,7 +642,9 @@ void contract_rows(pfr_solver* s, const double2* lam, const double2* x, int nv, 
 namespace pfr {
 void launch_flags_merge(const int* chunk, int nvalid, int* out, hipStream_t st);
 // a chunk's frequencies (padded with the last) and its flags cleared, one kernel
-void launch_chunk_start(double* freqs, const double* src, int nvalid, int64_t Fc, int* flags, hipStream_t st);
+void launch_chunk_start(double* freqs, const double* src, int nvalid, int64_t Fc, int* flags, hipStream_t st,
+                        double* loss = nullptr, double* w = nullptr, int nw = 0, int* out_flags = nullptr,
+                        double* berr = nullptr, int nfreq = 0);
 // p[0 .. n) = 0 (complex entries)
 void launch_zero(double2* p, int64_t n, hipStream_t st);
 }
@@ -1184,7 +1186,8 @@ int pfr_set_functional(pfr_solver* s, int32_t n_support, const int32_t* index, c
 namespace {
 // The launches of one sweep (pfr_sweep after its argument checks), direct or under stream capture.
 int sweep_launches(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t loss_type, const double* ref_dev,
-                   double scale, double* fr_dev, double* loss_dev, double* w_dev, int32_t* flags_dev, hipStream_t st) {
+                   double scale, double* fr_dev, double* loss_dev, double* w_dev, int32_t* flags_dev, hipStream_t st,
+                   bool fresh) {
   const bool reverse = loss_type != PFR_LOSS_NONE;
   reset_timing(s);
   const int64_t Fc = s->Fc;
@@ -1201,7 +1204,11 @@ int sweep_launches(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_
   bool used[5] = {true, true, true, adj, adj};
   for (int64_t q0 = 0; q0 < nfreq; q0 += Fc) {
     const int nv = (int)std::min<int64_t>(Fc, nfreq - q0);
-    pfr::launch_chunk_start(s->freqs, freqs_dev + q0, nv, Fc, s->flags, st);
+    if (fresh && q0 == 0)      // the caller's outputs initialised here (pfr_sweep_fresh)
+      pfr::launch_chunk_start(s->freqs, freqs_dev + q0, nv, Fc, s->flags, st, loss_dev, w_dev,
+                              reverse && w_dev ? 2 * s->n_stiff : 0, flags_dev, s->berr_out, nfreq);
+    else
+      pfr::launch_chunk_start(s->freqs, freqs_dev + q0, nv, Fc, s->flags, st);
     if (int rc0 = begin_chunk(s)) return rc0;
     record(s, 0, st);
     pfr::RhsDesc rd;
@@ -1383,8 +1390,10 @@ uint64_t key_bits(T v) {
 
 extern "C" {
 
-int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t loss_type, const double* ref_dev,
-              double scale, double* fr_dev, double* loss_dev, double* w_dev, int32_t* flags_dev, void* stream) {
+namespace {
+int sweep_impl(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t loss_type, const double* ref_dev,
+               double scale, double* fr_dev, double* loss_dev, double* w_dev, int32_t* flags_dev, void* stream,
+               bool fresh) {
   if (!s || nfreq <= 0 || !freqs_dev) return fail(PFR_ERR_ARG, "bad sweep arguments");
   if (!s->K || !s->M) return fail(PFR_ERR_STATE, "operator not set (pfr_set_operator)");
   if (!s->has_rhs) return fail(PFR_ERR_STATE, "rhs not set (pfr_set_rhs)");
@@ -1396,10 +1405,11 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
   HIP_TRY(hipSetDevice(s->device));
   hipStream_t st = (hipStream_t)stream;
   auto direct = [&] { return sweep_launches(s, nfreq, freqs_dev, loss_type, ref_dev, scale, fr_dev, loss_dev, w_dev,
-                                            flags_dev, st); };
+                                            flags_dev, st, fresh); };
   // per-launch timing events are host work between the launches: never under a graph
   if (!s->graph_mode || s->graph_off || s->timing) return direct();
-  const std::array<uint64_t, 14> key = {s->gen, key_bits(s->check_mode), key_bits(s->check_tol), key_bits(s->berr_out),
+  const std::array<uint64_t, 14> key = {s->gen * 2 + (fresh ? 1 : 0), key_bits(s->check_mode), key_bits(s->check_tol),
+                                        key_bits(s->berr_out),
                                         key_bits(nfreq), key_bits(freqs_dev), key_bits(loss_type), key_bits(ref_dev),
                                         key_bits(scale), key_bits(fr_dev), key_bits(loss_dev), key_bits(w_dev),
                                         key_bits(flags_dev), key_bits(st)};
@@ -1431,6 +1441,17 @@ int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t los
   HIP_TRY(hipGraphLaunch(s->gexec, st));
   ++s->graph_launches;
   return PFR_OK;
+}
+}  // namespace
+
+int pfr_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t loss_type, const double* ref_dev,
+              double scale, double* fr_dev, double* loss_dev, double* w_dev, int32_t* flags_dev, void* stream) {
+  return sweep_impl(s, nfreq, freqs_dev, loss_type, ref_dev, scale, fr_dev, loss_dev, w_dev, flags_dev, stream, false);
+}
+
+int pfr_sweep_fresh(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t loss_type, const double* ref_dev,
+                    double scale, double* fr_dev, double* loss_dev, double* w_dev, int32_t* flags_dev, void* stream) {
+  return sweep_impl(s, nfreq, freqs_dev, loss_type, ref_dev, scale, fr_dev, loss_dev, w_dev, flags_dev, stream, true);
 }
 
 int64_t pfr_sweep_graph_launches(const pfr_solver* s) { return s ? s->graph_launches : 0; }

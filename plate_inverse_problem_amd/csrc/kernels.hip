@@ -3777,17 +3777,47 @@ void launch_dirichlet_post(const DirDesc& d, int n_dir, double2* X, int64_t Fc, 
 
 // fill padded frequency slots with the last valid frequency (keeps padded lanes well-posed)
 // A chunk's start in one kernel (no memcpy / memset nodes in a captured sweep): its frequencies from the caller's
-// array, padded to Fc with the last one, and its flags cleared
+// array, padded to Fc with the last one, and its flags cleared.  Fresh outputs (pfr_sweep_fresh, first chunk): the
+// caller's loss, gradient partials and flags zeroed and the backward errors set to NaN here, instead of by separate
+// fills before the sweep.
+struct FreshOut {
+  double* loss = nullptr;
+  double* w = nullptr;
+  int nw = 0;               // doubles of w
+  int* flags = nullptr;
+  double* berr = nullptr;   // 2 per frequency
+  int nfreq = 0;
+};
 __global__ void k_chunk_start(double* __restrict__ freqs, const double* __restrict__ src, int nvalid, int64_t Fc,
-                              int* __restrict__ flags) {
+                              int* __restrict__ flags, FreshOut o) {
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q < Fc) {
     freqs[q] = src[q < nvalid ? q : nvalid - 1];
     flags[q] = 0;
   }
+  if (o.nfreq > 0) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = q; i < o.nfreq; i += stride) {
+      if (o.flags) o.flags[i] = 0;
+      if (o.berr) {
+        o.berr[2 * i] = __longlong_as_double(0x7ff8000000000000LL);
+        o.berr[2 * i + 1] = __longlong_as_double(0x7ff8000000000000LL);
+      }
+    }
+    if (o.loss && q == 0) o.loss[0] = 0.0;
+    if (o.w && q < o.nw) o.w[q] = 0.0;
+  }
 }
-void launch_chunk_start(double* freqs, const double* src, int nvalid, int64_t Fc, int* flags, hipStream_t st) {
-  LAUNCH(k_chunk_start, dim3((unsigned)((Fc + 255) / 256)), dim3(256), st, freqs, src, nvalid, Fc, flags);
+void launch_chunk_start(double* freqs, const double* src, int nvalid, int64_t Fc, int* flags, hipStream_t st,
+                        double* loss, double* w, int nw, int* out_flags, double* berr, int nfreq) {
+  FreshOut o;
+  o.loss = loss;
+  o.w = w;
+  o.nw = nw;
+  o.flags = out_flags;
+  o.berr = berr;
+  o.nfreq = nfreq;
+  LAUNCH(k_chunk_start, dim3((unsigned)((Fc + 255) / 256)), dim3(256), st, freqs, src, nvalid, Fc, flags, o);
 }
 __global__ void k_zero(double2* __restrict__ p, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)

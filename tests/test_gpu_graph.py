@@ -101,3 +101,48 @@ def test_graph_two_lanes_repeated_steps(monkeypatch):
         del p
         gc.collect()
         torch.cuda.empty_cache()
+
+
+def test_fresh_sweep_initialises_its_outputs():
+    """pfr_sweep_fresh (the loss step's sweeps): the loss / w slots, flags and backward errors are initialised by the
+    sweep itself -- with the step buffers poisoned beforehand, the loss, gradient partials and backward errors equal
+    those of the accumulating pfr_sweep into freshly zeroed / NaN-filled buffers, bit for bit."""
+    from plate_inverse_problem_amd import _native
+    from plate_inverse_problem_amd.distributed import shard_range
+    from plate_inverse_problem_amd.Problem import _coeffs18
+    T = np.load(os.path.join(GOLDEN, "c3_grad_truth.npz"))
+    lo, hi = shard_range(4096, 2, 8)
+    sel = np.arange(lo, hi)
+    p = make_problem("orthotropic", ny=25, device="cuda:0")
+    try:
+        eng = p.engine(sel.size)
+        eng.set_coefficients(_coeffs18(p._transform(), torch.as_tensor(T["theta"])).detach().numpy())
+        dev = eng.device
+        f = torch.as_tensor(T["freqs"][sel], device=dev)
+        ref = torch.view_as_real(torch.as_tensor(T["ref"][sel].astype(np.complex128), device=dev))
+        eng.loss_step(f, _native.LOSS_MSE_LOG_AFC, ref, 1.0 / sel.size)
+        for buf in eng._step_bufs.values():            # poison every step buffer
+            buf[0].fill_(1e300)
+            buf[2].fill_(7)
+            buf[3].fill_(123.0)
+        lsum, w, flags, nflag = eng.loss_step(f, _native.LOSS_MSE_LOG_AFC, ref, 1.0 / sel.size)
+        berr_fresh = eng.last_berr.cpu().numpy().copy()
+        loss = torch.zeros(1, dtype=torch.float64, device=dev)
+        wv = torch.zeros(eng.n_stiff, dtype=torch.complex128, device=dev)
+        fl = torch.zeros(sel.size, dtype=torch.int32, device=dev)
+        berr = torch.full((sel.size, 2), float("nan"), dtype=torch.float64, device=dev)
+        eng.sweep(f, _native.LOSS_MSE_LOG_AFC, ref=ref, scale=1.0 / sel.size, loss=loss, w=torch.view_as_real(wv),
+                  flags=fl, berr=berr)
+        w_acc = eng.expand(wv).cpu().numpy()
+        report("fresh_sweep", loss_fresh=lsum, loss_acc=float(loss.item()), nflag=nflag)
+        assert nflag == 0 and int(fl.count_nonzero()) == 0 and int(flags.count_nonzero()) == 0
+        assert lsum == float(loss.item())
+        assert np.array_equal(w, w_acc)
+        b = berr.cpu().numpy()
+        assert np.array_equal(np.isnan(berr_fresh), np.isnan(b)) and np.array_equal(np.nan_to_num(berr_fresh),
+                                                                                    np.nan_to_num(b))
+    finally:
+        p._engine = None
+        del p
+        gc.collect()
+        torch.cuda.empty_cache()
