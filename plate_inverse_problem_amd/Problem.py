@@ -311,13 +311,15 @@ class _Engine:
         per = (-(-n // self.n_lanes) + 63) // 64 * 64
         return [(min(n, i * per), min(n, (i + 1) * per)) for i in range(self.n_lanes)]
 
-    def _run(self, call, n, accum, lane_bufs=None):
+    def _run(self, call, n, accum, lane_bufs=None, raw=False):
         """``call(solver, lo, hi, bufs)`` on every lane's stream; per-lane ``accum``
         buffers (zeros like each given tensor) are summed into the given tensors -- or, with
         ``lane_bufs`` (the caller's zeroed per-lane buffers, one list per lane), accumulated there and
         left to the caller.  With several lanes each lane's launches are issued from its own host
         thread (the C calls release the GIL): issued one after the other, the second lane started a
-        whole sweep's enqueue time (~9 ms) after the first and finished that much later."""
+        whole sweep's enqueue time (~9 ms) after the first and finished that much later.  ``raw``: ``call`` issues
+        native work only and takes the lane's stream handle as a fifth argument (no torch device / stream context
+        per lane on the step's critical path)."""
         cur = torch.cuda.current_stream(self.device)
         jobs = []
         spans = [(i, sv, st, lo, hi) for i, (sv, st, (lo, hi)) in
@@ -335,6 +337,9 @@ class _Engine:
 
         def lane(job):
             sv, st, lo, hi, bufs = job
+            if raw:
+                call(sv, lo, hi, bufs, st.cuda_stream)
+                return
             with torch.cuda.device(self.device), torch.cuda.stream(st):
                 call(sv, lo, hi, bufs)
 
@@ -399,16 +404,17 @@ class _Engine:
             views = {lo: (berr[lo:hi], freqs[lo:hi], ref[lo:hi], flags[lo:hi]) for lo, hi in self._split(n)}
             self._step_views = {vkey: views}
 
-        def call(sv, lo, hi, bufs):
+        def call(sv, lo, hi, bufs, stream):
             vb, vf, vr, vfl = views[lo]
             sv.set_check(self.check_mode, self.check_tol, vb)
             try:
-                sv.sweep(vf, loss_type, ref=vr, scale=scale, loss=bufs[0], w=bufs[1], flags=vfl, fresh=True)
+                sv.sweep(vf, loss_type, ref=vr, scale=scale, loss=bufs[0], w=bufs[1], flags=vfl, fresh=True,
+                         stream=stream)
             finally:
                 sv.set_check(self.check_mode, self.check_tol)
         if self.check_mode & _native.PFR_CHECK_REFINE_ADJ:
             self._seeded = True
-        self._run(call, n, None, lane_bufs=lanes)
+        self._run(call, n, None, lane_bufs=lanes, raw=True)
         torch.sum(flags != 0, dim=0, dtype=torch.float64, out=acc[-1])
         h = acc.cpu().numpy()
         L, m = self.n_lanes, 2 + 2 * self.n_stiff

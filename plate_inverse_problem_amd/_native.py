@@ -275,12 +275,14 @@ class Solver:
         check(lib().pfr_set_functional(self._h, int(i.size), ip, ap, float(ts)), "pfr_set_functional")
 
     def sweep(self, freqs, loss_type=LOSS_NONE, ref=None, scale=1.0, fr=None, loss=None, w=None, flags=None,
-              fresh=False):
+              fresh=False, stream=None):
         """pfr_sweep (loss / w / flags accumulated into), or with ``fresh`` pfr_sweep_fresh (they and the
-        pfr_set_check backward errors initialised by the sweep's first kernel)."""
+        pfr_set_check backward errors initialised by the sweep's first kernel); on ``stream`` (a HIP stream
+        handle) or the current torch stream."""
         fn = lib().pfr_sweep_fresh if fresh else lib().pfr_sweep
         check(fn(self._h, int(freqs.numel()), _ptr(freqs), int(loss_type), _ptr(ref), float(scale),
-                 _ptr(fr), _ptr(loss), _ptr(w), _ptr(flags), self._stream(freqs)), "pfr_sweep")
+                 _ptr(fr), _ptr(loss), _ptr(w), _ptr(flags), self._stream(freqs) if stream is None else stream),
+              "pfr_sweep")
 
     def hessian_sweep(self, freqs, loss_type, ref, scale, dcoef, loss=None, w=None, h=None, flags=None):
         """Loss, gradient partials w (18 complex) and second-order partials h (n_dir x 18 complex) with the
