@@ -726,6 +726,9 @@ __device__ __forceinline__ void offdiag_chunk(cplx* __restrict__ base, const int
       for (int d = 0; d < D; ++d) {
         fm(lb[d], ub[d]);
         ld(lb[d], ub[d]);
+        // keep this pivot's loads here, in issue order: sunk below the later products (the scheduler's choice)
+        // they reach the next round's first wait as the youngest, and every load drains there
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
 #pragma unroll
