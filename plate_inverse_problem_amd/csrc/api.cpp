@@ -196,6 +196,9 @@ struct pfr_solver {
                                         // those whose largest pivot block has at least n pivots, 0 none, -1 auto
                                         // (default since round 3: 512-frequency sweeps +2.6 %, 4,096 unchanged)
   int fac_lds_wg = 160;                 // PFR_FAC_LDS_WG: auto mode threshold (workgroups of k_factor_sym)
+  int fac_g_wg = 0;                     // PFR_FAC_G_WG: k_factor_sym launches below this many workgroups take G = 4 / 8
+  int fac_gbig = 4, fac_g_ns = 64;      // PFR_FAC_GBIG / PFR_FAC_G_NS: k_factor_sym's lane groups per wave on the
+                                        // levels whose largest pivot block exceeds PFR_FAC_G_NS pivots
   int us2_nar = 256;                    // PFR_US2_NAR: solve launches (paired top-down, bottom-up chain) with fewer
                                         // (front, group) workgroups than this take the narrow-level forms -- pivot
                                         // blocks in LDS, left-looking, the update parts with their columns split
@@ -358,7 +361,14 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     // (symmetric kernel: up to 16 waves -- the top levels' few fronts are latency-bound, every
     // wave more takes rows off each wave's serial chain)
     const int fac_wmax = s->fac_wmax;
-    const int64_t wgs = (int64_t)nf * ngroups * pfr::FAC_G;
+    // lane groups per wave of the symmetric A11 kernel: FAC_G; fac_gbig on the levels with a pivot block of more
+    // than fac_g_ns pivots, whose long chains gain from more row slots per wave (the deep tree's level 25 with its
+    // 76-pivot separator at 2,048 frequencies: 0.61 -> 0.41 ms with 4; the levels of 2-3 fronts of <= 35 pivots
+    // below it were slower with 4, gpurun_out/fg2_t2048_*); raised to 4 / 8 while the launch has fewer than
+    // fac_g_wg workgroups (default off)
+    int G = (s->sym && s->level_maxns[l] > s->fac_g_ns) ? s->fac_gbig : pfr::FAC_G;
+    while (s->sym && G < 8 && (int64_t)nf * ngroups * G < s->fac_g_wg) G *= 2;
+    const int64_t wgs = (int64_t)nf * ngroups * G;
     const int64_t wfill = (4096 + wgs - 1) / wgs;
     const int Wp = (int)std::max<int64_t>(
         1, s->sym ? std::min<int64_t>(fac_wmax, wfill) : std::min<int64_t>(s->level_W[l], wfill));
@@ -369,7 +379,8 @@ int factor_all(pfr_solver* s, int mode, const double2* data, int64_t ds, int nva
     if (level_lds(s, l))
       pfr::launch_factor_lds(s->P, s->d_level_fronts + s->level_ptr[l], nf, s->level_maxns[l], s->F, s->Fc, s->flags, st);
     else
-      pfr::launch_factor(s->sym, s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st);
+      pfr::launch_factor(s->sym, s->P, s->d_level_fronts + s->level_ptr[l], nf, Wp, ngroups, s->F, s->Fc, s->flags, st,
+                         G);
     mark(l, 2);
     // the software-pipelined L21 prefix on the launches with few waves (symmetric analyses, operator form)
     const int64_t owaves = (int64_t)(s->item_ptr[l + 1] - s->item_ptr[l]) * ngroups;
@@ -794,6 +805,10 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   // Schur block-kernel threshold and the pipelined L21 prefix
   s->solve_wmax = knob("PFR_SOLVE_WMAX", 8, 1, 8);
   s->fac_wmax = knob("PFR_FAC_WMAX", 16, 1, 16);
+  s->fac_g_wg = knob("PFR_FAC_G_WG", 0, 0, 1 << 20);
+  s->fac_gbig = knob("PFR_FAC_GBIG", 4, 2, 8);
+  if (s->fac_gbig != 2 && s->fac_gbig != 8) s->fac_gbig = 4;
+  s->fac_g_ns = knob("PFR_FAC_G_NS", 64, 0, 1 << 20);
   s->us2_small = knob("PFR_US2_SMALL", 110, 0, pfr::MAX_FRONT);
   s->split_target = knob("PFR_SOLVE_SPLIT", 256, 0, 1 << 20);
   s->us2_nar = knob("PFR_US2_NAR", 256, 0, 1 << 30);

@@ -392,14 +392,15 @@ __device__ __forceinline__ void row_updateR(const cplx* __restrict__ rd, cplx* _
 constexpr int FAC_JBU = 2;   // trailing-update columns per read-modify-write step
 constexpr int FAC_SB = 2;    // 4-pivot blocks per super-block (rank of the trailing update / 4)
 
-// One front's A11 LU for the 64 / FAC_G frequencies of c.q's lane group: c.w / c.W the wave's index and count
+// One front's A11 LU for the 64 / G frequencies of c.q's lane group: c.w / c.W the wave's index and count
 // among the waves working on these frequencies (every wave of the workgroup reaches the same barriers)
+template <int G>
 __device__ __forceinline__ void factor_sym_front(const DevPattern& P, int front, cplx* __restrict__ F, int64_t Fc,
                                                  int* __restrict__ flags, const Ctx& c, int sub) {
   const Front fr = P.fronts[front];
   const int f = fr.f, ns = fr.ns;
   cplx* __restrict__ base = F + fr.off * Fc + c.q;
-  const int r0 = FAC_G * c.w + sub, rs = FAC_G * c.W;   // this lane's first row offset, row stride
+  const int r0 = G * c.w + sub, rs = G * c.W;   // this lane's first row offset, row stride
 #define E(a, b) base[((int64_t)(a) * f + (b)) * Fc]
   // 4-pivot diagonal block at k0 (kb pivots): one load burst from the lower triangle, LU in
   // registers (U = diag(U) L^T up to rounding), one store burst
@@ -502,15 +503,20 @@ __device__ __forceinline__ void factor_sym_front(const DevPattern& P, int front,
 #undef E
 }
 
+// G lane groups per wave (64 / G frequencies x G front rows): FAC_G, or 4 / 8 on the levels whose launch would
+// otherwise have few workgroups (a single 76-pivot separator at 2,048 frequencies: 64) -- more workgroups of
+// fewer frequencies, each wave-instruction advancing G rows, so each workgroup's pivot chain passes over fewer
+// row strides
+template <int G>
 __global__ __launch_bounds__(1024) void k_factor_sym(DevPattern P, const int* __restrict__ lvl, cplx* __restrict__ F,
                                                int64_t Fc, int* __restrict__ flags) {
   Ctx c;
   c.lane = threadIdx.x & 63;
   c.w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   c.W = blockDim.x >> 6;
-  constexpr int QG = 64 / FAC_G;     // frequencies per lane group
+  constexpr int QG = 64 / G;     // frequencies per lane group
   c.q = (int64_t)blockIdx.y * QG + c.lane % QG;
-  factor_sym_front(P, lvl[blockIdx.x], F, Fc, flags, c, c.lane / QG);
+  factor_sym_front<G>(P, lvl[blockIdx.x], F, Fc, flags, c, c.lane / QG);
 }
 
 // Symmetric A11 LU with the pivot block resident in LDS, for the levels where the frequency-minor kernel gets few
@@ -3465,8 +3471,10 @@ void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int max
 }
 
 void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F,
-                   int64_t Fc, int* flags, hipStream_t st) {
-  if (sym) LAUNCH(k_factor_sym, dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
+                   int64_t Fc, int* flags, hipStream_t st, int G) {
+  if (sym && G == 8) LAUNCH(k_factor_sym<8>, dim3(nfronts, ngroups * 8), dim3(64 * W), st, P, lvl, F, Fc, flags);
+  else if (sym && G == 4) LAUNCH(k_factor_sym<4>, dim3(nfronts, ngroups * 4), dim3(64 * W), st, P, lvl, F, Fc, flags);
+  else if (sym) LAUNCH(k_factor_sym<FAC_G>, dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
   else LAUNCH(k_factor_level<true>, dim3(nfronts, ngroups * FAC_G), dim3(64 * W), st, P, lvl, F, Fc, flags);
 }
 

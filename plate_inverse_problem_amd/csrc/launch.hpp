@@ -38,8 +38,9 @@ void launch_combine(const double* stiff, int n_stiff, int64_t nnz, const CoefPac
 void launch_assemble(int mode, const int4* recs, int nrec, const int* xptr, const int2* xl, int ngroups, double2* F,
                      int64_t Fc, const double* freqs, const double2* K, const double* M, const double2* data,
                      int64_t ds, int nvalid, hipStream_t st);
+// G: lane groups per wave of the symmetric kernel (FAC_G, 4 or 8)
 void launch_factor(bool sym, const DevPattern& P, const int* lvl, int nfronts, int W, int ngroups, double2* F, int64_t Fc,
-                   int* flags, hipStream_t st);
+                   int* flags, hipStream_t st, int G = FAC_G);
 // symmetric A11 LU with the pivot block in LDS (one front x one frequency per workgroup); maxns = the level's
 // largest pivot block (sizes the dynamic LDS: (maxns (maxns + 1) / 2 + 4 maxns) x 16 B)
 void launch_factor_lds(const DevPattern& P, const int* lvl, int nfronts, int maxns, double2* F, int64_t Fc, int* flags,

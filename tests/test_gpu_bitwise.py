@@ -8,7 +8,10 @@ operations per entry in the same order, so a difference means a wrong index, a l
   * PFR_OFF_PU_WAVES: the software-pipelined L21 prefix (k_offdiag_level<0, false, 3>) on every launch against
     none;
   * PFR_FRONT0: the bottom level fused into one kernel (k_front0: A11, L21 and the update block per frequency in
-    registers) against the four class kernels (assembly, A11 LU, L21 rows, Schur update) on level 0.
+    registers) against the four class kernels (assembly, A11 LU, L21 rows, Schur update) on level 0;
+  * PFR_FAC_GBIG / PFR_FAC_G_NS / PFR_FAC_G_WG: the A11 LU (k_factor_sym<G>) with 4 / 8 lane groups per wave on
+    the levels with big pivot blocks, on the launches with few workgroups, and on every level, against 2
+    everywhere.
 The measured-slower variants of round 4 (dependency-driven passes, right-looking / shared-U11 L21 rows, prefix
 batches, fused A11 gather, pipelined paired updates) were removed with their tests.
 """
@@ -86,3 +89,11 @@ def test_front0_fused_bottom_level_bitwise(monkeypatch, lo, hi):
     base = _run(monkeypatch, lo, hi, env={"PFR_FRONT0": "0"})
     _same(f"front0_{lo}_{hi}", base, _run(monkeypatch, lo, hi, env={"PFR_FRONT0": "1"}))
 
+
+
+@pytest.mark.parametrize("lo,hi", [(1024, 1536), (0, 2048)])
+def test_factor_lane_groups_bitwise(monkeypatch, lo, hi):
+    base = _run(monkeypatch, lo, hi, fac_lds="0", env={"PFR_FAC_G_WG": "0", "PFR_FAC_GBIG": "2"})
+    for gb, gns, wg in (("4", "64", "0"), ("8", "20", "0"), ("2", "64", "1024"), ("2", "64", "1000000000")):
+        _same(f"fac_gbig{gb}_ns{gns}_wg{wg}_{lo}_{hi}", base, _run(
+            monkeypatch, lo, hi, fac_lds="0", env={"PFR_FAC_G_WG": wg, "PFR_FAC_GBIG": gb, "PFR_FAC_G_NS": gns}))

@@ -162,6 +162,7 @@ def test_c2_forward_sweep_matches_truth():
     {"PFR_FAC_LDS": "1"},              # every level's A11 LU through the LDS-resident kernel (1 frequency / workgroup)
     {"PFR_FAC_LDS": "-1"},             # auto: the levels where k_factor_sym would get few workgroups
     {"PFR_FAC_LDS": "0"},              # never (the global-memory A11 LU on every level)
+    {"PFR_FAC_LDS": "0", "PFR_FAC_G_WG": "1000000000"},   # ... with 8 lane groups per wave on every level
     {"PFR_FN_DOT": "0"},               # fr from the top-down pass over the support's fronts
     {"PFR_CONTRACT_WALK": "0"},        # the gradient contraction as k_contract_eg's own walk
     {"PFR_FN_DOT": "0", "PFR_CONTRACT_WALK": "0"},

@@ -39,6 +39,24 @@ def sweep(self, *a, **k):
 PM._Engine.loss_step = loss_step
 _native.Solver.sweep = sweep
 
+# finer marks (HT_FINE=1): engine lookup, coefficient set, the lane runner, the per-lane set_check, stream waits
+if os.environ.get("HT_FINE") == "1":
+    import threading
+
+    def _wrap(owner, name, tag):
+        orig = getattr(owner, name)
+
+        def f(*a, **k):
+            main = threading.current_thread() is threading.main_thread()
+            mark(tag + ("" if main else "@pool"))
+            return orig(*a, **k)
+        setattr(owner, name, f)
+    _wrap(PM._Engine, "set_coefficients", "set_coef_in")
+    _wrap(PM._Engine, "_run", "run_in")
+    _wrap(_native.Solver, "set_check", "set_check_in")
+    _wrap(torch.cuda.Stream, "wait_stream", "wait_stream_in")
+    _wrap(PM.Problem, "engine", "engine_in")
+
 
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 512
@@ -71,9 +89,12 @@ def main():
     rows = []
     for i in range(1, steps):
         t_prev = outs[i - 1]
-        seg = [(tag, t) for tag, t in T if t > t_prev][:8]
+        seg = [(tag, t) for tag, t in T if t > t_prev][:24]
         first_native = next(t for tag, t in seg if tag == "native_sweep_in")
-        rows.append({tag: round((t - t_prev) * 1e6, 1) for tag, t in seg})
+        row = {}
+        for tag, t in seg:
+            row.setdefault(tag, round((t - t_prev) * 1e6, 1))     # first occurrence of each tag
+        rows.append(row)
         rows[-1]["first_native_us"] = round((first_native - t_prev) * 1e6, 1)
     for r in rows:
         print(r)
