@@ -220,6 +220,13 @@ PFR_API int pfr_sweep_fresh(pfr_solver* s, int32_t nfreq, const double* freqs_de
  * hipGraphLaunch afterwards -- the same kernels with the same arguments; only with PFR_GRAPH=1 (off by default).  The
  * reference's analogue is none: its sweep is a host loop of UMFPACK calls (InnerState.h:276-288). */
 PFR_API int64_t pfr_sweep_graph_launches(const pfr_solver* s);
+/* Stream ordering for a host that drives several solver lanes: work enqueued on `waiter` after this call starts
+ * only after the work enqueued on `signaller` before it (one event of the calling thread and device, recorded on
+ * signaller, waited for on waiter; both HIP stream handles of the current device).  The loss step orders each lane's
+ * stream after the caller's and the caller's after every lane with it (Problem._Engine._run) -- one C call where
+ * torch's Stream.wait_stream makes and destroys an event.  No reference analogue (its sweep is a host loop,
+ * InnerState.h:276-288). */
+PFR_API int pfr_stream_order(void* waiter, void* signaller);
 
 /* Exact second derivatives with the factors of the sweep reused (replaces the reference's
  * forward-over-reverse Hessian, `jax.jacobian(grad)` in Optimizers.py:125-136, whose mode-4

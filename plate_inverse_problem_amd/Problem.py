@@ -28,7 +28,7 @@ import scipy.sparse as sp
 import torch
 
 from . import _native
-from ._abd_jet import coeffs18 as _jet_coeffs18
+from ._abd_jet import coeffs18 as _jet_coeffs18, _cached_abd
 from .Accelerometer import Accelerometer, AccelerometerParams
 from .Geometry import Geometry, GeometryParams
 from .Material import Material, get_material
@@ -65,6 +65,47 @@ def decoupled_symmetric(rows, cols, vals, n, rtol=1e-10) -> bool:
         if amax > 0 and abs(A - A.T).max() > rtol * amax:
             return False
     return True
+
+
+class _LaneThread:
+    """One solver lane's host thread: the lane's launches are issued here while the caller's thread issues lane 0's
+    (the C calls release the GIL).  A queue pair instead of a ThreadPoolExecutor: submit is one C-level put (the
+    executor's submit took ~15 us of the step-to-step turnaround before lane 0's first launch)."""
+
+    def __init__(self):
+        import queue
+        import threading
+        self._in, self._out = queue.SimpleQueue(), queue.SimpleQueue()
+        self._th = threading.Thread(target=_LaneThread._loop, args=(self._in, self._out), name="pfr-lane",
+                                    daemon=True)
+        self._th.start()
+        # the thread holds the queues only: an engine dropped without close() ends its lane threads
+        weakref.finalize(self, self._in.put, None)
+
+    @staticmethod
+    def _loop(qin, qout):
+        while True:
+            item = qin.get()
+            if item is None:
+                return
+            fn, arg = item
+            try:
+                fn(arg)
+                qout.put(None)
+            except BaseException as e:       # noqa: BLE001 -- handed to the caller's result()
+                qout.put(e)
+            del fn, arg, item
+
+    def submit(self, fn, arg):
+        self._in.put((fn, arg))
+
+    def result(self):
+        """The exception the submitted call raised, or None; waits for it."""
+        return self._out.get()
+
+    def close(self):
+        self._in.put(None)
+        self._th.join()
 
 
 class _Engine:
@@ -114,6 +155,7 @@ class _Engine:
         self._lane_freqs = max(64, int(os.environ.get("PFR_LANE_FREQS", "256")))   # frequencies per lane at least
         self._fixed_batch = max_batch
         self.solvers, self.streams, self._pool = [], [], None
+        self._spin_wait = os.environ.get("PFR_STEP_WAIT", "spin") != "block"
         self.n_lanes = 0
         self._seeded = False
         self._sized_for = set()
@@ -242,15 +284,15 @@ class _Engine:
             torch.cuda.synchronize(self.device)
         self.solvers, self.streams = [], []       # free the old workspaces before allocating
         if self._pool is not None:
-            self._pool.shutdown(wait=True)
+            for t in self._pool:
+                t.close()
             self._pool = None
         self.n_lanes = lanes
         self.solvers = [_native.Solver(self.sym, self.device.index, batch) for _ in range(lanes)]
         self._seeded = False           # no refinement seed vector allocated in the new solvers yet
         self.streams = [torch.cuda.Stream(self.device) for i in range(lanes)]
         if lanes > 1 and os.environ.get("PFR_PAR_LAUNCH", "1") != "0":
-            from concurrent.futures import ThreadPoolExecutor
-            self._pool = ThreadPoolExecutor(max_workers=lanes, thread_name_prefix="pfr-lane")
+            self._pool = [_LaneThread() for _ in range(lanes - 1)]
         for sv in self.solvers:
             sv.set_stiffness(self.stiff, self.e[self.kidx])
             sv.set_operator(torch.view_as_real(self.K), self.mass)      # K(theta) shared by the lanes
@@ -324,6 +366,9 @@ class _Engine:
         jobs = []
         spans = [(i, sv, st, lo, hi) for i, (sv, st, (lo, hi)) in
                  enumerate(zip(self.solvers, self.streams, self._split(n))) if hi > lo]
+        # the lanes ordered after the current stream and it after them by pfr_stream_order (one C call each;
+        # Stream.wait_stream makes and destroys an event per call: host time before the first launch)
+        cur_h = cur.cuda_stream
         for i, sv, st, lo, hi in spans:
             # the lane's accumulation buffers are zero-filled on the current stream BEFORE the lane
             # stream is ordered after it (k_reduce accumulates into them with +=); one lane accumulates
@@ -332,11 +377,13 @@ class _Engine:
                 bufs = lane_bufs[i]
             else:
                 bufs = list(accum) if len(spans) == 1 else [None if a is None else torch.zeros_like(a) for a in accum]
-            st.wait_stream(cur)
-            jobs.append((sv, st, lo, hi, bufs))
+            _native.stream_order(st.cuda_stream, cur_h)
+            jobs.append((i, sv, st, lo, hi, bufs))
+        if _HT is not None:
+            _HT("lanes_ordered")
 
         def lane(job):
-            sv, st, lo, hi, bufs = job
+            _, sv, st, lo, hi, bufs = job
             if raw:
                 call(sv, lo, hi, bufs, st.cuda_stream)
                 return
@@ -345,16 +392,18 @@ class _Engine:
 
         err = None
         if len(jobs) > 1 and self._pool is not None:
-            from concurrent.futures import wait
-            # lanes 1.. on the pool, lane 0 on this thread meanwhile (one thread handoff less before the
+            # lanes 1.. on their threads, lane 0 on this thread meanwhile (one thread handoff less before the
             # first launch: the GPU idles from the previous step's result until then)
-            futs = [self._pool.submit(lane, j) for j in jobs[1:]]
+            for t, j in zip(self._pool, jobs[1:]):
+                t.submit(lane, j)
+            if _HT is not None:
+                _HT("submitted")
             try:
                 lane(jobs[0])
             except Exception as e:           # noqa: BLE001 -- re-raised once every lane is joined
                 err = e
-            wait(futs)                       # every lane has issued its work (or failed) ...
-            errs = [f.exception() for f in futs if f.exception() is not None]
+            errs = [t.result() for t, _ in zip(self._pool, jobs[1:])]   # every lane has issued its work (or failed) ...
+            errs = [e for e in errs if e is not None]
             err = err if err is not None else (errs[0] if errs else None)
         else:
             for j in jobs:
@@ -363,8 +412,8 @@ class _Engine:
                 except Exception as e:       # noqa: BLE001 -- re-raised once every lane is joined
                     err = e
                     break
-        for _, st, _, _, bufs in jobs:       # ... and the current stream is ordered after all of them
-            cur.wait_stream(st)
+        for i, _, st, _, _, bufs in jobs:    # ... and the current stream is ordered after all of them
+            _native.stream_order(cur_h, st.cuda_stream)
             for b in bufs:
                 if b is not None:
                     b.record_stream(cur)
@@ -372,7 +421,7 @@ class _Engine:
             raise err
         if lane_bufs is not None:
             return
-        for _, st, _, _, bufs in jobs:
+        for _, _, st, _, _, bufs in jobs:
             for a, b in zip(accum, bufs):
                 if a is not None and b is not a:
                     a.add_(b)
@@ -386,22 +435,28 @@ class _Engine:
         n = freqs.numel()
         key = (n, self.n_lanes, id(self.solvers[0]))
         b = self._step_bufs.get(key) if hasattr(self, "_step_bufs") else None
+        L, m = self.n_lanes, 2 + 2 * self.n_stiff
         if b is None:
-            L, m = self.n_lanes, 2 + 2 * self.n_stiff
-            acc = torch.empty(L * m + 1, dtype=torch.float64, device=self.device)
+            # the lanes' loss / w slots (float64) and the flags (int32) in one device buffer: one device->host
+            # copy per step, the flagged count taken on the host (no count kernels after the sweep)
+            raw = torch.empty(8 * L * m + 4 * n, dtype=torch.uint8, device=self.device)
+            acc = raw[:8 * L * m].view(torch.float64)
             lanes = [[acc[l * m:l * m + 1], acc[l * m + 2:(l + 1) * m].view(self.n_stiff, 2)] for l in range(L)]
-            b = (acc, lanes, torch.empty(n, dtype=torch.int32, device=self.device),
-                 torch.empty((n, 2), dtype=torch.float64, device=self.device))
+            b = (acc, lanes, raw[8 * L * m:].view(torch.int32),
+                 torch.empty((n, 2), dtype=torch.float64, device=self.device), raw,
+                 torch.empty(raw.numel(), dtype=torch.uint8, pin_memory=True), torch.cuda.Event())
             self._step_bufs = {key: b}            # one shape at a time (a new size replaces it)
-        acc, lanes, flags, berr = b
+        acc, lanes, flags, berr, raw, host, done = b
         # no fills here: every lane's sweep initialises its loss / w slots, flags and backward errors in its first
-        # kernel (pfr_sweep_fresh); acc[-1] is written by the flag count below
+        # kernel (pfr_sweep_fresh)
         # the lanes' views of this step's tensors, made once per (buffers, freqs, ref): slicing costs host time
         # on the step-to-step turnaround
         vkey = (key, freqs.data_ptr(), ref.data_ptr(), freqs.numel())
         views = self._step_views.get(vkey) if hasattr(self, "_step_views") else None
         if views is None:
             views = {lo: (berr[lo:hi], freqs[lo:hi], ref[lo:hi], flags[lo:hi]) for lo, hi in self._split(n)}
+            ran = [hi > lo for lo, hi in self._split(n)]
+            views["_act"] = None if all(ran) else np.nonzero(ran)[0]
             self._step_views = {vkey: views}
 
         def call(sv, lo, hi, bufs, stream):
@@ -415,16 +470,33 @@ class _Engine:
         if self.check_mode & _native.PFR_CHECK_REFINE_ADJ:
             self._seeded = True
         self._run(call, n, None, lane_bufs=lanes, raw=True)
-        torch.sum(flags != 0, dim=0, dtype=torch.float64, out=acc[-1])
-        h = acc.cpu().numpy()
-        L, m = self.n_lanes, 2 + 2 * self.n_stiff
-        # the lanes that swept (a lane with no frequencies ran nothing: its slot was never initialised)
-        per = h[:L * m].reshape(L, m)[[hi > lo for lo, hi in self._split(n)]]
-        wk = (per[:, 2::2] + 1j * per[:, 3::2]).sum(axis=0)
-        w = np.zeros(18, dtype=np.complex128)
-        w[self.kidx] = wk
+        # the result into pinned memory and the host polling for it: a blocking copy returned ~85 us after the copy
+        # had finished on the GPU (the host thread woken from its sleep, gpurun_out/tl/timeline.txt) -- GPU idle
+        # before the next step's first launch.  PFR_STEP_WAIT=block: the blocking copy.
+        if self._spin_wait:
+            host.copy_(raw, non_blocking=True)
+            done.record(torch.cuda.current_stream(self.device))
+            while not done.query():
+                pass
+            if _HT is not None:
+                _HT("copy_done")
+            hb = host.numpy()
+        else:
+            hb = raw.cpu().numpy()
+        h = hb[:8 * L * m].view(np.float64).reshape(L, m)
+        self.last_flags_host = hb[8 * L * m:].view(np.int32).copy()
+        # summed over the lanes that swept (a lane with no frequencies ran nothing: its slot was never initialised);
+        # a lane's slot: loss, (unused), then its n_stiff partials as complex pairs
+        act = views["_act"]
+        tot = h[act].sum(axis=0) if act is not None else h.sum(axis=0)
+        wk = tot[2:].view(np.complex128)
+        if wk.size == 18:
+            w = wk.copy()
+        else:
+            w = np.zeros(18, dtype=np.complex128)
+            w[self.kidx] = wk
         self.last_berr = berr
-        return float(per[:, 0].sum()), w, flags, int(h[-1])
+        return float(tot[0]), w, flags, int(np.count_nonzero(self.last_flags_host))
 
     def sweep(self, freqs, loss_type=_native.LOSS_NONE, ref=None, scale=1.0, fr=None, loss=None, w=None,
               flags=None, berr=None):
@@ -466,6 +538,7 @@ class _Engine:
 
 
 _JET_TYPES = ('isotropic', 'orthotropic', 'orthotropic_d4', 'sol', 'symm_sol')
+_HT = None          # host-turnaround marks (tools/host_turnaround.py sets a callable; None in use)
 
 
 def _coeffs18(transform, params: torch.Tensor) -> torch.Tensor:
@@ -542,6 +615,36 @@ class _SweepLoss(torch.autograd.Function):
     def backward(ctx, g):
         (w,) = ctx.saved_tensors
         return torch.conj(w) * g, None, None, None, None, None, None
+
+
+class _JetSweepLoss(torch.autograd.Function):
+    """params -> loss as ONE autograd node for the material types of the jet transform (_abd_jet.py): c(theta) and
+    its Jacobian J from the jet pass, loss and the partials w from the fused sweep (_Engine.loss_step), and
+    dL/dtheta = Re(w J) -- the product _Coeffs.backward forms from _SweepLoss.backward's conj(w) -- already in the
+    forward, so that the backward is one scale.  The same values, bit for bit, as the chain
+    params.to(float64).cpu() * scaling -> _Coeffs -> _SweepLoss, with three autograd nodes fewer on the host's
+    step-to-step turnaround (the GPU idles from one step's result to the next step's first launch)."""
+
+    @staticmethod
+    def forward(ctx, params, material, h, scaling, engine, freqs, ref, loss_id, n_total):
+        # scaling: 1.0 or a float64 numpy array (the host arithmetic in numpy: the same IEEE products as the
+        # chain's torch ones, a few us less per step)
+        ctx.cast = params.dtype != torch.float64 or params.device.type != "cpu"
+        p = (params.detach().to(torch.float64).cpu() if ctx.cast else params.detach()).numpy() * scaling
+        c, J = _cached_abd(material, h, p)
+        engine.set_coefficients(c)
+        lsum, w, flags, nflag = engine.loss_step(freqs, loss_id, torch.view_as_real(ref), 1.0 / n_total)
+        engine.last_flags = _check_flags(flags) if nflag else np.zeros(flags.numel(), np.int32)
+        # dL/dparams for an incoming gradient of 1 (the chain's values for it, bit for bit: Re(w J) * scaling)
+        ctx.gt = torch.from_numpy(np.real(w @ J) * scaling)
+        ctx.dtype, ctx.device = params.dtype, params.device
+        return torch.scalar_tensor(lsum / n_total, dtype=torch.float64)
+
+    @staticmethod
+    def backward(ctx, g):
+        grad = ctx.gt * g
+        return (grad.to(dtype=ctx.dtype, device=ctx.device) if ctx.cast else grad), None, None, None, None, None, \
+            None, None, None
 
 
 def _check_flags(flags):
@@ -807,6 +910,7 @@ class Problem:
             raise ValueError(f'Function type "{func_type}" is not supported!')
         loss_id = _native.LOSS_IDS[func_type]
         scaling = 1.0 if scaling_params is None else torch.as_tensor(np.array(scaling_params, dtype=np.float64))
+        scaling_np = 1.0 if scaling_params is None else np.array(scaling_params, dtype=np.float64)
         n_total = frequencies.shape[0]
         lo, hi, reduce_fn = 0, n_total, None
         if distributed:
@@ -819,6 +923,10 @@ class Problem:
 
         def loss(params):
             p = params if isinstance(params, torch.Tensor) else torch.as_tensor(np.asarray(params, dtype=np.float64))
+            if reduce_fn is None and self.material.atype in _JET_TYPES:
+                # one autograd node (host turnaround of the optimiser / bench loop)
+                return _JetSweepLoss.apply(p, self.material, self.geometry.height, scaling_np,
+                                           self.engine(max(1, hi - lo)), f_local, ref_local, loss_id, n_total)
             c = self._coeffs(transform, p.to(torch.float64).cpu() * scaling)
             return _SweepLoss.apply(c, self.engine(max(1, hi - lo)), f_local, ref_local, loss_id, n_total, reduce_fn)
 

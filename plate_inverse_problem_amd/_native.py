@@ -75,6 +75,7 @@ _PROTOS = {
     "pfr_set_functional": (C.c_int, [_P, C.c_int32, _I32P, _DP, C.c_double]),
     "pfr_sweep": (C.c_int, [_P, C.c_int32, _P, C.c_int32, _P, C.c_double, _P, _P, _P, _P, _P]),
     "pfr_sweep_graph_launches": (C.c_int64, [_P]),
+    "pfr_stream_order": (C.c_int, [_P, _P]),
     "pfr_sweep_fresh": (C.c_int, [_P, C.c_int32, _P, C.c_int32, _P, C.c_double, _P, _P, _P, _P, _P]),
     "pfr_solve_multi": (C.c_int, [_P, C.c_int32, C.c_int32, _P, C.c_int64, _P, C.c_int64, C.c_int64, _P, C.c_int64,
                                   C.c_int32, _P, _P]),
@@ -140,6 +141,12 @@ def _ptr(t) -> int:
     if not t.is_contiguous():
         raise ValueError("device tensors passed to libpfr must be contiguous")
     return t.data_ptr()
+
+
+def stream_order(waiter: int, signaller: int):
+    """pfr_stream_order: work enqueued on HIP stream ``waiter`` from now on runs after the work enqueued on
+    ``signaller`` so far (stream handles, e.g. torch.cuda.Stream.cuda_stream)."""
+    check(lib().pfr_stream_order(waiter, signaller), "pfr_stream_order")
 
 
 class Symbolic:

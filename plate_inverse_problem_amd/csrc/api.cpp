@@ -1471,6 +1471,19 @@ int pfr_sweep_fresh(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32
 
 int64_t pfr_sweep_graph_launches(const pfr_solver* s) { return s ? s->graph_launches : 0; }
 
+int pfr_stream_order(void* waiter, void* signaller) {
+  // one event per (thread, device), recorded again for every ordering: a wait takes the event's state at the time
+  // of the hipStreamWaitEvent call, so a later record does not move an earlier wait
+  thread_local std::vector<hipEvent_t> evs;
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  if ((int)evs.size() <= dev) evs.resize(dev + 1, nullptr);
+  if (!evs[dev]) HIP_TRY(hipEventCreateWithFlags(&evs[dev], hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(evs[dev], (hipStream_t)signaller));
+  HIP_TRY(hipStreamWaitEvent((hipStream_t)waiter, evs[dev], 0));
+  return PFR_OK;
+}
+
 int pfr_hessian_sweep(pfr_solver* s, int32_t nfreq, const double* freqs_dev, int32_t loss_type, const double* ref_dev,
                       double scale, int32_t n_dir, const double* dcoef, double* loss_dev, double* w_dev,
                       double* h_dev, int32_t* flags_dev, void* stream) {

@@ -146,3 +146,39 @@ def test_fresh_sweep_initialises_its_outputs():
         del p
         gc.collect()
         torch.cuda.empty_cache()
+
+
+def test_jet_loss_is_one_node_and_matches_the_chain():
+    """getLossFunction on a jet-transform material (Problem._JetSweepLoss): one autograd node from params to the
+    loss, and loss and gradient EQUAL the three-node chain params * scaling -> _Coeffs -> _SweepLoss on the same
+    engine, bit for bit (with a parameter scaling, as the reference's scaling_params)."""
+    from plate_inverse_problem_amd import _native
+    from plate_inverse_problem_amd.distributed import shard_range
+    from plate_inverse_problem_amd.Problem import _SweepLoss
+    T = np.load(os.path.join(GOLDEN, "c3_grad_truth.npz"))
+    lo, hi = shard_range(4096, 2, 8)
+    sel = np.arange(lo, hi)
+    p = make_problem("orthotropic", ny=25, device="cuda:0")
+    try:
+        scal = np.array([1.0, 2.0, 0.5, 1.0, 1.0])
+        th = np.asarray(T["theta"]) / scal
+        fn = p.getLossFunction(T["freqs"][sel], T["ref"][sel], "MSE_LOG_AFC", scaling_params=scal)
+        x = torch.tensor(th, requires_grad=True)
+        v = fn(x)
+        assert type(v.grad_fn).__name__ == "_JetSweepLossBackward"
+        assert [type(f).__name__ for f, _ in v.grad_fn.next_functions if f is not None] == ["AccumulateGrad"]
+        v.backward()
+        y = torch.tensor(th, requires_grad=True)
+        c = p._coeffs(p._transform(), y.to(torch.float64).cpu() * torch.as_tensor(scal))
+        u = _SweepLoss.apply(c, p.engine(sel.size), p._freqs(T["freqs"][sel]),
+                             torch.as_tensor(T["ref"][sel].astype(np.complex128), device=p.device),
+                             _native.LOSS_IDS["MSE_LOG_AFC"], sel.size, None)
+        u.backward()
+        report("jet_loss_node", loss=v.item(), grad_diff=float(np.max(np.abs(x.grad.numpy() - y.grad.numpy()))))
+        assert v.item() == u.item()
+        assert np.array_equal(x.grad.numpy(), y.grad.numpy())
+    finally:
+        p._engine = None
+        del p
+        gc.collect()
+        torch.cuda.empty_cache()

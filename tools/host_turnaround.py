@@ -56,6 +56,7 @@ if os.environ.get("HT_FINE") == "1":
     _wrap(_native.Solver, "set_check", "set_check_in")
     _wrap(torch.cuda.Stream, "wait_stream", "wait_stream_in")
     _wrap(PM.Problem, "engine", "engine_in")
+    PM._HT = mark
 
 
 def main():
@@ -98,6 +99,11 @@ def main():
         rows[-1]["first_native_us"] = round((first_native - t_prev) * 1e6, 1)
     for r in rows:
         print(r)
+    if os.environ.get("HT_DUMP"):
+        # absolute CLOCK_MONOTONIC ns of every mark (perf_counter on Linux), to line up with a rocprofv3 kernel trace
+        import json
+        off = time.monotonic_ns() - time.perf_counter_ns()
+        json.dump([(tag, int(t * 1e9) + off) for tag, t in T], open(os.environ["HT_DUMP"], "w"))
     print("mean host time from result to the next step's first native sweep call: %.1f us"
           % np.mean([r["first_native_us"] for r in rows]))
     ins = [t for tag, t in T if tag == "native_sweep_in"]
