@@ -196,6 +196,7 @@ struct pfr_solver {
                                         // those whose largest pivot block has at least n pivots, 0 none, -1 auto
                                         // (default since round 3: 512-frequency sweeps +2.6 %, 4,096 unchanged)
   int fac_lds_wg = 160;                 // PFR_FAC_LDS_WG: auto mode threshold (workgroups of k_factor_sym)
+  int res_unroll = 8;                   // PFR_RES_UNROLL: entries per gather batch of the adjoint check walk (4 / 8)
   int fac_g_wg = 0;                     // PFR_FAC_G_WG: k_factor_sym launches below this many workgroups take G = 4 / 8
   int fac_gbig = 4, fac_g_ns = 64;      // PFR_FAC_GBIG / PFR_FAC_G_NS: k_factor_sym's lane groups per wave on the
                                         // levels whose largest pivot block exceeds PFR_FAC_G_NS pivots
@@ -624,6 +625,7 @@ void check_solution(pfr_solver* s, int which, int mode, int rhs, const pfr::RhsD
   d.G = rd.G;
   d.walk = s->d_walk;
   d.glist = glist;
+  d.unroll = s->res_unroll;
   if (contract) {
     d.se = s->stiff;
     d.n_stiff = s->n_stiff;
@@ -806,6 +808,7 @@ int pfr_solver_create(const pfr_symbolic* sym, const int32_t* colptr, const int3
   s->solve_wmax = knob("PFR_SOLVE_WMAX", 8, 1, 8);
   s->fac_wmax = knob("PFR_FAC_WMAX", 16, 1, 16);
   s->fac_g_wg = knob("PFR_FAC_G_WG", 0, 0, 1 << 20);
+  s->res_unroll = knob("PFR_RES_UNROLL", 8, 4, 8) == 8 ? 8 : 4;
   s->fac_gbig = knob("PFR_FAC_GBIG", 4, 2, 8);
   if (s->fac_gbig != 2 && s->fac_gbig != 8) s->fac_gbig = 4;
   s->fac_g_ns = knob("PFR_FAC_G_NS", 64, 0, 1 << 20);

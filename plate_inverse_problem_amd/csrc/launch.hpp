@@ -147,6 +147,7 @@ struct ResidDesc {
   int n_stiff = 0;
   double2* kpart = nullptr;
   const int* glist = nullptr;  // the groups to walk (REFINE_CAP, -1: none; NULL: every group)
+  int unroll = 4;              // entries per gather batch of the adjoint check walk (4 or 8; the same bits)
 };
 // Mu != NULL (mode 0, rhs 0): also the functional-correction dot products sum_p Mu_p r_p, one partial
 // per workgroup and frequency in cpart (residual_parts(n) x Fc), summed by launch_correct_finish

@@ -11,7 +11,8 @@ operations per entry in the same order, so a difference means a wrong index, a l
     registers) against the four class kernels (assembly, A11 LU, L21 rows, Schur update) on level 0;
   * PFR_FAC_GBIG / PFR_FAC_G_NS / PFR_FAC_G_WG: the A11 LU (k_factor_sym<G>) with 4 / 8 lane groups per wave on
     the levels with big pivot blocks, on the launches with few workgroups, and on every level, against 2
-    everywhere.
+    everywhere;
+  * PFR_RES_UNROLL: the residual walks with 8 entries per gather batch against 4.
 The measured-slower variants of round 4 (dependency-driven passes, right-looking / shared-U11 L21 rows, prefix
 batches, fused A11 gather, pipelined paired updates) were removed with their tests.
 """
@@ -97,3 +98,9 @@ def test_factor_lane_groups_bitwise(monkeypatch, lo, hi):
     for gb, gns, wg in (("4", "64", "0"), ("8", "20", "0"), ("2", "64", "1024"), ("2", "64", "1000000000")):
         _same(f"fac_gbig{gb}_ns{gns}_wg{wg}_{lo}_{hi}", base, _run(
             monkeypatch, lo, hi, fac_lds="0", env={"PFR_FAC_G_WG": wg, "PFR_FAC_GBIG": gb, "PFR_FAC_G_NS": gns}))
+
+
+@pytest.mark.parametrize("lo,hi", [(1024, 1536), (0, 2048)])
+def test_residual_walk_unroll_bitwise(monkeypatch, lo, hi):
+    base = _run(monkeypatch, lo, hi, env={"PFR_RES_UNROLL": "4"})
+    _same(f"res_unroll8_{lo}_{hi}", base, _run(monkeypatch, lo, hi, env={"PFR_RES_UNROLL": "8"}))
