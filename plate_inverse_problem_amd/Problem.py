@@ -205,11 +205,14 @@ class _Engine:
         44.5-44.9k; 2,048 leaf 1,000 / 2,000 / 10,000: 53.0k / 55.2k / 55.4-55.8k; 4,096: 10,000 best.  Round 5, with
         512 frequencies on two lanes of 256: leaf 120 / 200 / 350 / 700 / 1,000 / 2,000 / 5,000 / 10,000: 36.1-36.2k /
         36.8-37.0k / 36.7-37.2k / 36.8-36.9k / 37.9-38.4k / 36.2-38.0k / 38.1-38.3k / 33.5k; 1,024 leaf 1,000 / 2,000 /
-        5,000 / 10,000: 48.4-48.6k / 50.3-50.4k / 50.2-50.8k / 48.5k; 2,048: 5,000 = 10,000 (gpurun_out/r6_leaf*)."""
+        5,000 / 10,000: 48.4-48.6k / 50.3-50.4k / 50.2-50.8k / 48.5k; 2,048: 5,000 = 10,000 (gpurun_out/r6_leaf*).
+        Round 6, C4's rank block (tools/ab_proxy.sh, 7 alternations on two boxes): leaf 600 / 1,000 / 2,000 / 3,000
+        40.7-41.7k / 41.3-42.9k / 41.5-43.4k / 40.6-41.2k, 2,000 ahead of 1,000 in 6 of 7 pairs (+0.8 %;
+        gpurun_out/lf_p512, lf2_p512): 2,000 for up to 512 frequencies."""
         if self._leaf_env is not None:
             return self._leaf_env
         n_freqs = max(1, n_freqs)
-        return 200 if n_freqs <= 256 else 1000 if n_freqs <= 512 else 2000 if n_freqs <= 1024 else 10000
+        return 200 if n_freqs <= 256 else 2000 if n_freqs <= 1024 else 10000
 
     def _use_symbolic(self, n_freqs: int) -> bool:
         """Select (building once) the symbolic analysis for a sweep width; True if it changed."""

@@ -137,7 +137,7 @@ def test_c4_rank_block_at_c3_size():
         e = _check_set("c4_rank2_grad_truth", p, T, sel, theta)
         eng = p.engine()
         assert eng.n_lanes == 2 and eng.max_batch == 256       # two lanes of 256 (Problem._lanes_for)
-        assert eng.leaf_size_for(512) == 1000 and eng.sym is eng._syms[1000]
+        assert eng.leaf_size_for(512) == 2000 and eng.sym is eng._syms[2000]
         assert eng.stats["n_levels"] < 38          # the shallow tree, not the deep one
         # fr at the fixture frequencies inside the block (forward sweep on the same engine)
         inside = (F["index"] >= lo) & (F["index"] < hi)
